@@ -1,0 +1,150 @@
+/*
+ * ntcomp_gpu.h -- C ABI of libntcomp_gpu.so, the MI355X (gfx950) encode/decode hot path
+ * of ntcomp.  Plain C types only: pointers, sizes, status codes.  No torch, no HIP types.
+ *
+ * What each entry point replaces in the reference (tmaklin/ntcomp, Rust):
+ *
+ *   ntc_index_upload        the in-memory (SbwtIndexVariant, LcsArray) pair returned by
+ *                           kbo::index::load_sbwt (src/main.rs:149, :190) -- uploaded once
+ *                           per GPU and kept resident in HBM.
+ *   ntc_encode_batch[_device]
+ *                           ntcomp::encode_sequence (src/lib.rs:163-230) FUSED with
+ *                           ntcomp::encode::encode_dictionary (src/encode.rs:129-166), over
+ *                           a batch of reads: the per-read loop of src/main.rs:162-173.
+ *                           Output is the u64 record stream, per read rightmost segment
+ *                           first with the `first` flag on it, bit-identical to
+ *                           encode_dictionary's, ready for write_block_to (src/lib.rs:232).
+ *   ntc_decode_batch[_device]
+ *                           ntcomp::decode_sequence (src/lib.rs:254-318) over the records
+ *                           of one or more blocks (what decode_block, src/lib.rs:320-368,
+ *                           calls after unzipping a block).
+ *
+ * Error behaviour: the reference panics (unwrap / assert!) or, for a base absent from
+ * the index, never terminates (lib.rs:206-207 with d = 0 underflows).  Across this ABI
+ * every such case is a status code; nothing aborts:
+ *   NTC_ERR_EMPTY_READ    encode.rs:133-135 / lib.rs:224 (EncodeError on empty input)
+ *   NTC_ERR_INVALID_BASE  non-ACGT byte, or a base the index does not contain
+ *   NTC_ERR_LENGTH        a match length >= 2^24 (assert at lib.rs:226)
+ *
+ * Threading: one ntc_ctx per GPU, driven by one host thread at a time.  Contexts on
+ * different devices are independent.  The index is read-only once uploaded.
+ */
+#ifndef NTCOMP_GPU_H
+#define NTCOMP_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NTC_ABI_VERSION 1
+
+typedef enum ntc_status {
+    NTC_OK = 0,
+    NTC_ERR_INVALID_ARG = 1,
+    NTC_ERR_INVALID_BASE = 2,
+    NTC_ERR_EMPTY_READ = 3,
+    NTC_ERR_LENGTH = 4,
+    NTC_ERR_CAPACITY = 5,
+    NTC_ERR_HIP = 6,
+    NTC_ERR_NO_INDEX = 7,
+    NTC_ERR_FORMAT = 8,
+    NTC_ERR_IO = 9,
+    NTC_ERR_UNSUPPORTED = 10
+} ntc_status;
+
+typedef struct ntc_ctx ntc_ctx;
+
+/* A host-memory view of an SBWT subset-matrix index + LCS array (sbwt 0.3.11 semantics,
+ * SURVEY.md Appendix A.1): n nodes in colex order, node 0 = root $^k.
+ *   rows[c]  (c = A,C,G,T): ceil(n/64) little-endian u64 words; bit j%64 of word j/64
+ *            set <=> node j's label set contains c.
+ *   C[c]     = 1 + #labels with a character < c (= first node ending with c).
+ *   lcs[j]   = longest common suffix of nodes j-1 and j (lcs[0] = 0); k <= 255.      */
+typedef struct ntc_index_view {
+    uint64_t n_nodes;
+    uint32_t k;
+    uint32_t reserved;
+    const uint64_t *rows[4];
+    uint64_t C[4];
+    const uint8_t *lcs;
+} ntc_index_view;
+
+/* Per-call device timings (milliseconds, HIP events on the context's stream). */
+typedef struct ntc_timing {
+    double total_ms;      /* first launch -> last launch of the call           */
+    double main_ms;       /* the dominant kernel: encode MS+parse / decode walk */
+    double aux_ms;        /* everything else (tiling, scans, record emit)       */
+    uint64_t units;       /* bases processed (encode: input, decode: output)   */
+    uint64_t records;     /* records produced (encode) / consumed (decode)     */
+} ntc_timing;
+
+int ntc_abi_version(void);
+
+int ntc_ctx_create(int device, ntc_ctx **out);
+void ntc_ctx_destroy(ntc_ctx *ctx);
+const char *ntc_last_error(const ntc_ctx *ctx);
+/* Optional: launch on a caller-owned hipStream_t (passed as void*); NULL = own stream. */
+int ntc_ctx_set_stream(ntc_ctx *ctx, void *hip_stream);
+int ntc_ctx_synchronize(ntc_ctx *ctx);
+
+/* Upload the index once; builds the device-side rank lines, the unique-predecessor
+ * bitvector and the inverse-walk jump table in HBM (DESIGN.md "Data layout"). */
+int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *ix);
+int ntc_index_info(const ntc_ctx *ctx, uint64_t *n_nodes, uint32_t *k, uint64_t *device_bytes);
+
+/* ---- encode ---------------------------------------------------------------------- */
+/* Host buffers: bases = reads back to back (ASCII, already normalize()d to upper case);
+ * read_offsets[n_reads+1].  On success rec_offsets_out[n_reads+1] delimits each read's
+ * records inside rec_out.  Synchronous.  On a per-read error *bad_read (if non-NULL)
+ * receives the first failing read index.                                            */
+int ntc_encode_batch(ntc_ctx *ctx, const uint8_t *bases, const uint64_t *read_offsets,
+                     uint64_t n_reads, uint64_t *rec_out, uint64_t rec_capacity,
+                     uint64_t *rec_offsets_out, int64_t *bad_read);
+
+/* Device buffers (HBM-resident, e.g. from hipMalloc or a torch tensor); read_offsets
+ * index d_bases directly.  Asynchronous on the context stream when max_read_len > 0 (an
+ * upper bound on every read's length, e.g. 150); with max_read_len = 0 the library
+ * first sizes its scratch from the offsets (one small device->host read).  Call
+ * ntc_encode_status() (which synchronises) for the verdict.  rec_capacity must be >=
+ * the total number of records (total bases is always enough).                       */
+int ntc_encode_batch_device(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_read_offsets,
+                            uint64_t n_reads, uint32_t max_read_len, uint64_t *d_rec_out,
+                            uint64_t rec_capacity, uint64_t *d_rec_offsets_out);
+int ntc_encode_status(ntc_ctx *ctx, int64_t *bad_read, uint64_t *n_records);
+
+/* ---- decode ---------------------------------------------------------------------- */
+/* recs: the u64 records of whole reads (one or more blocks, in file order).  Writes the
+ * reads back to back into bases_out and read_offsets_out[n_reads+1].  Synchronous.
+ * NTC_ERR_CAPACITY if bases_capacity / offsets_capacity are too small (the required
+ * sizes are returned in *n_bases_out and *n_reads_out).                              */
+int ntc_decode_batch(ntc_ctx *ctx, const uint64_t *recs, uint64_t n_recs, uint8_t *bases_out,
+                     uint64_t bases_capacity, uint64_t *read_offsets_out,
+                     uint64_t offsets_capacity, uint64_t *n_reads_out, uint64_t *n_bases_out);
+/* Device variant; asynchronous; verdict + sizes via ntc_decode_status().             */
+int ntc_decode_batch_device(ntc_ctx *ctx, const uint64_t *d_recs, uint64_t n_recs,
+                            uint8_t *d_bases_out, uint64_t bases_capacity,
+                            uint64_t *d_read_offsets_out, uint64_t offsets_capacity);
+int ntc_decode_status(ntc_ctx *ctx, uint64_t *n_reads, uint64_t *n_bases);
+
+/* Timings of the last encode/decode call (synchronises). */
+int ntc_last_timing(ntc_ctx *ctx, ntc_timing *out);
+
+/* Device memory helpers for callers without their own allocator (bench, tests). */
+int ntc_device_alloc(ntc_ctx *ctx, uint64_t bytes, void **d_ptr);
+int ntc_device_free(ntc_ctx *ctx, void *d_ptr);
+int ntc_memcpy_h2d(ntc_ctx *ctx, void *d_dst, const void *h_src, uint64_t bytes);
+int ntc_memcpy_d2h(ntc_ctx *ctx, void *h_dst, const void *d_src, uint64_t bytes);
+
+/* Diagnostics: the k-bounded matching statistics of each position (d, colex start of
+ * the interval) exactly as StreamingIndex::matching_statistics (lib.rs:172-173) returns
+ * them; host buffers sized to the total number of bases.                             */
+int ntc_debug_matching_statistics(ntc_ctx *ctx, const uint8_t *bases,
+                                  const uint64_t *read_offsets, uint64_t n_reads,
+                                  uint32_t *d_out, uint32_t *start_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,53 @@
+/*
+ * ntcomp_host.h -- host-side C ABI of libntcomp_gpu.so: the index producer and file
+ * I/O around the GPU hot path, plus the seeded synthetic workload generator used by
+ * bench.py and the tests.
+ *
+ *   ntc_build_index   replaces kbo::build(&[Vec<u8>], BuildOpts{add_revcomp: true, ..})
+ *                     (src/main.rs:111-134; tests/fasta_data.rs:56-63): a deterministic
+ *                     SBWT subset-matrix + LCS construction.
+ *   ntc_index_save /  replace kbo::index::serialize_sbwt (src/main.rs:138) and
+ *   ntc_index_load    kbo::index::load_sbwt (src/main.rs:149, :190): <prefix>.sbwt +
+ *                     <prefix>.lcs.  NOTE: this round writes this library's own layout
+ *                     (DESIGN.md "Index files"); the sbwt 0.3.11 byte layout is not
+ *                     available offline and is unpinned.
+ */
+#ifndef NTCOMP_HOST_H
+#define NTCOMP_HOST_H
+
+#include <stdint.h>
+
+#include "ntcomp_gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ntc_index_host ntc_index_host;
+
+/* seqs: sequences back to back, seq_offsets[n_seqs+1].  Bytes other than ACGTacgt split
+ * a sequence (k-mers containing them are skipped, as in kbo/sbwt).  k in [1,255].
+ * n_threads <= 0 picks the hardware concurrency.                                     */
+int ntc_build_index(const uint8_t *seqs, const uint64_t *seq_offsets, uint64_t n_seqs,
+                    uint32_t k, int add_revcomp, int n_threads, ntc_index_host **out);
+void ntc_index_free(ntc_index_host *ix);
+/* Borrowed view (valid until ntc_index_free) for ntc_index_upload or inspection. */
+int ntc_index_view_of(const ntc_index_host *ix, ntc_index_view *view);
+int ntc_index_save(const ntc_index_host *ix, const char *prefix);
+int ntc_index_load(const char *prefix, ntc_index_host **out);
+
+/* ---- synthetic workload ------------------------------------------- */
+/* i.i.d. uniform ACGT genome from SplitMix64(seed). */
+int ntc_synth_genome(uint64_t seed, uint64_t length, uint8_t *out);
+/* n_reads reads of read_len bases from genome; read r depends only on (seed, r): start
+ * uniform on [0, glen-read_len], reverse-complemented with probability 1/2, i.i.d.
+ * substitutions with probability err_per_million / 1e6.  out = n_reads*read_len bytes.
+ * Reads first_read .. first_read+n_reads-1 (so shards regenerate identical data).    */
+int ntc_synth_reads(const uint8_t *genome, uint64_t glen, uint64_t seed, uint64_t first_read,
+                    uint64_t n_reads, uint32_t read_len, uint32_t err_per_million,
+                    int n_threads, uint8_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,360 @@
+"""ntcomp_amd -- Python bindings (ctypes) to libntcomp_gpu.so, the MI355X encode/decode
+hot path of ntcomp (tmaklin/ntcomp).
+
+The compute runs in the HIP library; this module only marshals buffers.  There is NO CPU
+fallback: if the library is missing or no GPU is visible, the GPU entry points raise.
+
+Names mirror the reference's Rust API (src/lib.rs, src/encode.rs) where it has them:
+  encode_sequence(nucleotides, ctx)   ~ ntcomp::encode_sequence + encode::encode_dictionary
+                                        (lib.rs:163-230, encode.rs:129-166) -> u64 records
+  decode_sequence(encoding, ctx)      ~ ntcomp::decode_sequence (lib.rs:254-318)
+  Index.build(seqs, k)                ~ kbo::build(.., add_revcomp = true) (main.rs:111-134)
+  Index.load(prefix) / .save(prefix)  ~ kbo::index::load_sbwt / serialize_sbwt
+
+Process note: if torch is used in the same process, import torch BEFORE this module so
+the library binds to the already-loaded HIP runtime (one runtime per process).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libntcomp_gpu.so")
+
+NTC_OK = 0
+STATUS = {
+    0: "NTC_OK", 1: "NTC_ERR_INVALID_ARG", 2: "NTC_ERR_INVALID_BASE", 3: "NTC_ERR_EMPTY_READ",
+    4: "NTC_ERR_LENGTH", 5: "NTC_ERR_CAPACITY", 6: "NTC_ERR_HIP", 7: "NTC_ERR_NO_INDEX",
+    8: "NTC_ERR_FORMAT", 9: "NTC_ERR_IO", 10: "NTC_ERR_UNSUPPORTED",
+}
+
+# every symbol include/ntcomp_gpu.h and include/ntcomp_host.h declare
+EXPORTED = [
+    "ntc_abi_version", "ntc_ctx_create", "ntc_ctx_destroy", "ntc_last_error", "ntc_ctx_set_stream",
+    "ntc_ctx_synchronize", "ntc_index_upload", "ntc_index_info", "ntc_encode_batch",
+    "ntc_encode_batch_device", "ntc_encode_status", "ntc_decode_batch", "ntc_decode_batch_device",
+    "ntc_decode_status", "ntc_last_timing", "ntc_device_alloc", "ntc_device_free", "ntc_memcpy_h2d",
+    "ntc_memcpy_d2h", "ntc_debug_matching_statistics", "ntc_build_index", "ntc_index_free",
+    "ntc_index_view_of", "ntc_index_save", "ntc_index_load", "ntc_synth_genome", "ntc_synth_reads",
+]
+
+
+class NtcError(RuntimeError):
+    def __init__(self, code, msg=""):
+        self.code = code
+        super().__init__(f"{STATUS.get(code, code)}: {msg}")
+
+
+class IndexView(ctypes.Structure):
+    _fields_ = [("n_nodes", ctypes.c_uint64), ("k", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("rows", ctypes.c_void_p * 4), ("C", ctypes.c_uint64 * 4), ("lcs", ctypes.c_void_p)]
+
+
+class Timing(ctypes.Structure):
+    _fields_ = [("total_ms", ctypes.c_double), ("main_ms", ctypes.c_double), ("aux_ms", ctypes.c_double),
+                ("units", ctypes.c_uint64), ("records", ctypes.c_uint64)]
+
+
+_lib = None
+
+
+def build_library(force=False):
+    """Compile libntcomp_gpu.so in-tree for gfx950 (make -C ntcomp_amd/csrc)."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.check_call(["make", "-s", "-j8", "-C", os.path.join(_HERE, "csrc")])
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} missing: build it with `make -C ntcomp_amd/csrc` "
+                          "(or __graft_entry__.build()); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    P, u64, u32, i64 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int64
+    I = ctypes.c_int
+    sig = {
+        "ntc_abi_version": (I, []),
+        "ntc_ctx_create": (I, [I, ctypes.POINTER(P)]),
+        "ntc_ctx_destroy": (None, [P]),
+        "ntc_last_error": (ctypes.c_char_p, [P]),
+        "ntc_ctx_set_stream": (I, [P, P]),
+        "ntc_ctx_synchronize": (I, [P]),
+        "ntc_index_upload": (I, [P, ctypes.POINTER(IndexView)]),
+        "ntc_index_info": (I, [P, P, P, P]),
+        "ntc_encode_batch": (I, [P, P, P, u64, P, u64, P, P]),
+        "ntc_encode_batch_device": (I, [P, P, P, u64, u32, P, u64, P]),
+        "ntc_encode_status": (I, [P, P, P]),
+        "ntc_decode_batch": (I, [P, P, u64, P, u64, P, u64, P, P]),
+        "ntc_decode_batch_device": (I, [P, P, u64, P, u64, P, u64]),
+        "ntc_decode_status": (I, [P, P, P]),
+        "ntc_last_timing": (I, [P, ctypes.POINTER(Timing)]),
+        "ntc_device_alloc": (I, [P, u64, ctypes.POINTER(P)]),
+        "ntc_device_free": (I, [P, P]),
+        "ntc_memcpy_h2d": (I, [P, P, P, u64]),
+        "ntc_memcpy_d2h": (I, [P, P, P, u64]),
+        "ntc_debug_matching_statistics": (I, [P, P, P, u64, P, P]),
+        "ntc_build_index": (I, [P, P, u64, u32, I, I, ctypes.POINTER(P)]),
+        "ntc_index_free": (None, [P]),
+        "ntc_index_view_of": (I, [P, ctypes.POINTER(IndexView)]),
+        "ntc_index_save": (I, [P, ctypes.c_char_p]),
+        "ntc_index_load": (I, [ctypes.c_char_p, ctypes.POINTER(P)]),
+        "ntc_synth_genome": (I, [u64, u64, P]),
+        "ntc_synth_reads": (I, [P, u64, u64, u64, u64, u32, u32, I, P]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def pack_reads(reads):
+    """list[bytes|str] -> (uint8 bases, uint64 offsets[n+1])."""
+    bs = [r.encode() if isinstance(r, str) else bytes(r) for r in reads]
+    offs = np.zeros(len(bs) + 1, dtype=np.uint64)
+    if bs:
+        offs[1:] = np.cumsum([len(b) for b in bs], dtype=np.uint64)
+    return np.frombuffer(b"".join(bs) + b"\0", dtype=np.uint8)[: int(offs[-1])].copy(), offs
+
+
+class Index:
+    """Host SBWT subset matrix + LCS (ntc_index_host)."""
+
+    def __init__(self, handle):
+        self.h = handle
+        self._view = IndexView()
+        rc = lib().ntc_index_view_of(self.h, ctypes.byref(self._view))
+        if rc:
+            raise NtcError(rc, "index view")
+
+    @classmethod
+    def build(cls, seqs, k, add_revcomp=True, threads=0):
+        bases, offs = pack_reads(seqs)
+        h = ctypes.c_void_p()
+        rc = lib().ntc_build_index(_p(bases), _p(offs), len(offs) - 1, k, int(add_revcomp), threads,
+                                   ctypes.byref(h))
+        if rc:
+            raise NtcError(rc, "ntc_build_index")
+        return cls(h)
+
+    @classmethod
+    def load(cls, prefix):
+        h = ctypes.c_void_p()
+        rc = lib().ntc_index_load(str(prefix).encode(), ctypes.byref(h))
+        if rc:
+            raise NtcError(rc, f"ntc_index_load({prefix})")
+        return cls(h)
+
+    def save(self, prefix):
+        rc = lib().ntc_index_save(self.h, str(prefix).encode())
+        if rc:
+            raise NtcError(rc, f"ntc_index_save({prefix})")
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.ntc_index_free(self.h)
+            self.h = None
+
+    @property
+    def view(self):
+        return self._view
+
+    @property
+    def n(self):
+        return int(self._view.n_nodes)
+
+    @property
+    def k(self):
+        return int(self._view.k)
+
+    @property
+    def C(self):
+        return [int(x) for x in self._view.C]
+
+    def row(self, c):
+        words = (self.n + 63) // 64
+        buf = (ctypes.c_uint64 * words).from_address(self._view.rows[c])
+        return np.frombuffer(buf, dtype=np.uint64).copy()
+
+    @property
+    def rows(self):
+        return [self.row(c) for c in range(4)]
+
+    @property
+    def lcs(self):
+        buf = (ctypes.c_uint8 * self.n).from_address(self._view.lcs)
+        return np.frombuffer(buf, dtype=np.uint8).copy()
+
+
+class GpuContext:
+    """One HIP context (device + stream + resident index) of libntcomp_gpu.so."""
+
+    def __init__(self, device=0):
+        self.L = lib()
+        self.h = ctypes.c_void_p()
+        rc = self.L.ntc_ctx_create(device, ctypes.byref(self.h))
+        if rc:
+            raise NtcError(rc, f"ntc_ctx_create({device}): no usable GPU")
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.ntc_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def _check(self, rc, what):
+        if rc:
+            raise NtcError(rc, f"{what}: {self.L.ntc_last_error(self.h).decode(errors='replace')}")
+
+    def upload(self, index):
+        self._check(self.L.ntc_index_upload(self.h, ctypes.byref(index.view)), "ntc_index_upload")
+        return self
+
+    def upload_arrays(self, n, k, rows, C, lcs):
+        rows = [np.ascontiguousarray(r, dtype=np.uint64) for r in rows]
+        lcs = np.ascontiguousarray(lcs, dtype=np.uint8)
+        v = IndexView()
+        v.n_nodes, v.k = int(n), int(k)
+        for c in range(4):
+            v.rows[c] = rows[c].ctypes.data
+            v.C[c] = int(C[c])
+        v.lcs = lcs.ctypes.data
+        self._check(self.L.ntc_index_upload(self.h, ctypes.byref(v)), "ntc_index_upload")
+        return self
+
+    def index_info(self):
+        n, k, b = ctypes.c_uint64(), ctypes.c_uint32(), ctypes.c_uint64()
+        self._check(self.L.ntc_index_info(self.h, ctypes.byref(n), ctypes.byref(k), ctypes.byref(b)), "info")
+        return int(n.value), int(k.value), int(b.value)
+
+    # ---- encode ------------------------------------------------------------------
+    def encode(self, bases, offsets):
+        """-> (uint64 records, uint64 rec_offsets[n_reads+1]); raises NtcError(code) with
+        .bad_read on a failing read."""
+        bases = np.ascontiguousarray(bases, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        nreads = len(offsets) - 1
+        total = int(offsets[-1] - offsets[0]) if nreads >= 0 else 0
+        recs = np.zeros(total + 1, dtype=np.uint64)
+        roff = np.zeros(nreads + 1, dtype=np.uint64)
+        bad = ctypes.c_int64(-1)
+        rc = self.L.ntc_encode_batch(self.h, _p(bases), _p(offsets), nreads, _p(recs), len(recs), _p(roff),
+                                     ctypes.byref(bad))
+        if rc:
+            e = NtcError(rc, self.L.ntc_last_error(self.h).decode(errors="replace"))
+            e.bad_read = bad.value
+            raise e
+        return recs[: int(roff[-1])], roff
+
+    def decode(self, recs):
+        recs = np.ascontiguousarray(recs, dtype=np.uint64)
+        nr, nb = ctypes.c_uint64(), ctypes.c_uint64()
+        rc = self.L.ntc_decode_batch(self.h, _p(recs), len(recs), None, 0, None, 0, ctypes.byref(nr),
+                                     ctypes.byref(nb))
+        if rc not in (0, 5):
+            self._check(rc, "ntc_decode_batch")
+        out = np.zeros(int(nb.value) + 1, dtype=np.uint8)
+        offs = np.zeros(int(nr.value) + 1, dtype=np.uint64)
+        self._check(self.L.ntc_decode_batch(self.h, _p(recs), len(recs), _p(out), len(out), _p(offs), len(offs),
+                                            ctypes.byref(nr), ctypes.byref(nb)), "ntc_decode_batch")
+        return out[: int(nb.value)], offs
+
+    def matching_statistics(self, bases, offsets):
+        bases = np.ascontiguousarray(bases, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        total = int(offsets[-1] - offsets[0])
+        d = np.zeros(total + 1, dtype=np.uint32)
+        s = np.zeros(total + 1, dtype=np.uint32)
+        self._check(self.L.ntc_debug_matching_statistics(self.h, _p(bases), _p(offsets), len(offsets) - 1,
+                                                         _p(d), _p(s)), "ntc_debug_matching_statistics")
+        return d[:total], s[:total]
+
+    # ---- device-resident buffers (bench) ---------------------------------------------
+    def alloc(self, nbytes):
+        p = ctypes.c_void_p()
+        self._check(self.L.ntc_device_alloc(self.h, int(nbytes), ctypes.byref(p)), "ntc_device_alloc")
+        return p.value
+
+    def free(self, ptr):
+        self._check(self.L.ntc_device_free(self.h, ctypes.c_void_p(ptr)), "ntc_device_free")
+
+    def h2d(self, dptr, arr):
+        arr = np.ascontiguousarray(arr)
+        self._check(self.L.ntc_memcpy_h2d(self.h, ctypes.c_void_p(dptr), _p(arr), arr.nbytes), "h2d")
+
+    def d2h(self, arr, dptr):
+        self._check(self.L.ntc_memcpy_d2h(self.h, _p(arr), ctypes.c_void_p(dptr), arr.nbytes), "d2h")
+        return arr
+
+    def encode_device(self, d_bases, d_offs, n_reads, max_read_len, d_recs, cap, d_roffs):
+        self._check(self.L.ntc_encode_batch_device(self.h, ctypes.c_void_p(d_bases), ctypes.c_void_p(d_offs),
+                                                   n_reads, max_read_len, ctypes.c_void_p(d_recs), cap,
+                                                   ctypes.c_void_p(d_roffs)), "ntc_encode_batch_device")
+
+    def encode_status(self):
+        bad, n = ctypes.c_int64(-1), ctypes.c_uint64()
+        self._check(self.L.ntc_encode_status(self.h, ctypes.byref(bad), ctypes.byref(n)), "ntc_encode_status")
+        return int(n.value)
+
+    def decode_device(self, d_recs, n_recs, d_out, out_cap, d_offs, offs_cap):
+        self._check(self.L.ntc_decode_batch_device(self.h, ctypes.c_void_p(d_recs), n_recs, ctypes.c_void_p(d_out),
+                                                   out_cap, ctypes.c_void_p(d_offs), offs_cap),
+                    "ntc_decode_batch_device")
+
+    def decode_status(self):
+        nr, nb = ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(self.L.ntc_decode_status(self.h, ctypes.byref(nr), ctypes.byref(nb)), "ntc_decode_status")
+        return int(nr.value), int(nb.value)
+
+    def synchronize(self):
+        self._check(self.L.ntc_ctx_synchronize(self.h), "ntc_ctx_synchronize")
+
+    def timing(self):
+        t = Timing()
+        self._check(self.L.ntc_last_timing(self.h, ctypes.byref(t)), "ntc_last_timing")
+        return {"total_ms": t.total_ms, "main_ms": t.main_ms, "aux_ms": t.aux_ms}
+
+
+# ---- reference-shaped helpers --------------------------------------------------------
+def encode_sequence(nucleotides, ctx):
+    """encode_sequence + encode_dictionary for one read -> list of u64 records."""
+    bases, offs = pack_reads([nucleotides])
+    recs, _ = ctx.encode(bases, offs)
+    return [int(x) for x in recs]
+
+
+def decode_sequence(encoding, ctx):
+    """decode_sequence: u64 records of whole reads -> list of bytes (one per read)."""
+    out, offs = ctx.decode(np.asarray(encoding, dtype=np.uint64))
+    return [out[offs[i]:offs[i + 1]].tobytes() for i in range(len(offs) - 1)]
+
+
+def synth_genome(seed, length):
+    out = np.zeros(length, dtype=np.uint8)
+    rc = lib().ntc_synth_genome(seed, length, _p(out))
+    if rc:
+        raise NtcError(rc, "ntc_synth_genome")
+    return out
+
+
+def synth_reads(genome, seed, first_read, n_reads, read_len, err_per_million, threads=0):
+    genome = np.ascontiguousarray(genome, dtype=np.uint8)
+    out = np.zeros(n_reads * read_len, dtype=np.uint8)
+    rc = lib().ntc_synth_reads(_p(genome), len(genome), seed, first_read, n_reads, read_len, err_per_million,
+                               threads, _p(out))
+    if rc:
+        raise NtcError(rc, "ntc_synth_reads")
+    return out

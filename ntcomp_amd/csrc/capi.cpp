@@ -1,0 +1,668 @@
+// extern "C" boundary of libntcomp_gpu.so (include/ntcomp_gpu.h, include/ntcomp_host.h).
+// Every entry point returns an ntc_status; HIP failures and reference panics become
+// status codes plus ntc_last_error(); nothing aborts across the ABI.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <exception>
+#include <string>
+#include <vector>
+
+#include "../../include/ntcomp_gpu.h"
+#include "../../include/ntcomp_host.h"
+#include "derived.h"
+#include "kernels.h"
+#include "ntc_internal.h"
+
+using namespace ntc;
+
+namespace {
+
+struct DevBuf {
+    void *p = nullptr;
+    uint64_t bytes = 0;
+};
+
+enum CallKind { kNone = 0, kEncode = 1, kDecode = 2 };
+
+}  // namespace
+
+struct ntc_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = true;
+    std::string err;
+    // index
+    bool has_index = false;
+    DevIndex dix{};
+    std::vector<void *> index_mem;
+    uint64_t index_bytes = 0;
+    // workspace buffers (grown, never shrunk)
+    DevBuf ws[16];
+    unsigned long long *d_status = nullptr;
+    // last call
+    CallKind last = kNone;
+    uint64_t last_n = 0;           // reads (encode) / records (decode)
+    uint64_t *last_out_offs = nullptr;
+    uint64_t last_units = 0;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+};
+
+namespace {
+
+enum WsSlot {
+    WS_D = 0, WS_S, WS_F, WS_R, WS_RECCOUNT, WS_SCANTMP, WS_TILEBASE, WS_TILEROWS,
+    WS_STAGE_BASES, WS_STAGE_OFFS, WS_STAGE_RECS, WS_STAGE_OUT, WS_DEC_A, WS_DEC_B, WS_DEC_C,
+    WS_DEC_D
+};
+
+#define HIP_TRY(ctx, expr)                                                                   \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess) {                                                              \
+            (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_);                   \
+            return NTC_ERR_HIP;                                                              \
+        }                                                                                    \
+    } while (0)
+
+int set_err(ntc_ctx *ctx, int code, const std::string &msg) {
+    if (ctx) ctx->err = msg;
+    return code;
+}
+
+int ensure(ntc_ctx *ctx, int slot, uint64_t bytes, void **out) {
+    DevBuf &b = ctx->ws[slot];
+    if (bytes == 0) bytes = 64;
+    if (b.bytes < bytes) {
+        if (b.p) {
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            HIP_TRY(ctx, hipFree(b.p));
+            b.p = nullptr;
+            b.bytes = 0;
+        }
+        uint64_t want = bytes + bytes / 8;  // headroom for slightly larger next calls
+        HIP_TRY(ctx, hipMalloc(&b.p, want));
+        b.bytes = want;
+    }
+    *out = b.p;
+    return NTC_OK;
+}
+
+const char *status_name(int code) {
+    switch (code) {
+    case NTC_ERR_INVALID_BASE: return "invalid base (non-ACGT or absent from the index)";
+    case NTC_ERR_EMPTY_READ: return "empty read (EncodeError)";
+    case NTC_ERR_LENGTH: return "match length >= 2^24";
+    case NTC_ERR_CAPACITY: return "output capacity exceeded";
+    case NTC_ERR_FORMAT: return "malformed input";
+    default: return "error";
+    }
+}
+
+// Scratch layout for n_reads reads: either per-tile bases (tile_base, device pointer)
+// or uniform rows per tile.
+struct Layout {
+    const uint64_t *d_tile_base = nullptr;
+    uint64_t rows_uniform = 0;
+    uint64_t total_rows = 0;
+};
+
+int alloc_scratch(ntc_ctx *ctx, uint64_t n_reads, uint64_t total_rows, EncodeArgs &a) {
+    void *p;
+    int rc;
+    const uint64_t slots = total_rows * 64;
+    if ((rc = ensure(ctx, WS_D, slots, &p))) return rc;
+    a.D = (uint8_t *)p;
+    if ((rc = ensure(ctx, WS_S, slots * 4, &p))) return rc;
+    a.S = (uint32_t *)p;
+    if ((rc = ensure(ctx, WS_F, (total_rows / 32 + 1) * 64 * 4, &p))) return rc;
+    a.F = (uint32_t *)p;
+    if ((rc = ensure(ctx, WS_R, slots * 8, &p))) return rc;
+    a.R = (uint64_t *)p;
+    if ((rc = ensure(ctx, WS_RECCOUNT, (n_reads + 1) * 4, &p))) return rc;
+    a.rec_count = (uint32_t *)p;
+    return NTC_OK;
+}
+
+int encode_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, uint64_t n_reads,
+                const Layout &lay, uint64_t *d_rec_out, uint64_t cap, uint64_t *d_rec_offs,
+                uint64_t units) {
+    if (!ctx->has_index) return set_err(ctx, NTC_ERR_NO_INDEX, "no index uploaded");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    EncodeArgs a{};
+    a.ix = ctx->dix;
+    a.bases = d_bases;
+    a.offs = d_offs;
+    a.n_reads = n_reads;
+    a.tile_base = lay.d_tile_base;
+    a.rows_uniform = lay.rows_uniform;
+    a.status = ctx->d_status;
+    int rc = alloc_scratch(ctx, n_reads, lay.total_rows, a);
+    if (rc) return rc;
+    void *tmp;
+    if ((rc = ensure(ctx, WS_SCANTMP, scan_tmp_words(n_reads + 1) * 8, &tmp))) return rc;
+    HIP_TRY(ctx, hipMemsetAsync(ctx->d_status, 0xFF, 8, ctx->stream));
+    ctx->last = kEncode;
+    ctx->last_n = n_reads;
+    ctx->last_out_offs = d_rec_offs;
+    ctx->last_units = units;
+    if (n_reads == 0) {
+        HIP_TRY(ctx, hipMemsetAsync(d_rec_offs, 0, 8, ctx->stream));
+        for (int i = 0; i < 3; i++) HIP_TRY(ctx, hipEventRecord(ctx->ev[i], ctx->stream));
+        return NTC_OK;
+    }
+    HIP_TRY(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
+    launch_encode(a, ctx->stream);
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
+    scan_excl_u32(a.rec_count, n_reads, d_rec_offs, (uint64_t *)tmp, ctx->stream);
+    EmitArgs e{};
+    e.R = a.R;
+    e.tile_base = lay.d_tile_base;
+    e.rows_uniform = lay.rows_uniform;
+    e.rec_count = a.rec_count;
+    e.rec_offsets = d_rec_offs;
+    e.n_reads = n_reads;
+    e.out = d_rec_out;
+    e.capacity = cap;
+    e.status = ctx->d_status;
+    launch_emit(e, ctx->stream);
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
+    return NTC_OK;
+}
+
+int read_status(ntc_ctx *ctx, int64_t *bad_index) {
+    unsigned long long st = 0;
+    HIP_TRY(ctx, hipMemcpyAsync(&st, ctx->d_status, 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (st == ~0ULL) {
+        if (bad_index) *bad_index = -1;
+        return NTC_OK;
+    }
+    int code = (int)(st & 0xFF);
+    int64_t idx = (int64_t)(st >> 8);
+    if (bad_index) *bad_index = idx;
+    char buf[160];
+    std::snprintf(buf, sizeof(buf), "%s at index %lld", status_name(code), (long long)idx);
+    ctx->err = buf;
+    return code;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ntc_abi_version(void) { return NTC_ABI_VERSION; }
+
+int ntc_ctx_create(int device, ntc_ctx **out) {
+    if (!out) return NTC_ERR_INVALID_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return NTC_ERR_HIP;
+    if (device < 0 || device >= ndev) return NTC_ERR_INVALID_ARG;
+    ntc_ctx *ctx = new ntc_ctx();
+    ctx->device = device;
+    if (hipSetDevice(device) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc((void **)&ctx->d_status, 64) != hipSuccess) {
+        delete ctx;
+        return NTC_ERR_HIP;
+    }
+    for (auto &e : ctx->ev)
+        if (hipEventCreate(&e) != hipSuccess) {
+            delete ctx;
+            return NTC_ERR_HIP;
+        }
+    *out = ctx;
+    return NTC_OK;
+}
+
+void ntc_ctx_destroy(ntc_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (auto &b : ctx->ws)
+        if (b.p) (void)hipFree(b.p);
+    for (void *p : ctx->index_mem) (void)hipFree(p);
+    if (ctx->d_status) (void)hipFree(ctx->d_status);
+    for (auto &e : ctx->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->stream && ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char *ntc_last_error(const ntc_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int ntc_ctx_set_stream(ntc_ctx *ctx, void *hip_stream) {
+    if (!ctx) return NTC_ERR_INVALID_ARG;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->own_stream) HIP_TRY(ctx, hipStreamDestroy(ctx->stream));
+    if (hip_stream) {
+        ctx->stream = (hipStream_t)hip_stream;
+        ctx->own_stream = false;
+    } else {
+        HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+        ctx->own_stream = true;
+    }
+    return NTC_OK;
+}
+
+int ntc_ctx_synchronize(ntc_ctx *ctx) {
+    if (!ctx) return NTC_ERR_INVALID_ARG;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return NTC_OK;
+}
+
+int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
+    if (!ctx || !v || !v->lcs) return set_err(ctx, NTC_ERR_INVALID_ARG, "null index view");
+    for (int c = 0; c < 4; c++)
+        if (!v->rows[c]) return set_err(ctx, NTC_ERR_INVALID_ARG, "null subset-matrix row");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HostIndex hx;
+    hx.n = v->n_nodes;
+    hx.k = v->k;
+    const uint64_t nw = (v->n_nodes + 63) / 64;
+    for (int c = 0; c < 4; c++) {
+        hx.rows[c].assign(v->rows[c], v->rows[c] + nw);
+        hx.C[c] = v->C[c];
+    }
+    hx.lcs.assign(v->lcs, v->lcs + v->n_nodes);
+    Derived dv;
+    std::string err;
+    if (!build_derived(hx, dv, err, 0)) return set_err(ctx, NTC_ERR_FORMAT, err);
+    // free a previous index
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    for (void *p : ctx->index_mem) HIP_TRY(ctx, hipFree(p));
+    ctx->index_mem.clear();
+    ctx->has_index = false;
+    ctx->index_bytes = 0;
+    const uint64_t n = hx.n;
+    auto dalloc = [&](uint64_t bytes, void **p) -> int {
+        HIP_TRY(ctx, hipMalloc(p, bytes));
+        ctx->index_mem.push_back(*p);
+        ctx->index_bytes += bytes;
+        return NTC_OK;
+    };
+    void *d_lines, *d_lcs, *d_uniq, *d_walk_a, *d_walk_b, *d_pred, *d_code;
+    int rc;
+    if ((rc = dalloc(dv.lines.size() * sizeof(RankLine), &d_lines))) return rc;
+    if ((rc = dalloc(n + 256, &d_lcs))) return rc;
+    if ((rc = dalloc(dv.uniq.size() * 4, &d_uniq))) return rc;
+    if ((rc = dalloc(n * sizeof(WalkEntry), &d_walk_a))) return rc;
+    HIP_TRY(ctx, hipMalloc(&d_walk_b, n * sizeof(WalkEntry)));
+    HIP_TRY(ctx, hipMalloc(&d_pred, n * 4));
+    HIP_TRY(ctx, hipMalloc(&d_code, n + 64));
+    HIP_TRY(ctx, hipMemcpy(d_lines, dv.lines.data(), dv.lines.size() * sizeof(RankLine), hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemset(d_lcs, 0, n + 256));
+    HIP_TRY(ctx, hipMemcpy(d_lcs, hx.lcs.data(), n, hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(d_uniq, dv.uniq.data(), dv.uniq.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(d_pred, dv.pred.data(), n * 4, hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(d_code, dv.code.data(), n, hipMemcpyHostToDevice));
+    WalkEntry *result = nullptr;
+    launch_walk_build((const uint32_t *)d_pred, (const uint8_t *)d_code, n, (WalkEntry *)d_walk_a,
+                      (WalkEntry *)d_walk_b, &result, ctx->stream);
+    HIP_TRY(ctx, hipGetLastError());
+    if (result != (WalkEntry *)d_walk_a)
+        HIP_TRY(ctx, hipMemcpyAsync(d_walk_a, result, n * sizeof(WalkEntry), hipMemcpyDeviceToDevice,
+                                    ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipFree(d_walk_b));
+    HIP_TRY(ctx, hipFree(d_pred));
+    HIP_TRY(ctx, hipFree(d_code));
+    DevIndex &d = ctx->dix;
+    d.lines = (const RankLine *)d_lines;
+    d.lcs = (const uint8_t *)d_lcs;
+    d.uniq = (const uint32_t *)d_uniq;
+    d.walk = (const WalkEntry *)d_walk_a;
+    d.nlines = dv.nlines;
+    d.n = (uint32_t)n;
+    d.k = hx.k;
+    d.t_jump = dv.t_jump;
+    for (int c = 0; c < 5; c++) d.C[c] = dv.C[c];
+    ctx->has_index = true;
+    return NTC_OK;
+}
+
+int ntc_index_info(const ntc_ctx *ctx, uint64_t *n_nodes, uint32_t *k, uint64_t *device_bytes) {
+    if (!ctx) return NTC_ERR_INVALID_ARG;
+    if (!ctx->has_index) return NTC_ERR_NO_INDEX;
+    if (n_nodes) *n_nodes = ctx->dix.n;
+    if (k) *k = ctx->dix.k;
+    if (device_bytes) *device_bytes = ctx->index_bytes;
+    return NTC_OK;
+}
+
+int ntc_encode_batch_device(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_read_offsets,
+                            uint64_t n_reads, uint32_t max_read_len, uint64_t *d_rec_out,
+                            uint64_t rec_capacity, uint64_t *d_rec_offsets_out) {
+    if (!ctx || (!d_read_offsets && n_reads) || !d_rec_offsets_out)
+        return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    Layout lay;
+    const uint64_t tiles = (n_reads + 63) / 64;
+    if (max_read_len > 0) {
+        lay.rows_uniform = ((uint64_t)max_read_len + 31) & ~31ULL;
+        lay.total_rows = tiles * lay.rows_uniform;
+    } else if (n_reads > 0) {
+        void *rows, *tb, *tmp;
+        int rc;
+        if ((rc = ensure(ctx, WS_TILEROWS, tiles * 4, &rows))) return rc;
+        if ((rc = ensure(ctx, WS_TILEBASE, (tiles + 1) * 8, &tb))) return rc;
+        if ((rc = ensure(ctx, WS_SCANTMP, scan_tmp_words(std::max(tiles, n_reads) + 1) * 8, &tmp)))
+            return rc;
+        launch_tile_rows(d_read_offsets, n_reads, (uint32_t *)rows, ctx->stream);
+        scan_excl_u32((const uint32_t *)rows, tiles, (uint64_t *)tb, (uint64_t *)tmp, ctx->stream);
+        HIP_TRY(ctx, hipMemcpyAsync(&lay.total_rows, (uint64_t *)tb + tiles, 8, hipMemcpyDeviceToHost,
+                                    ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        lay.d_tile_base = (const uint64_t *)tb;
+    }
+    return encode_impl(ctx, d_bases, d_read_offsets, n_reads, lay, d_rec_out, rec_capacity,
+                       d_rec_offsets_out, 0);
+}
+
+int ntc_encode_status(ntc_ctx *ctx, int64_t *bad_read, uint64_t *n_records) {
+    if (!ctx) return NTC_ERR_INVALID_ARG;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    int rc = read_status(ctx, bad_read);
+    if (rc) return rc;
+    if (n_records) {
+        if (ctx->last != kEncode || !ctx->last_out_offs) return set_err(ctx, NTC_ERR_INVALID_ARG, "no encode call");
+        HIP_TRY(ctx, hipMemcpy(n_records, ctx->last_out_offs + ctx->last_n, 8, hipMemcpyDeviceToHost));
+    }
+    return NTC_OK;
+}
+
+int ntc_encode_batch(ntc_ctx *ctx, const uint8_t *bases, const uint64_t *read_offsets, uint64_t n_reads,
+                     uint64_t *rec_out, uint64_t rec_capacity, uint64_t *rec_offsets_out, int64_t *bad_read) {
+    if (bad_read) *bad_read = -1;
+    if (!ctx || !read_offsets || !rec_offsets_out || (n_reads && !bases))
+        return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const uint64_t o0 = read_offsets[0], total = read_offsets[n_reads] - o0;
+    for (uint64_t r = 0; r < n_reads; r++)
+        if (read_offsets[r + 1] < read_offsets[r])
+            return set_err(ctx, NTC_ERR_INVALID_ARG, "read offsets must be non-decreasing");
+    // per-tile scratch rows (host knows every length)
+    const uint64_t tiles = (n_reads + 63) / 64;
+    std::vector<uint64_t> tb(tiles + 1, 0), offs(n_reads + 1);
+    for (uint64_t t = 0; t < tiles; t++) {
+        uint64_t mx = 0;
+        for (uint64_t r = t * 64; r < std::min(n_reads, t * 64 + 64); r++)
+            mx = std::max(mx, read_offsets[r + 1] - read_offsets[r]);
+        tb[t + 1] = tb[t] + ((mx + 31) & ~31ULL);
+    }
+    for (uint64_t r = 0; r <= n_reads; r++) offs[r] = read_offsets[r] - o0;
+    void *d_bases, *d_offs, *d_tb, *d_recs, *d_roffs;
+    int rc;
+    if ((rc = ensure(ctx, WS_STAGE_BASES, total + 64, &d_bases))) return rc;
+    if ((rc = ensure(ctx, WS_STAGE_OFFS, (n_reads + 1) * 8 * 2, &d_offs))) return rc;
+    if ((rc = ensure(ctx, WS_TILEBASE, (tiles + 1) * 8, &d_tb))) return rc;
+    if ((rc = ensure(ctx, WS_STAGE_RECS, (total + 1) * 8, &d_recs))) return rc;
+    d_roffs = (uint64_t *)d_offs + (n_reads + 1);
+    if (total) HIP_TRY(ctx, hipMemcpyAsync(d_bases, bases + o0, total, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(d_offs, offs.data(), (n_reads + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(d_tb, tb.data(), (tiles + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+    Layout lay;
+    lay.d_tile_base = (const uint64_t *)d_tb;
+    lay.total_rows = tb[tiles];
+    rc = encode_impl(ctx, (const uint8_t *)d_bases, (const uint64_t *)d_offs, n_reads, lay, (uint64_t *)d_recs,
+                     total + 1, (uint64_t *)d_roffs, total);
+    if (rc) return rc;
+    int64_t bad = -1;
+    rc = read_status(ctx, &bad);
+    if (rc) {
+        if (bad_read) *bad_read = bad;
+        return rc;
+    }
+    HIP_TRY(ctx, hipMemcpy(rec_offsets_out, d_roffs, (n_reads + 1) * 8, hipMemcpyDeviceToHost));
+    const uint64_t nrec = rec_offsets_out[n_reads];
+    if (nrec > rec_capacity)
+        return set_err(ctx, NTC_ERR_CAPACITY, "rec_capacity smaller than the number of records");
+    if (nrec) HIP_TRY(ctx, hipMemcpy(rec_out, d_recs, nrec * 8, hipMemcpyDeviceToHost));
+    return NTC_OK;
+}
+
+int ntc_decode_batch_device(ntc_ctx *ctx, const uint64_t *d_recs, uint64_t n_recs, uint8_t *d_bases_out,
+                            uint64_t bases_capacity, uint64_t *d_read_offsets_out, uint64_t offsets_capacity) {
+    if (!ctx || (!d_recs && n_recs) || !d_read_offsets_out) return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument");
+    if (!ctx->has_index) return set_err(ctx, NTC_ERR_NO_INDEX, "no index uploaded");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    void *first, *lens, *fscan, *E, *rstart, *tmp;
+    int rc;
+    const uint64_t n = n_recs;
+    if ((rc = ensure(ctx, WS_DEC_A, (n + 1) * 4, &first))) return rc;
+    if ((rc = ensure(ctx, WS_DEC_B, (n + 1) * 4, &lens))) return rc;
+    if ((rc = ensure(ctx, WS_DEC_C, (n + 1) * 8 * 2, &fscan))) return rc;
+    E = (uint64_t *)fscan + (n + 1);
+    if ((rc = ensure(ctx, WS_DEC_D, (n + 1) * 8, &rstart))) return rc;
+    if ((rc = ensure(ctx, WS_SCANTMP, scan_tmp_words(n + 1) * 8, &tmp))) return rc;
+    HIP_TRY(ctx, hipMemsetAsync(ctx->d_status, 0xFF, 8, ctx->stream));
+    ctx->last = kDecode;
+    ctx->last_n = n;
+    ctx->last_out_offs = (uint64_t *)fscan;  // fscan[n] = reads, E[n] = bases
+    HIP_TRY(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
+    if (n == 0) {
+        HIP_TRY(ctx, hipMemsetAsync(fscan, 0, (n + 1) * 16, ctx->stream));
+        HIP_TRY(ctx, hipMemsetAsync(d_read_offsets_out, 0, 8, ctx->stream));
+        HIP_TRY(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
+        HIP_TRY(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
+        return NTC_OK;
+    }
+    launch_dec_prep(d_recs, n, (uint32_t *)first, (uint32_t *)lens, ctx->stream);
+    scan_excl_u32((const uint32_t *)first, n, (uint64_t *)fscan, (uint64_t *)tmp, ctx->stream);
+    scan_excl_u32((const uint32_t *)lens, n, (uint64_t *)E, (uint64_t *)tmp, ctx->stream);
+    DecIndexArgs ia{};
+    ia.recs = d_recs;
+    ia.n = n;
+    ia.fscan = (const uint64_t *)fscan;
+    ia.E = (const uint64_t *)E;
+    ia.rec_start = (uint64_t *)rstart;
+    ia.offs_out = d_read_offsets_out;
+    ia.offs_capacity = offsets_capacity;
+    ia.bases_capacity = bases_capacity;
+    ia.status = ctx->d_status;
+    launch_dec_index(ia, ctx->stream);
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
+    DecWalkArgs wa{};
+    wa.ix = ctx->dix;
+    wa.recs = d_recs;
+    wa.n = n;
+    wa.fscan = (const uint64_t *)fscan;
+    wa.E = (const uint64_t *)E;
+    wa.rec_start = (const uint64_t *)rstart;
+    wa.out = d_bases_out;
+    wa.status = ctx->d_status;
+    launch_dec_walk(wa, ctx->stream);
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
+    return NTC_OK;
+}
+
+int ntc_decode_status(ntc_ctx *ctx, uint64_t *n_reads, uint64_t *n_bases) {
+    if (!ctx) return NTC_ERR_INVALID_ARG;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    int rc = read_status(ctx, nullptr);
+    if (ctx->last != kDecode) return set_err(ctx, NTC_ERR_INVALID_ARG, "no decode call");
+    uint64_t nr = 0, nb = 0;
+    HIP_TRY(ctx, hipMemcpy(&nr, ctx->last_out_offs + ctx->last_n, 8, hipMemcpyDeviceToHost));
+    HIP_TRY(ctx, hipMemcpy(&nb, ctx->last_out_offs + (ctx->last_n + 1) + ctx->last_n, 8, hipMemcpyDeviceToHost));
+    if (n_reads) *n_reads = nr;
+    if (n_bases) *n_bases = nb;
+    ctx->last_units = nb;
+    return rc;
+}
+
+int ntc_decode_batch(ntc_ctx *ctx, const uint64_t *recs, uint64_t n_recs, uint8_t *bases_out,
+                     uint64_t bases_capacity, uint64_t *read_offsets_out, uint64_t offsets_capacity,
+                     uint64_t *n_reads_out, uint64_t *n_bases_out) {
+    if (!ctx || (!recs && n_recs)) return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    uint64_t nreads = 0, nbases = 0;
+    for (uint64_t r = 0; r < n_recs; r++) {
+        const uint32_t flag = (uint32_t)(recs[r] >> 56);
+        nreads += flag & 1;
+        nbases += (flag & 2) ? (flag >> 2) : ((uint32_t)(recs[r] >> 32) & 0xFFFFFFu);
+    }
+    if (n_reads_out) *n_reads_out = nreads;
+    if (n_bases_out) *n_bases_out = nbases;
+    if (n_recs && !((recs[0] >> 56) & 1)) return set_err(ctx, NTC_ERR_FORMAT, "records do not start a read");
+    if (nbases > bases_capacity || nreads + 1 > offsets_capacity || !read_offsets_out || (nbases && !bases_out))
+        return set_err(ctx, NTC_ERR_CAPACITY, "decode output buffers too small");
+    void *d_recs, *d_out, *d_offs;
+    int rc;
+    if ((rc = ensure(ctx, WS_STAGE_RECS, (n_recs + 1) * 8, &d_recs))) return rc;
+    if ((rc = ensure(ctx, WS_STAGE_BASES, nbases + 64, &d_out))) return rc;
+    if ((rc = ensure(ctx, WS_STAGE_OFFS, (nreads + 1) * 8, &d_offs))) return rc;
+    if (n_recs) HIP_TRY(ctx, hipMemcpyAsync(d_recs, recs, n_recs * 8, hipMemcpyHostToDevice, ctx->stream));
+    rc = ntc_decode_batch_device(ctx, (const uint64_t *)d_recs, n_recs, (uint8_t *)d_out, nbases,
+                                 (uint64_t *)d_offs, nreads + 1);
+    if (rc) return rc;
+    uint64_t nr = 0, nb = 0;
+    rc = ntc_decode_status(ctx, &nr, &nb);
+    if (rc) return rc;
+    if (nr != nreads || nb != nbases) return set_err(ctx, NTC_ERR_FORMAT, "decode size mismatch");
+    HIP_TRY(ctx, hipMemcpy(read_offsets_out, d_offs, (nreads + 1) * 8, hipMemcpyDeviceToHost));
+    if (nbases) HIP_TRY(ctx, hipMemcpy(bases_out, d_out, nbases, hipMemcpyDeviceToHost));
+    return NTC_OK;
+}
+
+int ntc_last_timing(ntc_ctx *ctx, ntc_timing *out) {
+    if (!ctx || !out) return NTC_ERR_INVALID_ARG;
+    if (ctx->last == kNone) return set_err(ctx, NTC_ERR_INVALID_ARG, "no call yet");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipEventSynchronize(ctx->ev[2]));
+    float a = 0, b = 0;
+    HIP_TRY(ctx, hipEventElapsedTime(&a, ctx->ev[0], ctx->ev[1]));
+    HIP_TRY(ctx, hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[2]));
+    std::memset(out, 0, sizeof(*out));
+    if (ctx->last == kEncode) {
+        out->main_ms = a;
+        out->aux_ms = b;
+    } else {
+        out->aux_ms = a;
+        out->main_ms = b;
+    }
+    out->total_ms = (double)a + (double)b;
+    out->units = ctx->last_units;
+    return NTC_OK;
+}
+
+int ntc_device_alloc(ntc_ctx *ctx, uint64_t bytes, void **d_ptr) {
+    if (!ctx || !d_ptr) return NTC_ERR_INVALID_ARG;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipMalloc(d_ptr, bytes ? bytes : 64));
+    return NTC_OK;
+}
+int ntc_device_free(ntc_ctx *ctx, void *d_ptr) {
+    if (!ctx) return NTC_ERR_INVALID_ARG;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipFree(d_ptr));
+    return NTC_OK;
+}
+int ntc_memcpy_h2d(ntc_ctx *ctx, void *d_dst, const void *h_src, uint64_t bytes) {
+    if (!ctx) return NTC_ERR_INVALID_ARG;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return NTC_OK;
+}
+int ntc_memcpy_d2h(ntc_ctx *ctx, void *h_dst, const void *d_src, uint64_t bytes) {
+    if (!ctx) return NTC_ERR_INVALID_ARG;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return NTC_OK;
+}
+
+int ntc_debug_matching_statistics(ntc_ctx *ctx, const uint8_t *bases, const uint64_t *read_offsets,
+                                  uint64_t n_reads, uint32_t *d_out, uint32_t *start_out) {
+    if (!ctx || !read_offsets || !d_out || !start_out) return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument");
+    const uint64_t total = read_offsets[n_reads] - read_offsets[0];
+    std::vector<uint64_t> recs(total + 1), roffs(n_reads + 1);
+    int64_t bad = -1;
+    int rc = ntc_encode_batch(ctx, bases, read_offsets, n_reads, recs.data(), total + 1, roffs.data(), &bad);
+    if (rc && rc != NTC_ERR_LENGTH) return rc;
+    DebugArgs g{};
+    g.D = (const uint8_t *)ctx->ws[WS_D].p;
+    g.S = (const uint32_t *)ctx->ws[WS_S].p;
+    g.tile_base = (const uint64_t *)ctx->ws[WS_TILEBASE].p;
+    g.offs = (const uint64_t *)ctx->ws[WS_STAGE_OFFS].p;
+    g.n_reads = n_reads;
+    void *dd, *ds;
+    if ((rc = ensure(ctx, WS_DEC_A, (total + 1) * 4, &dd))) return rc;
+    if ((rc = ensure(ctx, WS_DEC_B, (total + 1) * 4, &ds))) return rc;
+    g.d_out = (uint32_t *)dd;
+    g.s_out = (uint32_t *)ds;
+    launch_debug_gather(g, ctx->stream);
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipMemcpy(d_out, dd, total * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(ctx, hipMemcpy(start_out, ds, total * 4, hipMemcpyDeviceToHost));
+    return NTC_OK;
+}
+
+// ---- host-side index producer / files ---------------------------------------------------
+int ntc_build_index(const uint8_t *seqs, const uint64_t *seq_offsets, uint64_t n_seqs, uint32_t k,
+                    int add_revcomp, int n_threads, ntc_index_host **out) {
+    if (!out || !seq_offsets || (n_seqs && !seqs)) return NTC_ERR_INVALID_ARG;
+    if (k < 1 || k > 255) return NTC_ERR_UNSUPPORTED;
+    *out = nullptr;
+    try {
+        auto *h = new ntc_index_host();
+        build_index(seqs, seq_offsets, n_seqs, k, add_revcomp != 0, n_threads, h->ix);
+        *out = h;
+    } catch (const std::exception &e) {
+        std::fprintf(stderr, "ntc_build_index: %s\n", e.what());
+        return NTC_ERR_FORMAT;
+    }
+    return NTC_OK;
+}
+
+void ntc_index_free(ntc_index_host *ix) { delete ix; }
+
+int ntc_index_view_of(const ntc_index_host *ix, ntc_index_view *v) {
+    if (!ix || !v) return NTC_ERR_INVALID_ARG;
+    v->n_nodes = ix->ix.n;
+    v->k = ix->ix.k;
+    v->reserved = 0;
+    for (int c = 0; c < 4; c++) {
+        v->rows[c] = ix->ix.rows[c].data();
+        v->C[c] = ix->ix.C[c];
+    }
+    v->lcs = ix->ix.lcs.data();
+    return NTC_OK;
+}
+
+int ntc_index_save(const ntc_index_host *ix, const char *prefix) {
+    if (!ix || !prefix) return NTC_ERR_INVALID_ARG;
+    std::string err;
+    if (!save_index(ix->ix, prefix, err)) {
+        std::fprintf(stderr, "ntc_index_save: %s\n", err.c_str());
+        return NTC_ERR_IO;
+    }
+    return NTC_OK;
+}
+
+int ntc_index_load(const char *prefix, ntc_index_host **out) {
+    if (!prefix || !out) return NTC_ERR_INVALID_ARG;
+    *out = nullptr;
+    auto *h = new ntc_index_host();
+    std::string err;
+    if (!load_index(prefix, h->ix, err)) {
+        std::fprintf(stderr, "ntc_index_load: %s\n", err.c_str());
+        delete h;
+        return NTC_ERR_IO;
+    }
+    *out = h;
+    return NTC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,28 @@
+// Device-layout structures derived from a HostIndex at upload time (host part).
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "encode_core.h"
+#include "ntc_internal.h"
+
+namespace ntc {
+
+struct Derived {
+    uint32_t nlines = 0;
+    std::vector<RankLine> lines;  // [4][nlines]
+    std::vector<uint32_t> uniq;   // ceil(n/32) (+1) words
+    std::vector<uint32_t> pred;   // inverse-walk predecessor (select), pred[0] = 0
+    std::vector<uint8_t> code;    // last character of each node (root: 0)
+    uint32_t C[5] = {0, 0, 0, 0, 0};
+    uint32_t t_jump = 1;
+};
+
+// Validates the index and fills rank lines, unique-predecessor bits, pred and code.
+bool build_derived(const HostIndex &ix, Derived &out, std::string &err, int threads);
+// Host doubling of the walk table (the GPU builds the same table on device).
+void build_walk_host(const Derived &dv, uint64_t n, std::vector<WalkEntry> &walk);
+// DevIndex over host arrays (test emulation only).
+DevIndex host_dev_index(const HostIndex &ix, const Derived &dv, const std::vector<WalkEntry> &walk);
+
+}  // namespace ntc

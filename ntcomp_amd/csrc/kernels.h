@@ -1,0 +1,85 @@
+// Kernel argument structs and launchers (kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "encode_core.h"
+
+namespace ntc {
+
+struct EncodeArgs {
+    DevIndex ix;
+    const uint8_t *bases;
+    const uint64_t *offs;        // [n_reads+1], absolute into bases
+    uint64_t n_reads;
+    const uint64_t *tile_base;   // [tiles+1] scratch rows per tile, or null => uniform
+    uint64_t rows_uniform;       // multiple of 32
+    uint8_t *D;
+    uint32_t *S;
+    uint32_t *F;
+    uint64_t *R;
+    uint32_t *rec_count;
+    unsigned long long *status;  // min over (read << 8 | code); ~0 = ok
+};
+
+struct EmitArgs {
+    const uint64_t *R;
+    const uint64_t *tile_base;
+    uint64_t rows_uniform;
+    const uint32_t *rec_count;
+    const uint64_t *rec_offsets;
+    uint64_t n_reads;
+    uint64_t *out;
+    uint64_t capacity;
+    unsigned long long *status;
+};
+
+struct DebugArgs {
+    const uint8_t *D;
+    const uint32_t *S;
+    const uint64_t *tile_base;
+    uint64_t rows_uniform;
+    const uint64_t *offs;
+    uint64_t n_reads;
+    uint32_t *d_out;
+    uint32_t *s_out;
+};
+
+struct DecIndexArgs {
+    const uint64_t *recs;
+    uint64_t n;
+    const uint64_t *fscan;   // exclusive scan of first flags, [n+1]
+    const uint64_t *E;       // exclusive scan of segment lengths, [n+1]
+    uint64_t *rec_start;     // [n+1]
+    uint64_t *offs_out;      // caller's read offsets
+    uint64_t offs_capacity;
+    uint64_t bases_capacity;
+    unsigned long long *status;
+};
+
+struct DecWalkArgs {
+    DevIndex ix;
+    const uint64_t *recs;
+    uint64_t n;
+    const uint64_t *fscan;
+    const uint64_t *E;
+    const uint64_t *rec_start;
+    uint8_t *out;
+    unsigned long long *status;
+};
+
+void launch_encode(const EncodeArgs &a, hipStream_t s);
+void launch_tile_rows(const uint64_t *offs, uint64_t n_reads, uint32_t *tile_rows, hipStream_t s);
+void launch_emit(const EmitArgs &a, hipStream_t s);
+void launch_debug_gather(const DebugArgs &a, hipStream_t s);
+void launch_dec_prep(const uint64_t *recs, uint64_t n, uint32_t *first, uint32_t *lens, hipStream_t s);
+void launch_dec_index(const DecIndexArgs &a, hipStream_t s);
+void launch_dec_walk(const DecWalkArgs &a, hipStream_t s);
+void launch_walk_build(const uint32_t *pred, const uint8_t *code, uint64_t n, WalkEntry *a, WalkEntry *b,
+                       WalkEntry **result, hipStream_t s);
+uint64_t scan_tmp_words(uint64_t n);
+void scan_excl_u32(const uint32_t *in, uint64_t n, uint64_t *out, uint64_t *tmp, hipStream_t s);
+void scan_excl_u64(const uint64_t *in, uint64_t n, uint64_t *out, uint64_t *tmp, hipStream_t s);
+
+}  // namespace ntc

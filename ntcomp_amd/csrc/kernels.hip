@@ -1,0 +1,305 @@
+// HIP kernels for gfx950 (MI355X): encode (matching statistics + parse + record emit),
+// decode (inverse-SBWT walk), the walk-table build and device prefix scans.
+// Integer/indexing path: no MFMA.  One GPU lane per read (64 reads per wave); per-read
+// scratch is laid out [tile][position][lane] so that every per-position store of a wave
+// is one coalesced 64-lane access (DESIGN.md "Kernels").
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "encode_core.h"
+#include "kernels.h"
+
+namespace ntc {
+
+// ---------------------------------------------------------------------------------
+// encode
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_encode(EncodeArgs a) {
+    const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (gid >= a.n_reads) return;
+    const uint64_t tile = gid >> 6;
+    const uint32_t lane = (uint32_t)(gid & 63);
+    uint64_t base, rows;
+    if (a.tile_base) {
+        base = a.tile_base[tile];
+        rows = a.tile_base[tile + 1] - base;
+    } else {
+        base = tile * a.rows_uniform;
+        rows = a.rows_uniform;
+    }
+    const uint64_t beg = a.offs[gid], end = a.offs[gid + 1];
+    const uint64_t len64 = end >= beg ? end - beg : 0;
+    LaneScratch s;
+    s.D = a.D + base * 64 + lane;
+    s.S = a.S + base * 64 + lane;
+    s.F = a.F + (base >> 5) * 64 + lane;
+    s.R = a.R + base * 64 + lane;
+    int rc;
+    if (end < beg || len64 > 0xFFFFFFFFull) rc = -kErrFormat;
+    else rc = encode_lane(a.ix, a.bases + beg, (uint32_t)len64, (uint32_t)rows, s);
+    if (rc < 0) {
+        atomicMin(a.status, (unsigned long long)((gid << 8) | (uint64_t)(-rc)));
+        a.rec_count[gid] = 0;
+    } else {
+        a.rec_count[gid] = (uint32_t)rc;
+    }
+}
+
+// rows of scratch a tile of 64 reads needs = longest read, rounded up to 32
+__global__ __launch_bounds__(256) void k_tile_rows(const uint64_t *offs, uint64_t n_reads,
+                                                   uint32_t *tile_rows) {
+    const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t tile = gid >> 6;
+    if (tile * 64 >= n_reads) return;
+    uint64_t len = 0;
+    if (gid < n_reads) {
+        const uint64_t b = offs[gid], e = offs[gid + 1];
+        len = e > b ? e - b : 0;
+    }
+    uint32_t v = len > 0xFFFFFFE0ull ? 0xFFFFFFE0u : (uint32_t)len;
+    for (int o = 32; o > 0; o >>= 1) {
+        uint32_t t = __shfl_xor(v, o, 64);
+        v = t > v ? t : v;
+    }
+    if ((gid & 63) == 0) tile_rows[tile] = (v + 31) & ~31u;
+}
+
+__global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
+    const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (gid >= a.n_reads) return;
+    const uint64_t tile = gid >> 6;
+    const uint32_t lane = (uint32_t)(gid & 63);
+    const uint64_t base = a.tile_base ? a.tile_base[tile] : tile * a.rows_uniform;
+    const uint32_t cnt = a.rec_count[gid];
+    const uint64_t off = a.rec_offsets[gid];
+    if (off + cnt > a.capacity) {
+        atomicMin(a.status, (unsigned long long)((gid << 8) | (uint64_t)kErrCapacity));
+        return;
+    }
+    const uint64_t *src = a.R + base * 64 + lane;
+    for (uint32_t j = 0; j < cnt; j++) a.out[off + j] = src[(uint64_t)j * 64];
+}
+
+__global__ __launch_bounds__(256) void k_debug_gather(DebugArgs a) {
+    const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (gid >= a.n_reads) return;
+    const uint64_t tile = gid >> 6;
+    const uint32_t lane = (uint32_t)(gid & 63);
+    const uint64_t base = a.tile_base ? a.tile_base[tile] : tile * a.rows_uniform;
+    const uint64_t b = a.offs[gid], e = a.offs[gid + 1];
+    for (uint64_t p = 0; p < e - b; p++) {
+        a.d_out[b + p] = a.D[(base + p) * 64 + lane];
+        a.s_out[b + p] = a.S[(base + p) * 64 + lane];
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// decode
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_dec_prep(const uint64_t *recs, uint64_t n, uint32_t *first,
+                                                  uint32_t *lens) {
+    const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= n) return;
+    const uint64_t w = recs[r];
+    const uint32_t flag = (uint32_t)(w >> 56);
+    first[r] = flag & 1;
+    lens[r] = (flag & 2) ? (flag >> 2) : ((uint32_t)(w >> 32) & 0xFFFFFFu);
+}
+
+__global__ __launch_bounds__(256) void k_dec_index(DecIndexArgs a) {
+    const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r > a.n) return;
+    const uint64_t nreads = a.fscan[a.n];
+    if (r == a.n) {
+        a.rec_start[nreads] = a.n;
+        if (nreads + 1 > a.offs_capacity || a.E[a.n] > a.bases_capacity)
+            atomicMin(a.status, (unsigned long long)kErrCapacity);
+        else
+            a.offs_out[nreads] = a.E[a.n];
+        return;
+    }
+    const bool first = (a.recs[r] >> 56) & 1;
+    if (r == 0 && !first) atomicMin(a.status, (unsigned long long)kErrFormat);
+    if (first) {
+        const uint64_t rid = a.fscan[r];
+        a.rec_start[rid] = r;
+        if (rid < a.offs_capacity) a.offs_out[rid] = a.E[r];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_dec_walk(DecWalkArgs a) {
+    const uint64_t rid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (*a.status != ~0ull) return;
+    const uint64_t nreads = a.fscan[a.n];
+    if (rid >= nreads) return;
+    const uint64_t rb = a.rec_start[rid], re = a.rec_start[rid + 1];
+    const uint64_t ob = a.E[rb], oe = a.E[re];
+    const int rc = decode_read(a.ix, a.recs, rb, re, a.out + ob, oe - ob);
+    if (rc < 0) atomicMin(a.status, (unsigned long long)((rid << 8) | (uint64_t)(-rc)));
+}
+
+// ---------------------------------------------------------------------------------
+// walk table: W_{2m}(j) = W_m(pred^m(j)) . W_m(j)
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_walk_init(const uint32_t *pred, const uint8_t *code, uint64_t n,
+                                                   WalkEntry *w) {
+    const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    WalkEntry e;
+    e.chars = code[j];
+    e.jump = pred[j];
+    e.pad = 0;
+    w[j] = e;
+}
+
+__global__ __launch_bounds__(256) void k_walk_double(const WalkEntry *a, WalkEntry *b, uint64_t n,
+                                                     uint32_t m) {
+    const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    const WalkEntry x = a[j];
+    const WalkEntry y = a[x.jump];
+    WalkEntry o;
+    o.chars = y.chars | (x.chars << (2 * m));
+    o.jump = y.jump;
+    o.pad = 0;
+    b[j] = o;
+}
+
+// ---------------------------------------------------------------------------------
+// exclusive prefix scan, out[0..n] (out[n] = total); 256 threads x 16 items per block
+// ---------------------------------------------------------------------------------
+constexpr int kScanThreads = 256;
+constexpr int kScanItems = 16;
+constexpr uint64_t kScanTile = (uint64_t)kScanThreads * kScanItems;
+
+__device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int o) {
+    uint32_t lo = __shfl_up((uint32_t)v, o, 64), hi = __shfl_up((uint32_t)(v >> 32), o, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t &total) {
+    __shared__ uint64_t wsum[kScanThreads / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint64_t inc = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        uint64_t t = shfl_up64(inc, o);
+        if (lane >= o) inc += t;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    uint64_t off = 0;
+    total = 0;
+    for (int w = 0; w < kScanThreads / 64; w++) {
+        if (w < wave) off += wsum[w];
+        total += wsum[w];
+    }
+    __syncthreads();
+    return off + inc - v;
+}
+
+template <class T>
+__global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const T *in, uint64_t n, uint64_t *part) {
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
+    uint64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kScanItems; j++)
+        if (base + j < n) s += (uint64_t)in[base + j];
+    uint64_t total;
+    block_excl_scan(s, total);
+    if (threadIdx.x == 0) part[blockIdx.x] = total;
+}
+
+template <class T>
+__global__ __launch_bounds__(kScanThreads) void k_scan_apply(const T *in, uint64_t n, const uint64_t *boff,
+                                                             uint64_t *out) {
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
+    uint64_t v[kScanItems];
+    uint64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kScanItems; j++) {
+        v[j] = (base + j < n) ? (uint64_t)in[base + j] : 0;
+        s += v[j];
+    }
+    uint64_t total;
+    uint64_t run = block_excl_scan(s, total) + (boff ? boff[blockIdx.x] : 0);
+#pragma unroll
+    for (int j = 0; j < kScanItems; j++) {
+        if (base + j < n) out[base + j] = run;
+        run += v[j];
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kScanThreads - 1) out[n] = run;
+}
+
+template <class T>
+void scan_excl_t(const T *in, uint64_t n, uint64_t *out, uint64_t *tmp, hipStream_t s) {
+    const uint64_t nb = (n + kScanTile - 1) / kScanTile;
+    if (nb <= 1) {
+        hipLaunchKernelGGL(k_scan_apply<T>, dim3(1), dim3(kScanThreads), 0, s, in, n, nullptr, out);
+        return;
+    }
+    uint64_t *part = tmp, *part_scan = tmp + nb, *tmp2 = part_scan + nb + 1;
+    hipLaunchKernelGGL(k_scan_reduce<T>, dim3((uint32_t)nb), dim3(kScanThreads), 0, s, in, n, part);
+    scan_excl_t<uint64_t>(part, nb, part_scan, tmp2, s);
+    hipLaunchKernelGGL(k_scan_apply<T>, dim3((uint32_t)nb), dim3(kScanThreads), 0, s, in, n,
+                       (const uint64_t *)part_scan, out);
+}
+
+uint64_t scan_tmp_words(uint64_t n) {
+    uint64_t w = 0;
+    while (true) {
+        uint64_t nb = (n + kScanTile - 1) / kScanTile;
+        if (nb <= 1) break;
+        w += 2 * nb + 1;
+        n = nb;
+    }
+    return w + 8;
+}
+
+void scan_excl_u32(const uint32_t *in, uint64_t n, uint64_t *out, uint64_t *tmp, hipStream_t s) {
+    scan_excl_t<uint32_t>(in, n, out, tmp, s);
+}
+void scan_excl_u64(const uint64_t *in, uint64_t n, uint64_t *out, uint64_t *tmp, hipStream_t s) {
+    scan_excl_t<uint64_t>(in, n, out, tmp, s);
+}
+
+// ---------------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------------
+static inline dim3 grid_for(uint64_t n) { return dim3((uint32_t)((n + 255) / 256)); }
+
+void launch_encode(const EncodeArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL(k_encode, grid_for(a.n_reads), dim3(256), 0, s, a);
+}
+void launch_tile_rows(const uint64_t *offs, uint64_t n_reads, uint32_t *tile_rows, hipStream_t s) {
+    uint64_t threads = ((n_reads + 63) / 64) * 64;
+    hipLaunchKernelGGL(k_tile_rows, grid_for(threads), dim3(256), 0, s, offs, n_reads, tile_rows);
+}
+void launch_emit(const EmitArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL(k_emit, grid_for(a.n_reads), dim3(256), 0, s, a);
+}
+void launch_debug_gather(const DebugArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL(k_debug_gather, grid_for(a.n_reads), dim3(256), 0, s, a);
+}
+void launch_dec_prep(const uint64_t *recs, uint64_t n, uint32_t *first, uint32_t *lens, hipStream_t s) {
+    hipLaunchKernelGGL(k_dec_prep, grid_for(n), dim3(256), 0, s, recs, n, first, lens);
+}
+void launch_dec_index(const DecIndexArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL(k_dec_index, grid_for(a.n + 1), dim3(256), 0, s, a);
+}
+void launch_dec_walk(const DecWalkArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL(k_dec_walk, grid_for(a.n), dim3(256), 0, s, a);
+}
+void launch_walk_build(const uint32_t *pred, const uint8_t *code, uint64_t n, WalkEntry *a, WalkEntry *b,
+                       WalkEntry **result, hipStream_t s) {
+    hipLaunchKernelGGL(k_walk_init, grid_for(n), dim3(256), 0, s, pred, code, n, a);
+    for (uint32_t m = 1; m < 32; m *= 2) {
+        hipLaunchKernelGGL(k_walk_double, grid_for(n), dim3(256), 0, s, (const WalkEntry *)a, b, n, m);
+        WalkEntry *t = a;
+        a = b;
+        b = t;
+    }
+    *result = a;
+}
+
+}  // namespace ntc

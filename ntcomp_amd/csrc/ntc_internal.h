@@ -1,0 +1,27 @@
+// Host-side internal types shared by the builder, index I/O and the C ABI.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace ntc {
+
+// SBWT subset matrix + LCS in host memory (the form kbo::build / load_sbwt hand over).
+struct HostIndex {
+    uint64_t n = 0;
+    uint32_t k = 0;
+    std::vector<uint64_t> rows[4];  // ceil(n/64) words each, LSB-first
+    uint64_t C[4] = {0, 0, 0, 0};
+    std::vector<uint8_t> lcs;       // n bytes
+};
+
+void build_index(const uint8_t *seqs, const uint64_t *offs, uint64_t nseqs, uint32_t k,
+                 bool revcomp, int threads, HostIndex &out);
+bool save_index(const HostIndex &ix, const std::string &prefix, std::string &err);
+bool load_index(const std::string &prefix, HostIndex &ix, std::string &err);
+
+}  // namespace ntc
+
+struct ntc_index_host {
+    ntc::HostIndex ix;
+};

@@ -1,0 +1,107 @@
+// TEST-ONLY host emulation of the encode/decode kernels: runs the exact lane functions
+// of ntcomp_amd/csrc/encode_core.h (the ones k_encode / k_dec_walk call on the GPU) on
+// the CPU, one read at a time, with the kernels' [tile][position][lane] scratch layout.
+// It lets the -m "not gpu" suite check the kernel ALGORITHM against the oracle on a
+// machine without a GPU.  It is not part of libntcomp_gpu.so and no product path loads it.
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/ntcomp_gpu.h"
+#include "../../ntcomp_amd/csrc/derived.h"
+
+using namespace ntc;
+
+namespace {
+bool load(const ntc_index_view *v, HostIndex &hx, Derived &dv, std::vector<WalkEntry> &walk, DevIndex &d) {
+    hx.n = v->n_nodes;
+    hx.k = v->k;
+    uint64_t nw = (hx.n + 63) / 64;
+    for (int c = 0; c < 4; c++) {
+        hx.rows[c].assign(v->rows[c], v->rows[c] + nw);
+        hx.C[c] = v->C[c];
+    }
+    hx.lcs.assign(v->lcs, v->lcs + hx.n);
+    hx.lcs.resize(hx.n + 256, 0);
+    std::string err;
+    if (!build_derived(hx, dv, err, 1)) return false;
+    build_walk_host(dv, hx.n, walk);
+    d = host_dev_index(hx, dv, walk);
+    return true;
+}
+}  // namespace
+
+extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const uint64_t *offs, uint64_t n_reads,
+                          uint64_t *rec_out, uint64_t cap, uint64_t *rec_offsets, int64_t *bad, uint32_t *d_out,
+                          uint32_t *s_out) {
+    HostIndex hx;
+    Derived dv;
+    std::vector<WalkEntry> walk;
+    DevIndex d;
+    if (!load(v, hx, dv, walk, d)) return NTC_ERR_FORMAT;
+    *bad = -1;
+    uint64_t tiles = (n_reads + 63) / 64, total = 0;
+    rec_offsets[0] = 0;
+    for (uint64_t t = 0; t < tiles; t++) {
+        uint64_t mx = 0;
+        for (uint64_t r = t * 64; r < n_reads && r < t * 64 + 64; r++) mx = std::max(mx, offs[r + 1] - offs[r]);
+        uint64_t rows = (mx + 31) & ~31ULL;
+        std::vector<uint8_t> D(rows * 64 + 64);
+        std::vector<uint32_t> S(rows * 64 + 64), F((rows / 32 + 1) * 64);
+        std::vector<uint64_t> R(rows * 64 + 64);
+        for (uint64_t r = t * 64; r < n_reads && r < t * 64 + 64; r++) {
+            uint32_t lane = (uint32_t)(r & 63);
+            LaneScratch s{D.data() + lane, S.data() + lane, F.data() + lane, R.data() + lane};
+            uint32_t len = (uint32_t)(offs[r + 1] - offs[r]);
+            int rc = encode_lane(d, bases + offs[r], len, (uint32_t)rows, s);
+            if (d_out)
+                for (uint32_t p = 0; p < len; p++) {
+                    d_out[offs[r] - offs[0] + p] = D[(uint64_t)p * 64 + lane];
+                    s_out[offs[r] - offs[0] + p] = S[(uint64_t)p * 64 + lane];
+                }
+            if (rc < 0) {
+                *bad = (int64_t)r;
+                return -rc;
+            }
+            if (total + (uint64_t)rc > cap) return NTC_ERR_CAPACITY;
+            for (int j = 0; j < rc; j++) rec_out[total + j] = R[(uint64_t)j * 64 + lane];
+            total += (uint64_t)rc;
+            rec_offsets[r + 1] = total;
+        }
+    }
+    return NTC_OK;
+}
+
+extern "C" int emu_decode(const ntc_index_view *v, const uint64_t *recs, uint64_t n, uint8_t *out, uint64_t cap,
+                          uint64_t *offs, uint64_t offcap, uint64_t *nreads) {
+    HostIndex hx;
+    Derived dv;
+    std::vector<WalkEntry> walk;
+    DevIndex d;
+    if (!load(v, hx, dv, walk, d)) return NTC_ERR_FORMAT;
+    std::vector<uint64_t> starts;
+    uint64_t total = 0;
+    for (uint64_t r = 0; r < n; r++) {
+        uint32_t flag = (uint32_t)(recs[r] >> 56);
+        if (flag & 1) starts.push_back(r);
+        total += (flag & 2) ? (flag >> 2) : ((uint32_t)(recs[r] >> 32) & 0xFFFFFF);
+    }
+    if (total > cap || starts.size() + 1 > offcap) return NTC_ERR_CAPACITY;
+    if (n && (starts.empty() || starts[0] != 0)) return NTC_ERR_FORMAT;
+    starts.push_back(n);
+    uint64_t pos = 0;
+    offs[0] = 0;
+    for (size_t i = 0; i + 1 < starts.size(); i++) {
+        uint64_t len = 0;
+        for (uint64_t r = starts[i]; r < starts[i + 1]; r++) {
+            uint32_t flag = (uint32_t)(recs[r] >> 56);
+            len += (flag & 2) ? (flag >> 2) : ((uint32_t)(recs[r] >> 32) & 0xFFFFFF);
+        }
+        int rc = decode_read(d, recs, starts[i], starts[i + 1], out + pos, len);
+        if (rc < 0) return -rc;
+        pos += len;
+        offs[i + 1] = pos;
+    }
+    *nreads = starts.size() - 1;
+    return NTC_OK;
+}

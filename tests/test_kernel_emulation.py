@@ -1,0 +1,56 @@
+"""The kernels' lane logic (ntcomp_amd/csrc/encode_core.h: fast-contraction matching
+statistics, O(1)-per-step extension, record packing, jump-table inverse walk), compiled
+for the HOST by the test-only tests/emu library, against the golden vectors and against
+the faithful CPU oracle on larger seeded inputs.  The same functions run on the GPU in
+the -m gpu tests."""
+import numpy as np
+import pytest
+
+import ntcomp_amd as nt
+from emu_lib import emu_decode, emu_encode
+from oracle_lib import OracleIndex, golden_names, load_golden, pack_reads
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_emulated_kernel_matches_golden(name):
+    g = load_golden(name)
+    bases, offs = pack_reads(g["reads"])
+    recs, roff, d, s = emu_encode(g["n"], g["k"], g["rows_u64"], g["C"], g["lcs_u8"], bases, offs, want_ms=True)
+    exp_ms = np.array([x for r in g["ms"] for x in r], dtype=np.uint64).reshape(-1, 2)
+    assert np.array_equal(d.astype(np.uint64), exp_ms[:, 0])
+    assert np.array_equal(s.astype(np.uint64), exp_ms[:, 1])
+    assert recs.tolist() == [w for r in g["records"] for w in r]
+    out, o2 = emu_decode(g["n"], g["k"], g["rows_u64"], g["C"], g["lcs_u8"], recs)
+    assert [out[o2[i]:o2[i + 1]].tobytes().decode() for i in range(len(o2) - 1)] == g["reads"]
+
+
+@pytest.mark.parametrize("k,err_ppm", [(31, 10_000), (91, 10_000), (91, 0), (15, 30_000), (255, 5_000)])
+def test_emulated_kernel_matches_oracle_random(k, err_ppm):
+    genome = nt.synth_genome(100 + k, 60_000)
+    ix = nt.Index.build([genome.tobytes()], k, threads=4)
+    rows, C, lcs = ix.rows, ix.C, ix.lcs
+    L = 150 if k < 200 else 400
+    reads = nt.synth_reads(genome, 5, 0, 600, L, err_ppm)
+    offs = np.arange(0, 600 * L + 1, L, dtype=np.uint64)
+    orc = OracleIndex(ix.n, k, rows, C, lcs)
+    exp, eoff = orc.encode(reads, offs)
+    got, goff = emu_encode(ix.n, k, rows, C, lcs, reads, offs)
+    assert np.array_equal(goff, eoff)
+    assert np.array_equal(got, exp)
+    out, o2 = emu_decode(ix.n, k, rows, C, lcs, got)
+    assert np.array_equal(out, reads)
+
+
+def test_emulated_ms_matches_oracle_unrelated_reads():
+    # reads from a different genome: many contractions from short d
+    genome = nt.synth_genome(3, 50_000)
+    other = nt.synth_genome(4, 50_000)
+    ix = nt.Index.build([genome.tobytes()], 31)
+    reads = nt.synth_reads(other, 9, 0, 100, 150, 0)
+    offs = np.arange(0, 100 * 150 + 1, 150, dtype=np.uint64)
+    orc = OracleIndex(ix.n, 31, ix.rows, ix.C, ix.lcs)
+    _, _, d, s = emu_encode(ix.n, 31, ix.rows, ix.C, ix.lcs, reads, offs, want_ms=True)
+    for r in range(100):
+        od, olo = orc.ms(reads[r * 150:(r + 1) * 150].tobytes())
+        assert np.array_equal(d[r * 150:(r + 1) * 150], od)
+        assert np.array_equal(s[r * 150:(r + 1) * 150].astype(np.uint64), olo)
