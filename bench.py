@@ -1,0 +1,234 @@
+#!/usr/bin/env python3
+"""ntcomp encode (or decode) throughput on MI355X -- BASELINE.json's metric:
+"encode Mbases/sec at k=91, 150bp reads, 1/2/4/8 MI355X; bit-exact vs CPU".
+
+One process per GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N).
+Workload per GPU: 10M synthetic 150 bp reads (uniform
+starts, 50 % reverse complemented, 1 % i.i.d. substitutions) against the SBWT (k=91,
+with reverse complements) of a 5 Mbp synthetic genome.  Reads shard across GPUs with no
+data-path collective (weak scaling); torch.distributed only provides the barrier and the
+max-over-ranks of the timed region.
+
+A step = one ntc_encode_batch_device call over the GPU's whole 10M-read batch, inputs
+already resident in HBM.  The JSON line also carries the roofline of the dominant kernel
+(k_encode) and the CPU baseline (the faithful C oracle, one pinned core, bounded sample),
+plus a bit-exactness check of the GPU records against that same oracle sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+METRIC = "encode Mbases/sec at k=91, 150bp reads, 1/2/4/8 MI355X; bit-exact vs CPU"
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--mode", choices=["encode", "decode"], default="encode")
+    ap.add_argument("--k", type=int, default=91)
+    ap.add_argument("--reads-per-gpu", type=int, default=10_000_000)
+    ap.add_argument("--read-len", type=int, default=150)
+    ap.add_argument("--err-ppm", type=int, default=10_000)
+    ap.add_argument("--genome-bp", type=int, default=5_000_000)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+
+    import numpy as np
+    import torch  # before ntcomp_amd: one HIP runtime per process
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")  # barrier + max of the timed region only
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+
+    import ntcomp_amd as nt
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def sync(ctx):
+        ctx.synchronize()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+    nthreads = max(1, (os.cpu_count() or 8) // max(1, world))
+    nthreads = min(nthreads, 16)
+    t0 = time.time()
+    genome = nt.synth_genome(1, args.genome_bp)
+    index = nt.Index.build([genome.tobytes()], args.k, threads=nthreads)
+    log(f"[rank {rank}] index k={args.k} n={index.n} built in {time.time() - t0:.1f}s")
+    ctx = nt.GpuContext(local)
+    ctx.upload(index)
+
+    n, L = args.reads_per_gpu, args.read_len
+    first = rank * n
+    t0 = time.time()
+    reads = nt.synth_reads(genome, 2, first, n, L, args.err_ppm, threads=nthreads)
+    offs = np.arange(0, n * L + 1, L, dtype=np.uint64)
+    log(f"[rank {rank}] {n} reads generated in {time.time() - t0:.1f}s")
+    total_bases = n * L
+    cap = total_bases // 4 + 64
+    d_bases, d_offs = ctx.alloc(reads.nbytes), ctx.alloc(offs.nbytes)
+    d_recs, d_roffs = ctx.alloc(cap * 8), ctx.alloc(offs.nbytes)
+    ctx.h2d(d_bases, reads)
+    ctx.h2d(d_offs, offs)
+
+    # one encode pass (also the decode input)
+    ctx.encode_device(d_bases, d_offs, n, L, d_recs, cap, d_roffs)
+    n_recs = ctx.encode_status()
+    d_out = d_ooffs = None
+    if args.mode == "decode":
+        d_out, d_ooffs = ctx.alloc(total_bases + 64), ctx.alloc(offs.nbytes)
+
+    def step():
+        if args.mode == "encode":
+            ctx.encode_device(d_bases, d_offs, n, L, d_recs, cap, d_roffs)
+            got = ctx.encode_status()
+            assert got == n_recs
+        else:
+            ctx.decode_device(d_recs, n_recs, d_out, total_bases + 64, d_ooffs, n + 1)
+            assert ctx.decode_status() == (n, total_bases)
+        return ctx.timing()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    sync(ctx)
+    tt = time.perf_counter()
+    mains, totals = [], []
+    for _ in range(args.steps):
+        t = step()
+        mains.append(t["main_ms"])
+        totals.append(t["total_ms"])
+    sync(ctx)
+    elapsed = time.perf_counter() - tt
+    barrier()
+    if dist is not None:
+        tm = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        elapsed = float(tm.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    units_all = total_bases * world * args.steps
+    value = units_all / elapsed / 1e6  # Mbases/s, whole job
+
+    main_ms = sum(mains) / len(mains)
+    if args.mode == "encode":
+        alg_bytes = total_bases * (1 + 2 * 64) + 8 * n_recs  # SURVEY.md 8(d) B_enc
+        kname = "k_encode"
+    else:
+        n_long_bases = None
+        alg_bytes = None
+        kname = "k_dec_walk"
+    # decode: B_dec = 64 B per walked base + 1 B/base out + 8 B/record
+    if args.mode == "decode":
+        recs_h = ctx.d2h(np.zeros(n_recs, dtype=np.uint64), d_recs)
+        flags = (recs_h >> np.uint64(56)).astype(np.uint8)
+        longm = (flags & 2) == 0
+        n_long_bases = int(((recs_h[longm] >> np.uint64(32)) & np.uint64(0xFFFFFF)).sum())
+        alg_bytes = 64 * n_long_bases + total_bases + 8 * n_recs
+    achieved = alg_bytes / (main_ms / 1e3) / 1e9
+    traffic = None
+    try:
+        with open(args.traffic_json) as f:
+            tj = json.load(f)
+        traffic = tj.get(kname, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "kernel": kname, "kernel_ms": round(main_ms, 3),
+                "alg_bytes_per_launch": int(alg_bytes)}
+
+    cpu = None
+    parity = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        from oracle_lib import OracleIndex
+        orc = OracleIndex(index.n, args.k, index.rows, index.C, index.lcs)
+        rec_offs_h = ctx.d2h(np.zeros(n + 1, dtype=np.uint64), d_roffs)
+        ctx.synchronize()
+        old_aff = os.sched_getaffinity(0)
+        core = sorted(old_aff)[-1]
+        os.sched_setaffinity(0, {core})
+        try:
+            chunk, done, spent, ok = 2000, 0, 0.0, True
+            while spent < args.cpu_seconds and done + chunk <= n:
+                sl = reads[done * L:(done + chunk) * L]
+                o = np.arange(0, chunk * L + 1, L, dtype=np.uint64)
+                if args.mode == "encode":
+                    t1 = time.perf_counter()
+                    exp, eoff = orc.encode(sl, o)
+                    spent += time.perf_counter() - t1
+                    a, b = int(rec_offs_h[done]), int(rec_offs_h[done + chunk])
+                    got = ctx.d2h(np.zeros(b - a, dtype=np.uint64), d_recs + 8 * a) if b > a else np.zeros(0, np.uint64)
+                    ok &= bool(np.array_equal(got, exp))
+                else:
+                    exp, eoff = orc.encode(sl, o)
+                    t1 = time.perf_counter()
+                    out, _ = orc.decode(exp)
+                    spent += time.perf_counter() - t1
+                    ok &= bool(np.array_equal(out, sl))
+                done += chunk
+        finally:
+            os.sched_setaffinity(0, old_aff)
+        cpu_val = done * L / spent / 1e6
+        cpu = {"value": round(cpu_val, 3), "unit": "Mbases/s", "cores": 1, "kind": "port",
+               "sample": f"first {done} of the {n} reads ({done * L} bases), faithful C oracle "
+                         f"(oracle/ntcomp_oracle.c), one pinned core ({core}) of {os.cpu_count()}",
+               "speedup_gpu_vs_cpu": round(value / cpu_val, 1)}
+        parity = {"bit_exact_vs_oracle": ok, "reads_checked": done}
+
+    if rank == 0:
+        if args.mode == "encode":
+            workload = (f"C{args.k}: {n} x {L}bp synthetic reads per GPU ({args.err_ppm / 1e4:g}% subst, 50% revcomp) "
+                        f"vs SBWT of a {args.genome_bp / 1e6:g} Mbp synthetic genome (+revcomp), k={args.k}")
+            metric = METRIC
+        else:
+            workload = (f"D{args.k}: decode of the C{args.k} records ({n_recs} records, {n} reads) "
+                        f"-> bases via inverse-SBWT walk, k={args.k}")
+            metric = f"decode Mbases/sec at k={args.k}, 150bp reads (output bases), MI355X"
+        line = {
+            "metric": metric, "value": round(value, 2), "unit": "Mbases/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (seeded; reads regenerate per shard)",
+            "config": {"workload": workload, "k": args.k, "reads_per_gpu": n, "read_len": L,
+                       "genome_bp": args.genome_bp, "index_nodes": index.n, "records_per_gpu": n_recs,
+                       "parallelism": f"reads sharded over {world} GPU(s), index replicated, no collective"},
+            "roofline": roofline, "cpu_baseline": cpu, "parity": parity,
+            "kernel_ms_per_step": round(main_ms, 3), "device_ms_per_step": round(sum(totals) / len(totals), 3),
+        }
+        print(json.dumps(line), flush=True)
+    for p in (d_bases, d_offs, d_recs, d_roffs, d_out, d_ooffs):
+        if p:
+            ctx.free(p)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,157 @@
+"""GPU parity: the HIP kernels (through the C ABI of libntcomp_gpu.so) against the golden
+vectors and the faithful CPU oracle on the same seeded inputs; bit-exact records and
+decoded bases; error behaviour; size-independent properties at full scale."""
+import numpy as np
+import pytest
+
+import ntcomp_amd as nt
+from oracle_lib import OracleIndex, golden_names, load_golden, pack_reads
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = nt.GpuContext(0)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_gpu_golden_records_ms_decode(ctx, name):
+    g = load_golden(name)
+    ctx.upload_arrays(g["n"], g["k"], g["rows_u64"], g["C"], g["lcs_u8"])
+    bases, offs = pack_reads(g["reads"])
+    recs, roff = ctx.encode(bases, offs)
+    assert recs.tolist() == [w for r in g["records"] for w in r]
+    assert np.diff(roff).tolist() == [len(r) for r in g["records"]]
+    d, s = ctx.matching_statistics(bases, offs)
+    exp = np.array([x for r in g["ms"] for x in r], dtype=np.uint64).reshape(-1, 2)
+    assert np.array_equal(d.astype(np.uint64), exp[:, 0])
+    assert np.array_equal(s.astype(np.uint64), exp[:, 1])
+    out, o2 = ctx.decode(recs)
+    assert [out[o2[i]:o2[i + 1]].tobytes().decode() for i in range(len(o2) - 1)] == g["reads"]
+
+
+@pytest.mark.parametrize("k,err_ppm,glen", [(31, 10_000, 400_000), (91, 10_000, 400_000), (91, 0, 400_000),
+                                             (15, 30_000, 200_000), (255, 5_000, 100_000), (11, 10_000, 100_000)])
+def test_gpu_matches_oracle_random(ctx, k, err_ppm, glen):
+    genome = nt.synth_genome(1000 + k, glen)
+    ix = nt.Index.build([genome.tobytes()], k)
+    ctx.upload(ix)
+    L = 150 if k < 200 else 400
+    n = 4000
+    reads = nt.synth_reads(genome, 77, 0, n, L, err_ppm)
+    offs = np.arange(0, n * L + 1, L, dtype=np.uint64)
+    orc = OracleIndex(ix.n, k, ix.rows, ix.C, ix.lcs)
+    exp, eoff = orc.encode(reads, offs)
+    got, goff = ctx.encode(reads, offs)
+    assert np.array_equal(goff, eoff)
+    assert np.array_equal(got, exp)
+    out, o2 = ctx.decode(got)
+    assert np.array_equal(out, reads)
+    assert np.array_equal(o2, offs)
+
+
+def test_gpu_ragged_and_edge_lengths(ctx):
+    genome = nt.synth_genome(5, 200_000)
+    k = 31
+    ix = nt.Index.build([genome.tobytes()], k)
+    ctx.upload(ix)
+    rng = np.random.default_rng(3)
+    g = genome.tobytes()
+    reads = []
+    for L in [1, 2, 11, 12, 30, 31, 32, 33, 34, 63, 64, 65, 150, 151, 1000, 5000]:
+        st = int(rng.integers(0, len(g) - L))
+        reads.append(g[st:st + L])
+    reads += [bytes(rng.choice(list(b"ACGT"), size=int(rng.integers(1, 400))).tolist()) for _ in range(300)]
+    bases, offs = pack_reads(reads)
+    orc = OracleIndex(ix.n, k, ix.rows, ix.C, ix.lcs)
+    exp, eoff = orc.encode(bases, offs)
+    got, goff = ctx.encode(bases, offs)
+    assert np.array_equal(goff, eoff) and np.array_equal(got, exp)
+    out, o2 = ctx.decode(got)
+    assert np.array_equal(out, bases) and np.array_equal(o2, offs)
+
+
+def test_gpu_device_api_matches_host_api(ctx):
+    genome = nt.synth_genome(9, 300_000)
+    ix = nt.Index.build([genome.tobytes()], 91)
+    ctx.upload(ix)
+    n, L = 20_000, 150
+    reads = nt.synth_reads(genome, 4, 0, n, L, 10_000)
+    offs = np.arange(0, n * L + 1, L, dtype=np.uint64)
+    exp, eoff = ctx.encode(reads, offs)
+    db, do = ctx.alloc(reads.nbytes), ctx.alloc(offs.nbytes)
+    dr, dro = ctx.alloc(n * L * 8), ctx.alloc(offs.nbytes)
+    try:
+        ctx.h2d(db, reads)
+        ctx.h2d(do, offs)
+        for max_len in (150, 0):
+            ctx.encode_device(db, do, n, max_len, dr, n * L, dro)
+            nrec = ctx.encode_status()
+            assert nrec == len(exp)
+            got = ctx.d2h(np.zeros(nrec, dtype=np.uint64), dr)
+            gro = ctx.d2h(np.zeros(n + 1, dtype=np.uint64), dro)
+            assert np.array_equal(got, exp) and np.array_equal(gro, eoff)
+        dout, doffs = ctx.alloc(n * L), ctx.alloc((n + 1) * 8)
+        ctx.decode_device(dr, len(exp), dout, n * L, doffs, n + 1)
+        assert ctx.decode_status() == (n, n * L)
+        out = ctx.d2h(np.zeros(n * L, dtype=np.uint8), dout)
+        assert np.array_equal(out, reads)
+        t = ctx.timing()
+        assert t["main_ms"] > 0
+        ctx.free(dout)
+        ctx.free(doffs)
+    finally:
+        for p in (db, do, dr, dro):
+            ctx.free(p)
+
+
+def test_gpu_error_behaviour(ctx):
+    genome = nt.synth_genome(11, 50_000)
+    ix = nt.Index.build([genome.tobytes()], 31)
+    ctx.upload(ix)
+    good = genome[100:250].tobytes()
+    for bad_read, code in ((b"", 3), (good[:50] + b"N" + good[51:], 2), (good[:10] + b"a" + good[11:], 2)):
+        bases, offs = pack_reads([good, good, bad_read, good])
+        with pytest.raises(nt.NtcError) as e:
+            ctx.encode(bases, offs)
+        assert e.value.code == code
+        assert e.value.bad_read == 2
+    # decode: records that do not start with a read's first record
+    recs, _ = ctx.encode(*pack_reads([good, good]))
+    with pytest.raises(nt.NtcError) as e:
+        ctx.decode(recs[1:])
+    assert e.value.code == 8
+
+
+def test_gpu_index_without_a_base():
+    # an index whose genome lacks 'T' entirely: any read with T must be rejected, not hang
+    ix = nt.Index.build(["ACGACGGACCAGACGAGGCAACGAGCACCGA" * 3], 7, add_revcomp=False)
+    ctx = nt.GpuContext(0)
+    ctx.upload(ix)
+    with pytest.raises(nt.NtcError) as e:
+        ctx.encode(*pack_reads(["ACGACGGAC", "ACGT"]))
+    assert e.value.code == 2 and e.value.bad_read == 1
+    ctx.close()
+
+
+def test_gpu_full_scale_roundtrip_c91():
+    """C91 index (5 Mbp, k=91) with 1M reads: decode(encode(x)) == x for every read, and a
+    20k-read sample bit-exact against the oracle."""
+    genome = nt.synth_genome(1, 5_000_000)
+    ix = nt.Index.build([genome.tobytes()], 91)
+    ctx = nt.GpuContext(0)
+    ctx.upload(ix)
+    n, L = 1_000_000, 150
+    reads = nt.synth_reads(genome, 2, 0, n, L, 10_000)
+    offs = np.arange(0, n * L + 1, L, dtype=np.uint64)
+    recs, roff = ctx.encode(reads, offs)
+    out, o2 = ctx.decode(recs)
+    assert np.array_equal(out, reads)
+    orc = OracleIndex(ix.n, 91, ix.rows, ix.C, ix.lcs)
+    m = 20_000
+    exp, eoff = orc.encode(reads[: m * L], offs[: m + 1])
+    assert np.array_equal(recs[: int(roff[m])], exp)
+    ctx.close()
