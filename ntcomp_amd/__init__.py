@@ -38,6 +38,7 @@ EXPORTED = [
     "ntc_decode_status", "ntc_last_timing", "ntc_device_alloc", "ntc_device_free", "ntc_memcpy_h2d",
     "ntc_memcpy_d2h", "ntc_debug_matching_statistics", "ntc_build_index", "ntc_index_free",
     "ntc_index_view_of", "ntc_index_save", "ntc_index_load", "ntc_synth_genome", "ntc_synth_reads",
+    "ntc_file_header", "ntc_write_block", "ntc_read_block", "ntc_buffer_free",
 ]
 
 
@@ -105,6 +106,11 @@ def lib():
         "ntc_index_load": (I, [ctypes.c_char_p, ctypes.POINTER(P)]),
         "ntc_synth_genome": (I, [u64, u64, P]),
         "ntc_synth_reads": (I, [P, u64, u64, u64, u64, u32, u32, I, P]),
+        "ntc_file_header": (None, [P]),
+        "ntc_write_block": (I, [P, u64, u64, ctypes.POINTER(P), ctypes.POINTER(u64)]),
+        "ntc_read_block": (I, [P, u64, ctypes.POINTER(u64), ctypes.POINTER(P), ctypes.POINTER(u64),
+                               ctypes.POINTER(u64)]),
+        "ntc_buffer_free": (None, [P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -358,3 +364,43 @@ def synth_reads(genome, seed, first_read, n_reads, read_len, err_per_million, th
     if rc:
         raise NtcError(rc, "ntc_synth_reads")
     return out
+
+
+# ---- block container (encoded.dat) ------------------------------------------------------
+def file_header():
+    """encode_file_header(0,0,0,0): 32 zero bytes (lib.rs:52-67)."""
+    buf = (ctypes.c_uint8 * 32)()
+    lib().ntc_file_header(buf)
+    return bytes(buf)
+
+
+def write_block(records, num_records):
+    """write_block_to (lib.rs:232-252) -> bytes of the 4 (header, gzip payload) blocks.
+    Raises NtcError(NTC_ERR_EMPTY_READ) where the reference's write_block_to errs (and
+    its CLI then silently drops the block)."""
+    recs = np.ascontiguousarray(records, dtype=np.uint64)
+    out, n = ctypes.c_void_p(), ctypes.c_uint64()
+    rc = lib().ntc_write_block(_p(recs), len(recs), num_records, ctypes.byref(out), ctypes.byref(n))
+    if rc:
+        raise NtcError(rc, "ntc_write_block")
+    try:
+        return ctypes.string_at(out.value, n.value)
+    finally:
+        lib().ntc_buffer_free(out)
+
+
+def read_block(data):
+    """One block of decode_block (lib.rs:320-363) -> (u64 records, bytes consumed,
+    num_records header field).  NtcError(NTC_ERR_IO) at a clean end of input."""
+    buf = np.frombuffer(bytes(data), dtype=np.uint8) if len(data) else np.zeros(1, dtype=np.uint8)
+    used, recs, n, nrec = ctypes.c_uint64(), ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_uint64()
+    rc = lib().ntc_read_block(_p(buf), len(data), ctypes.byref(used), ctypes.byref(recs), ctypes.byref(n),
+                              ctypes.byref(nrec))
+    if rc:
+        raise NtcError(rc, "ntc_read_block")
+    try:
+        arr = np.ctypeslib.as_array((ctypes.c_uint64 * n.value).from_address(recs.value)).copy() \
+            if n.value else np.zeros(0, dtype=np.uint64)
+    finally:
+        lib().ntc_buffer_free(recs)
+    return arr, int(used.value), int(nrec.value)

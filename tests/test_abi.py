@@ -12,7 +12,7 @@ from oracle_lib import REPO
 
 def declared_symbols():
     names = set()
-    for h in ("ntcomp_gpu.h", "ntcomp_host.h"):
+    for h in ("ntcomp_gpu.h", "ntcomp_host.h", "ntcomp_codec.h"):
         src = open(os.path.join(REPO, "include", h)).read()
         names |= set(re.findall(r"\b(ntc_[a-z0-9_]+)\s*\(", src))
     return names
