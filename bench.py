@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--genome-bp", type=int, default=5_000_000)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--variant", type=int, default=2, help="encode kernel variant (1 = v1 A/B)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -82,7 +83,11 @@ def main():
     index = nt.Index.build([genome.tobytes()], args.k, threads=nthreads)
     log(f"[rank {rank}] index k={args.k} n={index.n} built in {time.time() - t0:.1f}s")
     ctx = nt.GpuContext(local)
+    ctx.set_option("encode_variant", args.variant)
+    t0 = time.time()
     ctx.upload(index)
+    log(f"[rank {rank}] upload (derived structures + path cover) {time.time() - t0:.1f}s, "
+        f"{ctx.get_option('n_paths')} paths, text {ctx.get_option('path_text_len')}")
 
     n, L = args.reads_per_gpu, args.read_len
     first = rank * n
@@ -219,7 +224,7 @@ def main():
                        "genome_bp": args.genome_bp, "index_nodes": index.n, "records_per_gpu": n_recs,
                        "parallelism": f"reads sharded over {world} GPU(s), index replicated, no collective"},
             "roofline": roofline, "cpu_baseline": cpu, "parity": parity,
-            "kernel_ms_per_step": round(main_ms, 3), "device_ms_per_step": round(sum(totals) / len(totals), 3),
+            "kernel_ms_per_step": round(main_ms, 3), "encode_variant": args.variant, "device_ms_per_step": round(sum(totals) / len(totals), 3),
         }
         print(json.dumps(line), flush=True)
     for p in (d_bases, d_offs, d_recs, d_roffs, d_out, d_ooffs):

@@ -88,6 +88,12 @@ const char *ntc_last_error(const ntc_ctx *ctx);
 /* Optional: launch on a caller-owned hipStream_t (passed as void*); NULL = own stream. */
 int ntc_ctx_set_stream(ntc_ctx *ctx, void *hip_stream);
 int ntc_ctx_synchronize(ntc_ctx *ctx);
+/* Tuning / diagnostics.  "encode_variant": 2 (default: flattened lanes + path walk) or 1
+ * (phase-synchronous lanes; kept for A/B measurement).  Read-only: "n_paths",
+ * "path_text_len" (the path cover built at upload).  Env NTC_ENCODE_VARIANT sets the
+ * default at ntc_ctx_create.                                                          */
+int ntc_ctx_set_option(ntc_ctx *ctx, const char *key, int64_t value);
+int ntc_ctx_get_option(const ntc_ctx *ctx, const char *key, int64_t *value);
 
 /* Upload the index once; builds the device-side rank lines, the unique-predecessor
  * bitvector and the inverse-walk jump table in HBM (DESIGN.md "Data layout"). */

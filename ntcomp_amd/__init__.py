@@ -33,7 +33,7 @@ STATUS = {
 # every symbol include/ntcomp_gpu.h and include/ntcomp_host.h declare
 EXPORTED = [
     "ntc_abi_version", "ntc_ctx_create", "ntc_ctx_destroy", "ntc_last_error", "ntc_ctx_set_stream",
-    "ntc_ctx_synchronize", "ntc_index_upload", "ntc_index_info", "ntc_encode_batch",
+    "ntc_ctx_synchronize", "ntc_ctx_set_option", "ntc_ctx_get_option", "ntc_index_upload", "ntc_index_info", "ntc_encode_batch",
     "ntc_encode_batch_device", "ntc_encode_status", "ntc_decode_batch", "ntc_decode_batch_device",
     "ntc_decode_status", "ntc_last_timing", "ntc_device_alloc", "ntc_device_free", "ntc_memcpy_h2d",
     "ntc_memcpy_d2h", "ntc_debug_matching_statistics", "ntc_build_index", "ntc_index_free",
@@ -85,6 +85,8 @@ def lib():
         "ntc_last_error": (ctypes.c_char_p, [P]),
         "ntc_ctx_set_stream": (I, [P, P]),
         "ntc_ctx_synchronize": (I, [P]),
+        "ntc_ctx_set_option": (I, [P, ctypes.c_char_p, i64]),
+        "ntc_ctx_get_option": (I, [P, ctypes.c_char_p, ctypes.POINTER(i64)]),
         "ntc_index_upload": (I, [P, ctypes.POINTER(IndexView)]),
         "ntc_index_info": (I, [P, P, P, P]),
         "ntc_encode_batch": (I, [P, P, P, u64, P, u64, P, P]),
@@ -240,6 +242,14 @@ class GpuContext:
         v.lcs = lcs.ctypes.data
         self._check(self.L.ntc_index_upload(self.h, ctypes.byref(v)), "ntc_index_upload")
         return self
+
+    def set_option(self, key, value):
+        self._check(self.L.ntc_ctx_set_option(self.h, key.encode(), int(value)), f"set_option({key})")
+
+    def get_option(self, key):
+        v = ctypes.c_int64()
+        self._check(self.L.ntc_ctx_get_option(self.h, key.encode(), ctypes.byref(v)), f"get_option({key})")
+        return int(v.value)
 
     def index_info(self):
         n, k, b = ctypes.c_uint64(), ctypes.c_uint32(), ctypes.c_uint64()

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <string>
@@ -48,13 +49,15 @@ struct ntc_ctx {
     uint64_t *last_out_offs = nullptr;
     uint64_t last_units = 0;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    int encode_variant = 2;
+    uint64_t n_paths = 0, path_text_len = 0;
 };
 
 namespace {
 
 enum WsSlot {
     WS_D = 0, WS_S, WS_F, WS_R, WS_RECCOUNT, WS_SCANTMP, WS_TILEBASE, WS_TILEROWS,
-    WS_STAGE_BASES, WS_STAGE_OFFS, WS_STAGE_RECS, WS_STAGE_OUT, WS_DEC_A, WS_DEC_B, WS_DEC_C,
+    WS_STAGE_BASES, WS_STAGE_OFFS, WS_STAGE_RECS, WS_E, WS_DEC_A, WS_DEC_B, WS_DEC_C,
     WS_DEC_D
 };
 
@@ -115,8 +118,14 @@ int alloc_scratch(ntc_ctx *ctx, uint64_t n_reads, uint64_t total_rows, EncodeArg
     const uint64_t slots = total_rows * 64;
     if ((rc = ensure(ctx, WS_D, slots, &p))) return rc;
     a.D = (uint8_t *)p;
-    if ((rc = ensure(ctx, WS_S, slots * 4, &p))) return rc;
-    a.S = (uint32_t *)p;
+    if (a.variant == 2) {
+        if ((rc = ensure(ctx, WS_E, slots * 8, &p))) return rc;
+        a.E = (uint64_t *)p;
+        a.S = nullptr;
+    } else {
+        if ((rc = ensure(ctx, WS_S, slots * 4, &p))) return rc;
+        a.S = (uint32_t *)p;
+    }
     if ((rc = ensure(ctx, WS_F, (total_rows / 32 + 1) * 64 * 4, &p))) return rc;
     a.F = (uint32_t *)p;
     if ((rc = ensure(ctx, WS_R, slots * 8, &p))) return rc;
@@ -139,6 +148,7 @@ int encode_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, ui
     a.tile_base = lay.d_tile_base;
     a.rows_uniform = lay.rows_uniform;
     a.status = ctx->d_status;
+    a.variant = ctx->encode_variant;
     int rc = alloc_scratch(ctx, n_reads, lay.total_rows, a);
     if (rc) return rc;
     void *tmp;
@@ -159,6 +169,7 @@ int encode_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, ui
     HIP_TRY(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
     scan_excl_u32(a.rec_count, n_reads, d_rec_offs, (uint64_t *)tmp, ctx->stream);
     EmitArgs e{};
+    e.variant = a.variant;
     e.R = a.R;
     e.tile_base = lay.d_tile_base;
     e.rows_uniform = lay.rows_uniform;
@@ -216,6 +227,7 @@ int ntc_ctx_create(int device, ntc_ctx **out) {
             delete ctx;
             return NTC_ERR_HIP;
         }
+    if (const char *v = std::getenv("NTC_ENCODE_VARIANT")) ctx->encode_variant = std::atoi(v) == 1 ? 1 : 2;
     *out = ctx;
     return NTC_OK;
 }
@@ -310,6 +322,15 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     if (result != (WalkEntry *)d_walk_a)
         HIP_TRY(ctx, hipMemcpyAsync(d_walk_a, result, n * sizeof(WalkEntry), hipMemcpyDeviceToDevice,
                                     ctx->stream));
+    void *d_ptext = nullptr, *d_colex_at = nullptr, *d_pos = nullptr;
+    if (dv.has_paths) {
+        if ((rc = dalloc(dv.ptext.size() * 8, &d_ptext))) return rc;
+        if ((rc = dalloc(dv.colex_at.size() * 4 + 64, &d_colex_at))) return rc;
+        if ((rc = dalloc(dv.pos_of_node.size() * 4, &d_pos))) return rc;
+        HIP_TRY(ctx, hipMemcpy(d_ptext, dv.ptext.data(), dv.ptext.size() * 8, hipMemcpyHostToDevice));
+        HIP_TRY(ctx, hipMemcpy(d_colex_at, dv.colex_at.data(), dv.colex_at.size() * 4, hipMemcpyHostToDevice));
+        HIP_TRY(ctx, hipMemcpy(d_pos, dv.pos_of_node.data(), dv.pos_of_node.size() * 4, hipMemcpyHostToDevice));
+    }
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     HIP_TRY(ctx, hipFree(d_walk_b));
     HIP_TRY(ctx, hipFree(d_pred));
@@ -324,7 +345,32 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     d.k = hx.k;
     d.t_jump = dv.t_jump;
     for (int c = 0; c < 5; c++) d.C[c] = dv.C[c];
+    d.has_paths = dv.has_paths ? 1u : 0u;
+    d.ptext = (const uint64_t *)d_ptext;
+    d.colex_at = (const uint32_t *)d_colex_at;
+    d.pos_of_node = (const uint32_t *)d_pos;
+    ctx->n_paths = dv.n_paths;
+    ctx->path_text_len = dv.tlen;
     ctx->has_index = true;
+    return NTC_OK;
+}
+
+int ntc_ctx_set_option(ntc_ctx *ctx, const char *key, int64_t value) {
+    if (!ctx || !key) return NTC_ERR_INVALID_ARG;
+    if (std::strcmp(key, "encode_variant") == 0) {
+        if (value != 1 && value != 2) return set_err(ctx, NTC_ERR_INVALID_ARG, "encode_variant must be 1 or 2");
+        ctx->encode_variant = (int)value;
+        return NTC_OK;
+    }
+    return set_err(ctx, NTC_ERR_INVALID_ARG, std::string("unknown option ") + key);
+}
+
+int ntc_ctx_get_option(const ntc_ctx *ctx, const char *key, int64_t *value) {
+    if (!ctx || !key || !value) return NTC_ERR_INVALID_ARG;
+    if (std::strcmp(key, "encode_variant") == 0) *value = ctx->encode_variant;
+    else if (std::strcmp(key, "n_paths") == 0) *value = (int64_t)ctx->n_paths;
+    else if (std::strcmp(key, "path_text_len") == 0) *value = (int64_t)ctx->path_text_len;
+    else return NTC_ERR_INVALID_ARG;
     return NTC_OK;
 }
 
@@ -591,6 +637,9 @@ int ntc_debug_matching_statistics(ntc_ctx *ctx, const uint8_t *bases, const uint
     int rc = ntc_encode_batch(ctx, bases, read_offsets, n_reads, recs.data(), total + 1, roffs.data(), &bad);
     if (rc && rc != NTC_ERR_LENGTH) return rc;
     DebugArgs g{};
+    g.variant = ctx->encode_variant;
+    g.E = (const uint64_t *)ctx->ws[WS_E].p;
+    g.ix = ctx->dix;
     g.D = (const uint8_t *)ctx->ws[WS_D].p;
     g.S = (const uint32_t *)ctx->ws[WS_S].p;
     g.tile_base = (const uint64_t *)ctx->ws[WS_TILEBASE].p;

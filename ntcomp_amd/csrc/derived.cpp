@@ -101,7 +101,135 @@ bool build_derived(const HostIndex &ix, Derived &out, std::string &err, int thre
     double l4 = std::log((double)n) / std::log(4.0);
     uint32_t tj = (uint32_t)std::ceil(l4) + 2;
     out.t_jump = std::max<uint32_t>(1, tj);
+    build_paths(ix, out);
     return true;
+}
+
+namespace {
+inline uint32_t host_rank(const Derived &dv, int c, uint64_t i) {
+    LineRegs L;
+    const uint64_t li = i / kRankBlock;
+    load_line(&dv.lines[(uint64_t)c * dv.nlines + li], L);
+    return rank_in(L, (uint32_t)(i - li * kRankBlock));
+}
+inline uint32_t labels_of(const Derived &dv, uint64_t g) {  // 4-bit label set of node g
+    const uint64_t li = g / kRankBlock, off = g - li * kRankBlock;
+    uint32_t m = 0;
+    for (int c = 0; c < 4; c++)
+        m |= (uint32_t)((dv.lines[(uint64_t)c * dv.nlines + li].w[off >> 6] >> (off & 63)) & 1) << c;
+    return m;
+}
+}  // namespace
+
+// Path cover: walk the de Bruijn graph from path starts (source k-mers, in-degree != 1,
+// or a predecessor with out-degree != 1), then from any still-unvisited node (cycles),
+// always moving to an unvisited successor.  Only speed depends on the cover; the kernel
+// uses a path step only when it provably equals the SBWT step (encode_core.h).
+void build_paths(const HostIndex &ix, Derived &dv) {
+    const uint64_t n = ix.n;
+    const uint32_t k = ix.k;
+    dv.has_paths = false;
+    if (n >= (1ULL << 31) || k < 1) return;
+    // dummies: BFS from the root through labels, depth < k
+    std::vector<uint8_t> dummy(n, 0);
+    {
+        std::vector<std::pair<uint32_t, uint32_t>> q;
+        q.push_back({0, 0});
+        dummy[0] = 1;
+        for (size_t h = 0; h < q.size(); h++) {
+            auto [v, dep] = q[h];
+            if (dep + 1 >= k) continue;
+            uint32_t m = labels_of(dv, v);
+            for (int c = 0; c < 4; c++)
+                if (m >> c & 1) {
+                    uint32_t z = dv.C[c] + host_rank(dv, c, v);
+                    if (!dummy[z]) {
+                        dummy[z] = 1;
+                        q.push_back({z, dep + 1});
+                    }
+                }
+        }
+    }
+    auto group_first = [&](uint64_t z) {
+        while (z > 0 && k >= 2 && ix.lcs[z] >= k - 1) z--;
+        return z;
+    };
+    auto succ_mask = [&](uint64_t z) { return labels_of(dv, group_first(z)); };
+    auto group_size = [&](uint64_t g) {  // nodes sharing g's (k-1)-suffix, g group-first
+        uint64_t e = g + 1;
+        while (e < n && k >= 2 && ix.lcs[e] >= k - 1) e++;
+        return e - g;
+    };
+    std::vector<uint8_t> visited(n, 0);
+    std::vector<uint32_t> order;  // node sequence of all paths
+    std::vector<uint64_t> path_start;
+    order.reserve(n);
+    auto walk = [&](uint32_t z) {
+        path_start.push_back(order.size());
+        visited[z] = 1;
+        order.push_back(z);
+        for (;;) {
+            const uint64_t g = group_first(z);
+            const uint32_t m = labels_of(dv, g);
+            uint32_t next = kNoNode;
+            for (int c = 0; c < 4 && next == kNoNode; c++)
+                if (m >> c & 1) {
+                    uint32_t y = dv.C[c] + host_rank(dv, c, g);
+                    if (!visited[y] && !dummy[y]) next = y;
+                }
+            if (next == kNoNode) break;
+            visited[next] = 1;
+            order.push_back(next);
+            z = next;
+        }
+    };
+    for (uint64_t z = 1; z < n; z++) {
+        if (dummy[z]) continue;
+        const uint32_t pz = dv.pred[z];
+        bool start = dummy[pz] != 0;
+        if (!start) {
+            const uint64_t pg = group_first(pz);
+            start = group_size(pg) != 1 || __builtin_popcount(succ_mask(pz)) != 1;
+        }
+        if (start && !visited[z]) walk((uint32_t)z);
+    }
+    for (uint64_t z = 1; z < n; z++)
+        if (!dummy[z] && !visited[z]) walk((uint32_t)z);
+    path_start.push_back(order.size());
+    const uint64_t np = path_start.size() - 1;
+    // text layout: per path k chars of its first k-mer, one char per further node, then
+    // one pad position; colex_at is valid exactly at the k-mer start of each path node
+    uint64_t tlen = 0;
+    for (uint64_t p = 0; p < np; p++) tlen += (path_start[p + 1] - path_start[p]) + k;
+    if (tlen + 64 >= (1ULL << 31)) return;
+    dv.colex_at.assign(tlen + 8, kNoNode);
+    dv.pos_of_node.assign(n, kNoNode);
+    dv.ptext.assign(tlen / 32 + 4, 0);
+    auto put = [&](uint64_t t, uint32_t c) { dv.ptext[t >> 5] |= (uint64_t)(c & 3) << (2 * (t & 31)); };
+    uint64_t b = 0;
+    std::vector<uint8_t> first(k);
+    for (uint64_t p = 0; p < np; p++) {
+        const uint64_t a = path_start[p], e = path_start[p + 1];
+        // characters of the first k-mer: walk back k-1 predecessors
+        uint32_t z = order[a];
+        for (int64_t t = (int64_t)k - 1; t >= 0; t--) {
+            first[t] = dv.code[z];
+            z = dv.pred[z];
+        }
+        for (uint32_t t = 0; t < k; t++) put(b + t, first[t]);
+        for (uint64_t i = a; i < e; i++) {
+            const uint32_t node = order[i];
+            const uint64_t pos = b + (i - a);
+            if (i > a) put(pos + k - 1, dv.code[node]);
+            const uint32_t u = (dv.uniq[node >> 5] >> (node & 31)) & 1u;
+            dv.colex_at[pos] = node | (u << 31);
+            dv.pos_of_node[node] = (uint32_t)pos;
+        }
+        b += (e - a) + k;  // last node at b+(e-a)-1; positions up to b+(e-a)+k-1 hold no node
+    }
+    dv.tlen = tlen;
+    dv.n_paths = np;
+    dv.has_paths = true;
 }
 
 void build_walk_host(const Derived &dv, uint64_t n, std::vector<WalkEntry> &walk) {
@@ -135,6 +263,10 @@ DevIndex host_dev_index(const HostIndex &ix, const Derived &dv, const std::vecto
     d.k = ix.k;
     d.t_jump = dv.t_jump;
     for (int c = 0; c < 5; c++) d.C[c] = dv.C[c];
+    d.has_paths = dv.has_paths ? 1u : 0u;
+    d.ptext = dv.ptext.empty() ? nullptr : dv.ptext.data();
+    d.colex_at = dv.colex_at.empty() ? nullptr : dv.colex_at.data();
+    d.pos_of_node = dv.pos_of_node.empty() ? nullptr : dv.pos_of_node.data();
     return d;
 }
 

@@ -16,7 +16,20 @@ struct Derived {
     std::vector<uint8_t> code;    // last character of each node (root: 0)
     uint32_t C[5] = {0, 0, 0, 0, 0};
     uint32_t t_jump = 1;
+    // path cover of the de Bruijn graph (DESIGN.md "Path walk"): every real k-mer node
+    // sits at one position of a path text; consecutive positions are graph edges.
+    bool has_paths = false;
+    uint64_t tlen = 0;               // path text length (characters)
+    std::vector<uint64_t> ptext;     // 2-bit, char t at bits 2(t%32) of word t/32
+    std::vector<uint32_t> colex_at;  // per text position: node | uniq << 31, or kNoNode
+    std::vector<uint32_t> pos_of_node;  // per node: text position of its k-mer, or kNoNode
+    uint64_t n_paths = 0;
 };
+
+constexpr uint32_t kNoNode = 0xFFFFFFFFu;
+
+// Builds the path cover (fills has_paths, tlen, ptext, colex_at, pos_of_node).
+void build_paths(const HostIndex &ix, Derived &dv);
 
 // Validates the index and fills rank lines, unique-predecessor bits, pred and code.
 bool build_derived(const HostIndex &ix, Derived &out, std::string &err, int threads);

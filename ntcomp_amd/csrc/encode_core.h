@@ -49,6 +49,11 @@ struct DevIndex {
     uint32_t k;
     uint32_t t_jump;        // first contraction probe below d-1 (see ms_step)
     uint32_t C[5];          // C[4] = n
+    // path walk (encode v2): a path cover of the de Bruijn graph, see derived.cpp
+    uint32_t has_paths;
+    const uint64_t *ptext;        // path text, 2-bit, char t at bits 2(t%32) of word t/32
+    const uint32_t *colex_at;     // node | uniq << 31 at each k-mer start, 0xFFFFFFFF elsewhere
+    const uint32_t *pos_of_node;  // text position of each real node's k-mer, or 0xFFFFFFFF
 };
 
 // per-read status codes (values of ntc_status)
@@ -220,15 +225,15 @@ struct LaneScratch {
 };
 
 // consecutive set flags at positions p, p-1, ... (at most cap)
-NTC_HD uint32_t run_from(const uint32_t *F, uint32_t p, uint32_t cap) {
+NTC_HD uint32_t run_from(const uint32_t *F, uint32_t p, uint32_t cap, uint32_t stride = 64) {
     int64_t w = p >> 5;
     const uint32_t b = p & 31;
-    uint32_t x = F[w * 64];
+    uint32_t x = F[w * stride];
     const uint32_t z = clz32((~x) << (31 - b));
     if (z <= b) return z < cap ? z : cap;
     uint32_t cnt = b + 1;
     for (w = w - 1; w >= 0 && cnt < cap; w--) {
-        x = F[w * 64];
+        x = F[w * stride];
         if (x == 0xFFFFFFFFu) {
             cnt += 32;
             continue;
@@ -307,6 +312,234 @@ NTC_HD int encode_lane(const DevIndex &ix, const uint8_t *q, uint32_t len, uint3
             w = bits | ((uint64_t)((first + 2) | (seglen << 2)) << 56);
         }
         s.R[(uint64_t)nrec * 64] = w;
+        nrec++;
+        if (i > 0) i -= 1;
+        else break;
+    }
+    return nrec;
+}
+
+// ======================================================================================
+// encode v2: one read per lane, the whole read in ONE flattened loop.  Every iteration a
+// lane does exactly one unit of work -- a path step, an extension, or one contraction
+// probe -- so lanes of a wave never wait for each other's contraction loops (v1 spent
+// ~7x its instructions on that divergence, profiles/round1).
+//
+// Path step: when the matching-statistics interval is ONE node z (always so at d = k;
+// at d < k the node z is then also group-first, so its labels are its out-edges) and z
+// sits at text position j of the path cover with the next path character equal to the
+// query character c, extend_right([z, z+1), c) is exactly the next path node: the
+// node z[1..k].c (for d = k via the contraction to z's group and back, which yields the
+// same node and d = k).  Such steps read the path arrays sequentially instead of a
+// random rank line.  Any other case runs the SBWT step of ms_step (same probes).
+// ======================================================================================
+constexpr uint32_t kFastTag = 0x80000000u;
+
+struct LaneScratch2 {
+    uint8_t *D;   // D[p], per-read contiguous, 16-byte aligned
+    uint32_t *F;  // F[p / 32]
+    uint64_t *E;  // (p << 32 | node) for an SBWT-step position, (p << 32 | j | kFastTag)
+                  // where a run of path steps starts at text position j
+    uint64_t *R;  // records
+};
+
+struct BaseReader {
+    const uint8_t *q;
+    uint64_t blk;
+    uint32_t w0, w1, w2, w3;
+    NTC_HD explicit BaseReader(const uint8_t *qq) : q(qq), blk(~0ULL), w0(0), w1(0), w2(0), w3(0) {}
+    NTC_HD uint32_t get(uint32_t p) {
+        const uint64_t a = (uint64_t)(uintptr_t)(q + p);
+        if ((a >> 4) != blk) {
+            blk = a >> 4;
+#ifdef __HIP_DEVICE_COMPILE__
+            const uint4 v = *reinterpret_cast<const uint4 *>((uintptr_t)(blk << 4));
+            w0 = v.x; w1 = v.y; w2 = v.z; w3 = v.w;
+#else
+            const uint32_t *v = reinterpret_cast<const uint32_t *>((uintptr_t)(blk << 4));
+            w0 = v[0]; w1 = v[1]; w2 = v[2]; w3 = v[3];
+#endif
+        }
+        const uint32_t b = (uint32_t)(a & 15);
+        const uint32_t w = (b & 8) ? ((b & 4) ? w3 : w2) : ((b & 4) ? w1 : w0);
+        return (w >> ((b & 3) * 8)) & 0xFFu;
+    }
+};
+
+enum : uint32_t { kModeExt = 0, kModeP1 = 1, kModeTj = 2, kModeBs = 3, kModeLin = 4 };
+
+NTC_HD int encode_lane2(const DevIndex &ix, const uint8_t *q, uint32_t len, uint32_t rows, LaneScratch2 s) {
+    if (len == 0) return -kErrEmptyRead;
+    if (len > rows) return -kErrCapacity;
+    const uint32_t k = ix.k, tj = ix.t_jump;
+    BaseReader br(q);
+    int c = base_code((uint8_t)br.get(0));
+    if (c < 0) return -kErrInvalidBase;
+    uint32_t p = 0, d = 0, l = 0, r = ix.n, j = 0xFFFFFFFFu;
+    uint32_t mode = kModeExt, hi = 0, lo = 0, l1 = 0, r1 = 0, cl = 0, cr = 0, bl = 0, bR = 0;
+    uint32_t fw = 0, d0 = 0, d1 = 0, d2 = 0, d3 = 0, ne = 0;
+    bool run_open = false;
+    uint32_t cblk = 0xFFFFFFFFu, c0 = 0, c1 = 0, c2 = 0, c3 = 0;  // colex_at cache (4 entries)
+    uint32_t tblk = 0xFFFFFFFFu;
+    uint64_t tw = 0;  // path text cache (32 chars)
+    while (p < len) {
+        bool commit = false, fast = false;
+        uint32_t nl = 0, nr = 0, nd = 0, flag = 0;
+        if (mode == kModeExt && j != 0xFFFFFFFFu) {
+            const uint32_t tpos = j + k;
+            if ((tpos >> 5) != tblk) {
+                tblk = tpos >> 5;
+                tw = ix.ptext[tblk];
+            }
+            const uint32_t tc = (uint32_t)(tw >> (2 * (tpos & 31))) & 3u;
+            const uint32_t jn = j + 1;
+            if ((jn >> 2) != cblk) {
+                cblk = jn >> 2;
+#ifdef __HIP_DEVICE_COMPILE__
+                const uint4 v = *reinterpret_cast<const uint4 *>(ix.colex_at + ((uint64_t)cblk << 2));
+                c0 = v.x; c1 = v.y; c2 = v.z; c3 = v.w;
+#else
+                const uint32_t *v = ix.colex_at + ((uint64_t)cblk << 2);
+                c0 = v[0]; c1 = v[1]; c2 = v[2]; c3 = v[3];
+#endif
+            }
+            const uint32_t cn = (jn & 2) ? ((jn & 1) ? c3 : c2) : ((jn & 1) ? c1 : c0);
+            if (tc == (uint32_t)c && cn != 0xFFFFFFFFu) {
+                fast = commit = true;
+                nl = cn & 0x7FFFFFFFu;
+                nr = nl + 1;
+                nd = d + 1 < k ? d + 1 : k;
+                flag = nd == k ? (cn >> 31) : 0u;
+                j = jn;
+            }
+        }
+        if (!fast) {
+            // ---- one SBWT unit: query, (widen), extend, transition (= ms_step) ----------
+            uint32_t ql = l, qr = r, t = 0;
+            bool wid = true;
+            if (mode == kModeExt) wid = false;
+            else if (mode == kModeP1) t = hi;
+            else if (mode == kModeTj) { ql = l1; qr = r1; t = tj; }
+            else if (mode == kModeBs) { ql = l1; qr = r1; t = (lo + hi) >> 1; }
+            else { ql = cl; qr = cr; t = hi - 1; }
+            if (wid) widen(ix, ql, qr, t);
+            uint32_t el, er;
+            extend(ix, c, ql, qr, el, er);
+            const bool ok = el < er;
+            if (mode == kModeExt) {
+                if (ok) { commit = true; nl = el; nr = er; nd = d + 1 < k ? d + 1 : k; }
+                else if (d == 0) return -kErrInvalidBase;
+                else { hi = d - 1; mode = kModeP1; }
+            } else if (mode == kModeP1) {
+                l1 = ql; r1 = qr;
+                if (ok) { commit = true; nl = el; nr = er; nd = hi + 1; }
+                else if (hi > tj + 1) mode = kModeTj;
+                else if (hi == 0) return -kErrInvalidBase;
+                else { cl = ql; cr = qr; mode = kModeLin; }
+            } else if (mode == kModeTj) {
+                if (ok) {
+                    lo = tj; bl = el; bR = er;
+                    if (hi - lo > 1) mode = kModeBs;
+                    else { commit = true; nl = bl; nr = bR; nd = lo + 1; }
+                } else { hi = tj; cl = ql; cr = qr; mode = kModeLin; }
+            } else if (mode == kModeBs) {
+                if (ok) { lo = t; bl = el; bR = er; } else hi = t;
+                if (hi - lo <= 1) { commit = true; nl = bl; nr = bR; nd = lo + 1; }
+            } else {
+                cl = ql; cr = qr;
+                if (ok) { commit = true; nl = el; nr = er; nd = t + 1; }
+                else if (t == 0) return -kErrInvalidBase;
+                else hi = t;
+            }
+            if (commit) {
+                j = 0xFFFFFFFFu;
+                if (ix.has_paths && nr == nl + 1) j = ix.pos_of_node[nl];
+                if (nd == k) flag = (ix.uniq[nl >> 5] >> (nl & 31)) & 1u;
+            }
+        }
+        if (commit) {
+            l = nl; r = nr; d = nd;
+            if (fast) {
+                if (!run_open) {
+                    s.E[ne++] = ((uint64_t)p << 32) | (uint64_t)(j | kFastTag);
+                    run_open = true;
+                }
+            } else {
+                s.E[ne++] = ((uint64_t)p << 32) | (uint64_t)l;
+                run_open = false;
+            }
+            const uint32_t b = p & 15, sh = (b & 3) * 8, v = d << sh;
+            if (b < 4) d0 |= v; else if (b < 8) d1 |= v; else if (b < 12) d2 |= v; else d3 |= v;
+            if (b == 15 || p + 1 == len) {
+#ifdef __HIP_DEVICE_COMPILE__
+                *reinterpret_cast<uint4 *>(s.D + (p & ~15u)) = make_uint4(d0, d1, d2, d3);
+#else
+                uint32_t *dd = reinterpret_cast<uint32_t *>(s.D + (p & ~15u));
+                dd[0] = d0; dd[1] = d1; dd[2] = d2; dd[3] = d3;
+#endif
+                d0 = d1 = d2 = d3 = 0;
+            }
+            fw |= flag << (p & 31);
+            if ((p & 31) == 31 || p + 1 == len) {
+                s.F[p >> 5] = fw;
+                fw = 0;
+            }
+            p++;
+            mode = kModeExt;
+            if (p < len) {
+                c = base_code((uint8_t)br.get(p));
+                if (c < 0) return -kErrInvalidBase;
+            }
+        }
+    }
+    if (ne < rows) s.E[ne] = 0xFFFFFFFF00000000ULL;  // terminator for diagnostics
+    // ---- greedy right-to-left parse, lib.rs:175-218 (as encode_lane) ------------------
+    int32_t e = (int32_t)ne - 1;
+    uint32_t i = len;
+    int nrec = 0;
+    while (i > 0) {
+        const uint32_t x = i - 1;
+        const uint32_t di = s.D[x];
+        while (e > 0 && (uint32_t)(s.E[e] >> 32) > x) e--;
+        const uint64_t ent = s.E[e];
+        uint32_t st = (uint32_t)ent;
+        if (ix.has_paths && (st & kFastTag))
+            st = ix.colex_at[(st & ~kFastTag) + (x - (uint32_t)(ent >> 32))] & 0x7FFFFFFFu;
+        const uint32_t segend = i;
+        uint32_t seglen;
+        if (di == k && i > k + 1) {
+            const uint32_t ext = run_from(s.F, i - 2, i - k - 1, 1);
+            const uint32_t L = k + ext;
+            uint32_t m = L, pp = i;
+            for (;;) {
+                const uint32_t dp = s.D[pp - 1];
+                if (dp < m) {
+                    if (dp >= pp) return -kErrFormat;
+                    m -= dp;
+                    pp -= dp;
+                } else {
+                    break;
+                }
+            }
+            seglen = L - (m - 1);
+            i = pp;
+        } else {
+            seglen = di;
+            if (i > di) i -= di - 1;
+            else i = 0;
+        }
+        if (seglen >= (1u << 24)) return -kErrLength;
+        const uint64_t first = nrec == 0 ? 1u : 0u;
+        uint64_t w;
+        if (seglen > 11) {
+            w = (uint64_t)st | ((uint64_t)(seglen & 0xFFFFFFu) << 32) | (first << 56);
+        } else {
+            uint64_t bits = 0;
+            for (uint32_t t = 0; t < seglen; t++)
+                bits |= (uint64_t)base_code(q[segend - seglen + t]) << (2 * t);
+            w = bits | ((uint64_t)((first + 2) | (seglen << 2)) << 56);
+        }
+        s.R[nrec] = w;
         nrec++;
         if (i > 0) i -= 1;
         else break;

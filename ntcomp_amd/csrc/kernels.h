@@ -21,9 +21,12 @@ struct EncodeArgs {
     uint64_t *R;
     uint32_t *rec_count;
     unsigned long long *status;  // min over (read << 8 | code); ~0 = ok
+    uint64_t *E;                 // v2: entries (per-lane contiguous, like D and R)
+    int variant;                 // 1 = phase-synchronous lanes, 2 = flattened + path walk
 };
 
 struct EmitArgs {
+    int variant;                 // 1: R is [tile][j][lane]; 2: R is [tile][lane][j]
     const uint64_t *R;
     const uint64_t *tile_base;
     uint64_t rows_uniform;
@@ -36,6 +39,9 @@ struct EmitArgs {
 };
 
 struct DebugArgs {
+    int variant;
+    const uint64_t *E;
+    DevIndex ix;
     const uint8_t *D;
     const uint32_t *S;
     const uint64_t *tile_base;

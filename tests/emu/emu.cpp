@@ -33,12 +33,13 @@ bool load(const ntc_index_view *v, HostIndex &hx, Derived &dv, std::vector<WalkE
 
 extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const uint64_t *offs, uint64_t n_reads,
                           uint64_t *rec_out, uint64_t cap, uint64_t *rec_offsets, int64_t *bad, uint32_t *d_out,
-                          uint32_t *s_out) {
+                          uint32_t *s_out, int variant, int use_paths) {
     HostIndex hx;
     Derived dv;
     std::vector<WalkEntry> walk;
     DevIndex d;
     if (!load(v, hx, dv, walk, d)) return NTC_ERR_FORMAT;
+    if (!use_paths) d.has_paths = 0;
     *bad = -1;
     uint64_t tiles = (n_reads + 63) / 64, total = 0;
     rec_offsets[0] = 0;
@@ -49,22 +50,43 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
         std::vector<uint8_t> D(rows * 64 + 64);
         std::vector<uint32_t> S(rows * 64 + 64), F((rows / 32 + 1) * 64);
         std::vector<uint64_t> R(rows * 64 + 64);
+        std::vector<uint64_t> E(rows * 64 + 64);
         for (uint64_t r = t * 64; r < n_reads && r < t * 64 + 64; r++) {
             uint32_t lane = (uint32_t)(r & 63);
-            LaneScratch s{D.data() + lane, S.data() + lane, F.data() + lane, R.data() + lane};
             uint32_t len = (uint32_t)(offs[r + 1] - offs[r]);
-            int rc = encode_lane(d, bases + offs[r], len, (uint32_t)rows, s);
-            if (d_out)
-                for (uint32_t p = 0; p < len; p++) {
-                    d_out[offs[r] - offs[0] + p] = D[(uint64_t)p * 64 + lane];
-                    s_out[offs[r] - offs[0] + p] = S[(uint64_t)p * 64 + lane];
+            int rc;
+            if (variant == 2) {
+                LaneScratch2 s{D.data() + lane * rows, F.data() + lane * (rows / 32), E.data() + lane * rows,
+                               R.data() + lane * rows};
+                rc = encode_lane2(d, bases + offs[r], len, (uint32_t)rows, s);
+                if (d_out && rc >= 0) {
+                    const uint64_t *El = E.data() + lane * rows;
+                    uint64_t ei = 0;
+                    for (uint32_t p = 0; p < len; p++) {
+                        while (ei + 1 < rows && (uint32_t)(El[ei + 1] >> 32) <= p) ei++;
+                        uint32_t st = (uint32_t)El[ei];
+                        if (d.has_paths && (st & kFastTag))
+                            st = d.colex_at[(st & ~kFastTag) + (p - (uint32_t)(El[ei] >> 32))] & 0x7FFFFFFFu;
+                        d_out[offs[r] - offs[0] + p] = D[lane * rows + p];
+                        s_out[offs[r] - offs[0] + p] = st;
+                    }
                 }
+            } else {
+                LaneScratch s{D.data() + lane, S.data() + lane, F.data() + lane, R.data() + lane};
+                rc = encode_lane(d, bases + offs[r], len, (uint32_t)rows, s);
+                if (d_out)
+                    for (uint32_t p = 0; p < len; p++) {
+                        d_out[offs[r] - offs[0] + p] = D[(uint64_t)p * 64 + lane];
+                        s_out[offs[r] - offs[0] + p] = S[(uint64_t)p * 64 + lane];
+                    }
+            }
             if (rc < 0) {
                 *bad = (int64_t)r;
                 return -rc;
             }
             if (total + (uint64_t)rc > cap) return NTC_ERR_CAPACITY;
-            for (int j = 0; j < rc; j++) rec_out[total + j] = R[(uint64_t)j * 64 + lane];
+            for (int j = 0; j < rc; j++)
+                rec_out[total + j] = variant == 2 ? R[lane * rows + j] : R[(uint64_t)j * 64 + lane];
             total += (uint64_t)rc;
             rec_offsets[r + 1] = total;
         }

@@ -33,12 +33,14 @@ def test_gpu_golden_records_ms_decode(ctx, name):
     assert [out[o2[i]:o2[i + 1]].tobytes().decode() for i in range(len(o2) - 1)] == g["reads"]
 
 
+@pytest.mark.parametrize("variant", [2, 1])
 @pytest.mark.parametrize("k,err_ppm,glen", [(31, 10_000, 400_000), (91, 10_000, 400_000), (91, 0, 400_000),
                                              (15, 30_000, 200_000), (255, 5_000, 100_000), (11, 10_000, 100_000)])
-def test_gpu_matches_oracle_random(ctx, k, err_ppm, glen):
+def test_gpu_matches_oracle_random(ctx, k, err_ppm, glen, variant):
     genome = nt.synth_genome(1000 + k, glen)
     ix = nt.Index.build([genome.tobytes()], k)
     ctx.upload(ix)
+    ctx.set_option("encode_variant", variant)
     L = 150 if k < 200 else 400
     n = 4000
     reads = nt.synth_reads(genome, 77, 0, n, L, err_ppm)
@@ -51,6 +53,34 @@ def test_gpu_matches_oracle_random(ctx, k, err_ppm, glen):
     out, o2 = ctx.decode(got)
     assert np.array_equal(out, reads)
     assert np.array_equal(o2, offs)
+    ctx.set_option("encode_variant", 2)
+
+
+def test_gpu_v2_repetitive_genome_and_ms(ctx):
+    rng = np.random.default_rng(5)
+    unit = nt.synth_genome(21, 400).tobytes()
+    parts = []
+    for _ in range(200):
+        u = bytearray(unit)
+        for _ in range(3):
+            u[int(rng.integers(0, len(u)))] = b"ACGT"[int(rng.integers(0, 4))]
+        parts.append(bytes(u) + nt.synth_genome(int(rng.integers(1, 1 << 30)), 97).tobytes())
+    genome = np.frombuffer(b"".join(parts), dtype=np.uint8)
+    for k in (31, 91):
+        ix = nt.Index.build([genome.tobytes()], k)
+        ctx.upload(ix)
+        assert ctx.get_option("n_paths") > 0
+        reads = nt.synth_reads(genome, 8, 0, 5000, 150, 10_000)
+        offs = np.arange(0, 5000 * 150 + 1, 150, dtype=np.uint64)
+        orc = OracleIndex(ix.n, k, ix.rows, ix.C, ix.lcs)
+        exp, eoff = orc.encode(reads, offs)
+        got, goff = ctx.encode(reads, offs)
+        assert np.array_equal(goff, eoff) and np.array_equal(got, exp)
+        d, s = ctx.matching_statistics(reads[:300 * 150], offs[:301])
+        for r in range(0, 300, 7):
+            od, olo = orc.ms(reads[r * 150:(r + 1) * 150].tobytes())
+            assert np.array_equal(d[r * 150:(r + 1) * 150], od)
+            assert np.array_equal(s[r * 150:(r + 1) * 150].astype(np.uint64), olo)
 
 
 def test_gpu_ragged_and_edge_lengths(ctx):

@@ -11,11 +11,16 @@ from emu_lib import emu_decode, emu_encode
 from oracle_lib import OracleIndex, golden_names, load_golden, pack_reads
 
 
+VARIANTS = [(2, True), (2, False), (1, False)]  # (kernel variant, path walk)
+
+
+@pytest.mark.parametrize("variant,paths", VARIANTS)
 @pytest.mark.parametrize("name", golden_names())
-def test_emulated_kernel_matches_golden(name):
+def test_emulated_kernel_matches_golden(name, variant, paths):
     g = load_golden(name)
     bases, offs = pack_reads(g["reads"])
-    recs, roff, d, s = emu_encode(g["n"], g["k"], g["rows_u64"], g["C"], g["lcs_u8"], bases, offs, want_ms=True)
+    recs, roff, d, s = emu_encode(g["n"], g["k"], g["rows_u64"], g["C"], g["lcs_u8"], bases, offs, want_ms=True,
+                                  variant=variant, use_paths=paths)
     exp_ms = np.array([x for r in g["ms"] for x in r], dtype=np.uint64).reshape(-1, 2)
     assert np.array_equal(d.astype(np.uint64), exp_ms[:, 0])
     assert np.array_equal(s.astype(np.uint64), exp_ms[:, 1])
@@ -24,8 +29,9 @@ def test_emulated_kernel_matches_golden(name):
     assert [out[o2[i]:o2[i + 1]].tobytes().decode() for i in range(len(o2) - 1)] == g["reads"]
 
 
-@pytest.mark.parametrize("k,err_ppm", [(31, 10_000), (91, 10_000), (91, 0), (15, 30_000), (255, 5_000)])
-def test_emulated_kernel_matches_oracle_random(k, err_ppm):
+@pytest.mark.parametrize("variant,paths", VARIANTS)
+@pytest.mark.parametrize("k,err_ppm", [(31, 10_000), (91, 10_000), (91, 0), (15, 30_000), (255, 5_000), (11, 10_000)])
+def test_emulated_kernel_matches_oracle_random(k, err_ppm, variant, paths):
     genome = nt.synth_genome(100 + k, 60_000)
     ix = nt.Index.build([genome.tobytes()], k, threads=4)
     rows, C, lcs = ix.rows, ix.C, ix.lcs
@@ -34,14 +40,15 @@ def test_emulated_kernel_matches_oracle_random(k, err_ppm):
     offs = np.arange(0, 600 * L + 1, L, dtype=np.uint64)
     orc = OracleIndex(ix.n, k, rows, C, lcs)
     exp, eoff = orc.encode(reads, offs)
-    got, goff = emu_encode(ix.n, k, rows, C, lcs, reads, offs)
+    got, goff = emu_encode(ix.n, k, rows, C, lcs, reads, offs, variant=variant, use_paths=paths)
     assert np.array_equal(goff, eoff)
     assert np.array_equal(got, exp)
     out, o2 = emu_decode(ix.n, k, rows, C, lcs, got)
     assert np.array_equal(out, reads)
 
 
-def test_emulated_ms_matches_oracle_unrelated_reads():
+@pytest.mark.parametrize("variant,paths", VARIANTS)
+def test_emulated_ms_matches_oracle_unrelated_reads(variant, paths):
     # reads from a different genome: many contractions from short d
     genome = nt.synth_genome(3, 50_000)
     other = nt.synth_genome(4, 50_000)
@@ -49,8 +56,35 @@ def test_emulated_ms_matches_oracle_unrelated_reads():
     reads = nt.synth_reads(other, 9, 0, 100, 150, 0)
     offs = np.arange(0, 100 * 150 + 1, 150, dtype=np.uint64)
     orc = OracleIndex(ix.n, 31, ix.rows, ix.C, ix.lcs)
-    _, _, d, s = emu_encode(ix.n, 31, ix.rows, ix.C, ix.lcs, reads, offs, want_ms=True)
+    _, _, d, s = emu_encode(ix.n, 31, ix.rows, ix.C, ix.lcs, reads, offs, want_ms=True, variant=variant,
+                            use_paths=paths)
     for r in range(100):
+        od, olo = orc.ms(reads[r * 150:(r + 1) * 150].tobytes())
+        assert np.array_equal(d[r * 150:(r + 1) * 150], od)
+        assert np.array_equal(s[r * 150:(r + 1) * 150].astype(np.uint64), olo)
+
+
+@pytest.mark.parametrize("k", [31, 91])
+def test_emulated_v2_ms_on_repetitive_genome(k):
+    # a genome built from repeated blocks: branching de Bruijn graph, many short paths,
+    # non-singleton suffix groups -- the path walk must fall back correctly
+    rng = np.random.default_rng(k)
+    unit = nt.synth_genome(21, 400).tobytes()
+    parts = []
+    for _ in range(60):
+        u = bytearray(unit)
+        for _ in range(3):
+            u[int(rng.integers(0, len(u)))] = b"ACGT"[int(rng.integers(0, 4))]
+        parts.append(bytes(u) + nt.synth_genome(int(rng.integers(1, 1 << 30)), 97).tobytes())
+    genome = np.frombuffer(b"".join(parts), dtype=np.uint8)
+    ix = nt.Index.build([genome.tobytes()], k)
+    reads = nt.synth_reads(genome, 8, 0, 800, 150, 10_000)
+    offs = np.arange(0, 800 * 150 + 1, 150, dtype=np.uint64)
+    orc = OracleIndex(ix.n, k, ix.rows, ix.C, ix.lcs)
+    exp, eoff = orc.encode(reads, offs)
+    got, goff, d, s = emu_encode(ix.n, k, ix.rows, ix.C, ix.lcs, reads, offs, want_ms=True)
+    assert np.array_equal(goff, eoff) and np.array_equal(got, exp)
+    for r in range(0, 800, 37):
         od, olo = orc.ms(reads[r * 150:(r + 1) * 150].tobytes())
         assert np.array_equal(d[r * 150:(r + 1) * 150], od)
         assert np.array_equal(s[r * 150:(r + 1) * 150].astype(np.uint64), olo)
