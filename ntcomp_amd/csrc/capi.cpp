@@ -41,7 +41,7 @@ struct ntc_ctx {
     std::vector<void *> index_mem;
     uint64_t index_bytes = 0;
     // workspace buffers (grown, never shrunk)
-    DevBuf ws[16];
+    DevBuf ws[20];
     unsigned long long *d_status = nullptr;
     // last call
     CallKind last = kNone;
@@ -49,7 +49,7 @@ struct ntc_ctx {
     uint64_t *last_out_offs = nullptr;
     uint64_t last_units = 0;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    int encode_variant = 2;
+    int encode_variant = 3;
     uint64_t n_paths = 0, path_text_len = 0;
 };
 
@@ -58,7 +58,7 @@ namespace {
 enum WsSlot {
     WS_D = 0, WS_S, WS_F, WS_R, WS_RECCOUNT, WS_SCANTMP, WS_TILEBASE, WS_TILEROWS,
     WS_STAGE_BASES, WS_STAGE_OFFS, WS_STAGE_RECS, WS_E, WS_DEC_A, WS_DEC_B, WS_DEC_C,
-    WS_DEC_D
+    WS_DEC_D, WS_Q, WS_E3
 };
 
 #define HIP_TRY(ctx, expr)                                                                   \
@@ -116,6 +116,18 @@ int alloc_scratch(ntc_ctx *ctx, uint64_t n_reads, uint64_t total_rows, EncodeArg
     void *p;
     int rc;
     const uint64_t slots = total_rows * 64;
+    if (a.variant == 3) {
+        const uint64_t tiles = (n_reads + 63) / 64;
+        if ((rc = ensure(ctx, WS_Q, (total_rows / 32 + 2 * tiles + 2) * 64 * 8, &p))) return rc;
+        a.Q = (uint64_t *)p;
+        if ((rc = ensure(ctx, WS_E3, slots * sizeof(Entry), &p))) return rc;
+        a.E3 = (Entry *)p;
+        if ((rc = ensure(ctx, WS_R, slots * 8, &p))) return rc;
+        a.R = (uint64_t *)p;
+        if ((rc = ensure(ctx, WS_RECCOUNT, (n_reads + 1) * 4, &p))) return rc;
+        a.rec_count = (uint32_t *)p;
+        return NTC_OK;
+    }
     if ((rc = ensure(ctx, WS_D, slots, &p))) return rc;
     a.D = (uint8_t *)p;
     if (a.variant == 2) {
@@ -227,7 +239,10 @@ int ntc_ctx_create(int device, ntc_ctx **out) {
             delete ctx;
             return NTC_ERR_HIP;
         }
-    if (const char *v = std::getenv("NTC_ENCODE_VARIANT")) ctx->encode_variant = std::atoi(v) == 1 ? 1 : 2;
+    if (const char *v = std::getenv("NTC_ENCODE_VARIANT")) {
+        int x = std::atoi(v);
+        if (x >= 1 && x <= 3) ctx->encode_variant = x;
+    }
     *out = ctx;
     return NTC_OK;
 }
@@ -322,8 +337,12 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     if (result != (WalkEntry *)d_walk_a)
         HIP_TRY(ctx, hipMemcpyAsync(d_walk_a, result, n * sizeof(WalkEntry), hipMemcpyDeviceToDevice,
                                     ctx->stream));
-    void *d_ptext = nullptr, *d_colex_at = nullptr, *d_pos = nullptr;
+    void *d_ptext = nullptr, *d_colex_at = nullptr, *d_pos = nullptr, *d_pvalid = nullptr, *d_puniq = nullptr;
     if (dv.has_paths) {
+        if ((rc = dalloc(dv.pvalid.size() * 8, &d_pvalid))) return rc;
+        if ((rc = dalloc(dv.puniq.size() * 8, &d_puniq))) return rc;
+        HIP_TRY(ctx, hipMemcpy(d_pvalid, dv.pvalid.data(), dv.pvalid.size() * 8, hipMemcpyHostToDevice));
+        HIP_TRY(ctx, hipMemcpy(d_puniq, dv.puniq.data(), dv.puniq.size() * 8, hipMemcpyHostToDevice));
         if ((rc = dalloc(dv.ptext.size() * 8, &d_ptext))) return rc;
         if ((rc = dalloc(dv.colex_at.size() * 4 + 64, &d_colex_at))) return rc;
         if ((rc = dalloc(dv.pos_of_node.size() * 4, &d_pos))) return rc;
@@ -349,6 +368,8 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     d.ptext = (const uint64_t *)d_ptext;
     d.colex_at = (const uint32_t *)d_colex_at;
     d.pos_of_node = (const uint32_t *)d_pos;
+    d.pvalid = (const uint64_t *)d_pvalid;
+    d.puniq = (const uint64_t *)d_puniq;
     ctx->n_paths = dv.n_paths;
     ctx->path_text_len = dv.tlen;
     ctx->has_index = true;
@@ -358,7 +379,7 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
 int ntc_ctx_set_option(ntc_ctx *ctx, const char *key, int64_t value) {
     if (!ctx || !key) return NTC_ERR_INVALID_ARG;
     if (std::strcmp(key, "encode_variant") == 0) {
-        if (value != 1 && value != 2) return set_err(ctx, NTC_ERR_INVALID_ARG, "encode_variant must be 1 or 2");
+        if (value < 1 || value > 3) return set_err(ctx, NTC_ERR_INVALID_ARG, "encode_variant must be 1, 2 or 3");
         ctx->encode_variant = (int)value;
         return NTC_OK;
     }
@@ -638,6 +659,7 @@ int ntc_debug_matching_statistics(ntc_ctx *ctx, const uint8_t *bases, const uint
     if (rc && rc != NTC_ERR_LENGTH) return rc;
     DebugArgs g{};
     g.variant = ctx->encode_variant;
+    g.E3 = (const Entry *)ctx->ws[WS_E3].p;
     g.E = (const uint64_t *)ctx->ws[WS_E].p;
     g.ix = ctx->dix;
     g.D = (const uint8_t *)ctx->ws[WS_D].p;

@@ -204,7 +204,9 @@ void build_paths(const HostIndex &ix, Derived &dv) {
     if (tlen + 64 >= (1ULL << 31)) return;
     dv.colex_at.assign(tlen + 8, kNoNode);
     dv.pos_of_node.assign(n, kNoNode);
-    dv.ptext.assign(tlen / 32 + 4, 0);
+    dv.ptext.assign(tlen / 32 + k / 32 + 8, 0);  // windows read up to k + 64 chars past a node
+    dv.pvalid.assign(tlen / 64 + 4, 0);
+    dv.puniq.assign(tlen / 64 + 4, 0);
     auto put = [&](uint64_t t, uint32_t c) { dv.ptext[t >> 5] |= (uint64_t)(c & 3) << (2 * (t & 31)); };
     uint64_t b = 0;
     std::vector<uint8_t> first(k);
@@ -224,6 +226,8 @@ void build_paths(const HostIndex &ix, Derived &dv) {
             const uint32_t u = (dv.uniq[node >> 5] >> (node & 31)) & 1u;
             dv.colex_at[pos] = node | (u << 31);
             dv.pos_of_node[node] = (uint32_t)pos;
+            dv.pvalid[pos >> 6] |= 1ULL << (pos & 63);
+            if (u) dv.puniq[pos >> 6] |= 1ULL << (pos & 63);
         }
         b += (e - a) + k;  // last node at b+(e-a)-1; positions up to b+(e-a)+k-1 hold no node
     }
@@ -267,6 +271,8 @@ DevIndex host_dev_index(const HostIndex &ix, const Derived &dv, const std::vecto
     d.ptext = dv.ptext.empty() ? nullptr : dv.ptext.data();
     d.colex_at = dv.colex_at.empty() ? nullptr : dv.colex_at.data();
     d.pos_of_node = dv.pos_of_node.empty() ? nullptr : dv.pos_of_node.data();
+    d.pvalid = dv.pvalid.empty() ? nullptr : dv.pvalid.data();
+    d.puniq = dv.puniq.empty() ? nullptr : dv.puniq.data();
     return d;
 }
 

@@ -54,6 +54,8 @@ struct DevIndex {
     const uint64_t *ptext;        // path text, 2-bit, char t at bits 2(t%32) of word t/32
     const uint32_t *colex_at;     // node | uniq << 31 at each k-mer start, 0xFFFFFFFF elsewhere
     const uint32_t *pos_of_node;  // text position of each real node's k-mer, or 0xFFFFFFFF
+    const uint64_t *pvalid;       // bit j: colex_at[j] holds a node (encode v3)
+    const uint64_t *puniq;        // bit j: that node's (k-1)-suffix group is a singleton
 };
 
 // per-read status codes (values of ntc_status)
@@ -538,6 +540,275 @@ NTC_HD int encode_lane2(const DevIndex &ix, const uint8_t *q, uint32_t len, uint
             for (uint32_t t = 0; t < seglen; t++)
                 bits |= (uint64_t)base_code(q[segend - seglen + t]) << (2 * t);
             w = bits | ((uint64_t)((first + 2) | (seglen << 2)) << 56);
+        }
+        s.R[nrec] = w;
+        nrec++;
+        if (i > 0) i -= 1;
+        else break;
+    }
+    return nrec;
+}
+
+// ======================================================================================
+// encode v3: matching statistics as RUN-LENGTH entries.  A lane alternates SBWT units
+// (ms_step's extension / contraction probes, one per loop iteration) with path RUNS:
+// once the interval is a single node at path position j, the next m positions follow
+// the path for as long as the query equals the path text and the path continues.  m is
+// found 32 bases at a time by XOR-ing 2-bit words of the query and the path text, so a
+// run costs a few word loads instead of m dependent rank lookups.  Per position the
+// run implies d = min(d0 + t, k), S = colex_at[j0 + t], flag = (d = k) & puniq[j0 + t].
+// The parse reads D, S and the extension flags back from the entries.
+// ======================================================================================
+struct Entry {       // 16 bytes, one uint4 store
+    uint32_t p;      // first position
+    uint32_t v;      // SBWT entry: colex start S; run entry: path position of node at p
+    uint32_t m;      // positions covered (1 for an SBWT entry)
+    uint32_t dk;     // d at p | flag << 8 (SBWT entries) | run << 31
+};
+constexpr uint32_t kRunTag = 0x80000000u;
+
+struct LaneScratch3 {
+    uint64_t *Q;     // query, 2 bits per base (char t at bits 2(t%32) of word t/32)
+    Entry *E;        // entries, increasing p
+    uint64_t *R;     // records
+};
+
+// 32 two-bit characters starting at character offset off of a packed array
+NTC_HD uint64_t window2(const uint64_t *w, uint32_t off) {
+    const uint32_t i = off >> 5, sh = (off & 31) * 2;
+    const uint64_t a = w[i];
+    return sh ? ((a >> sh) | (w[i + 1] << (64 - sh))) : a;
+}
+// 64 bits starting at bit offset off of a bitvector
+NTC_HD uint64_t window1(const uint64_t *w, uint32_t off) {
+    const uint32_t i = off >> 6, sh = off & 63;
+    const uint64_t a = w[i];
+    return sh ? ((a >> sh) | (w[i + 1] << (64 - sh))) : a;
+}
+NTC_HD uint32_t ctz64(uint64_t x) { return x ? (uint32_t)__builtin_ctzll(x) : 64u; }
+
+// consecutive set bits at positions a, a-1, ... (at most maxn) of bitvector w
+NTC_HD uint32_t ones_down(const uint64_t *w, uint32_t a, uint32_t maxn) {
+    uint32_t cnt = 0;
+    int64_t pos = a;
+    while (cnt < maxn) {
+        const uint32_t wi = (uint32_t)(pos >> 6), b = (uint32_t)(pos & 63);
+        const uint64_t x = ~w[wi] << (63 - b);  // bit b -> bit 63
+        const uint32_t z = x ? (uint32_t)__builtin_clzll(x) : 64u;
+        if (z <= b) { cnt += z; break; }
+        cnt += b + 1;
+        pos -= b + 1;
+        if (pos < 0) break;
+    }
+    return cnt < maxn ? cnt : maxn;
+}
+
+struct EntryView {
+    const Entry *E;
+    const DevIndex *ix;
+    uint32_t k;
+    int32_t e;  // cursor
+    NTC_HD void seek(uint32_t x) {  // entries never move right of x; x >= E[0].p = 0
+        while (e > 0 && E[e].p > x) e--;
+    }
+    NTC_HD uint32_t dval(const Entry &en, uint32_t x) const {
+        const uint32_t d0 = en.dk & 0xFFu;
+        const uint32_t d = d0 + (x - en.p);
+        return (en.dk & kRunTag) ? (d < k ? d : k) : d0;
+    }
+    NTC_HD uint32_t D(uint32_t x) { seek(x); return dval(E[e], x); }
+    NTC_HD uint32_t S(uint32_t x) {
+        seek(x);
+        const Entry &en = E[e];
+        if (en.dk & kRunTag) return ix->colex_at[en.v + (x - en.p)] & 0x7FFFFFFFu;
+        return en.v;
+    }
+    // consecutive positions x, x-1, ... with d = k and a singleton (k-1)-suffix group
+    NTC_HD uint32_t run_from(uint32_t x, uint32_t cap) const {
+        int32_t c = e;
+        uint32_t cnt = 0;
+        int64_t pos = x;
+        while (cnt < cap && pos >= 0) {
+            while (c > 0 && E[c].p > (uint32_t)pos) c--;
+            const Entry &en = E[c];
+            const uint32_t d0 = en.dk & 0xFFu;
+            if (!(en.dk & kRunTag)) {
+                if (!((en.dk >> 8) & 1u)) break;
+                cnt++;
+                pos--;
+                continue;
+            }
+            const uint32_t tx = (uint32_t)pos - en.p;
+            const uint32_t tk = d0 >= k ? 0u : k - d0;  // first t with d = k
+            if (tx < tk) break;
+            const uint32_t want = tx - tk + 1;
+            const uint32_t got = ones_down(ix->puniq, en.v + tx, want);
+            cnt += got;
+            if (got < want || tk > 0) break;
+            pos = (int64_t)en.p - 1;
+        }
+        return cnt < cap ? cnt : cap;
+    }
+};
+
+NTC_HD int encode_lane3(const DevIndex &ix, const uint8_t *q, uint32_t len, uint32_t rows, LaneScratch3 s) {
+    if (len == 0) return -kErrEmptyRead;
+    if (len > rows) return -kErrCapacity;
+    const uint32_t k = ix.k, tj = ix.t_jump;
+    // ---- pack the query to 2 bits per base (and validate it) --------------------------
+    {
+        BaseReader br(q);
+        uint64_t acc = 0;
+        for (uint32_t p = 0; p < len; p++) {
+            const int c = base_code((uint8_t)br.get(p));
+            if (c < 0) return -kErrInvalidBase;
+            acc |= (uint64_t)c << (2 * (p & 31));
+            if ((p & 31) == 31) {
+                s.Q[p >> 5] = acc;
+                acc = 0;
+            }
+        }
+        s.Q[len >> 5] = acc;
+        s.Q[(len >> 5) + 1] = 0;
+    }
+    uint32_t p = 0, d = 0, l = 0, r = ix.n, j = 0xFFFFFFFFu, ne = 0;
+    uint32_t mode = kModeExt, hi = 0, lo = 0, l1 = 0, r1 = 0, cl = 0, cr = 0, bl = 0, bR = 0;
+    bool try_run = false;
+    while (p < len) {
+        if (try_run) {
+            // ---- path run: positions p.. follow the path from node at j ----------------
+            try_run = false;
+            uint32_t m = 0;
+            for (;;) {
+                const uint64_t a = window2(s.Q, p + m);
+                const uint64_t b = window2(ix.ptext, j + k + m);
+                const uint64_t x = a ^ b;
+                uint32_t lim = x ? ctz64(x) >> 1 : 32u;
+                const uint32_t inv = ctz64(~window1(ix.pvalid, j + 1 + m));
+                if (inv < lim) lim = inv;
+                if (len - p - m < lim) lim = len - p - m;
+                m += lim;
+                if (lim < 32) break;
+            }
+            if (m > 0) {
+                Entry en;
+                en.p = p;
+                en.v = j + 1;
+                en.m = m;
+                en.dk = (d + 1 < k ? d + 1 : k) | kRunTag;
+#ifdef __HIP_DEVICE_COMPILE__
+                *reinterpret_cast<uint4 *>(s.E + ne) = make_uint4(en.p, en.v, en.m, en.dk);
+#else
+                s.E[ne] = en;
+#endif
+                ne++;
+                p += m;
+                j += m;
+                d = d + m < k ? d + m : k;
+                l = ix.colex_at[j] & 0x7FFFFFFFu;
+                r = l + 1;
+                continue;
+            }
+        }
+        // ---- one SBWT unit (query, widen, extend, transition) -------------------------
+        const int c = (int)((s.Q[p >> 5] >> (2 * (p & 31))) & 3u);
+        uint32_t ql = l, qr = r, t = 0;
+        bool wid = true;
+        if (mode == kModeExt) wid = false;
+        else if (mode == kModeP1) t = hi;
+        else if (mode == kModeTj) { ql = l1; qr = r1; t = tj; }
+        else if (mode == kModeBs) { ql = l1; qr = r1; t = (lo + hi) >> 1; }
+        else { ql = cl; qr = cr; t = hi - 1; }
+        if (wid) widen(ix, ql, qr, t);
+        uint32_t el, er;
+        extend(ix, c, ql, qr, el, er);
+        const bool ok = el < er;
+        bool commit = false;
+        uint32_t nl = 0, nr = 0, nd = 0;
+        if (mode == kModeExt) {
+            if (ok) { commit = true; nl = el; nr = er; nd = d + 1 < k ? d + 1 : k; }
+            else if (d == 0) return -kErrInvalidBase;
+            else { hi = d - 1; mode = kModeP1; }
+        } else if (mode == kModeP1) {
+            l1 = ql; r1 = qr;
+            if (ok) { commit = true; nl = el; nr = er; nd = hi + 1; }
+            else if (hi > tj + 1) mode = kModeTj;
+            else if (hi == 0) return -kErrInvalidBase;
+            else { cl = ql; cr = qr; mode = kModeLin; }
+        } else if (mode == kModeTj) {
+            if (ok) {
+                lo = tj; bl = el; bR = er;
+                if (hi - lo > 1) mode = kModeBs;
+                else { commit = true; nl = bl; nr = bR; nd = lo + 1; }
+            } else { hi = tj; cl = ql; cr = qr; mode = kModeLin; }
+        } else if (mode == kModeBs) {
+            if (ok) { lo = t; bl = el; bR = er; } else hi = t;
+            if (hi - lo <= 1) { commit = true; nl = bl; nr = bR; nd = lo + 1; }
+        } else {
+            cl = ql; cr = qr;
+            if (ok) { commit = true; nl = el; nr = er; nd = t + 1; }
+            else if (t == 0) return -kErrInvalidBase;
+            else hi = t;
+        }
+        if (commit) {
+            l = nl; r = nr; d = nd;
+            uint32_t flag = 0;
+            if (d == k) flag = (ix.uniq[l >> 5] >> (l & 31)) & 1u;
+#ifdef __HIP_DEVICE_COMPILE__
+            *reinterpret_cast<uint4 *>(s.E + ne) = make_uint4(p, l, 1u, d | (flag << 8));
+#else
+            s.E[ne] = Entry{p, l, 1u, d | (flag << 8)};
+#endif
+            ne++;
+            p++;
+            mode = kModeExt;
+            j = 0xFFFFFFFFu;
+            if (ix.has_paths && r == l + 1) {
+                j = ix.pos_of_node[l];
+                try_run = j != 0xFFFFFFFFu;
+            }
+        }
+    }
+    // ---- greedy right-to-left parse, lib.rs:175-218 ----------------------------------
+    EntryView ev{s.E, &ix, k, (int32_t)ne - 1};
+    uint32_t i = len;
+    int nrec = 0;
+    while (i > 0) {
+        const uint32_t x = i - 1;
+        const uint32_t di = ev.D(x);
+        const uint32_t st = ev.S(x);
+        const uint32_t segend = i;
+        uint32_t seglen;
+        if (di == k && i > k + 1) {
+            const uint32_t ext = ev.run_from(i - 2, i - k - 1);
+            const uint32_t L = k + ext;
+            uint32_t m = L, pp = i;
+            for (;;) {  // jump loop lib.rs:193-203
+                const uint32_t dp = ev.D(pp - 1);
+                if (dp < m) {
+                    if (dp >= pp || dp == 0) return -kErrFormat;
+                    m -= dp;
+                    pp -= dp;
+                } else {
+                    break;
+                }
+            }
+            seglen = L - (m - 1);
+            i = pp;
+        } else {
+            seglen = di;
+            if (i > di) i -= di - 1;
+            else i = 0;
+        }
+        if (seglen >= (1u << 24)) return -kErrLength;
+        const uint64_t first = nrec == 0 ? 1u : 0u;
+        uint64_t w;
+        if (seglen > 11) {
+            w = (uint64_t)st | ((uint64_t)(seglen & 0xFFFFFFu) << 32) | (first << 56);
+        } else {
+            // bitnuc::as_2bit of the segment == its query bases (packed LSB-first already)
+            const uint64_t bits = window2(s.Q, segend - seglen);
+            w = (bits & ((1ULL << (2 * seglen)) - 1)) | ((uint64_t)((first + 2) | (seglen << 2)) << 56);
         }
         s.R[nrec] = w;
         nrec++;

@@ -22,7 +22,10 @@ struct EncodeArgs {
     uint32_t *rec_count;
     unsigned long long *status;  // min over (read << 8 | code); ~0 = ok
     uint64_t *E;                 // v2: entries (per-lane contiguous, like D and R)
-    int variant;                 // 1 = phase-synchronous lanes, 2 = flattened + path walk
+    int variant;                 // 1 = phase-synchronous lanes, 2 = flattened + path walk,
+                                 // 3 = run-length entries with word-parallel path runs
+    uint64_t *Q;                 // v3: packed query words
+    Entry *E3;                   // v3: entries
 };
 
 struct EmitArgs {
@@ -40,6 +43,7 @@ struct EmitArgs {
 
 struct DebugArgs {
     int variant;
+    const Entry *E3;
     const uint64_t *E;
     DevIndex ix;
     const uint8_t *D;

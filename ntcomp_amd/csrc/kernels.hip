@@ -78,6 +78,38 @@ __global__ __launch_bounds__(256) void k_encode2(EncodeArgs a) {
     }
 }
 
+// v3: per-lane contiguous scratch: Q (rows/32 + 2 words), E (rows entries), R (rows)
+__global__ __launch_bounds__(256) void k_encode3(EncodeArgs a) {
+    const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (gid >= a.n_reads) return;
+    const uint64_t tile = gid >> 6;
+    const uint32_t lane = (uint32_t)(gid & 63);
+    uint64_t base, rows;
+    if (a.tile_base) {
+        base = a.tile_base[tile];
+        rows = a.tile_base[tile + 1] - base;
+    } else {
+        base = tile * a.rows_uniform;
+        rows = a.rows_uniform;
+    }
+    const uint64_t beg = a.offs[gid], end = a.offs[gid + 1];
+    const uint64_t len64 = end >= beg ? end - beg : 0;
+    const uint64_t qw = (rows >> 5) + 2;
+    LaneScratch3 s;
+    s.Q = a.Q + ((base >> 5) + 2 * tile) * 64 + lane * qw;
+    s.E = a.E3 + base * 64 + lane * rows;
+    s.R = a.R + base * 64 + lane * rows;
+    int rc;
+    if (end < beg || len64 > 0xFFFFFFFFull) rc = -kErrFormat;
+    else rc = encode_lane3(a.ix, a.bases + beg, (uint32_t)len64, (uint32_t)rows, s);
+    if (rc < 0) {
+        atomicMin(a.status, (unsigned long long)((gid << 8) | (uint64_t)(-rc)));
+        a.rec_count[gid] = 0;
+    } else {
+        a.rec_count[gid] = (uint32_t)rc;
+    }
+}
+
 // rows of scratch a tile of 64 reads needs = longest read, rounded up to 32
 __global__ __launch_bounds__(256) void k_tile_rows(const uint64_t *offs, uint64_t n_reads,
                                                    uint32_t *tile_rows) {
@@ -109,7 +141,7 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
         atomicMin(a.status, (unsigned long long)((gid << 8) | (uint64_t)kErrCapacity));
         return;
     }
-    if (a.variant == 2) {
+    if (a.variant >= 2) {
         const uint64_t rows = a.tile_base ? a.tile_base[tile + 1] - base : a.rows_uniform;
         const uint64_t *src = a.R + base * 64 + lane * rows;
         for (uint32_t j = 0; j < cnt; j++) a.out[off + j] = src[j];
@@ -126,6 +158,20 @@ __global__ __launch_bounds__(256) void k_debug_gather(DebugArgs a) {
     const uint32_t lane = (uint32_t)(gid & 63);
     const uint64_t base = a.tile_base ? a.tile_base[tile] : tile * a.rows_uniform;
     const uint64_t b = a.offs[gid], e = a.offs[gid + 1];
+    if (a.variant == 3) {
+        const uint64_t rows = a.tile_base ? a.tile_base[tile + 1] - base : a.rows_uniform;
+        EntryView ev{a.E3 + base * 64 + lane * rows, &a.ix, a.ix.k, 0};
+        uint32_t cnt = 0;  // entries cover [0, len) contiguously
+        for (uint64_t p = 0; p < e - b;) {
+            const Entry &en = ev.E[cnt];
+            for (uint32_t t = 0; t < en.m && p < e - b; t++, p++) {
+                a.d_out[b + p] = ev.dval(en, (uint32_t)p);
+                a.s_out[b + p] = (en.dk & kRunTag) ? (a.ix.colex_at[en.v + t] & 0x7FFFFFFFu) : en.v;
+            }
+            cnt++;
+        }
+        return;
+    }
     if (a.variant == 2) {
         const uint64_t rows = a.tile_base ? a.tile_base[tile + 1] - base : a.rows_uniform;
         const uint8_t *D = a.D + base * 64 + lane * rows;
@@ -323,7 +369,8 @@ void scan_excl_u64(const uint64_t *in, uint64_t n, uint64_t *out, uint64_t *tmp,
 static inline dim3 grid_for(uint64_t n) { return dim3((uint32_t)((n + 255) / 256)); }
 
 void launch_encode(const EncodeArgs &a, hipStream_t s) {
-    if (a.variant == 2) hipLaunchKernelGGL(k_encode2, grid_for(a.n_reads), dim3(256), 0, s, a);
+    if (a.variant == 3) hipLaunchKernelGGL(k_encode3, grid_for(a.n_reads), dim3(256), 0, s, a);
+    else if (a.variant == 2) hipLaunchKernelGGL(k_encode2, grid_for(a.n_reads), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(k_encode, grid_for(a.n_reads), dim3(256), 0, s, a);
 }
 void launch_tile_rows(const uint64_t *offs, uint64_t n_reads, uint32_t *tile_rows, hipStream_t s) {

@@ -55,7 +55,32 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
             uint32_t lane = (uint32_t)(r & 63);
             uint32_t len = (uint32_t)(offs[r + 1] - offs[r]);
             int rc;
-            if (variant == 2) {
+            if (variant == 3) {
+                std::vector<uint64_t> Q(rows / 32 + 2);
+                std::vector<Entry> E3(rows + 1);
+                std::vector<uint64_t> R3(rows + 1);
+                LaneScratch3 s{Q.data(), E3.data(), R3.data()};
+                rc = encode_lane3(d, bases + offs[r], len, (uint32_t)rows, s);
+                if (d_out && rc >= 0) {
+                    uint32_t p = 0;
+                    for (size_t ei = 0; p < len; ei++) {
+                        const Entry &en = E3[ei];
+                        EntryView ev{E3.data(), &d, d.k, 0};
+                        for (uint32_t t = 0; t < en.m && p < len; t++, p++) {
+                            d_out[offs[r] - offs[0] + p] = ev.dval(en, p);
+                            s_out[offs[r] - offs[0] + p] =
+                                (en.dk & kRunTag) ? (d.colex_at[en.v + t] & 0x7FFFFFFFu) : en.v;
+                        }
+                    }
+                }
+                if (rc >= 0) {
+                    if (total + (uint64_t)rc > cap) return NTC_ERR_CAPACITY;
+                    for (int jj = 0; jj < rc; jj++) rec_out[total + jj] = R3[jj];
+                    total += (uint64_t)rc;
+                    rec_offsets[r + 1] = total;
+                    continue;
+                }
+            } else if (variant == 2) {
                 LaneScratch2 s{D.data() + lane * rows, F.data() + lane * (rows / 32), E.data() + lane * rows,
                                R.data() + lane * rows};
                 rc = encode_lane2(d, bases + offs[r], len, (uint32_t)rows, s);

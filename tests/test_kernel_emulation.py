@@ -11,7 +11,7 @@ from emu_lib import emu_decode, emu_encode
 from oracle_lib import OracleIndex, golden_names, load_golden, pack_reads
 
 
-VARIANTS = [(2, True), (2, False), (1, False)]  # (kernel variant, path walk)
+VARIANTS = [(3, True), (3, False), (2, True), (1, False)]  # (kernel variant, path walk)
 
 
 @pytest.mark.parametrize("variant,paths", VARIANTS)
@@ -82,8 +82,9 @@ def test_emulated_v2_ms_on_repetitive_genome(k):
     offs = np.arange(0, 800 * 150 + 1, 150, dtype=np.uint64)
     orc = OracleIndex(ix.n, k, ix.rows, ix.C, ix.lcs)
     exp, eoff = orc.encode(reads, offs)
-    got, goff, d, s = emu_encode(ix.n, k, ix.rows, ix.C, ix.lcs, reads, offs, want_ms=True)
-    assert np.array_equal(goff, eoff) and np.array_equal(got, exp)
+    for variant in (3, 2):
+        got, goff, d, s = emu_encode(ix.n, k, ix.rows, ix.C, ix.lcs, reads, offs, want_ms=True, variant=variant)
+        assert np.array_equal(goff, eoff) and np.array_equal(got, exp)
     for r in range(0, 800, 37):
         od, olo = orc.ms(reads[r * 150:(r + 1) * 150].tobytes())
         assert np.array_equal(d[r * 150:(r + 1) * 150], od)
