@@ -50,6 +50,7 @@ struct ntc_ctx {
     uint64_t last_units = 0;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     int encode_variant = 3;
+    int exact_ms = 0;       // set only by the diagnostics entry point
     uint64_t n_paths = 0, path_text_len = 0;
 };
 
@@ -161,6 +162,7 @@ int encode_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, ui
     a.rows_uniform = lay.rows_uniform;
     a.status = ctx->d_status;
     a.variant = ctx->encode_variant;
+    a.exact_ms = ctx->exact_ms;
     int rc = alloc_scratch(ctx, n_reads, lay.total_rows, a);
     if (rc) return rc;
     void *tmp;
@@ -338,6 +340,11 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
         HIP_TRY(ctx, hipMemcpyAsync(d_walk_a, result, n * sizeof(WalkEntry), hipMemcpyDeviceToDevice,
                                     ctx->stream));
     void *d_ptext = nullptr, *d_colex_at = nullptr, *d_pos = nullptr, *d_pvalid = nullptr, *d_puniq = nullptr;
+    void *d_ptab = nullptr;
+    if (!dv.prefix_tab.empty()) {
+        if ((rc = dalloc(dv.prefix_tab.size() * 4, &d_ptab))) return rc;
+        HIP_TRY(ctx, hipMemcpy(d_ptab, dv.prefix_tab.data(), dv.prefix_tab.size() * 4, hipMemcpyHostToDevice));
+    }
     if (dv.has_paths) {
         if ((rc = dalloc(dv.pvalid.size() * 8, &d_pvalid))) return rc;
         if ((rc = dalloc(dv.puniq.size() * 8, &d_puniq))) return rc;
@@ -370,6 +377,8 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     d.pos_of_node = (const uint32_t *)d_pos;
     d.pvalid = (const uint64_t *)d_pvalid;
     d.puniq = (const uint64_t *)d_puniq;
+    d.prefix_tab = (const uint2 *)d_ptab;
+    d.prefix_len = d_ptab ? kPrefixLen : 0u;
     ctx->n_paths = dv.n_paths;
     ctx->path_text_len = dv.tlen;
     ctx->has_index = true;
@@ -655,7 +664,9 @@ int ntc_debug_matching_statistics(ntc_ctx *ctx, const uint8_t *bases, const uint
     const uint64_t total = read_offsets[n_reads] - read_offsets[0];
     std::vector<uint64_t> recs(total + 1), roffs(n_reads + 1);
     int64_t bad = -1;
+    ctx->exact_ms = 1;
     int rc = ntc_encode_batch(ctx, bases, read_offsets, n_reads, recs.data(), total + 1, roffs.data(), &bad);
+    ctx->exact_ms = 0;
     if (rc && rc != NTC_ERR_LENGTH) return rc;
     DebugArgs g{};
     g.variant = ctx->encode_variant;

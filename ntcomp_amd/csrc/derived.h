@@ -26,12 +26,15 @@ struct Derived {
     std::vector<uint64_t> pvalid;       // bit j: colex_at[j] != kNoNode
     std::vector<uint64_t> puniq;        // bit j: colex_at[j]'s group is a singleton
     uint64_t n_paths = 0;
+    std::vector<uint32_t> prefix_tab;   // 2 x u32 (l, r) per kPrefixLen-mer, or empty
 };
 
 constexpr uint32_t kNoNode = 0xFFFFFFFFu;
 
 // Builds the path cover (fills has_paths, tlen, ptext, colex_at, pos_of_node).
 void build_paths(const HostIndex &ix, Derived &dv);
+// Intervals of all kPrefixLen-mers (k > kPrefixLen only).
+void build_prefix_table(const HostIndex &ix, Derived &dv, int threads);
 
 // Validates the index and fills rank lines, unique-predecessor bits, pred and code.
 bool build_derived(const HostIndex &ix, Derived &out, std::string &err, int threads);

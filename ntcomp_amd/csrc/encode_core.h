@@ -56,7 +56,11 @@ struct DevIndex {
     const uint32_t *pos_of_node;  // text position of each real node's k-mer, or 0xFFFFFFFF
     const uint64_t *pvalid;       // bit j: colex_at[j] holds a node (encode v3)
     const uint64_t *puniq;        // bit j: that node's (k-1)-suffix group is a singleton
+    const uint2 *prefix_tab;      // interval of every kPrefixLen-mer (key: char t at bits 2t)
+    uint32_t prefix_len;          // kPrefixLen, or 0 = no table (k < 12 or disabled)
 };
+
+constexpr uint32_t kPrefixLen = 11;
 
 // per-read status codes (values of ntc_status)
 enum : int {
@@ -566,6 +570,8 @@ struct Entry {       // 16 bytes, one uint4 store
     uint32_t dk;     // d at p | flag << 8 (SBWT entries) | run << 31
 };
 constexpr uint32_t kRunTag = 0x80000000u;
+constexpr uint32_t kPrefixTag = 0x40000000u;  // positions 0..10 from the prefix table:
+                                              // d = p + 1 <= 11, S never needed (short)
 
 struct LaneScratch3 {
     uint64_t *Q;     // query, 2 bits per base (char t at bits 2(t%32) of word t/32)
@@ -614,7 +620,7 @@ struct EntryView {
     NTC_HD uint32_t dval(const Entry &en, uint32_t x) const {
         const uint32_t d0 = en.dk & 0xFFu;
         const uint32_t d = d0 + (x - en.p);
-        return (en.dk & kRunTag) ? (d < k ? d : k) : d0;
+        return (en.dk & (kRunTag | kPrefixTag)) ? (d < k ? d : k) : d0;
     }
     NTC_HD uint32_t D(uint32_t x) { seek(x); return dval(E[e], x); }
     NTC_HD uint32_t S(uint32_t x) {
@@ -651,7 +657,8 @@ struct EntryView {
     }
 };
 
-NTC_HD int encode_lane3(const DevIndex &ix, const uint8_t *q, uint32_t len, uint32_t rows, LaneScratch3 s) {
+NTC_HD int encode_lane3(const DevIndex &ix, const uint8_t *q, uint32_t len, uint32_t rows, LaneScratch3 s,
+                        bool use_prefix = true) {
     if (len == 0) return -kErrEmptyRead;
     if (len > rows) return -kErrCapacity;
     const uint32_t k = ix.k, tj = ix.t_jump;
@@ -674,6 +681,27 @@ NTC_HD int encode_lane3(const DevIndex &ix, const uint8_t *q, uint32_t len, uint
     uint32_t p = 0, d = 0, l = 0, r = ix.n, j = 0xFFFFFFFFu, ne = 0;
     uint32_t mode = kModeExt, hi = 0, lo = 0, l1 = 0, r1 = 0, cl = 0, cr = 0, bl = 0, bR = 0;
     bool try_run = false;
+    if (use_prefix && ix.prefix_len && len >= kPrefixLen) {
+        // the first 11 extensions from [0, n) in one lookup: if q[0..11] occurs, so do all
+        // its prefixes, hence d = p + 1 for p < 11 (short records only: d <= 11 < k)
+        const uint2 iv = ix.prefix_tab[s.Q[0] & ((1ULL << (2 * kPrefixLen)) - 1)];
+        if (iv.y > iv.x) {
+#ifdef __HIP_DEVICE_COMPILE__
+            *reinterpret_cast<uint4 *>(s.E) = make_uint4(0u, 0xFFFFFFFFu, kPrefixLen, 1u | kPrefixTag);
+#else
+            s.E[0] = Entry{0u, 0xFFFFFFFFu, kPrefixLen, 1u | kPrefixTag};
+#endif
+            ne = 1;
+            p = kPrefixLen;
+            d = kPrefixLen;
+            l = iv.x;
+            r = iv.y;
+            if (ix.has_paths && r == l + 1) {
+                j = ix.pos_of_node[l];
+                try_run = j != 0xFFFFFFFFu;
+            }
+        }
+    }
     while (p < len) {
         if (try_run) {
             // ---- path run: positions p.. follow the path from node at j ----------------

@@ -24,6 +24,7 @@ struct EncodeArgs {
     uint64_t *E;                 // v2: entries (per-lane contiguous, like D and R)
     int variant;                 // 1 = phase-synchronous lanes, 2 = flattened + path walk,
                                  // 3 = run-length entries with word-parallel path runs
+    int exact_ms;                // v3: 1 = no prefix table (diagnostics want S everywhere)
     uint64_t *Q;                 // v3: packed query words
     Entry *E3;                   // v3: entries
 };

@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256) void k_encode3(EncodeArgs a) {
     s.R = a.R + base * 64 + lane * rows;
     int rc;
     if (end < beg || len64 > 0xFFFFFFFFull) rc = -kErrFormat;
-    else rc = encode_lane3(a.ix, a.bases + beg, (uint32_t)len64, (uint32_t)rows, s);
+    else rc = encode_lane3(a.ix, a.bases + beg, (uint32_t)len64, (uint32_t)rows, s, !a.exact_ms);
     if (rc < 0) {
         atomicMin(a.status, (unsigned long long)((gid << 8) | (uint64_t)(-rc)));
         a.rec_count[gid] = 0;

@@ -33,13 +33,14 @@ bool load(const ntc_index_view *v, HostIndex &hx, Derived &dv, std::vector<WalkE
 
 extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const uint64_t *offs, uint64_t n_reads,
                           uint64_t *rec_out, uint64_t cap, uint64_t *rec_offsets, int64_t *bad, uint32_t *d_out,
-                          uint32_t *s_out, int variant, int use_paths) {
+                          uint32_t *s_out, int variant, int use_paths, int use_prefix) {
     HostIndex hx;
     Derived dv;
     std::vector<WalkEntry> walk;
     DevIndex d;
     if (!load(v, hx, dv, walk, d)) return NTC_ERR_FORMAT;
     if (!use_paths) d.has_paths = 0;
+    if (!use_prefix) d.prefix_len = 0;
     *bad = -1;
     uint64_t tiles = (n_reads + 63) / 64, total = 0;
     rec_offsets[0] = 0;

@@ -24,7 +24,7 @@ def emu_lib():
         L = ctypes.CDLL(EMU_SO)
         P, u64 = ctypes.c_void_p, ctypes.c_uint64
         L.emu_encode.restype = ctypes.c_int
-        L.emu_encode.argtypes = [P, P, P, u64, P, u64, P, P, P, P, ctypes.c_int, ctypes.c_int]
+        L.emu_encode.argtypes = [P, P, P, u64, P, u64, P, P, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.emu_decode.restype = ctypes.c_int
         L.emu_decode.argtypes = [P, P, u64, P, u64, P, u64, P]
         _lib = L
@@ -47,7 +47,7 @@ def make_view(n, k, rows, C, lcs):
     return v, keep
 
 
-def emu_encode(n, k, rows, C, lcs, bases, offs, want_ms=False, variant=2, use_paths=True):
+def emu_encode(n, k, rows, C, lcs, bases, offs, want_ms=False, variant=3, use_paths=True, use_prefix=None):
     v, keep = make_view(n, k, rows, C, lcs)
     bases = np.ascontiguousarray(bases, dtype=np.uint8)
     offs = np.ascontiguousarray(offs, dtype=np.uint64)
@@ -59,7 +59,7 @@ def emu_encode(n, k, rows, C, lcs, bases, offs, want_ms=False, variant=2, use_pa
     s = np.zeros(total + 1, dtype=np.uint32)
     rc = emu_lib().emu_encode(ctypes.byref(v), _p(bases), _p(offs), len(offs) - 1, _p(recs), len(recs), _p(roff),
                               ctypes.byref(bad), _p(d) if want_ms else None, _p(s) if want_ms else None,
-                              variant, int(use_paths))
+                              variant, int(use_paths), int((not want_ms) if use_prefix is None else use_prefix))
     if rc:
         raise RuntimeError(f"emu_encode rc={rc} bad={bad.value}")
     out = (recs[: int(roff[-1])], roff)

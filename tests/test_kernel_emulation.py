@@ -89,3 +89,15 @@ def test_emulated_v2_ms_on_repetitive_genome(k):
         od, olo = orc.ms(reads[r * 150:(r + 1) * 150].tobytes())
         assert np.array_equal(d[r * 150:(r + 1) * 150], od)
         assert np.array_equal(s[r * 150:(r + 1) * 150].astype(np.uint64), olo)
+
+
+@pytest.mark.parametrize("k", [12, 31, 91])
+def test_emulated_prefix_table_records_identical(k):
+    genome = nt.synth_genome(300 + k, 80_000)
+    ix = nt.Index.build([genome.tobytes()], k)
+    reads = nt.synth_reads(genome, 3, 0, 1000, 150, 10_000)
+    offs = np.arange(0, 1000 * 150 + 1, 150, dtype=np.uint64)
+    a, ao = emu_encode(ix.n, k, ix.rows, ix.C, ix.lcs, reads, offs, use_prefix=True)
+    b, bo = emu_encode(ix.n, k, ix.rows, ix.C, ix.lcs, reads, offs, use_prefix=False)
+    exp, eoff = OracleIndex(ix.n, k, ix.rows, ix.C, ix.lcs).encode(reads, offs)
+    assert np.array_equal(a, exp) and np.array_equal(b, exp) and np.array_equal(ao, eoff)
