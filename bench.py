@@ -45,7 +45,7 @@ def main():
     ap.add_argument("--genome-bp", type=int, default=5_000_000)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--variant", type=int, default=3, help="encode kernel variant (1, 2 = earlier designs, for A/B)")
+    ap.add_argument("--variant", type=int, default=4, help="encode kernel variant (1, 2 = earlier designs, for A/B)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 

@@ -49,7 +49,10 @@ struct ntc_ctx {
     uint64_t *last_out_offs = nullptr;
     uint64_t last_units = 0;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    int encode_variant = 3;
+    int encode_variant = 4;
+    int last_variant = 0;
+    int num_cus = 0;
+    Enc4Args last4{};
     int exact_ms = 0;       // set only by the diagnostics entry point
     uint64_t n_paths = 0, path_text_len = 0;
 };
@@ -59,7 +62,7 @@ namespace {
 enum WsSlot {
     WS_D = 0, WS_S, WS_F, WS_R, WS_RECCOUNT, WS_SCANTMP, WS_TILEBASE, WS_TILEROWS,
     WS_STAGE_BASES, WS_STAGE_OFFS, WS_STAGE_RECS, WS_E, WS_DEC_A, WS_DEC_B, WS_DEC_C,
-    WS_DEC_D, WS_Q, WS_E3
+    WS_DEC_D, WS_Q, WS_E3, WS_NE, WS_COUNTER
 };
 
 #define HIP_TRY(ctx, expr)                                                                   \
@@ -148,11 +151,64 @@ int alloc_scratch(ntc_ctx *ctx, uint64_t n_reads, uint64_t total_rows, EncodeArg
     return NTC_OK;
 }
 
+// v4: pack -> persistent MS -> parse -> scan -> emit, all in position space.
+// total_bases = offs[n] - offs[0] (known to the caller).
+int encode4_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, uint64_t n_reads,
+                 uint64_t total_bases, uint64_t *d_rec_out, uint64_t cap, uint64_t *d_rec_offs) {
+    Enc4Args a{};
+    a.ix = ctx->dix;
+    a.bases = d_bases;
+    a.offs = d_offs;
+    a.n_reads = n_reads;
+    a.status = ctx->d_status;
+    a.use_prefix = ctx->exact_ms ? 0 : 1;
+    void *p;
+    int rc;
+    if ((rc = ensure(ctx, WS_Q, (total_bases / 32 + n_reads + 4) * 8, &p))) return rc;
+    a.Q = (uint64_t *)p;
+    if ((rc = ensure(ctx, WS_E3, (total_bases + 1) * sizeof(Entry), &p))) return rc;
+    a.E = (Entry *)p;
+    if ((rc = ensure(ctx, WS_NE, (n_reads + 1) * 4, &p))) return rc;
+    a.ne = (uint32_t *)p;
+    if ((rc = ensure(ctx, WS_R, (total_bases + 1) * 8, &p))) return rc;
+    a.R = (uint64_t *)p;
+    if ((rc = ensure(ctx, WS_RECCOUNT, (n_reads + 1) * 4, &p))) return rc;
+    a.rec_count = (uint32_t *)p;
+    if ((rc = ensure(ctx, WS_COUNTER, 64, &p))) return rc;
+    a.counter = (unsigned long long *)p;
+    void *tmp;
+    if ((rc = ensure(ctx, WS_SCANTMP, scan_tmp_words(n_reads + 1) * 8, &tmp))) return rc;
+    HIP_TRY(ctx, hipMemsetAsync(ctx->d_status, 0xFF, 8, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(a.counter, 0, 64, ctx->stream));
+    ctx->last = kEncode;
+    ctx->last_variant = 4;
+    ctx->last_n = n_reads;
+    ctx->last_out_offs = d_rec_offs;
+    ctx->last_units = total_bases;
+    ctx->last4 = a;
+    HIP_TRY(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
+    if (n_reads == 0) {
+        HIP_TRY(ctx, hipMemsetAsync(d_rec_offs, 0, 8, ctx->stream));
+        for (int i = 1; i < 4; i++) HIP_TRY(ctx, hipEventRecord(ctx->ev[i], ctx->stream));
+        return NTC_OK;
+    }
+    static int bpc = 0;
+    if (!bpc) bpc = ms4_blocks_per_cu();
+    launch_encode4(a, (uint32_t)(ctx->num_cus * bpc), ctx->stream, ctx->ev[3], ctx->ev[1]);
+    HIP_TRY(ctx, hipGetLastError());
+    scan_excl_u32(a.rec_count, n_reads, d_rec_offs, (uint64_t *)tmp, ctx->stream);
+    launch_emit4(a, d_rec_offs, d_rec_out, cap, ctx->stream);
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
+    return NTC_OK;
+}
+
 int encode_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, uint64_t n_reads,
                 const Layout &lay, uint64_t *d_rec_out, uint64_t cap, uint64_t *d_rec_offs,
                 uint64_t units) {
     if (!ctx->has_index) return set_err(ctx, NTC_ERR_NO_INDEX, "no index uploaded");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    ctx->last_variant = ctx->encode_variant;
     EncodeArgs a{};
     a.ix = ctx->dix;
     a.bases = d_bases;
@@ -241,9 +297,12 @@ int ntc_ctx_create(int device, ntc_ctx **out) {
             delete ctx;
             return NTC_ERR_HIP;
         }
+    if (hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+        ctx->num_cus <= 0)
+        ctx->num_cus = 256;
     if (const char *v = std::getenv("NTC_ENCODE_VARIANT")) {
         int x = std::atoi(v);
-        if (x >= 1 && x <= 3) ctx->encode_variant = x;
+        if (x >= 1 && x <= 4) ctx->encode_variant = x;
     }
     *out = ctx;
     return NTC_OK;
@@ -388,7 +447,7 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
 int ntc_ctx_set_option(ntc_ctx *ctx, const char *key, int64_t value) {
     if (!ctx || !key) return NTC_ERR_INVALID_ARG;
     if (std::strcmp(key, "encode_variant") == 0) {
-        if (value < 1 || value > 3) return set_err(ctx, NTC_ERR_INVALID_ARG, "encode_variant must be 1, 2 or 3");
+        if (value < 1 || value > 4) return set_err(ctx, NTC_ERR_INVALID_ARG, "encode_variant must be 1..4");
         ctx->encode_variant = (int)value;
         return NTC_OK;
     }
@@ -419,6 +478,23 @@ int ntc_encode_batch_device(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t
     if (!ctx || (!d_read_offsets && n_reads) || !d_rec_offsets_out)
         return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (ctx->encode_variant == 4) {
+        if (!ctx->has_index) return set_err(ctx, NTC_ERR_NO_INDEX, "no index uploaded");
+        uint64_t total = 0;
+        if (n_reads) {
+            if (max_read_len > 0) {
+                total = n_reads * (uint64_t)max_read_len;  // an upper bound is enough
+            } else {
+                uint64_t ends[2] = {0, 0};
+                HIP_TRY(ctx, hipMemcpyAsync(&ends[0], d_read_offsets, 8, hipMemcpyDeviceToHost, ctx->stream));
+                HIP_TRY(ctx, hipMemcpyAsync(&ends[1], d_read_offsets + n_reads, 8, hipMemcpyDeviceToHost, ctx->stream));
+                HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+                total = ends[1] - ends[0];
+            }
+        }
+        return encode4_impl(ctx, d_bases, d_read_offsets, n_reads, total, d_rec_out, rec_capacity,
+                            d_rec_offsets_out);
+    }
     Layout lay;
     const uint64_t tiles = (n_reads + 63) / 64;
     if (max_read_len > 0) {
@@ -487,8 +563,14 @@ int ntc_encode_batch(ntc_ctx *ctx, const uint8_t *bases, const uint64_t *read_of
     Layout lay;
     lay.d_tile_base = (const uint64_t *)d_tb;
     lay.total_rows = tb[tiles];
-    rc = encode_impl(ctx, (const uint8_t *)d_bases, (const uint64_t *)d_offs, n_reads, lay, (uint64_t *)d_recs,
-                     total + 1, (uint64_t *)d_roffs, total);
+    if (ctx->encode_variant == 4) {
+        if (!ctx->has_index) return set_err(ctx, NTC_ERR_NO_INDEX, "no index uploaded");
+        rc = encode4_impl(ctx, (const uint8_t *)d_bases, (const uint64_t *)d_offs, n_reads, total,
+                          (uint64_t *)d_recs, total + 1, (uint64_t *)d_roffs);
+    } else {
+        rc = encode_impl(ctx, (const uint8_t *)d_bases, (const uint64_t *)d_offs, n_reads, lay,
+                         (uint64_t *)d_recs, total + 1, (uint64_t *)d_roffs, total);
+    }
     if (rc) return rc;
     int64_t bad = -1;
     rc = read_status(ctx, &bad);
@@ -615,9 +697,19 @@ int ntc_last_timing(ntc_ctx *ctx, ntc_timing *out) {
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     HIP_TRY(ctx, hipEventSynchronize(ctx->ev[2]));
     float a = 0, b = 0;
+    std::memset(out, 0, sizeof(*out));
+    if (ctx->last == kEncode && ctx->last_variant == 4) {
+        float tot = 0, ms = 0;
+        HIP_TRY(ctx, hipEventElapsedTime(&tot, ctx->ev[0], ctx->ev[2]));
+        HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->ev[3], ctx->ev[1]));
+        out->main_ms = ms;
+        out->aux_ms = (double)tot - (double)ms;
+        out->total_ms = tot;
+        out->units = ctx->last_units;
+        return NTC_OK;
+    }
     HIP_TRY(ctx, hipEventElapsedTime(&a, ctx->ev[0], ctx->ev[1]));
     HIP_TRY(ctx, hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[2]));
-    std::memset(out, 0, sizeof(*out));
     if (ctx->last == kEncode) {
         out->main_ms = a;
         out->aux_ms = b;
@@ -668,6 +760,17 @@ int ntc_debug_matching_statistics(ntc_ctx *ctx, const uint8_t *bases, const uint
     int rc = ntc_encode_batch(ctx, bases, read_offsets, n_reads, recs.data(), total + 1, roffs.data(), &bad);
     ctx->exact_ms = 0;
     if (rc && rc != NTC_ERR_LENGTH) return rc;
+    if (ctx->encode_variant == 4) {
+        void *dd, *ds;
+        if ((rc = ensure(ctx, WS_DEC_A, (total + 1) * 4, &dd))) return rc;
+        if ((rc = ensure(ctx, WS_DEC_B, (total + 1) * 4, &ds))) return rc;
+        launch_debug_gather4(ctx->last4, (uint32_t *)dd, (uint32_t *)ds, ctx->stream);
+        HIP_TRY(ctx, hipGetLastError());
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        HIP_TRY(ctx, hipMemcpy(d_out, dd, total * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(ctx, hipMemcpy(start_out, ds, total * 4, hipMemcpyDeviceToHost));
+        return NTC_OK;
+    }
     DebugArgs g{};
     g.variant = ctx->encode_variant;
     g.E3 = (const Entry *)ctx->ws[WS_E3].p;

@@ -846,6 +846,211 @@ NTC_HD int encode_lane3(const DevIndex &ix, const uint8_t *q, uint32_t len, uint
     return nrec;
 }
 
+// ======================================================================================
+// encode v4: the v3 algorithm split for load balance.
+//   k_pack   : reads -> 2-bit words (read r's words at Qall[(P_r >> 5) + r], P_r = its
+//              first base's position in the batch); validates bases.
+//   k_ms4    : persistent waves; each lane runs MsLane units (one SBWT unit or one path
+//              run per iteration) and, when its read is done, takes the next read from a
+//              wave-local pool refilled by one atomicAdd per 64 reads.  A lane stuck on a
+//              read with many errors no longer holds 63 finished lanes hostage (v3 waves
+//              ran for the max over 64 reads, ~3x the mean).
+//   k_parse4 : one lane per read: right-to-left parse over the entries -> records.
+// Entries and records live in "position space" (read r at [P_r, P_r + len_r)).
+// ======================================================================================
+NTC_HD uint64_t qword_base(uint64_t P, uint64_t r) { return (P >> 5) + r; }
+
+NTC_HD int pack_read(const uint8_t *q, uint32_t len, uint64_t *Q) {
+    if (len == 0) return -kErrEmptyRead;
+    BaseReader br(q);
+    uint64_t acc = 0;
+    for (uint32_t p = 0; p < len; p++) {
+        const int c = base_code((uint8_t)br.get(p));
+        if (c < 0) return -kErrInvalidBase;
+        acc |= (uint64_t)c << (2 * (p & 31));
+        if ((p & 31) == 31) {
+            Q[p >> 5] = acc;
+            acc = 0;
+        }
+    }
+    if (len & 31) Q[len >> 5] = acc;
+    return 0;
+}
+
+NTC_HD void store_entry(Entry *E, uint32_t i, uint32_t p, uint32_t v, uint32_t m, uint32_t dk) {
+#ifdef __HIP_DEVICE_COMPILE__
+    *reinterpret_cast<uint4 *>(E + i) = make_uint4(p, v, m, dk);
+#else
+    E[i] = Entry{p, v, m, dk};
+#endif
+}
+
+struct MsLane {
+    const uint64_t *Q;
+    Entry *E;
+    uint32_t len, p, d, l, r, j, ne, mode, hi, lo, l1, r1, cl, cr, bl, bR;
+    bool try_run;
+
+    NTC_HD void start(const DevIndex &ix, const uint64_t *Q_, Entry *E_, uint32_t len_, bool use_prefix) {
+        Q = Q_;
+        E = E_;
+        len = len_;
+        p = 0; d = 0; l = 0; r = ix.n; j = 0xFFFFFFFFu; ne = 0;
+        mode = kModeExt; hi = lo = l1 = r1 = cl = cr = bl = bR = 0;
+        try_run = false;
+        if (use_prefix && ix.prefix_len && len >= kPrefixLen) {
+            const uint2 iv = ix.prefix_tab[Q[0] & ((1ULL << (2 * kPrefixLen)) - 1)];
+            if (iv.y > iv.x) {
+                store_entry(E, 0, 0u, 0xFFFFFFFFu, kPrefixLen, 1u | kPrefixTag);
+                ne = 1;
+                p = kPrefixLen;
+                d = kPrefixLen;
+                l = iv.x;
+                r = iv.y;
+                note_single(ix);
+            }
+        }
+    }
+    // after a commit: look for the path position of a single-node interval
+    NTC_HD void note_single(const DevIndex &ix) {
+        j = 0xFFFFFFFFu;
+        if (ix.has_paths && r == l + 1 && d >= ix.t_jump) {
+            j = ix.pos_of_node[l];
+            try_run = j != 0xFFFFFFFFu;
+        }
+    }
+    // one unit of work: 1 = read finished, 0 = continue, < 0 = error
+    NTC_HD int step(const DevIndex &ix) {
+        const uint32_t k = ix.k, tj = ix.t_jump;
+        if (p >= len) return 1;
+        if (try_run) {
+            try_run = false;
+            uint32_t m = 0;
+            for (;;) {
+                const uint64_t x = window2(Q, p + m) ^ window2(ix.ptext, j + k + m);
+                uint32_t lim = x ? ctz64(x) >> 1 : 32u;
+                const uint32_t inv = ctz64(~window1(ix.pvalid, j + 1 + m));
+                if (inv < lim) lim = inv;
+                if (len - p - m < lim) lim = len - p - m;
+                m += lim;
+                if (lim < 32) break;
+            }
+            if (m > 0) {
+                store_entry(E, ne++, p, j + 1, m, (d + 1 < k ? d + 1 : k) | kRunTag);
+                p += m;
+                j += m;
+                d = d + m < k ? d + m : k;
+                l = ix.colex_at[j] & 0x7FFFFFFFu;
+                r = l + 1;
+                return p >= len ? 1 : 0;
+            }
+        }
+        const int c = (int)((Q[p >> 5] >> (2 * (p & 31))) & 3u);
+        uint32_t ql = l, qr = r, t = 0;
+        bool wid = true;
+        if (mode == kModeExt) wid = false;
+        else if (mode == kModeP1) t = hi;
+        else if (mode == kModeTj) { ql = l1; qr = r1; t = tj; }
+        else if (mode == kModeBs) { ql = l1; qr = r1; t = (lo + hi) >> 1; }
+        else { ql = cl; qr = cr; t = hi - 1; }
+        if (wid) widen(ix, ql, qr, t);
+        uint32_t el, er;
+        extend(ix, c, ql, qr, el, er);
+        const bool ok = el < er;
+        bool commit = false;
+        uint32_t nl = 0, nr = 0, nd = 0;
+        if (mode == kModeExt) {
+            if (ok) { commit = true; nl = el; nr = er; nd = d + 1 < k ? d + 1 : k; }
+            else if (d == 0) return -kErrInvalidBase;
+            else { hi = d - 1; mode = kModeP1; }
+        } else if (mode == kModeP1) {
+            l1 = ql; r1 = qr;
+            if (ok) { commit = true; nl = el; nr = er; nd = hi + 1; }
+            else if (hi > tj + 1) mode = kModeTj;
+            else if (hi == 0) return -kErrInvalidBase;
+            else { cl = ql; cr = qr; mode = kModeLin; }
+        } else if (mode == kModeTj) {
+            if (ok) {
+                lo = tj; bl = el; bR = er;
+                if (hi - lo > 1) mode = kModeBs;
+                else { commit = true; nl = bl; nr = bR; nd = lo + 1; }
+            } else { hi = tj; cl = ql; cr = qr; mode = kModeLin; }
+        } else if (mode == kModeBs) {
+            if (ok) { lo = t; bl = el; bR = er; } else hi = t;
+            if (hi - lo <= 1) { commit = true; nl = bl; nr = bR; nd = lo + 1; }
+        } else {
+            cl = ql; cr = qr;
+            if (ok) { commit = true; nl = el; nr = er; nd = t + 1; }
+            else if (t == 0) return -kErrInvalidBase;
+            else hi = t;
+        }
+        if (commit) {
+            l = nl; r = nr; d = nd;
+            uint32_t flag = 0;
+            if (d == k) flag = (ix.uniq[l >> 5] >> (l & 31)) & 1u;
+            store_entry(E, ne++, p, l, 1u, d | (flag << 8));
+            p++;
+            mode = kModeExt;
+            note_single(ix);
+            return p >= len ? 1 : 0;
+        }
+        return 0;
+    }
+};
+
+// greedy right-to-left parse over the entries, lib.rs:175-218 (+ encode.rs:144-158)
+NTC_HD int parse_read(const DevIndex &ix, const uint64_t *Q, const Entry *E, uint32_t ne, uint32_t len,
+                      uint64_t *R) {
+    const uint32_t k = ix.k;
+    if (ne == 0) return -kErrFormat;
+    EntryView ev{E, &ix, k, (int32_t)ne - 1};
+    uint32_t i = len;
+    int nrec = 0;
+    while (i > 0) {
+        const uint32_t x = i - 1;
+        const uint32_t di = ev.D(x);
+        const uint32_t segend = i;
+        uint32_t seglen;
+        uint32_t st = 0;
+        if (di > 11 || di == k) st = ev.S(x);
+        if (di == k && i > k + 1) {
+            const uint32_t ext = ev.run_from(i - 2, i - k - 1);
+            const uint32_t L = k + ext;
+            uint32_t m = L, pp = i;
+            for (;;) {  // jump loop lib.rs:193-203
+                const uint32_t dp = ev.D(pp - 1);
+                if (dp < m) {
+                    if (dp >= pp || dp == 0) return -kErrFormat;
+                    m -= dp;
+                    pp -= dp;
+                } else {
+                    break;
+                }
+            }
+            seglen = L - (m - 1);
+            i = pp;
+        } else {
+            seglen = di;
+            if (i > di) i -= di - 1;
+            else i = 0;
+        }
+        if (seglen >= (1u << 24)) return -kErrLength;
+        const uint64_t first = nrec == 0 ? 1u : 0u;
+        uint64_t w;
+        if (seglen > 11) {
+            w = (uint64_t)st | ((uint64_t)(seglen & 0xFFFFFFu) << 32) | (first << 56);
+        } else {
+            const uint64_t bits = window2(Q, segend - seglen);
+            w = (bits & ((1ULL << (2 * seglen)) - 1)) | ((uint64_t)((first + 2) | (seglen << 2)) << 56);
+        }
+        R[nrec] = w;
+        nrec++;
+        if (i > 0) i -= 1;
+        else break;
+    }
+    return nrec;
+}
+
 // Writes the L characters of the L-step inverse walk from node j into out[0..L).
 NTC_HD bool walk_record(const DevIndex &ix, uint32_t j, uint32_t L, uint8_t *out) {
     uint32_t end = L, cur = j;

@@ -29,6 +29,21 @@ struct EncodeArgs {
     Entry *E3;                   // v3: entries
 };
 
+struct Enc4Args {
+    DevIndex ix;
+    const uint8_t *bases;
+    const uint64_t *offs;        // [n_reads+1], absolute into bases
+    uint64_t n_reads;
+    uint64_t *Q;                 // packed reads, read r at Q[(P_r >> 5) + r]
+    Entry *E;                    // entries, position space
+    uint32_t *ne;                // entries per read
+    uint64_t *R;                 // records, position space
+    uint32_t *rec_count;
+    unsigned long long *status;
+    unsigned long long *counter; // work queue head (zeroed per call)
+    int use_prefix;
+};
+
 struct EmitArgs {
     int variant;                 // 1: R is [tile][j][lane]; 2: R is [tile][lane][j]
     const uint64_t *R;
@@ -81,6 +96,12 @@ struct DecWalkArgs {
 };
 
 void launch_encode(const EncodeArgs &a, hipStream_t s);
+void launch_encode4(const Enc4Args &a, uint32_t ms_blocks, hipStream_t s, hipEvent_t ev_ms_begin,
+                    hipEvent_t ev_ms_end);
+void launch_emit4(const Enc4Args &a, const uint64_t *rec_offsets, uint64_t *out, uint64_t capacity,
+                  hipStream_t s);
+int ms4_blocks_per_cu();
+void launch_debug_gather4(const Enc4Args &a, uint32_t *d_out, uint32_t *s_out, hipStream_t s);
 void launch_tile_rows(const uint64_t *offs, uint64_t n_reads, uint32_t *tile_rows, hipStream_t s);
 void launch_emit(const EmitArgs &a, hipStream_t s);
 void launch_debug_gather(const DebugArgs &a, hipStream_t s);

@@ -110,6 +110,105 @@ __global__ __launch_bounds__(256) void k_encode3(EncodeArgs a) {
     }
 }
 
+// ---- v4 ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pack(Enc4Args a) {
+    const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= a.n_reads) return;
+    const uint64_t o0 = a.offs[0], b = a.offs[r], e = a.offs[r + 1];
+    if (e < b || e - b > 0xFFFFFFFFull) {
+        atomicMin(a.status, (unsigned long long)((r << 8) | (uint64_t)kErrFormat));
+        return;
+    }
+    const int rc = pack_read(a.bases + b, (uint32_t)(e - b), a.Q + qword_base(b - o0, r));
+    if (rc < 0) atomicMin(a.status, (unsigned long long)((r << 8) | (uint64_t)(-rc)));
+}
+
+constexpr uint32_t kPoolChunk = 64;
+
+__global__ __launch_bounds__(256) void k_ms4(Enc4Args a) {
+    const uint32_t lane = threadIdx.x & 63;
+    if (*a.status != ~0ull) return;  // a read failed to pack: nothing to do
+    const uint64_t o0 = a.offs[0];
+    uint64_t pool_lo = 0, pool_hi = 0;
+    bool exhausted = false, idle = true;
+    uint64_t rd = 0;
+    MsLane st;
+    for (;;) {
+        // ---- hand idle lanes the next reads (wave-uniform control flow) ----------------
+        const uint64_t want = __ballot(idle);
+        if (want) {
+            if (pool_lo >= pool_hi && !exhausted) {
+                unsigned long long got = 0;
+                if (lane == 0) got = atomicAdd(a.counter, (unsigned long long)kPoolChunk);
+                got = __shfl(got, 0, 64);
+                if (got >= a.n_reads) {
+                    exhausted = true;
+                } else {
+                    pool_lo = got;
+                    pool_hi = got + kPoolChunk < a.n_reads ? got + kPoolChunk : a.n_reads;
+                }
+            }
+            const uint32_t rank = (uint32_t)__popcll(want & ((1ULL << lane) - 1));
+            const uint64_t avail = pool_hi - pool_lo;
+            if (idle && rank < avail) {
+                rd = pool_lo + rank;
+                idle = false;
+                const uint64_t b = a.offs[rd], e = a.offs[rd + 1];
+                const uint64_t P = b - o0;
+                st.start(a.ix, a.Q + qword_base(P, rd), a.E + P, (uint32_t)(e - b), a.use_prefix != 0);
+            }
+            const uint64_t took = (uint64_t)__popcll(want);
+            pool_lo += took < avail ? took : avail;
+        }
+        if (__ballot(!idle) == 0 && exhausted) break;
+        // ---- one unit of work per busy lane --------------------------------------------
+        if (!idle) {
+            const int rc = st.step(a.ix);
+            if (rc != 0) {
+                if (rc < 0) {
+                    atomicMin(a.status, (unsigned long long)((rd << 8) | (uint64_t)(-rc)));
+                    a.ne[rd] = 0;
+                } else {
+                    a.ne[rd] = st.ne;
+                }
+                idle = true;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_parse4(Enc4Args a) {
+    const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= a.n_reads) return;
+    if (*a.status != ~0ull) {
+        a.rec_count[r] = 0;
+        return;
+    }
+    const uint64_t o0 = a.offs[0], b = a.offs[r], e = a.offs[r + 1];
+    const uint64_t P = b - o0;
+    const int rc = parse_read(a.ix, a.Q + qword_base(P, r), a.E + P, a.ne[r], (uint32_t)(e - b), a.R + P);
+    if (rc < 0) {
+        atomicMin(a.status, (unsigned long long)((r << 8) | (uint64_t)(-rc)));
+        a.rec_count[r] = 0;
+    } else {
+        a.rec_count[r] = (uint32_t)rc;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_emit4(Enc4Args a, const uint64_t *rec_offsets, uint64_t *out,
+                                               uint64_t capacity) {
+    const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= a.n_reads) return;
+    const uint32_t cnt = a.rec_count[r];
+    const uint64_t off = rec_offsets[r];
+    if (off + cnt > capacity) {
+        atomicMin(a.status, (unsigned long long)((r << 8) | (uint64_t)kErrCapacity));
+        return;
+    }
+    const uint64_t *src = a.R + (a.offs[r] - a.offs[0]);
+    for (uint32_t j = 0; j < cnt; j++) out[off + j] = src[j];
+}
+
 // rows of scratch a tile of 64 reads needs = longest read, rounded up to 32
 __global__ __launch_bounds__(256) void k_tile_rows(const uint64_t *offs, uint64_t n_reads,
                                                    uint32_t *tile_rows) {
@@ -373,6 +472,48 @@ void launch_encode(const EncodeArgs &a, hipStream_t s) {
     else if (a.variant == 2) hipLaunchKernelGGL(k_encode2, grid_for(a.n_reads), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(k_encode, grid_for(a.n_reads), dim3(256), 0, s, a);
 }
+__global__ __launch_bounds__(256) void k_debug_gather4(Enc4Args a, uint32_t *d_out, uint32_t *s_out) {
+    const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= a.n_reads) return;
+    const uint64_t o0 = a.offs[0], b = a.offs[r], e = a.offs[r + 1];
+    const uint64_t P = b - o0;
+    EntryView ev{a.E + P, &a.ix, a.ix.k, 0};
+    uint32_t p = 0;
+    for (uint32_t i = 0; i < a.ne[r] && p < e - b; i++) {
+        const Entry &en = ev.E[i];
+        for (uint32_t t = 0; t < en.m && p < e - b; t++, p++) {
+            d_out[P + p] = ev.dval(en, p);
+            s_out[P + p] = (en.dk & kRunTag) ? (a.ix.colex_at[en.v + t] & 0x7FFFFFFFu) : en.v;
+        }
+    }
+}
+
+void launch_debug_gather4(const Enc4Args &a, uint32_t *d_out, uint32_t *s_out, hipStream_t s) {
+    hipLaunchKernelGGL(k_debug_gather4, grid_for(a.n_reads), dim3(256), 0, s, a, d_out, s_out);
+}
+
+int ms4_blocks_per_cu() {
+    int blocks = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_ms4, 256, 0) != hipSuccess || blocks <= 0)
+        blocks = 4;
+    return blocks;
+}
+
+void launch_encode4(const Enc4Args &a, uint32_t ms_blocks, hipStream_t s, hipEvent_t ev_ms_begin,
+                    hipEvent_t ev_ms_end) {
+    hipLaunchKernelGGL(k_pack, grid_for(a.n_reads), dim3(256), 0, s, a);
+    (void)hipEventRecord(ev_ms_begin, s);
+    const uint64_t need = (a.n_reads + 255) / 256;
+    hipLaunchKernelGGL(k_ms4, dim3(need < ms_blocks ? (uint32_t)need : ms_blocks), dim3(256), 0, s, a);
+    (void)hipEventRecord(ev_ms_end, s);
+    hipLaunchKernelGGL(k_parse4, grid_for(a.n_reads), dim3(256), 0, s, a);
+}
+
+void launch_emit4(const Enc4Args &a, const uint64_t *rec_offsets, uint64_t *out, uint64_t capacity,
+                  hipStream_t s) {
+    hipLaunchKernelGGL(k_emit4, grid_for(a.n_reads), dim3(256), 0, s, a, rec_offsets, out, capacity);
+}
+
 void launch_tile_rows(const uint64_t *offs, uint64_t n_reads, uint32_t *tile_rows, hipStream_t s) {
     uint64_t threads = ((n_reads + 63) / 64) * 64;
     hipLaunchKernelGGL(k_tile_rows, grid_for(threads), dim3(256), 0, s, offs, n_reads, tile_rows);

@@ -56,7 +56,43 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
             uint32_t lane = (uint32_t)(r & 63);
             uint32_t len = (uint32_t)(offs[r + 1] - offs[r]);
             int rc;
-            if (variant == 3) {
+            if (variant == 4) {
+                std::vector<uint64_t> Q(len / 32 + 3, 0);
+                std::vector<Entry> E4(len + 1);
+                std::vector<uint64_t> R4(len + 1);
+                rc = pack_read(bases + offs[r], len, Q.data());
+                MsLane ms;
+                uint32_t ne = 0;
+                if (rc == 0) {
+                    ms.start(d, Q.data(), E4.data(), len, use_prefix != 0);
+                    for (;;) {
+                        int st = ms.step(d);
+                        if (st < 0) { rc = st; break; }
+                        if (st == 1) break;
+                    }
+                    ne = ms.ne;
+                }
+                if (rc == 0) rc = parse_read(d, Q.data(), E4.data(), ne, len, R4.data());
+                if (d_out && rc >= 0) {
+                    uint32_t p = 0;
+                    EntryView ev{E4.data(), &d, d.k, 0};
+                    for (uint32_t ei = 0; ei < ne && p < len; ei++) {
+                        const Entry &en = E4[ei];
+                        for (uint32_t t = 0; t < en.m && p < len; t++, p++) {
+                            d_out[offs[r] - offs[0] + p] = ev.dval(en, p);
+                            s_out[offs[r] - offs[0] + p] =
+                                (en.dk & kRunTag) ? (d.colex_at[en.v + t] & 0x7FFFFFFFu) : en.v;
+                        }
+                    }
+                }
+                if (rc >= 0) {
+                    if (total + (uint64_t)rc > cap) return NTC_ERR_CAPACITY;
+                    for (int jj = 0; jj < rc; jj++) rec_out[total + jj] = R4[jj];
+                    total += (uint64_t)rc;
+                    rec_offsets[r + 1] = total;
+                    continue;
+                }
+            } else if (variant == 3) {
                 std::vector<uint64_t> Q(rows / 32 + 2);
                 std::vector<Entry> E3(rows + 1);
                 std::vector<uint64_t> R3(rows + 1);

@@ -47,7 +47,7 @@ def make_view(n, k, rows, C, lcs):
     return v, keep
 
 
-def emu_encode(n, k, rows, C, lcs, bases, offs, want_ms=False, variant=3, use_paths=True, use_prefix=None):
+def emu_encode(n, k, rows, C, lcs, bases, offs, want_ms=False, variant=4, use_paths=True, use_prefix=None):
     v, keep = make_view(n, k, rows, C, lcs)
     bases = np.ascontiguousarray(bases, dtype=np.uint8)
     offs = np.ascontiguousarray(offs, dtype=np.uint64)
