@@ -164,7 +164,7 @@ int encode4_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, u
     a.use_prefix = ctx->exact_ms ? 0 : 1;
     void *p;
     int rc;
-    if ((rc = ensure(ctx, WS_Q, (total_bases / 32 + n_reads + 4) * 8, &p))) return rc;
+    if ((rc = ensure(ctx, WS_Q, (total_bases / 32 + 4) * 8, &p))) return rc;
     a.Q = (uint64_t *)p;
     if ((rc = ensure(ctx, WS_E3, (total_bases + 1) * sizeof(Entry), &p))) return rc;
     a.E = (Entry *)p;
@@ -194,7 +194,7 @@ int encode4_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, u
     }
     static int bpc = 0;
     if (!bpc) bpc = ms4_blocks_per_cu();
-    launch_encode4(a, (uint32_t)(ctx->num_cus * bpc), ctx->stream, ctx->ev[3], ctx->ev[1]);
+    launch_encode4(a, total_bases, (uint32_t)(ctx->num_cus * bpc), ctx->stream, ctx->ev[3], ctx->ev[1]);
     HIP_TRY(ctx, hipGetLastError());
     scan_excl_u32(a.rec_count, n_reads, d_rec_offs, (uint64_t *)tmp, ctx->stream);
     launch_emit4(a, d_rec_offs, d_rec_out, cap, ctx->stream);

@@ -580,8 +580,9 @@ struct LaneScratch3 {
 };
 
 // 32 two-bit characters starting at character offset off of a packed array
-NTC_HD uint64_t window2(const uint64_t *w, uint32_t off) {
-    const uint32_t i = off >> 5, sh = (off & 31) * 2;
+NTC_HD uint64_t window2(const uint64_t *w, uint64_t off) {
+    const uint64_t i = off >> 5;
+    const uint32_t sh = (uint32_t)(off & 31) * 2;
     const uint64_t a = w[i];
     return sh ? ((a >> sh) | (w[i + 1] << (64 - sh))) : a;
 }
@@ -614,8 +615,14 @@ struct EntryView {
     const DevIndex *ix;
     uint32_t k;
     int32_t e;  // cursor
-    NTC_HD void seek(uint32_t x) {  // entries never move right of x; x >= E[0].p = 0
-        while (e > 0 && E[e].p > x) e--;
+    NTC_HD void seek(uint32_t x) {  // last entry with p <= x (E[0].p = 0); cursor moves left
+        uint32_t pe = E[e].p;
+        if (pe <= x) return;
+        // every entry covers >= 1 position, so entry e - (pe - x) starts at or before x
+        int32_t g = e - (int32_t)(pe - x);
+        if (g < 0) g = 0;
+        while (g + 1 < e && E[g + 1].p <= x) g++;
+        e = g;
     }
     NTC_HD uint32_t dval(const Entry &en, uint32_t x) const {
         const uint32_t d0 = en.dk & 0xFFu;
@@ -877,6 +884,10 @@ NTC_HD int pack_read(const uint8_t *q, uint32_t len, uint64_t *Q) {
     return 0;
 }
 
+// 2-bit code of an ASCII base: ((b >> 1) ^ (b >> 2)) & 3 maps A,C,G,T to 0,1,2,3
+NTC_HD uint32_t fast_code(uint32_t b) { return ((b >> 1) ^ (b >> 2)) & 3u; }
+NTC_HD bool is_acgt(uint32_t b) { return b == 'A' || b == 'C' || b == 'G' || b == 'T'; }
+
 NTC_HD void store_entry(Entry *E, uint32_t i, uint32_t p, uint32_t v, uint32_t m, uint32_t dk) {
 #ifdef __HIP_DEVICE_COMPILE__
     *reinterpret_cast<uint4 *>(E + i) = make_uint4(p, v, m, dk);
@@ -885,21 +896,38 @@ NTC_HD void store_entry(Entry *E, uint32_t i, uint32_t p, uint32_t v, uint32_t m
 #endif
 }
 
+#if defined(NTC_STATS) && !defined(__HIP_DEVICE_COMPILE__)
+extern uint64_t ntc_stats[16];  // host emulation only: unit counts by kind
+#define NTC_STAT(i) (ntc_stats[i]++)
+inline void ntc_stat_add(int i, uint64_t v) { ntc_stats[i] += v; }
+#else
+#define NTC_STAT(i) ((void)0)
+NTC_HD void ntc_stat_add(int, uint64_t) {}
+#endif
+
 struct MsLane {
-    const uint64_t *Q;
+    const uint64_t *Q;  // packed query stream; this read starts at character qo
     Entry *E;
+    uint64_t qo;
     uint32_t len, p, d, l, r, j, ne, mode, hi, lo, l1, r1, cl, cr, bl, bR;
     bool try_run;
 
-    NTC_HD void start(const DevIndex &ix, const uint64_t *Q_, Entry *E_, uint32_t len_, bool use_prefix) {
+    NTC_HD uint32_t qchar(uint32_t x) const {
+        const uint64_t a = qo + x;
+        return (uint32_t)(Q[a >> 5] >> (2 * (a & 31))) & 3u;
+    }
+
+    NTC_HD void start(const DevIndex &ix, const uint64_t *Q_, uint64_t qo_, Entry *E_, uint32_t len_,
+                      bool use_prefix) {
         Q = Q_;
+        qo = qo_;
         E = E_;
         len = len_;
         p = 0; d = 0; l = 0; r = ix.n; j = 0xFFFFFFFFu; ne = 0;
         mode = kModeExt; hi = lo = l1 = r1 = cl = cr = bl = bR = 0;
         try_run = false;
         if (use_prefix && ix.prefix_len && len >= kPrefixLen) {
-            const uint2 iv = ix.prefix_tab[Q[0] & ((1ULL << (2 * kPrefixLen)) - 1)];
+            const uint2 iv = ix.prefix_tab[window2(Q, qo) & ((1ULL << (2 * kPrefixLen)) - 1)];
             if (iv.y > iv.x) {
                 store_entry(E, 0, 0u, 0xFFFFFFFFu, kPrefixLen, 1u | kPrefixTag);
                 ne = 1;
@@ -926,8 +954,10 @@ struct MsLane {
         if (try_run) {
             try_run = false;
             uint32_t m = 0;
+            NTC_STAT(0);
             for (;;) {
-                const uint64_t x = window2(Q, p + m) ^ window2(ix.ptext, j + k + m);
+                NTC_STAT(1);
+                const uint64_t x = window2(Q, qo + p + m) ^ window2(ix.ptext, j + k + m);
                 uint32_t lim = x ? ctz64(x) >> 1 : 32u;
                 const uint32_t inv = ctz64(~window1(ix.pvalid, j + 1 + m));
                 if (inv < lim) lim = inv;
@@ -936,6 +966,8 @@ struct MsLane {
                 if (lim < 32) break;
             }
             if (m > 0) {
+                NTC_STAT(2);
+                ntc_stat_add(3, m);
                 store_entry(E, ne++, p, j + 1, m, (d + 1 < k ? d + 1 : k) | kRunTag);
                 p += m;
                 j += m;
@@ -945,7 +977,8 @@ struct MsLane {
                 return p >= len ? 1 : 0;
             }
         }
-        const int c = (int)((Q[p >> 5] >> (2 * (p & 31))) & 3u);
+        const int c = (int)qchar(p);
+        NTC_STAT(4 + mode);
         uint32_t ql = l, qr = r, t = 0;
         bool wid = true;
         if (mode == kModeExt) wid = false;
@@ -999,8 +1032,8 @@ struct MsLane {
 };
 
 // greedy right-to-left parse over the entries, lib.rs:175-218 (+ encode.rs:144-158)
-NTC_HD int parse_read(const DevIndex &ix, const uint64_t *Q, const Entry *E, uint32_t ne, uint32_t len,
-                      uint64_t *R) {
+NTC_HD int parse_read(const DevIndex &ix, const uint64_t *Q, uint64_t qo, const Entry *E, uint32_t ne,
+                      uint32_t len, uint64_t *R) {
     const uint32_t k = ix.k;
     if (ne == 0) return -kErrFormat;
     EntryView ev{E, &ix, k, (int32_t)ne - 1};
@@ -1040,7 +1073,7 @@ NTC_HD int parse_read(const DevIndex &ix, const uint64_t *Q, const Entry *E, uin
         if (seglen > 11) {
             w = (uint64_t)st | ((uint64_t)(seglen & 0xFFFFFFu) << 32) | (first << 56);
         } else {
-            const uint64_t bits = window2(Q, segend - seglen);
+            const uint64_t bits = window2(Q, qo + segend - seglen);
             w = (bits & ((1ULL << (2 * seglen)) - 1)) | ((uint64_t)((first + 2) | (seglen << 2)) << 56);
         }
         R[nrec] = w;

@@ -34,7 +34,7 @@ struct Enc4Args {
     const uint8_t *bases;
     const uint64_t *offs;        // [n_reads+1], absolute into bases
     uint64_t n_reads;
-    uint64_t *Q;                 // packed reads, read r at Q[(P_r >> 5) + r]
+    uint64_t *Q;                 // packed bases, position space (2 bits, 32 per word)
     Entry *E;                    // entries, position space
     uint32_t *ne;                // entries per read
     uint64_t *R;                 // records, position space
@@ -96,8 +96,8 @@ struct DecWalkArgs {
 };
 
 void launch_encode(const EncodeArgs &a, hipStream_t s);
-void launch_encode4(const Enc4Args &a, uint32_t ms_blocks, hipStream_t s, hipEvent_t ev_ms_begin,
-                    hipEvent_t ev_ms_end);
+void launch_encode4(const Enc4Args &a, uint64_t total, uint32_t ms_blocks, hipStream_t s,
+                    hipEvent_t ev_ms_begin, hipEvent_t ev_ms_end);
 void launch_emit4(const Enc4Args &a, const uint64_t *rec_offsets, uint64_t *out, uint64_t capacity,
                   hipStream_t s);
 int ms4_blocks_per_cu();

@@ -111,16 +111,60 @@ __global__ __launch_bounds__(256) void k_encode3(EncodeArgs a) {
 }
 
 // ---- v4 ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_pack(Enc4Args a) {
-    const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (r >= a.n_reads) return;
-    const uint64_t o0 = a.offs[0], b = a.offs[r], e = a.offs[r + 1];
-    if (e < b || e - b > 0xFFFFFFFFull) {
-        atomicMin(a.status, (unsigned long long)((r << 8) | (uint64_t)kErrFormat));
-        return;
+// pack the batch's bases (position space: character x = batch position x) 32 per thread:
+// consecutive threads read consecutive 32-byte chunks (coalesced); bad bytes report the
+// read that holds them.
+__global__ __launch_bounds__(256) void k_pack(Enc4Args a, uint64_t total) {
+    const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t x0 = b * 32;
+    if (x0 >= total) return;
+    const uint8_t *B = a.bases + a.offs[0];
+    const uint8_t *end = B + total;
+    const uint8_t *p = B + x0;
+    const uintptr_t al = (uintptr_t)p & ~(uintptr_t)15;
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 15);
+    uint32_t w[12];
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        const uint8_t *blk = (const uint8_t *)(al + 16 * q);
+        if (blk < end) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(blk);
+            w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+        } else {
+            w[4 * q] = w[4 * q + 1] = w[4 * q + 2] = w[4 * q + 3] = 0x41414141u;
+        }
     }
-    const int rc = pack_read(a.bases + b, (uint32_t)(e - b), a.Q + qword_base(b - o0, r));
-    if (rc < 0) atomicMin(a.status, (unsigned long long)((r << 8) | (uint64_t)(-rc)));
+    const uint32_t n = total - x0 < 32 ? (uint32_t)(total - x0) : 32u;
+    uint64_t acc = 0;
+    bool bad = false;
+#pragma unroll
+    for (uint32_t t = 0; t < 32; t++) {
+        const uint32_t o = sh + t;  // byte index into w (static after unrolling but sh)
+        const uint32_t word = o >> 2;
+        uint32_t wv = w[0];
+#pragma unroll
+        for (uint32_t q = 1; q < 12; q++) wv = (word == q) ? w[q] : wv;
+        const uint32_t ch = (wv >> (8 * (o & 3))) & 0xFFu;
+        if (t < n) {
+            bad |= !is_acgt(ch);
+            acc |= (uint64_t)fast_code(ch) << (2 * t);
+        }
+    }
+    a.Q[b] = acc;
+    if (bad) {
+        for (uint32_t t = 0; t < n; t++) {
+            if (!is_acgt(B[x0 + t])) {  // the read holding the first bad byte
+                uint64_t lo = 0, hi = a.n_reads;
+                const uint64_t pos = a.offs[0] + x0 + t;
+                while (hi - lo > 1) {
+                    const uint64_t mid = (lo + hi) >> 1;
+                    if (a.offs[mid] <= pos) lo = mid; else hi = mid;
+                }
+                atomicMin(a.status, (unsigned long long)((lo << 8) | (uint64_t)kErrInvalidBase));
+                break;
+            }
+        }
+    }
 }
 
 constexpr uint32_t kPoolChunk = 64;
@@ -155,7 +199,12 @@ __global__ __launch_bounds__(256) void k_ms4(Enc4Args a) {
                 idle = false;
                 const uint64_t b = a.offs[rd], e = a.offs[rd + 1];
                 const uint64_t P = b - o0;
-                st.start(a.ix, a.Q + qword_base(P, rd), a.E + P, (uint32_t)(e - b), a.use_prefix != 0);
+                st.start(a.ix, a.Q, P, a.E + P, (uint32_t)(e - b), a.use_prefix != 0);
+                if (e <= b) {  // empty read (EncodeError, encode.rs:133-135) or bad offsets
+                    atomicMin(a.status, (unsigned long long)((rd << 8) | (uint64_t)(e == b ? kErrEmptyRead : kErrFormat)));
+                    a.ne[rd] = 0;
+                    idle = true;
+                }
             }
             const uint64_t took = (uint64_t)__popcll(want);
             pool_lo += took < avail ? took : avail;
@@ -186,7 +235,7 @@ __global__ __launch_bounds__(256) void k_parse4(Enc4Args a) {
     }
     const uint64_t o0 = a.offs[0], b = a.offs[r], e = a.offs[r + 1];
     const uint64_t P = b - o0;
-    const int rc = parse_read(a.ix, a.Q + qword_base(P, r), a.E + P, a.ne[r], (uint32_t)(e - b), a.R + P);
+    const int rc = parse_read(a.ix, a.Q, P, a.E + P, a.ne[r], (uint32_t)(e - b), a.R + P);
     if (rc < 0) {
         atomicMin(a.status, (unsigned long long)((r << 8) | (uint64_t)(-rc)));
         a.rec_count[r] = 0;
@@ -499,9 +548,9 @@ int ms4_blocks_per_cu() {
     return blocks;
 }
 
-void launch_encode4(const Enc4Args &a, uint32_t ms_blocks, hipStream_t s, hipEvent_t ev_ms_begin,
+void launch_encode4(const Enc4Args &a, uint64_t total, uint32_t ms_blocks, hipStream_t s, hipEvent_t ev_ms_begin,
                     hipEvent_t ev_ms_end) {
-    hipLaunchKernelGGL(k_pack, grid_for(a.n_reads), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_pack, grid_for((total + 31) / 32), dim3(256), 0, s, a, total);
     (void)hipEventRecord(ev_ms_begin, s);
     const uint64_t need = (a.n_reads + 255) / 256;
     hipLaunchKernelGGL(k_ms4, dim3(need < ms_blocks ? (uint32_t)need : ms_blocks), dim3(256), 0, s, a);

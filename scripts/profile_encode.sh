@@ -7,7 +7,7 @@ set -u
 OUT=${OUT:-gpurun_out/prof}
 MODE=${MODE:-encode}
 BENCH="bench.py --mode $MODE"
-KRE=${KRE:-'k_encode|k_dec_walk'}
+KRE=${KRE:-'k_encode|k_ms4|k_parse4|k_pack|k_emit4|k_dec_walk'}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 run() {  # name, limit, rocprof args...
@@ -19,11 +19,13 @@ run() {  # name, limit, rocprof args...
   echo "=== $name rc=$rc" >&2
   if [ $rc -ne 0 ]; then tail -20 "$OUT/$name.stderr" >&2; exit $rc; fi
 }
-run kt 420 --kernel-trace --stats
+PASSES=${PASSES:-"kt fetch write tcc sq grbm"}
+has() { case " $PASSES " in *" $1 "*) return 0;; esac; return 1; }
+has kt && run kt 420 --kernel-trace --stats
 BENCH_ARGS="--no-cpu --steps 2 --warmup 0"
-run pmc_fetch 300 --kernel-include-regex "$KRE" --pmc FETCH_SIZE
-run pmc_write 300 --kernel-include-regex "$KRE" --pmc WRITE_SIZE
-run pmc_tcc 300 --kernel-include-regex "$KRE" --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum
-run pmc_sq 300 --kernel-include-regex "$KRE" --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU
-run pmc_grbm 300 --kernel-include-regex "$KRE" --pmc GRBM_GUI_ACTIVE GRBM_COUNT
+has fetch && run pmc_fetch 300 --kernel-include-regex "$KRE" --pmc FETCH_SIZE
+has write && run pmc_write 300 --kernel-include-regex "$KRE" --pmc WRITE_SIZE
+has tcc && run pmc_tcc 300 --kernel-include-regex "$KRE" --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum
+has sq && run pmc_sq 300 --kernel-include-regex "$KRE" --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU
+has grbm && run pmc_grbm 300 --kernel-include-regex "$KRE" --pmc GRBM_GUI_ACTIVE GRBM_COUNT
 echo done >&2

@@ -64,7 +64,7 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
                 MsLane ms;
                 uint32_t ne = 0;
                 if (rc == 0) {
-                    ms.start(d, Q.data(), E4.data(), len, use_prefix != 0);
+                    ms.start(d, Q.data(), 0, E4.data(), len, use_prefix != 0);
                     for (;;) {
                         int st = ms.step(d);
                         if (st < 0) { rc = st; break; }
@@ -72,7 +72,7 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
                     }
                     ne = ms.ne;
                 }
-                if (rc == 0) rc = parse_read(d, Q.data(), E4.data(), ne, len, R4.data());
+                if (rc == 0) rc = parse_read(d, Q.data(), 0, E4.data(), ne, len, R4.data());
                 if (d_out && rc >= 0) {
                     uint32_t p = 0;
                     EntryView ev{E4.data(), &d, d.k, 0};
