@@ -88,8 +88,9 @@ const char *ntc_last_error(const ntc_ctx *ctx);
 /* Optional: launch on a caller-owned hipStream_t (passed as void*); NULL = own stream. */
 int ntc_ctx_set_stream(ntc_ctx *ctx, void *hip_stream);
 int ntc_ctx_synchronize(ntc_ctx *ctx);
-/* Tuning / diagnostics.  "encode_variant": 2 (default: flattened lanes + path walk) or 1
- * (phase-synchronous lanes; kept for A/B measurement).  Read-only: "n_paths",
+/* Tuning / diagnostics.  "encode_variant": 4 (default: packed bases, persistent MS kernel
+ * with dynamic read assignment, path runs, speculative contraction, separate parse) or 1
+ * (the first design: phase-synchronous lanes, kept for A/B).  Read-only: "n_paths",
  * "path_text_len" (the path cover built at upload).  Env NTC_ENCODE_VARIANT sets the
  * default at ntc_ctx_create.                                                          */
 int ntc_ctx_set_option(ntc_ctx *ctx, const char *key, int64_t value);

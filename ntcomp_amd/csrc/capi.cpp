@@ -120,28 +120,10 @@ int alloc_scratch(ntc_ctx *ctx, uint64_t n_reads, uint64_t total_rows, EncodeArg
     void *p;
     int rc;
     const uint64_t slots = total_rows * 64;
-    if (a.variant == 3) {
-        const uint64_t tiles = (n_reads + 63) / 64;
-        if ((rc = ensure(ctx, WS_Q, (total_rows / 32 + 2 * tiles + 2) * 64 * 8, &p))) return rc;
-        a.Q = (uint64_t *)p;
-        if ((rc = ensure(ctx, WS_E3, slots * sizeof(Entry), &p))) return rc;
-        a.E3 = (Entry *)p;
-        if ((rc = ensure(ctx, WS_R, slots * 8, &p))) return rc;
-        a.R = (uint64_t *)p;
-        if ((rc = ensure(ctx, WS_RECCOUNT, (n_reads + 1) * 4, &p))) return rc;
-        a.rec_count = (uint32_t *)p;
-        return NTC_OK;
-    }
     if ((rc = ensure(ctx, WS_D, slots, &p))) return rc;
     a.D = (uint8_t *)p;
-    if (a.variant == 2) {
-        if ((rc = ensure(ctx, WS_E, slots * 8, &p))) return rc;
-        a.E = (uint64_t *)p;
-        a.S = nullptr;
-    } else {
-        if ((rc = ensure(ctx, WS_S, slots * 4, &p))) return rc;
-        a.S = (uint32_t *)p;
-    }
+    if ((rc = ensure(ctx, WS_S, slots * 4, &p))) return rc;
+    a.S = (uint32_t *)p;
     if ((rc = ensure(ctx, WS_F, (total_rows / 32 + 1) * 64 * 4, &p))) return rc;
     a.F = (uint32_t *)p;
     if ((rc = ensure(ctx, WS_R, slots * 8, &p))) return rc;
@@ -217,8 +199,6 @@ int encode_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, ui
     a.tile_base = lay.d_tile_base;
     a.rows_uniform = lay.rows_uniform;
     a.status = ctx->d_status;
-    a.variant = ctx->encode_variant;
-    a.exact_ms = ctx->exact_ms;
     int rc = alloc_scratch(ctx, n_reads, lay.total_rows, a);
     if (rc) return rc;
     void *tmp;
@@ -239,7 +219,6 @@ int encode_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, ui
     HIP_TRY(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
     scan_excl_u32(a.rec_count, n_reads, d_rec_offs, (uint64_t *)tmp, ctx->stream);
     EmitArgs e{};
-    e.variant = a.variant;
     e.R = a.R;
     e.tile_base = lay.d_tile_base;
     e.rows_uniform = lay.rows_uniform;
@@ -302,7 +281,7 @@ int ntc_ctx_create(int device, ntc_ctx **out) {
         ctx->num_cus = 256;
     if (const char *v = std::getenv("NTC_ENCODE_VARIANT")) {
         int x = std::atoi(v);
-        if (x >= 1 && x <= 4) ctx->encode_variant = x;
+        if (x == 1 || x == 4) ctx->encode_variant = x;
     }
     *out = ctx;
     return NTC_OK;
@@ -447,7 +426,8 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
 int ntc_ctx_set_option(ntc_ctx *ctx, const char *key, int64_t value) {
     if (!ctx || !key) return NTC_ERR_INVALID_ARG;
     if (std::strcmp(key, "encode_variant") == 0) {
-        if (value < 1 || value > 4) return set_err(ctx, NTC_ERR_INVALID_ARG, "encode_variant must be 1..4");
+        if (value != 1 && value != 4)
+            return set_err(ctx, NTC_ERR_INVALID_ARG, "encode_variant must be 4 (default) or 1 (A/B baseline)");
         ctx->encode_variant = (int)value;
         return NTC_OK;
     }
@@ -772,10 +752,6 @@ int ntc_debug_matching_statistics(ntc_ctx *ctx, const uint8_t *bases, const uint
         return NTC_OK;
     }
     DebugArgs g{};
-    g.variant = ctx->encode_variant;
-    g.E3 = (const Entry *)ctx->ws[WS_E3].p;
-    g.E = (const uint64_t *)ctx->ws[WS_E].p;
-    g.ix = ctx->dix;
     g.D = (const uint8_t *)ctx->ws[WS_D].p;
     g.S = (const uint32_t *)ctx->ws[WS_S].p;
     g.tile_base = (const uint64_t *)ctx->ws[WS_TILEBASE].p;

@@ -20,6 +20,15 @@
 
 namespace ntc {
 
+#if defined(NTC_STATS) && !defined(__HIP_DEVICE_COMPILE__)
+extern uint64_t ntc_stats[16];  // host emulation only: unit counts by kind
+#define NTC_STAT(i) (ntc_stats[i]++)
+inline void ntc_stat_add(int i, uint64_t v) { ntc_stats[i] += v; }
+#else
+#define NTC_STAT(i) ((void)0)
+NTC_HD void ntc_stat_add(int, uint64_t) {}
+#endif
+
 constexpr uint32_t kRankBlock = 448;  // positions per 64-byte rank line (7 x u64)
 
 // One row's rank line: the row's ones before the line + 448 bits of the row.  A rank is
@@ -139,6 +148,52 @@ NTC_HD void extend(const DevIndex &ix, int c, uint32_t l, uint32_t r, uint32_t &
     nl = ix.C[c] + rl;
     nr = ix.C[c] + rr;
 }
+
+// extend_right keeping the rank line(s) it loaded (A = line of l, B = line of r)
+NTC_HD void extend_keep(const DevIndex &ix, int c, uint32_t l, uint32_t r, uint32_t &nl, uint32_t &nr,
+                        LineRegs &A, LineRegs &B, uint32_t &li, uint32_t &ri) {
+    const RankLine *rows = ix.lines + (uint64_t)c * ix.nlines;
+    li = l / kRankBlock;
+    ri = r / kRankBlock;
+    load_line(rows + li, A);
+    nl = ix.C[c] + rank_in(A, l - li * kRankBlock);
+    if (ri == li) {
+        nr = ix.C[c] + rank_in(A, r - li * kRankBlock);
+    } else {
+        load_line(rows + ri, B);
+        nr = ix.C[c] + rank_in(B, r - ri * kRankBlock);
+    }
+}
+
+// 16 LCS bytes [base, base + 16) as 4 words (base 8-aligned; zeros below index 0)
+struct LcsWin {
+    int64_t base;
+    uint32_t w0, w1, w2, w3;
+    NTC_HD void load(const uint8_t *lcs, int64_t b) {
+        base = b;
+#ifdef __HIP_DEVICE_COMPILE__
+        uint2 lo = make_uint2(0, 0), hi;
+        if (b >= 0) lo = *reinterpret_cast<const uint2 *>(lcs + b);
+        hi = *reinterpret_cast<const uint2 *>(lcs + b + 8);
+        w0 = lo.x; w1 = lo.y; w2 = hi.x; w3 = hi.y;
+#else
+        const uint32_t *q = reinterpret_cast<const uint32_t *>(lcs + b + 8);
+        if (b >= 0) {
+            const uint32_t *p = reinterpret_cast<const uint32_t *>(lcs + b);
+            w0 = p[0]; w1 = p[1];
+        } else {
+            w0 = w1 = 0;
+        }
+        w2 = q[0]; w3 = q[1];
+#endif
+    }
+    NTC_HD bool has(int64_t x) const { return x >= base && x < base + 16; }
+    NTC_HD uint32_t at(int64_t x) const {
+        const uint32_t o = (uint32_t)(x - base);
+        const uint32_t w = (o & 8) ? ((o & 4) ? w3 : w2) : ((o & 4) ? w1 : w0);
+        return (w >> ((o & 3) * 8)) & 0xFFu;
+    }
+};
 
 // contract_left(I, t) [ext sbwt]: widen I to all nodes sharing the last t characters.
 NTC_HD void widen(const DevIndex &ix, uint32_t &l, uint32_t &r, uint32_t t) {
@@ -326,29 +381,8 @@ NTC_HD int encode_lane(const DevIndex &ix, const uint8_t *q, uint32_t len, uint3
 }
 
 // ======================================================================================
-// encode v2: one read per lane, the whole read in ONE flattened loop.  Every iteration a
-// lane does exactly one unit of work -- a path step, an extension, or one contraction
-// probe -- so lanes of a wave never wait for each other's contraction loops (v1 spent
-// ~7x its instructions on that divergence, profiles/round1).
-//
-// Path step: when the matching-statistics interval is ONE node z (always so at d = k;
-// at d < k the node z is then also group-first, so its labels are its out-edges) and z
-// sits at text position j of the path cover with the next path character equal to the
-// query character c, extend_right([z, z+1), c) is exactly the next path node: the
-// node z[1..k].c (for d = k via the contraction to z's group and back, which yields the
-// same node and d = k).  Such steps read the path arrays sequentially instead of a
-// random rank line.  Any other case runs the SBWT step of ms_step (same probes).
+// shared by the flattened encoders
 // ======================================================================================
-constexpr uint32_t kFastTag = 0x80000000u;
-
-struct LaneScratch2 {
-    uint8_t *D;   // D[p], per-read contiguous, 16-byte aligned
-    uint32_t *F;  // F[p / 32]
-    uint64_t *E;  // (p << 32 | node) for an SBWT-step position, (p << 32 | j | kFastTag)
-                  // where a run of path steps starts at text position j
-    uint64_t *R;  // records
-};
-
 struct BaseReader {
     const uint8_t *q;
     uint64_t blk;
@@ -373,188 +407,10 @@ struct BaseReader {
 };
 
 enum : uint32_t { kModeExt = 0, kModeP1 = 1, kModeTj = 2, kModeBs = 3, kModeLin = 4 };
-
-NTC_HD int encode_lane2(const DevIndex &ix, const uint8_t *q, uint32_t len, uint32_t rows, LaneScratch2 s) {
-    if (len == 0) return -kErrEmptyRead;
-    if (len > rows) return -kErrCapacity;
-    const uint32_t k = ix.k, tj = ix.t_jump;
-    BaseReader br(q);
-    int c = base_code((uint8_t)br.get(0));
-    if (c < 0) return -kErrInvalidBase;
-    uint32_t p = 0, d = 0, l = 0, r = ix.n, j = 0xFFFFFFFFu;
-    uint32_t mode = kModeExt, hi = 0, lo = 0, l1 = 0, r1 = 0, cl = 0, cr = 0, bl = 0, bR = 0;
-    uint32_t fw = 0, d0 = 0, d1 = 0, d2 = 0, d3 = 0, ne = 0;
-    bool run_open = false;
-    uint32_t cblk = 0xFFFFFFFFu, c0 = 0, c1 = 0, c2 = 0, c3 = 0;  // colex_at cache (4 entries)
-    uint32_t tblk = 0xFFFFFFFFu;
-    uint64_t tw = 0;  // path text cache (32 chars)
-    while (p < len) {
-        bool commit = false, fast = false;
-        uint32_t nl = 0, nr = 0, nd = 0, flag = 0;
-        if (mode == kModeExt && j != 0xFFFFFFFFu) {
-            const uint32_t tpos = j + k;
-            if ((tpos >> 5) != tblk) {
-                tblk = tpos >> 5;
-                tw = ix.ptext[tblk];
-            }
-            const uint32_t tc = (uint32_t)(tw >> (2 * (tpos & 31))) & 3u;
-            const uint32_t jn = j + 1;
-            if ((jn >> 2) != cblk) {
-                cblk = jn >> 2;
-#ifdef __HIP_DEVICE_COMPILE__
-                const uint4 v = *reinterpret_cast<const uint4 *>(ix.colex_at + ((uint64_t)cblk << 2));
-                c0 = v.x; c1 = v.y; c2 = v.z; c3 = v.w;
-#else
-                const uint32_t *v = ix.colex_at + ((uint64_t)cblk << 2);
-                c0 = v[0]; c1 = v[1]; c2 = v[2]; c3 = v[3];
-#endif
-            }
-            const uint32_t cn = (jn & 2) ? ((jn & 1) ? c3 : c2) : ((jn & 1) ? c1 : c0);
-            if (tc == (uint32_t)c && cn != 0xFFFFFFFFu) {
-                fast = commit = true;
-                nl = cn & 0x7FFFFFFFu;
-                nr = nl + 1;
-                nd = d + 1 < k ? d + 1 : k;
-                flag = nd == k ? (cn >> 31) : 0u;
-                j = jn;
-            }
-        }
-        if (!fast) {
-            // ---- one SBWT unit: query, (widen), extend, transition (= ms_step) ----------
-            uint32_t ql = l, qr = r, t = 0;
-            bool wid = true;
-            if (mode == kModeExt) wid = false;
-            else if (mode == kModeP1) t = hi;
-            else if (mode == kModeTj) { ql = l1; qr = r1; t = tj; }
-            else if (mode == kModeBs) { ql = l1; qr = r1; t = (lo + hi) >> 1; }
-            else { ql = cl; qr = cr; t = hi - 1; }
-            if (wid) widen(ix, ql, qr, t);
-            uint32_t el, er;
-            extend(ix, c, ql, qr, el, er);
-            const bool ok = el < er;
-            if (mode == kModeExt) {
-                if (ok) { commit = true; nl = el; nr = er; nd = d + 1 < k ? d + 1 : k; }
-                else if (d == 0) return -kErrInvalidBase;
-                else { hi = d - 1; mode = kModeP1; }
-            } else if (mode == kModeP1) {
-                l1 = ql; r1 = qr;
-                if (ok) { commit = true; nl = el; nr = er; nd = hi + 1; }
-                else if (hi > tj + 1) mode = kModeTj;
-                else if (hi == 0) return -kErrInvalidBase;
-                else { cl = ql; cr = qr; mode = kModeLin; }
-            } else if (mode == kModeTj) {
-                if (ok) {
-                    lo = tj; bl = el; bR = er;
-                    if (hi - lo > 1) mode = kModeBs;
-                    else { commit = true; nl = bl; nr = bR; nd = lo + 1; }
-                } else { hi = tj; cl = ql; cr = qr; mode = kModeLin; }
-            } else if (mode == kModeBs) {
-                if (ok) { lo = t; bl = el; bR = er; } else hi = t;
-                if (hi - lo <= 1) { commit = true; nl = bl; nr = bR; nd = lo + 1; }
-            } else {
-                cl = ql; cr = qr;
-                if (ok) { commit = true; nl = el; nr = er; nd = t + 1; }
-                else if (t == 0) return -kErrInvalidBase;
-                else hi = t;
-            }
-            if (commit) {
-                j = 0xFFFFFFFFu;
-                if (ix.has_paths && nr == nl + 1) j = ix.pos_of_node[nl];
-                if (nd == k) flag = (ix.uniq[nl >> 5] >> (nl & 31)) & 1u;
-            }
-        }
-        if (commit) {
-            l = nl; r = nr; d = nd;
-            if (fast) {
-                if (!run_open) {
-                    s.E[ne++] = ((uint64_t)p << 32) | (uint64_t)(j | kFastTag);
-                    run_open = true;
-                }
-            } else {
-                s.E[ne++] = ((uint64_t)p << 32) | (uint64_t)l;
-                run_open = false;
-            }
-            const uint32_t b = p & 15, sh = (b & 3) * 8, v = d << sh;
-            if (b < 4) d0 |= v; else if (b < 8) d1 |= v; else if (b < 12) d2 |= v; else d3 |= v;
-            if (b == 15 || p + 1 == len) {
-#ifdef __HIP_DEVICE_COMPILE__
-                *reinterpret_cast<uint4 *>(s.D + (p & ~15u)) = make_uint4(d0, d1, d2, d3);
-#else
-                uint32_t *dd = reinterpret_cast<uint32_t *>(s.D + (p & ~15u));
-                dd[0] = d0; dd[1] = d1; dd[2] = d2; dd[3] = d3;
-#endif
-                d0 = d1 = d2 = d3 = 0;
-            }
-            fw |= flag << (p & 31);
-            if ((p & 31) == 31 || p + 1 == len) {
-                s.F[p >> 5] = fw;
-                fw = 0;
-            }
-            p++;
-            mode = kModeExt;
-            if (p < len) {
-                c = base_code((uint8_t)br.get(p));
-                if (c < 0) return -kErrInvalidBase;
-            }
-        }
-    }
-    if (ne < rows) s.E[ne] = 0xFFFFFFFF00000000ULL;  // terminator for diagnostics
-    // ---- greedy right-to-left parse, lib.rs:175-218 (as encode_lane) ------------------
-    int32_t e = (int32_t)ne - 1;
-    uint32_t i = len;
-    int nrec = 0;
-    while (i > 0) {
-        const uint32_t x = i - 1;
-        const uint32_t di = s.D[x];
-        while (e > 0 && (uint32_t)(s.E[e] >> 32) > x) e--;
-        const uint64_t ent = s.E[e];
-        uint32_t st = (uint32_t)ent;
-        if (ix.has_paths && (st & kFastTag))
-            st = ix.colex_at[(st & ~kFastTag) + (x - (uint32_t)(ent >> 32))] & 0x7FFFFFFFu;
-        const uint32_t segend = i;
-        uint32_t seglen;
-        if (di == k && i > k + 1) {
-            const uint32_t ext = run_from(s.F, i - 2, i - k - 1, 1);
-            const uint32_t L = k + ext;
-            uint32_t m = L, pp = i;
-            for (;;) {
-                const uint32_t dp = s.D[pp - 1];
-                if (dp < m) {
-                    if (dp >= pp) return -kErrFormat;
-                    m -= dp;
-                    pp -= dp;
-                } else {
-                    break;
-                }
-            }
-            seglen = L - (m - 1);
-            i = pp;
-        } else {
-            seglen = di;
-            if (i > di) i -= di - 1;
-            else i = 0;
-        }
-        if (seglen >= (1u << 24)) return -kErrLength;
-        const uint64_t first = nrec == 0 ? 1u : 0u;
-        uint64_t w;
-        if (seglen > 11) {
-            w = (uint64_t)st | ((uint64_t)(seglen & 0xFFFFFFu) << 32) | (first << 56);
-        } else {
-            uint64_t bits = 0;
-            for (uint32_t t = 0; t < seglen; t++)
-                bits |= (uint64_t)base_code(q[segend - seglen + t]) << (2 * t);
-            w = bits | ((uint64_t)((first + 2) | (seglen << 2)) << 56);
-        }
-        s.R[nrec] = w;
-        nrec++;
-        if (i > 0) i -= 1;
-        else break;
-    }
-    return nrec;
-}
+constexpr uint32_t kSpecSpan = 8;  // thresholds tested per speculative probe
 
 // ======================================================================================
-// encode v3: matching statistics as RUN-LENGTH entries.  A lane alternates SBWT units
+// Matching statistics as RUN-LENGTH entries (encode v4 below).  A lane alternates SBWT units
 // (ms_step's extension / contraction probes, one per loop iteration) with path RUNS:
 // once the interval is a single node at path position j, the next m positions follow
 // the path for as long as the query equals the path text and the path continues.  m is
@@ -572,12 +428,6 @@ struct Entry {       // 16 bytes, one uint4 store
 constexpr uint32_t kRunTag = 0x80000000u;
 constexpr uint32_t kPrefixTag = 0x40000000u;  // positions 0..10 from the prefix table:
                                               // d = p + 1 <= 11, S never needed (short)
-
-struct LaneScratch3 {
-    uint64_t *Q;     // query, 2 bits per base (char t at bits 2(t%32) of word t/32)
-    Entry *E;        // entries, increasing p
-    uint64_t *R;     // records
-};
 
 // 32 two-bit characters starting at character offset off of a packed array
 NTC_HD uint64_t window2(const uint64_t *w, uint64_t off) {
@@ -664,195 +514,6 @@ struct EntryView {
     }
 };
 
-NTC_HD int encode_lane3(const DevIndex &ix, const uint8_t *q, uint32_t len, uint32_t rows, LaneScratch3 s,
-                        bool use_prefix = true) {
-    if (len == 0) return -kErrEmptyRead;
-    if (len > rows) return -kErrCapacity;
-    const uint32_t k = ix.k, tj = ix.t_jump;
-    // ---- pack the query to 2 bits per base (and validate it) --------------------------
-    {
-        BaseReader br(q);
-        uint64_t acc = 0;
-        for (uint32_t p = 0; p < len; p++) {
-            const int c = base_code((uint8_t)br.get(p));
-            if (c < 0) return -kErrInvalidBase;
-            acc |= (uint64_t)c << (2 * (p & 31));
-            if ((p & 31) == 31) {
-                s.Q[p >> 5] = acc;
-                acc = 0;
-            }
-        }
-        s.Q[len >> 5] = acc;
-        s.Q[(len >> 5) + 1] = 0;
-    }
-    uint32_t p = 0, d = 0, l = 0, r = ix.n, j = 0xFFFFFFFFu, ne = 0;
-    uint32_t mode = kModeExt, hi = 0, lo = 0, l1 = 0, r1 = 0, cl = 0, cr = 0, bl = 0, bR = 0;
-    bool try_run = false;
-    if (use_prefix && ix.prefix_len && len >= kPrefixLen) {
-        // the first 11 extensions from [0, n) in one lookup: if q[0..11] occurs, so do all
-        // its prefixes, hence d = p + 1 for p < 11 (short records only: d <= 11 < k)
-        const uint2 iv = ix.prefix_tab[s.Q[0] & ((1ULL << (2 * kPrefixLen)) - 1)];
-        if (iv.y > iv.x) {
-#ifdef __HIP_DEVICE_COMPILE__
-            *reinterpret_cast<uint4 *>(s.E) = make_uint4(0u, 0xFFFFFFFFu, kPrefixLen, 1u | kPrefixTag);
-#else
-            s.E[0] = Entry{0u, 0xFFFFFFFFu, kPrefixLen, 1u | kPrefixTag};
-#endif
-            ne = 1;
-            p = kPrefixLen;
-            d = kPrefixLen;
-            l = iv.x;
-            r = iv.y;
-            if (ix.has_paths && r == l + 1) {
-                j = ix.pos_of_node[l];
-                try_run = j != 0xFFFFFFFFu;
-            }
-        }
-    }
-    while (p < len) {
-        if (try_run) {
-            // ---- path run: positions p.. follow the path from node at j ----------------
-            try_run = false;
-            uint32_t m = 0;
-            for (;;) {
-                const uint64_t a = window2(s.Q, p + m);
-                const uint64_t b = window2(ix.ptext, j + k + m);
-                const uint64_t x = a ^ b;
-                uint32_t lim = x ? ctz64(x) >> 1 : 32u;
-                const uint32_t inv = ctz64(~window1(ix.pvalid, j + 1 + m));
-                if (inv < lim) lim = inv;
-                if (len - p - m < lim) lim = len - p - m;
-                m += lim;
-                if (lim < 32) break;
-            }
-            if (m > 0) {
-                Entry en;
-                en.p = p;
-                en.v = j + 1;
-                en.m = m;
-                en.dk = (d + 1 < k ? d + 1 : k) | kRunTag;
-#ifdef __HIP_DEVICE_COMPILE__
-                *reinterpret_cast<uint4 *>(s.E + ne) = make_uint4(en.p, en.v, en.m, en.dk);
-#else
-                s.E[ne] = en;
-#endif
-                ne++;
-                p += m;
-                j += m;
-                d = d + m < k ? d + m : k;
-                l = ix.colex_at[j] & 0x7FFFFFFFu;
-                r = l + 1;
-                continue;
-            }
-        }
-        // ---- one SBWT unit (query, widen, extend, transition) -------------------------
-        const int c = (int)((s.Q[p >> 5] >> (2 * (p & 31))) & 3u);
-        uint32_t ql = l, qr = r, t = 0;
-        bool wid = true;
-        if (mode == kModeExt) wid = false;
-        else if (mode == kModeP1) t = hi;
-        else if (mode == kModeTj) { ql = l1; qr = r1; t = tj; }
-        else if (mode == kModeBs) { ql = l1; qr = r1; t = (lo + hi) >> 1; }
-        else { ql = cl; qr = cr; t = hi - 1; }
-        if (wid) widen(ix, ql, qr, t);
-        uint32_t el, er;
-        extend(ix, c, ql, qr, el, er);
-        const bool ok = el < er;
-        bool commit = false;
-        uint32_t nl = 0, nr = 0, nd = 0;
-        if (mode == kModeExt) {
-            if (ok) { commit = true; nl = el; nr = er; nd = d + 1 < k ? d + 1 : k; }
-            else if (d == 0) return -kErrInvalidBase;
-            else { hi = d - 1; mode = kModeP1; }
-        } else if (mode == kModeP1) {
-            l1 = ql; r1 = qr;
-            if (ok) { commit = true; nl = el; nr = er; nd = hi + 1; }
-            else if (hi > tj + 1) mode = kModeTj;
-            else if (hi == 0) return -kErrInvalidBase;
-            else { cl = ql; cr = qr; mode = kModeLin; }
-        } else if (mode == kModeTj) {
-            if (ok) {
-                lo = tj; bl = el; bR = er;
-                if (hi - lo > 1) mode = kModeBs;
-                else { commit = true; nl = bl; nr = bR; nd = lo + 1; }
-            } else { hi = tj; cl = ql; cr = qr; mode = kModeLin; }
-        } else if (mode == kModeBs) {
-            if (ok) { lo = t; bl = el; bR = er; } else hi = t;
-            if (hi - lo <= 1) { commit = true; nl = bl; nr = bR; nd = lo + 1; }
-        } else {
-            cl = ql; cr = qr;
-            if (ok) { commit = true; nl = el; nr = er; nd = t + 1; }
-            else if (t == 0) return -kErrInvalidBase;
-            else hi = t;
-        }
-        if (commit) {
-            l = nl; r = nr; d = nd;
-            uint32_t flag = 0;
-            if (d == k) flag = (ix.uniq[l >> 5] >> (l & 31)) & 1u;
-#ifdef __HIP_DEVICE_COMPILE__
-            *reinterpret_cast<uint4 *>(s.E + ne) = make_uint4(p, l, 1u, d | (flag << 8));
-#else
-            s.E[ne] = Entry{p, l, 1u, d | (flag << 8)};
-#endif
-            ne++;
-            p++;
-            mode = kModeExt;
-            j = 0xFFFFFFFFu;
-            if (ix.has_paths && r == l + 1) {
-                j = ix.pos_of_node[l];
-                try_run = j != 0xFFFFFFFFu;
-            }
-        }
-    }
-    // ---- greedy right-to-left parse, lib.rs:175-218 ----------------------------------
-    EntryView ev{s.E, &ix, k, (int32_t)ne - 1};
-    uint32_t i = len;
-    int nrec = 0;
-    while (i > 0) {
-        const uint32_t x = i - 1;
-        const uint32_t di = ev.D(x);
-        const uint32_t st = ev.S(x);
-        const uint32_t segend = i;
-        uint32_t seglen;
-        if (di == k && i > k + 1) {
-            const uint32_t ext = ev.run_from(i - 2, i - k - 1);
-            const uint32_t L = k + ext;
-            uint32_t m = L, pp = i;
-            for (;;) {  // jump loop lib.rs:193-203
-                const uint32_t dp = ev.D(pp - 1);
-                if (dp < m) {
-                    if (dp >= pp || dp == 0) return -kErrFormat;
-                    m -= dp;
-                    pp -= dp;
-                } else {
-                    break;
-                }
-            }
-            seglen = L - (m - 1);
-            i = pp;
-        } else {
-            seglen = di;
-            if (i > di) i -= di - 1;
-            else i = 0;
-        }
-        if (seglen >= (1u << 24)) return -kErrLength;
-        const uint64_t first = nrec == 0 ? 1u : 0u;
-        uint64_t w;
-        if (seglen > 11) {
-            w = (uint64_t)st | ((uint64_t)(seglen & 0xFFFFFFu) << 32) | (first << 56);
-        } else {
-            // bitnuc::as_2bit of the segment == its query bases (packed LSB-first already)
-            const uint64_t bits = window2(s.Q, segend - seglen);
-            w = (bits & ((1ULL << (2 * seglen)) - 1)) | ((uint64_t)((first + 2) | (seglen << 2)) << 56);
-        }
-        s.R[nrec] = w;
-        nrec++;
-        if (i > 0) i -= 1;
-        else break;
-    }
-    return nrec;
-}
-
 // ======================================================================================
 // encode v4: the v3 algorithm split for load balance.
 //   k_pack   : reads -> 2-bit words (read r's words at Qall[(P_r >> 5) + r], P_r = its
@@ -895,15 +556,6 @@ NTC_HD void store_entry(Entry *E, uint32_t i, uint32_t p, uint32_t v, uint32_t m
     E[i] = Entry{p, v, m, dk};
 #endif
 }
-
-#if defined(NTC_STATS) && !defined(__HIP_DEVICE_COMPILE__)
-extern uint64_t ntc_stats[16];  // host emulation only: unit counts by kind
-#define NTC_STAT(i) (ntc_stats[i]++)
-inline void ntc_stat_add(int i, uint64_t v) { ntc_stats[i] += v; }
-#else
-#define NTC_STAT(i) ((void)0)
-NTC_HD void ntc_stat_add(int, uint64_t) {}
-#endif
 
 struct MsLane {
     const uint64_t *Q;  // packed query stream; this read starts at character qo
@@ -988,13 +640,65 @@ struct MsLane {
         else { ql = cl; qr = cr; t = hi - 1; }
         if (wid) widen(ix, ql, qr, t);
         uint32_t el, er;
-        extend(ix, c, ql, qr, el, er);
+        const bool spec = mode == kModeExt && d > 0 && d < k && d <= tj + kSpecSpan;
+        LineRegs A, B;
+        uint32_t li = 0, ri = 0;
+        LcsWin wl, wr;
+        if (spec) {
+            // issue the LCS windows around [l, r) together with the rank line(s): if the
+            // extension fails, thresholds d-1, d-2, ... are tested from registers
+            wl.load(ix.lcs, (int64_t)(ql & ~7u) - 8);
+            wr.load(ix.lcs, (int64_t)(qr & ~7u));
+            extend_keep(ix, c, ql, qr, el, er, A, B, li, ri);
+        } else {
+            extend(ix, c, ql, qr, el, er);
+        }
         const bool ok = el < er;
         bool commit = false;
         uint32_t nl = 0, nr = 0, nd = 0;
         if (mode == kModeExt) {
             if (ok) { commit = true; nl = el; nr = er; nd = d + 1 < k ? d + 1 : k; }
             else if (d == 0) return -kErrInvalidBase;
+            else if (spec) {
+                // t = d-1, d-2, ...: widen from registers, rank from the kept lines; the
+                // first t whose extension is non-empty is the reference's t*
+                uint32_t Lp = ql, Rp = qr, t = d, tested = 0;
+                bool known = true;
+                NTC_STAT(9);
+                while (known && t > 1 && d - t < kSpecSpan) {
+                    t--;
+                    while (Lp > 0) {
+                        if (!wl.has(Lp)) { known = false; break; }
+                        if (wl.at(Lp) < t) break;
+                        Lp--;
+                    }
+                    while (known && Rp < ix.n) {
+                        if (!wr.has(Rp)) { known = false; break; }
+                        if (wr.at(Rp) < t) break;
+                        Rp++;
+                    }
+                    if (!known) break;
+                    const uint32_t lb = Lp / kRankBlock, rb = Rp / kRankBlock;
+                    if ((lb != li && lb != ri) || (rb != li && rb != ri)) { known = false; break; }
+                    const uint32_t a = ix.C[c] + rank_in(lb == li ? A : B, Lp - lb * kRankBlock);
+                    const uint32_t b = ix.C[c] + rank_in(rb == li ? A : B, Rp - rb * kRankBlock);
+                    if (a < b) {
+                        NTC_STAT(10);
+                        commit = true; nl = a; nr = b; nd = t + 1;
+                        break;
+                    }
+                    hi = t; cl = Lp; cr = Rp;  // extension fails at t, interval I_t
+                    tested++;
+                }
+                if (!commit) {
+                    if (tested == 0) {  // nothing decided: ordinary P1 probe next
+                        hi = d - 1; mode = kModeP1;
+                    } else {  // every t in [hi, d-1] fails; search below hi from I_hi
+                        l1 = cl; r1 = cr;
+                        mode = hi > tj + 1 ? kModeTj : kModeLin;
+                    }
+                }
+            }
             else { hi = d - 1; mode = kModeP1; }
         } else if (mode == kModeP1) {
             l1 = ql; r1 = qr;

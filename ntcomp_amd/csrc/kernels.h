@@ -21,12 +21,6 @@ struct EncodeArgs {
     uint64_t *R;
     uint32_t *rec_count;
     unsigned long long *status;  // min over (read << 8 | code); ~0 = ok
-    uint64_t *E;                 // v2: entries (per-lane contiguous, like D and R)
-    int variant;                 // 1 = phase-synchronous lanes, 2 = flattened + path walk,
-                                 // 3 = run-length entries with word-parallel path runs
-    int exact_ms;                // v3: 1 = no prefix table (diagnostics want S everywhere)
-    uint64_t *Q;                 // v3: packed query words
-    Entry *E3;                   // v3: entries
 };
 
 struct Enc4Args {
@@ -45,8 +39,7 @@ struct Enc4Args {
 };
 
 struct EmitArgs {
-    int variant;                 // 1: R is [tile][j][lane]; 2: R is [tile][lane][j]
-    const uint64_t *R;
+    const uint64_t *R;           // [tile][j][lane]
     const uint64_t *tile_base;
     uint64_t rows_uniform;
     const uint32_t *rec_count;
@@ -58,10 +51,6 @@ struct EmitArgs {
 };
 
 struct DebugArgs {
-    int variant;
-    const Entry *E3;
-    const uint64_t *E;
-    DevIndex ix;
     const uint8_t *D;
     const uint32_t *S;
     const uint64_t *tile_base;

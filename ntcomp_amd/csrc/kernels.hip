@@ -46,70 +46,6 @@ __global__ __launch_bounds__(256) void k_encode(EncodeArgs a) {
     }
 }
 
-// v2: one lane per read, per-lane contiguous scratch inside the tile's area
-__global__ __launch_bounds__(256) void k_encode2(EncodeArgs a) {
-    const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (gid >= a.n_reads) return;
-    const uint64_t tile = gid >> 6;
-    const uint32_t lane = (uint32_t)(gid & 63);
-    uint64_t base, rows;
-    if (a.tile_base) {
-        base = a.tile_base[tile];
-        rows = a.tile_base[tile + 1] - base;
-    } else {
-        base = tile * a.rows_uniform;
-        rows = a.rows_uniform;
-    }
-    const uint64_t beg = a.offs[gid], end = a.offs[gid + 1];
-    const uint64_t len64 = end >= beg ? end - beg : 0;
-    LaneScratch2 s;
-    s.D = a.D + base * 64 + lane * rows;
-    s.F = a.F + (base >> 5) * 64 + lane * (rows >> 5);
-    s.E = a.E + base * 64 + lane * rows;
-    s.R = a.R + base * 64 + lane * rows;
-    int rc;
-    if (end < beg || len64 > 0xFFFFFFFFull) rc = -kErrFormat;
-    else rc = encode_lane2(a.ix, a.bases + beg, (uint32_t)len64, (uint32_t)rows, s);
-    if (rc < 0) {
-        atomicMin(a.status, (unsigned long long)((gid << 8) | (uint64_t)(-rc)));
-        a.rec_count[gid] = 0;
-    } else {
-        a.rec_count[gid] = (uint32_t)rc;
-    }
-}
-
-// v3: per-lane contiguous scratch: Q (rows/32 + 2 words), E (rows entries), R (rows)
-__global__ __launch_bounds__(256) void k_encode3(EncodeArgs a) {
-    const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (gid >= a.n_reads) return;
-    const uint64_t tile = gid >> 6;
-    const uint32_t lane = (uint32_t)(gid & 63);
-    uint64_t base, rows;
-    if (a.tile_base) {
-        base = a.tile_base[tile];
-        rows = a.tile_base[tile + 1] - base;
-    } else {
-        base = tile * a.rows_uniform;
-        rows = a.rows_uniform;
-    }
-    const uint64_t beg = a.offs[gid], end = a.offs[gid + 1];
-    const uint64_t len64 = end >= beg ? end - beg : 0;
-    const uint64_t qw = (rows >> 5) + 2;
-    LaneScratch3 s;
-    s.Q = a.Q + ((base >> 5) + 2 * tile) * 64 + lane * qw;
-    s.E = a.E3 + base * 64 + lane * rows;
-    s.R = a.R + base * 64 + lane * rows;
-    int rc;
-    if (end < beg || len64 > 0xFFFFFFFFull) rc = -kErrFormat;
-    else rc = encode_lane3(a.ix, a.bases + beg, (uint32_t)len64, (uint32_t)rows, s, !a.exact_ms);
-    if (rc < 0) {
-        atomicMin(a.status, (unsigned long long)((gid << 8) | (uint64_t)(-rc)));
-        a.rec_count[gid] = 0;
-    } else {
-        a.rec_count[gid] = (uint32_t)rc;
-    }
-}
-
 // ---- v4 ---------------------------------------------------------------------------
 // pack the batch's bases (position space: character x = batch position x) 32 per thread:
 // consecutive threads read consecutive 32-byte chunks (coalesced); bad bytes report the
@@ -289,14 +225,8 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
         atomicMin(a.status, (unsigned long long)((gid << 8) | (uint64_t)kErrCapacity));
         return;
     }
-    if (a.variant >= 2) {
-        const uint64_t rows = a.tile_base ? a.tile_base[tile + 1] - base : a.rows_uniform;
-        const uint64_t *src = a.R + base * 64 + lane * rows;
-        for (uint32_t j = 0; j < cnt; j++) a.out[off + j] = src[j];
-    } else {
-        const uint64_t *src = a.R + base * 64 + lane;
-        for (uint32_t j = 0; j < cnt; j++) a.out[off + j] = src[(uint64_t)j * 64];
-    }
+    const uint64_t *src = a.R + base * 64 + lane;
+    for (uint32_t j = 0; j < cnt; j++) a.out[off + j] = src[(uint64_t)j * 64];
 }
 
 __global__ __launch_bounds__(256) void k_debug_gather(DebugArgs a) {
@@ -306,36 +236,6 @@ __global__ __launch_bounds__(256) void k_debug_gather(DebugArgs a) {
     const uint32_t lane = (uint32_t)(gid & 63);
     const uint64_t base = a.tile_base ? a.tile_base[tile] : tile * a.rows_uniform;
     const uint64_t b = a.offs[gid], e = a.offs[gid + 1];
-    if (a.variant == 3) {
-        const uint64_t rows = a.tile_base ? a.tile_base[tile + 1] - base : a.rows_uniform;
-        EntryView ev{a.E3 + base * 64 + lane * rows, &a.ix, a.ix.k, 0};
-        uint32_t cnt = 0;  // entries cover [0, len) contiguously
-        for (uint64_t p = 0; p < e - b;) {
-            const Entry &en = ev.E[cnt];
-            for (uint32_t t = 0; t < en.m && p < e - b; t++, p++) {
-                a.d_out[b + p] = ev.dval(en, (uint32_t)p);
-                a.s_out[b + p] = (en.dk & kRunTag) ? (a.ix.colex_at[en.v + t] & 0x7FFFFFFFu) : en.v;
-            }
-            cnt++;
-        }
-        return;
-    }
-    if (a.variant == 2) {
-        const uint64_t rows = a.tile_base ? a.tile_base[tile + 1] - base : a.rows_uniform;
-        const uint8_t *D = a.D + base * 64 + lane * rows;
-        const uint64_t *E = a.E + base * 64 + lane * rows;
-        int64_t ei = 0;
-        for (uint64_t p = 0; p < e - b; p++) {
-            while ((uint64_t)(ei + 1) < rows && (uint32_t)(E[ei + 1] >> 32) <= p) ei++;
-            const uint64_t ent = E[ei];
-            uint32_t st = (uint32_t)ent;
-            if (a.ix.has_paths && (st & kFastTag))
-                st = a.ix.colex_at[(st & ~kFastTag) + (p - (uint32_t)(ent >> 32))] & 0x7FFFFFFFu;
-            a.d_out[b + p] = D[p];
-            a.s_out[b + p] = st;
-        }
-        return;
-    }
     for (uint64_t p = 0; p < e - b; p++) {
         a.d_out[b + p] = a.D[(base + p) * 64 + lane];
         a.s_out[b + p] = a.S[(base + p) * 64 + lane];
@@ -517,9 +417,7 @@ void scan_excl_u64(const uint64_t *in, uint64_t n, uint64_t *out, uint64_t *tmp,
 static inline dim3 grid_for(uint64_t n) { return dim3((uint32_t)((n + 255) / 256)); }
 
 void launch_encode(const EncodeArgs &a, hipStream_t s) {
-    if (a.variant == 3) hipLaunchKernelGGL(k_encode3, grid_for(a.n_reads), dim3(256), 0, s, a);
-    else if (a.variant == 2) hipLaunchKernelGGL(k_encode2, grid_for(a.n_reads), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(k_encode, grid_for(a.n_reads), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_encode, grid_for(a.n_reads), dim3(256), 0, s, a);
 }
 __global__ __launch_bounds__(256) void k_debug_gather4(Enc4Args a, uint32_t *d_out, uint32_t *s_out) {
     const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;

@@ -51,7 +51,6 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
         std::vector<uint8_t> D(rows * 64 + 64);
         std::vector<uint32_t> S(rows * 64 + 64), F((rows / 32 + 1) * 64);
         std::vector<uint64_t> R(rows * 64 + 64);
-        std::vector<uint64_t> E(rows * 64 + 64);
         for (uint64_t r = t * 64; r < n_reads && r < t * 64 + 64; r++) {
             uint32_t lane = (uint32_t)(r & 63);
             uint32_t len = (uint32_t)(offs[r + 1] - offs[r]);
@@ -92,47 +91,6 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
                     rec_offsets[r + 1] = total;
                     continue;
                 }
-            } else if (variant == 3) {
-                std::vector<uint64_t> Q(rows / 32 + 2);
-                std::vector<Entry> E3(rows + 1);
-                std::vector<uint64_t> R3(rows + 1);
-                LaneScratch3 s{Q.data(), E3.data(), R3.data()};
-                rc = encode_lane3(d, bases + offs[r], len, (uint32_t)rows, s);
-                if (d_out && rc >= 0) {
-                    uint32_t p = 0;
-                    for (size_t ei = 0; p < len; ei++) {
-                        const Entry &en = E3[ei];
-                        EntryView ev{E3.data(), &d, d.k, 0};
-                        for (uint32_t t = 0; t < en.m && p < len; t++, p++) {
-                            d_out[offs[r] - offs[0] + p] = ev.dval(en, p);
-                            s_out[offs[r] - offs[0] + p] =
-                                (en.dk & kRunTag) ? (d.colex_at[en.v + t] & 0x7FFFFFFFu) : en.v;
-                        }
-                    }
-                }
-                if (rc >= 0) {
-                    if (total + (uint64_t)rc > cap) return NTC_ERR_CAPACITY;
-                    for (int jj = 0; jj < rc; jj++) rec_out[total + jj] = R3[jj];
-                    total += (uint64_t)rc;
-                    rec_offsets[r + 1] = total;
-                    continue;
-                }
-            } else if (variant == 2) {
-                LaneScratch2 s{D.data() + lane * rows, F.data() + lane * (rows / 32), E.data() + lane * rows,
-                               R.data() + lane * rows};
-                rc = encode_lane2(d, bases + offs[r], len, (uint32_t)rows, s);
-                if (d_out && rc >= 0) {
-                    const uint64_t *El = E.data() + lane * rows;
-                    uint64_t ei = 0;
-                    for (uint32_t p = 0; p < len; p++) {
-                        while (ei + 1 < rows && (uint32_t)(El[ei + 1] >> 32) <= p) ei++;
-                        uint32_t st = (uint32_t)El[ei];
-                        if (d.has_paths && (st & kFastTag))
-                            st = d.colex_at[(st & ~kFastTag) + (p - (uint32_t)(El[ei] >> 32))] & 0x7FFFFFFFu;
-                        d_out[offs[r] - offs[0] + p] = D[lane * rows + p];
-                        s_out[offs[r] - offs[0] + p] = st;
-                    }
-                }
             } else {
                 LaneScratch s{D.data() + lane, S.data() + lane, F.data() + lane, R.data() + lane};
                 rc = encode_lane(d, bases + offs[r], len, (uint32_t)rows, s);
@@ -148,7 +106,7 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
             }
             if (total + (uint64_t)rc > cap) return NTC_ERR_CAPACITY;
             for (int j = 0; j < rc; j++)
-                rec_out[total + j] = variant == 2 ? R[lane * rows + j] : R[(uint64_t)j * 64 + lane];
+                rec_out[total + j] = R[(uint64_t)j * 64 + lane];
             total += (uint64_t)rc;
             rec_offsets[r + 1] = total;
         }

@@ -33,7 +33,7 @@ def test_gpu_golden_records_ms_decode(ctx, name):
     assert [out[o2[i]:o2[i + 1]].tobytes().decode() for i in range(len(o2) - 1)] == g["reads"]
 
 
-@pytest.mark.parametrize("variant", [4, 3, 2, 1])
+@pytest.mark.parametrize("variant", [4, 1])
 @pytest.mark.parametrize("k,err_ppm,glen", [(31, 10_000, 400_000), (91, 10_000, 400_000), (91, 0, 400_000),
                                              (15, 30_000, 200_000), (255, 5_000, 100_000), (11, 10_000, 100_000)])
 def test_gpu_matches_oracle_random(ctx, k, err_ppm, glen, variant):
@@ -66,7 +66,7 @@ def test_gpu_v2_repetitive_genome_and_ms(ctx):
             u[int(rng.integers(0, len(u)))] = b"ACGT"[int(rng.integers(0, 4))]
         parts.append(bytes(u) + nt.synth_genome(int(rng.integers(1, 1 << 30)), 97).tobytes())
     genome = np.frombuffer(b"".join(parts), dtype=np.uint8)
-    for k, variant in ((31, 4), (91, 4), (31, 3), (91, 3), (91, 2)):
+    for k, variant in ((31, 4), (91, 4), (91, 1)):
         ix = nt.Index.build([genome.tobytes()], k)
         ctx.upload(ix)
         ctx.set_option("encode_variant", variant)
