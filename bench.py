@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--variant", type=int, default=4, help="encode kernel variant (1, 2 = earlier designs, for A/B)")
+    ap.add_argument("--opt", action="append", default=[], help="ctx option key=value (A/B)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -84,6 +85,9 @@ def main():
     log(f"[rank {rank}] index k={args.k} n={index.n} built in {time.time() - t0:.1f}s")
     ctx = nt.GpuContext(local)
     ctx.set_option("encode_variant", args.variant)
+    for kv in args.opt:
+        key, val = kv.split("=")
+        ctx.set_option(key, int(val))
     t0 = time.time()
     ctx.upload(index)
     log(f"[rank {rank}] upload (derived structures + path cover) {time.time() - t0:.1f}s, "

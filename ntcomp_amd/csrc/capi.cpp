@@ -53,7 +53,7 @@ struct ntc_ctx {
     int last_variant = 0;
     int num_cus = 0;
     Enc4Args last4{};
-    int exact_ms = 0;       // set only by the diagnostics entry point
+    uint32_t tab_u_opt = 0;  // suffix-table depth for the next upload (0 = default_tab_u)
     uint64_t n_paths = 0, path_text_len = 0;
 };
 
@@ -143,7 +143,6 @@ int encode4_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, u
     a.offs = d_offs;
     a.n_reads = n_reads;
     a.status = ctx->d_status;
-    a.use_prefix = ctx->exact_ms ? 0 : 1;
     void *p;
     int rc;
     if ((rc = ensure(ctx, WS_Q, (total_bases / 32 + 4) * 8, &p))) return rc;
@@ -378,11 +377,6 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
         HIP_TRY(ctx, hipMemcpyAsync(d_walk_a, result, n * sizeof(WalkEntry), hipMemcpyDeviceToDevice,
                                     ctx->stream));
     void *d_ptext = nullptr, *d_colex_at = nullptr, *d_pos = nullptr, *d_pvalid = nullptr, *d_puniq = nullptr;
-    void *d_ptab = nullptr;
-    if (!dv.prefix_tab.empty()) {
-        if ((rc = dalloc(dv.prefix_tab.size() * 4, &d_ptab))) return rc;
-        HIP_TRY(ctx, hipMemcpy(d_ptab, dv.prefix_tab.data(), dv.prefix_tab.size() * 4, hipMemcpyHostToDevice));
-    }
     if (dv.has_paths) {
         if ((rc = dalloc(dv.pvalid.size() * 8, &d_pvalid))) return rc;
         if ((rc = dalloc(dv.puniq.size() * 8, &d_puniq))) return rc;
@@ -415,8 +409,17 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     d.pos_of_node = (const uint32_t *)d_pos;
     d.pvalid = (const uint64_t *)d_pvalid;
     d.puniq = (const uint64_t *)d_puniq;
-    d.prefix_tab = (const uint2 *)d_ptab;
-    d.prefix_len = d_ptab ? kPrefixLen : 0u;
+    d.absent = dv.absent;
+    // suffix table, levels 1..U, built on the device from the rank lines
+    uint32_t U = ctx->tab_u_opt ? std::min<uint32_t>(ctx->tab_u_opt, std::min<uint32_t>(hx.k, kTabMaxU))
+                                : default_tab_u(n, hx.k);
+    void *d_tab;
+    if ((rc = dalloc(tab_base(U + 1) * sizeof(uint2), &d_tab))) return rc;
+    d.tab = (const uint2 *)d_tab;
+    d.tab_u = U;
+    launch_tab_build(d, U, (uint2 *)d_tab, ctx->stream);
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     ctx->n_paths = dv.n_paths;
     ctx->path_text_len = dv.tlen;
     ctx->has_index = true;
@@ -425,6 +428,12 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
 
 int ntc_ctx_set_option(ntc_ctx *ctx, const char *key, int64_t value) {
     if (!ctx || !key) return NTC_ERR_INVALID_ARG;
+    if (std::strcmp(key, "tab_u") == 0) {  // applies to the next ntc_index_upload
+        if (value < 0 || value > (int64_t)kTabMaxU)
+            return set_err(ctx, NTC_ERR_INVALID_ARG, "tab_u must be 0 (default) or 1..14");
+        ctx->tab_u_opt = (uint32_t)value;
+        return NTC_OK;
+    }
     if (std::strcmp(key, "encode_variant") == 0) {
         if (value != 1 && value != 4)
             return set_err(ctx, NTC_ERR_INVALID_ARG, "encode_variant must be 4 (default) or 1 (A/B baseline)");
@@ -437,6 +446,7 @@ int ntc_ctx_set_option(ntc_ctx *ctx, const char *key, int64_t value) {
 int ntc_ctx_get_option(const ntc_ctx *ctx, const char *key, int64_t *value) {
     if (!ctx || !key || !value) return NTC_ERR_INVALID_ARG;
     if (std::strcmp(key, "encode_variant") == 0) *value = ctx->encode_variant;
+    else if (std::strcmp(key, "tab_u") == 0) *value = ctx->has_index ? ctx->dix.tab_u : ctx->tab_u_opt;
     else if (std::strcmp(key, "n_paths") == 0) *value = (int64_t)ctx->n_paths;
     else if (std::strcmp(key, "path_text_len") == 0) *value = (int64_t)ctx->path_text_len;
     else return NTC_ERR_INVALID_ARG;
@@ -736,9 +746,7 @@ int ntc_debug_matching_statistics(ntc_ctx *ctx, const uint8_t *bases, const uint
     const uint64_t total = read_offsets[n_reads] - read_offsets[0];
     std::vector<uint64_t> recs(total + 1), roffs(n_reads + 1);
     int64_t bad = -1;
-    ctx->exact_ms = 1;
     int rc = ntc_encode_batch(ctx, bases, read_offsets, n_reads, recs.data(), total + 1, roffs.data(), &bad);
-    ctx->exact_ms = 0;
     if (rc && rc != NTC_ERR_LENGTH) return rc;
     if (ctx->encode_variant == 4) {
         void *dd, *ds;

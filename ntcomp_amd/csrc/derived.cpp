@@ -12,8 +12,8 @@ bool build_derived(const HostIndex &ix, Derived &out, std::string &err, int thre
     (void)threads;
     const uint64_t n = ix.n;
     const uint32_t k = ix.k;
-    if (n == 0 || n >= (1ULL << 32) - 1) {
-        err = "index must have 1 <= n < 2^32 - 1 nodes";
+    if (n == 0 || n >= (uint64_t)kTabShort) {
+        err = "index must have 1 <= n < 2^32 - 256 nodes";
         return false;
     }
     if (k < 1 || k > 255) {
@@ -102,50 +102,29 @@ bool build_derived(const HostIndex &ix, Derived &out, std::string &err, int thre
     uint32_t tj = (uint32_t)std::ceil(l4) + 2;
     out.t_jump = std::max<uint32_t>(1, tj);
     build_paths(ix, out);
-    build_prefix_table(ix, out, threads);
+    out.absent = 0;
+    for (int c = 0; c < 4; c++)
+        if (out.C[c + 1] == out.C[c]) out.absent |= 1u << c;
     return true;
 }
 
-// Interval of every kPrefixLen-mer, by depth-first extension (sum 4^i extends); key =
-// the 2-bit codes with character t at bits 2t (as the kernel's packed query word).
-void build_prefix_table(const HostIndex &ix, Derived &dv, int threads) {
-    dv.prefix_tab.clear();
-    if (ix.k <= kPrefixLen) return;  // needs d = p + 1 < k on the prefix
-    const uint32_t P = kPrefixLen;
-    dv.prefix_tab.assign(2ULL << (2 * P), 0);
-    DevIndex d{};
-    d.lines = dv.lines.data();
-    d.nlines = dv.nlines;
-    d.n = (uint32_t)ix.n;
-    for (int c = 0; c < 5; c++) d.C[c] = dv.C[c];
-    auto rec = [&](auto &&self, uint32_t depth, uint64_t key, uint32_t l, uint32_t r) -> void {
-        if (depth == P) {
-            dv.prefix_tab[2 * key] = l;
-            dv.prefix_tab[2 * key + 1] = r;
-            return;
-        }
-        for (int c = 0; c < 4; c++) {
-            uint32_t nl, nr;
-            extend(d, c, l, r, nl, nr);
-            if (nl < nr) self(self, depth + 1, key | ((uint64_t)c << (2 * depth)), nl, nr);
-        }
-    };
-    if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
-    std::vector<std::thread> ts;
-    for (int c0 = 0; c0 < 4; c0++) {  // 16 independent subtrees
-        for (int c1 = 0; c1 < 4; c1++) {
-            ts.emplace_back([&, c0, c1] {
-                uint32_t l = 0, r = (uint32_t)ix.n, nl, nr;
-                extend(d, c0, l, r, nl, nr);
-                if (nl >= nr) return;
-                uint32_t ml, mr;
-                extend(d, c1, nl, nr, ml, mr);
-                if (ml >= mr) return;
-                rec(rec, 2, (uint64_t)c0 | ((uint64_t)c1 << 2), ml, mr);
-            });
-        }
+uint32_t default_tab_u(uint64_t n, uint32_t k) {
+    // random (t+1)-mers stop matching around log4(n): at U = ceil(log4 n) + 2 few absent
+    // U-mers are present by chance, so few table-long positions need the SBWT
+    const double l4 = std::log((double)std::max<uint64_t>(n, 2)) / std::log(4.0);
+    uint32_t u = (uint32_t)std::ceil(l4) + 2;
+    u = std::min<uint32_t>(u, kTabMaxU);
+    return std::max<uint32_t>(1u, std::min<uint32_t>(u, k));
+}
+
+void build_tab_host(const DevIndex &d, uint32_t U, std::vector<uint2> &tab) {
+    tab.assign(tab_base(U + 1), mk2(0, 0));
+    for (uint32_t u = 1; u <= U; u++) {
+        uint2 *cur = tab.data() + tab_base(u);
+        const uint2 *prev = u > 1 ? tab.data() + tab_base(u - 1) : nullptr;
+        const uint64_t cnt = 1ULL << (2 * u);
+        for (uint64_t key = 0; key < cnt; key++) cur[key] = tab_make(d, u, key, prev);
     }
-    for (auto &t : ts) t.join();
 }
 
 namespace {
@@ -316,8 +295,9 @@ DevIndex host_dev_index(const HostIndex &ix, const Derived &dv, const std::vecto
     d.pos_of_node = dv.pos_of_node.empty() ? nullptr : dv.pos_of_node.data();
     d.pvalid = dv.pvalid.empty() ? nullptr : dv.pvalid.data();
     d.puniq = dv.puniq.empty() ? nullptr : dv.puniq.data();
-    d.prefix_tab = dv.prefix_tab.empty() ? nullptr : reinterpret_cast<const uint2 *>(dv.prefix_tab.data());
-    d.prefix_len = dv.prefix_tab.empty() ? 0u : kPrefixLen;
+    d.absent = dv.absent;
+    d.tab = nullptr;  // see build_tab_host
+    d.tab_u = 0;
     return d;
 }
 

@@ -26,15 +26,17 @@ struct Derived {
     std::vector<uint64_t> pvalid;       // bit j: colex_at[j] != kNoNode
     std::vector<uint64_t> puniq;        // bit j: colex_at[j]'s group is a singleton
     uint64_t n_paths = 0;
-    std::vector<uint32_t> prefix_tab;   // 2 x u32 (l, r) per kPrefixLen-mer, or empty
+    uint32_t absent = 0;                // bit c: C[c+1] == C[c] (no node ends with c)
 };
 
 constexpr uint32_t kNoNode = 0xFFFFFFFFu;
 
 // Builds the path cover (fills has_paths, tlen, ptext, colex_at, pos_of_node).
 void build_paths(const HostIndex &ix, Derived &dv);
-// Intervals of all kPrefixLen-mers (k > kPrefixLen only).
-void build_prefix_table(const HostIndex &ix, Derived &dv, int threads);
+// Suffix-table depth U for an index of n nodes (encode_core.h "Suffix table").
+uint32_t default_tab_u(uint64_t n, uint32_t k);
+// Host build of the suffix table levels 1..U (test emulation; the GPU builds it on device).
+void build_tab_host(const DevIndex &d, uint32_t U, std::vector<uint2> &tab);
 
 // Validates the index and fills rank lines, unique-predecessor bits, pred and code.
 bool build_derived(const HostIndex &ix, Derived &out, std::string &err, int threads);

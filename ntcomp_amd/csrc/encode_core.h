@@ -65,11 +65,10 @@ struct DevIndex {
     const uint32_t *pos_of_node;  // text position of each real node's k-mer, or 0xFFFFFFFF
     const uint64_t *pvalid;       // bit j: colex_at[j] holds a node (encode v3)
     const uint64_t *puniq;        // bit j: that node's (k-1)-suffix group is a singleton
-    const uint2 *prefix_tab;      // interval of every kPrefixLen-mer (key: char t at bits 2t)
-    uint32_t prefix_len;          // kPrefixLen, or 0 = no table (k < 12 or disabled)
+    const uint2 *tab;             // suffix table, levels 1..tab_u (see tab_make)
+    uint32_t tab_u;               // U: longest tabulated length (1 <= U <= min(k, 14))
+    uint32_t absent;              // bit c: no node ends with character c
 };
-
-constexpr uint32_t kPrefixLen = 11;
 
 // per-read status codes (values of ntc_status)
 enum : int {
@@ -148,52 +147,6 @@ NTC_HD void extend(const DevIndex &ix, int c, uint32_t l, uint32_t r, uint32_t &
     nl = ix.C[c] + rl;
     nr = ix.C[c] + rr;
 }
-
-// extend_right keeping the rank line(s) it loaded (A = line of l, B = line of r)
-NTC_HD void extend_keep(const DevIndex &ix, int c, uint32_t l, uint32_t r, uint32_t &nl, uint32_t &nr,
-                        LineRegs &A, LineRegs &B, uint32_t &li, uint32_t &ri) {
-    const RankLine *rows = ix.lines + (uint64_t)c * ix.nlines;
-    li = l / kRankBlock;
-    ri = r / kRankBlock;
-    load_line(rows + li, A);
-    nl = ix.C[c] + rank_in(A, l - li * kRankBlock);
-    if (ri == li) {
-        nr = ix.C[c] + rank_in(A, r - li * kRankBlock);
-    } else {
-        load_line(rows + ri, B);
-        nr = ix.C[c] + rank_in(B, r - ri * kRankBlock);
-    }
-}
-
-// 16 LCS bytes [base, base + 16) as 4 words (base 8-aligned; zeros below index 0)
-struct LcsWin {
-    int64_t base;
-    uint32_t w0, w1, w2, w3;
-    NTC_HD void load(const uint8_t *lcs, int64_t b) {
-        base = b;
-#ifdef __HIP_DEVICE_COMPILE__
-        uint2 lo = make_uint2(0, 0), hi;
-        if (b >= 0) lo = *reinterpret_cast<const uint2 *>(lcs + b);
-        hi = *reinterpret_cast<const uint2 *>(lcs + b + 8);
-        w0 = lo.x; w1 = lo.y; w2 = hi.x; w3 = hi.y;
-#else
-        const uint32_t *q = reinterpret_cast<const uint32_t *>(lcs + b + 8);
-        if (b >= 0) {
-            const uint32_t *p = reinterpret_cast<const uint32_t *>(lcs + b);
-            w0 = p[0]; w1 = p[1];
-        } else {
-            w0 = w1 = 0;
-        }
-        w2 = q[0]; w3 = q[1];
-#endif
-    }
-    NTC_HD bool has(int64_t x) const { return x >= base && x < base + 16; }
-    NTC_HD uint32_t at(int64_t x) const {
-        const uint32_t o = (uint32_t)(x - base);
-        const uint32_t w = (o & 8) ? ((o & 4) ? w3 : w2) : ((o & 4) ? w1 : w0);
-        return (w >> ((o & 3) * 8)) & 0xFFu;
-    }
-};
 
 // contract_left(I, t) [ext sbwt]: widen I to all nodes sharing the last t characters.
 NTC_HD void widen(const DevIndex &ix, uint32_t &l, uint32_t &r, uint32_t t) {
@@ -381,6 +334,48 @@ NTC_HD int encode_lane(const DevIndex &ix, const uint8_t *q, uint32_t len, uint3
 }
 
 // ======================================================================================
+// Suffix table (encode v5).  d_p, the matching statistic at query position p, is BY
+// DEFINITION the length of the longest suffix (<= k) of q[0..p] that is a suffix of some
+// node (make_golden.py; StreamingIndex::matching_statistics, lib.rs:172-173), so it only
+// depends on q[p-U+1..p] whenever that U-mer is absent.  For every u-mer (u <= U) the
+// table holds either its colex interval [x, y) (the u-mer is a node suffix: "long") or,
+// when it is absent, y = kTabShort | m and x = S, where m is the length of its longest
+// present suffix and S the interval start of that suffix ("short").  Level u holds 4^u
+// entries at tab_base(u); key = the u 2-bit codes, first character in the low bits.
+// ======================================================================================
+constexpr uint32_t kTabShort = 0xFFFFFF00u;  // y >= kTabShort: absent, m = y & 0xFF
+constexpr uint32_t kTabMaxU = 14;            // 4^14 entries x 8 B at the top level
+
+NTC_HD uint64_t tab_base(uint32_t u) { return ((1ULL << (2 * u)) - 4) / 3; }
+NTC_HD bool tab_long(uint2 e) { return e.y < kTabShort; }
+NTC_HD uint2 mk2(uint32_t x, uint32_t y) {
+    uint2 v;
+    v.x = x;
+    v.y = y;
+    return v;
+}
+
+// entry of u-mer `key` from level u-1 (`prev`; unused for u = 1): the u-mer is present
+// iff its (u-1)-prefix is and extends by its last character; else it inherits the
+// longest present suffix of its (u-1)-suffix.
+NTC_HD uint2 tab_make(const DevIndex &ix, uint32_t u, uint64_t key, const uint2 *prev) {
+    const int c = (int)((key >> (2 * (u - 1))) & 3u);
+    if (u == 1) {
+        const uint32_t a = ix.C[c], b = ix.C[c + 1];
+        return a < b ? mk2(a, b) : mk2(0u, kTabShort);
+    }
+    const uint64_t m1 = (1ULL << (2 * (u - 1))) - 1;
+    const uint2 pre = prev[key & m1];
+    if (tab_long(pre)) {
+        uint32_t nl, nr;
+        extend(ix, c, pre.x, pre.y, nl, nr);
+        if (nl < nr) return mk2(nl, nr);
+    }
+    const uint2 suf = prev[key >> 2];
+    return tab_long(suf) ? mk2(suf.x, kTabShort | (u - 1)) : suf;
+}
+
+// ======================================================================================
 // shared by the flattened encoders
 // ======================================================================================
 struct BaseReader {
@@ -406,28 +401,30 @@ struct BaseReader {
     }
 };
 
-enum : uint32_t { kModeExt = 0, kModeP1 = 1, kModeTj = 2, kModeBs = 3, kModeLin = 4 };
-constexpr uint32_t kSpecSpan = 8;  // thresholds tested per speculative probe
+enum : uint32_t { kModeScan = 0, kModeExt = 1, kModeP1 = 2, kModeBs = 3 };
+constexpr uint32_t kScanW = 16;  // suffix-table probes per SCAN unit (U + kScanW - 1 <= 32)
 
 // ======================================================================================
-// Matching statistics as RUN-LENGTH entries (encode v4 below).  A lane alternates SBWT units
-// (ms_step's extension / contraction probes, one per loop iteration) with path RUNS:
-// once the interval is a single node at path position j, the next m positions follow
-// the path for as long as the query equals the path text and the path continues.  m is
-// found 32 bases at a time by XOR-ing 2-bit words of the query and the path text, so a
-// run costs a few word loads instead of m dependent rank lookups.  Per position the
-// run implies d = min(d0 + t, k), S = colex_at[j0 + t], flag = (d = k) & puniq[j0 + t].
-// The parse reads D, S and the extension flags back from the entries.
+// Matching statistics as RUN-LENGTH entries.  Positions whose U-mer is absent ("short")
+// are not walked at all: the suffix table gives their (d, S).  A position whose U-mer is
+// present ("long") right after a short one has d = U exactly (d_p <= d_{p-1} + 1) and S =
+// the U-mer's interval start, so it is table-determined too.  A lane only walks the SBWT
+// inside stretches of >= 2 consecutive long positions, starting from the first one's
+// table interval: one extension per position, or a path RUN once the interval is a single
+// node (the next m positions follow the path while the query equals the path text; m is
+// found 32 bases at a time by XOR-ing 2-bit words, see derived.cpp "path cover").  When an
+// extension fails at a long position, the contraction target t* = max{t < d : ext(I_t, c)}
+// is >= U-1 (the U-mer ending there is present), so only the probes above U-1 remain
+// (t = d-1, then binary search between U-1 and d-1, each a widen + extend).
+// Entries cover exactly the walked positions; the parse reads the rest from the table.
 // ======================================================================================
 struct Entry {       // 16 bytes, one uint4 store
     uint32_t p;      // first position
     uint32_t v;      // SBWT entry: colex start S; run entry: path position of node at p
     uint32_t m;      // positions covered (1 for an SBWT entry)
-    uint32_t dk;     // d at p | flag << 8 (SBWT entries) | run << 31
+    uint32_t dk;     // d at p | run << 31
 };
 constexpr uint32_t kRunTag = 0x80000000u;
-constexpr uint32_t kPrefixTag = 0x40000000u;  // positions 0..10 from the prefix table:
-                                              // d = p + 1 <= 11, S never needed (short)
 
 // 32 two-bit characters starting at character offset off of a packed array
 NTC_HD uint64_t window2(const uint64_t *w, uint64_t off) {
@@ -443,6 +440,18 @@ NTC_HD uint64_t window1(const uint64_t *w, uint32_t off) {
     return sh ? ((a >> sh) | (w[i + 1] << (64 - sh))) : a;
 }
 NTC_HD uint32_t ctz64(uint64_t x) { return x ? (uint32_t)__builtin_ctzll(x) : 64u; }
+NTC_HD uint32_t uniq_bit(const DevIndex &ix, uint32_t v) { return (ix.uniq[v >> 5] >> (v & 31)) & 1u; }
+
+// (d, S) of a position not covered by an entry, from the suffix table: u = min(x+1, U)
+// characters ending at x; long => d = u (x < U-1: the whole prefix; else the predecessor
+// is short, so d = U), short => d = m.
+NTC_HD void tab_ds(const DevIndex &ix, const uint64_t *Q, uint64_t qo, uint32_t x, uint32_t &d, uint32_t &s) {
+    const uint32_t u = x + 1 < ix.tab_u ? x + 1 : ix.tab_u;
+    const uint64_t key = window2(Q, qo + x + 1 - u) & ((1ULL << (2 * u)) - 1);
+    const uint2 e = ix.tab[tab_base(u) + key];
+    d = tab_long(e) ? u : (e.y & 0xFFu);
+    s = e.x;
+}
 
 // consecutive set bits at positions a, a-1, ... (at most maxn) of bitvector w
 NTC_HD uint32_t ones_down(const uint64_t *w, uint32_t a, uint32_t maxn) {
@@ -460,13 +469,17 @@ NTC_HD uint32_t ones_down(const uint64_t *w, uint32_t a, uint32_t maxn) {
     return cnt < maxn ? cnt : maxn;
 }
 
+// Right-to-left reader of one read's entries (+ suffix table for uncovered positions).
 struct EntryView {
     const Entry *E;
     const DevIndex *ix;
+    const uint64_t *Q;
+    uint64_t qo;
     uint32_t k;
-    int32_t e;  // cursor
-    NTC_HD void seek(uint32_t x) {  // last entry with p <= x (E[0].p = 0); cursor moves left
-        uint32_t pe = E[e].p;
+    int32_t e;  // cursor (-1: the read has no entries); moves left only
+    NTC_HD void seek(uint32_t x) {  // last entry with p <= x, or entry 0
+        if (e <= 0) return;
+        const uint32_t pe = E[e].p;
         if (pe <= x) return;
         // every entry covers >= 1 position, so entry e - (pe - x) starts at or before x
         int32_t g = e - (int32_t)(pe - x);
@@ -474,29 +487,52 @@ struct EntryView {
         while (g + 1 < e && E[g + 1].p <= x) g++;
         e = g;
     }
+    NTC_HD bool covered(uint32_t x) {
+        seek(x);
+        return e >= 0 && E[e].p <= x && x < E[e].p + E[e].m;
+    }
     NTC_HD uint32_t dval(const Entry &en, uint32_t x) const {
         const uint32_t d0 = en.dk & 0xFFu;
         const uint32_t d = d0 + (x - en.p);
-        return (en.dk & (kRunTag | kPrefixTag)) ? (d < k ? d : k) : d0;
+        return (en.dk & kRunTag) ? (d < k ? d : k) : d0;
     }
-    NTC_HD uint32_t D(uint32_t x) { seek(x); return dval(E[e], x); }
+    NTC_HD uint32_t sval(const Entry &en, uint32_t x) const {
+        return (en.dk & kRunTag) ? (ix->colex_at[en.v + (x - en.p)] & 0x7FFFFFFFu) : en.v;
+    }
+    NTC_HD uint32_t D(uint32_t x) {
+        if (covered(x)) return dval(E[e], x);
+        uint32_t d, s;
+        tab_ds(*ix, Q, qo, x, d, s);
+        return d;
+    }
     NTC_HD uint32_t S(uint32_t x) {
-        seek(x);
-        const Entry &en = E[e];
-        if (en.dk & kRunTag) return ix->colex_at[en.v + (x - en.p)] & 0x7FFFFFFFu;
-        return en.v;
+        if (covered(x)) return sval(E[e], x);
+        uint32_t d, s;
+        tab_ds(*ix, Q, qo, x, d, s);
+        return s;
     }
     // consecutive positions x, x-1, ... with d = k and a singleton (k-1)-suffix group
+    // (left_extend_kmer's per-step test)
     NTC_HD uint32_t run_from(uint32_t x, uint32_t cap) const {
         int32_t c = e;
         uint32_t cnt = 0;
         int64_t pos = x;
         while (cnt < cap && pos >= 0) {
             while (c > 0 && E[c].p > (uint32_t)pos) c--;
+            if (!(c >= 0 && E[c].p <= (uint32_t)pos && (uint32_t)pos < E[c].p + E[c].m)) {
+                // uncovered: d = min(pos + 1, U), = k only for U = k and a long position
+                if (ix->tab_u != k || (uint32_t)pos + 1 < k) break;
+                uint32_t d, s;
+                tab_ds(*ix, Q, qo, (uint32_t)pos, d, s);
+                if (d != k || !uniq_bit(*ix, s)) break;
+                cnt++;
+                pos--;
+                continue;
+            }
             const Entry &en = E[c];
             const uint32_t d0 = en.dk & 0xFFu;
             if (!(en.dk & kRunTag)) {
-                if (!((en.dk >> 8) & 1u)) break;
+                if (d0 != k || !uniq_bit(*ix, en.v)) break;
                 cnt++;
                 pos--;
                 continue;
@@ -515,26 +551,23 @@ struct EntryView {
 };
 
 // ======================================================================================
-// encode v4: the v3 algorithm split for load balance.
-//   k_pack   : reads -> 2-bit words (read r's words at Qall[(P_r >> 5) + r], P_r = its
-//              first base's position in the batch); validates bases.
-//   k_ms4    : persistent waves; each lane runs MsLane units (one SBWT unit or one path
-//              run per iteration) and, when its read is done, takes the next read from a
-//              wave-local pool refilled by one atomicAdd per 64 reads.  A lane stuck on a
-//              read with many errors no longer holds 63 finished lanes hostage (v3 waves
-//              ran for the max over 64 reads, ~3x the mean).
-//   k_parse4 : one lane per read: right-to-left parse over the entries -> records.
-// Entries and records live in "position space" (read r at [P_r, P_r + len_r)).
+// encode pipeline:
+//   k_pack   : reads -> 2-bit words in "position space" (character x of the batch at
+//              bits 2(x%32) of word x/32); validates bases.
+//   k_ms     : persistent waves; each lane runs MsLane units (one per loop iteration) and,
+//              when its read is done, takes the next read from a wave-local pool refilled
+//              by one atomicAdd per 64 reads (a read with many errors does not hold 63
+//              finished lanes hostage).
+//   k_parse  : one lane per read: right-to-left parse over the entries -> records.
+// Entries and records live in position space (read r at [P_r, P_r + len_r)).
 // ======================================================================================
-NTC_HD uint64_t qword_base(uint64_t P, uint64_t r) { return (P >> 5) + r; }
-
-NTC_HD int pack_read(const uint8_t *q, uint32_t len, uint64_t *Q) {
+NTC_HD int pack_read(const uint8_t *q, uint32_t len, uint64_t *Q, uint32_t absent) {
     if (len == 0) return -kErrEmptyRead;
     BaseReader br(q);
     uint64_t acc = 0;
     for (uint32_t p = 0; p < len; p++) {
         const int c = base_code((uint8_t)br.get(p));
-        if (c < 0) return -kErrInvalidBase;
+        if (c < 0 || ((absent >> c) & 1u)) return -kErrInvalidBase;
         acc |= (uint64_t)c << (2 * (p & 31));
         if ((p & 31) == 31) {
             Q[p >> 5] = acc;
@@ -557,39 +590,41 @@ NTC_HD void store_entry(Entry *E, uint32_t i, uint32_t p, uint32_t v, uint32_t m
 #endif
 }
 
+NTC_HD uint2 load2(const uint2 *p) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return *p;
+#else
+    return mk2(p->x, p->y);
+#endif
+}
+
 struct MsLane {
     const uint64_t *Q;  // packed query stream; this read starts at character qo
     Entry *E;
     uint64_t qo;
-    uint32_t len, p, d, l, r, j, ne, mode, hi, lo, l1, r1, cl, cr, bl, bR;
+    uint64_t qw;        // query characters [qb, qb + 32) of this read, cached
+    uint32_t qb;
+    uint32_t len, p, d, l, r, j, ne, mode, hi, lo, l1, r1, bl, bR;
     bool try_run;
 
-    NTC_HD uint32_t qchar(uint32_t x) const {
-        const uint64_t a = qo + x;
-        return (uint32_t)(Q[a >> 5] >> (2 * (a & 31))) & 3u;
-    }
-
-    NTC_HD void start(const DevIndex &ix, const uint64_t *Q_, uint64_t qo_, Entry *E_, uint32_t len_,
-                      bool use_prefix) {
+    NTC_HD void start(const DevIndex &ix, const uint64_t *Q_, uint64_t qo_, Entry *E_, uint32_t len_) {
         Q = Q_;
         qo = qo_;
         E = E_;
         len = len_;
+        qw = 0;
+        qb = 0xFFFFFFFFu;
         p = 0; d = 0; l = 0; r = ix.n; j = 0xFFFFFFFFu; ne = 0;
-        mode = kModeExt; hi = lo = l1 = r1 = cl = cr = bl = bR = 0;
+        mode = kModeScan; hi = lo = l1 = r1 = bl = bR = 0;
         try_run = false;
-        if (use_prefix && ix.prefix_len && len >= kPrefixLen) {
-            const uint2 iv = ix.prefix_tab[window2(Q, qo) & ((1ULL << (2 * kPrefixLen)) - 1)];
-            if (iv.y > iv.x) {
-                store_entry(E, 0, 0u, 0xFFFFFFFFu, kPrefixLen, 1u | kPrefixTag);
-                ne = 1;
-                p = kPrefixLen;
-                d = kPrefixLen;
-                l = iv.x;
-                r = iv.y;
-                note_single(ix);
-            }
-        }
+    }
+    NTC_HD void window(uint32_t from) {
+        qb = from;
+        qw = window2(Q, qo + from);
+    }
+    NTC_HD bool covers(uint32_t x0, uint32_t x1) const { return qb != 0xFFFFFFFFu && x0 >= qb && x1 < qb + 32; }
+    NTC_HD uint64_t key_at(uint32_t x, uint32_t U) const {  // U-mer ending at x (cached window)
+        return (qw >> (2 * (x + 1 - U - qb))) & ((1ULL << (2 * U)) - 1);
     }
     // after a commit: look for the path position of a single-node interval
     NTC_HD void note_single(const DevIndex &ix) {
@@ -599,16 +634,22 @@ struct MsLane {
             try_run = j != 0xFFFFFFFFu;
         }
     }
+    NTC_HD int commit(const DevIndex &ix, uint32_t nl, uint32_t nr, uint32_t nd) {
+        l = nl; r = nr; d = nd;
+        store_entry(E, ne++, p, l, 1u, d);
+        p++;
+        mode = kModeExt;
+        note_single(ix);
+        return p >= len ? 1 : 0;
+    }
     // one unit of work: 1 = read finished, 0 = continue, < 0 = error
     NTC_HD int step(const DevIndex &ix) {
-        const uint32_t k = ix.k, tj = ix.t_jump;
+        const uint32_t k = ix.k, U = ix.tab_u;
         if (p >= len) return 1;
         if (try_run) {
             try_run = false;
             uint32_t m = 0;
-            NTC_STAT(0);
             for (;;) {
-                NTC_STAT(1);
                 const uint64_t x = window2(Q, qo + p + m) ^ window2(ix.ptext, j + k + m);
                 uint32_t lim = x ? ctz64(x) >> 1 : 32u;
                 const uint32_t inv = ctz64(~window1(ix.pvalid, j + 1 + m));
@@ -618,129 +659,103 @@ struct MsLane {
                 if (lim < 32) break;
             }
             if (m > 0) {
-                NTC_STAT(2);
-                ntc_stat_add(3, m);
                 store_entry(E, ne++, p, j + 1, m, (d + 1 < k ? d + 1 : k) | kRunTag);
                 p += m;
                 j += m;
                 d = d + m < k ? d + m : k;
                 l = ix.colex_at[j] & 0x7FFFFFFFu;
                 r = l + 1;
-                return p >= len ? 1 : 0;
+                if (p >= len) return 1;
+                window(p + 1 - U);  // issued with the colex_at load
+                return 0;
             }
         }
-        const int c = (int)qchar(p);
-        NTC_STAT(4 + mode);
-        uint32_t ql = l, qr = r, t = 0;
-        bool wid = true;
-        if (mode == kModeExt) wid = false;
-        else if (mode == kModeP1) t = hi;
-        else if (mode == kModeTj) { ql = l1; qr = r1; t = tj; }
-        else if (mode == kModeBs) { ql = l1; qr = r1; t = (lo + hi) >> 1; }
-        else { ql = cl; qr = cr; t = hi - 1; }
-        if (wid) widen(ix, ql, qr, t);
-        uint32_t el, er;
-        const bool spec = mode == kModeExt && d > 0 && d < k && d <= tj + kSpecSpan;
-        LineRegs A, B;
-        uint32_t li = 0, ri = 0;
-        LcsWin wl, wr;
-        if (spec) {
-            // issue the LCS windows around [l, r) together with the rank line(s): if the
-            // extension fails, thresholds d-1, d-2, ... are tested from registers
-            wl.load(ix.lcs, (int64_t)(ql & ~7u) - 8);
-            wr.load(ix.lcs, (int64_t)(qr & ~7u));
-            extend_keep(ix, c, ql, qr, el, er, A, B, li, ri);
-        } else {
-            extend(ix, c, ql, qr, el, er);
-        }
-        const bool ok = el < er;
-        bool commit = false;
-        uint32_t nl = 0, nr = 0, nd = 0;
-        if (mode == kModeExt) {
-            if (ok) { commit = true; nl = el; nr = er; nd = d + 1 < k ? d + 1 : k; }
-            else if (d == 0) return -kErrInvalidBase;
-            else if (spec) {
-                // t = d-1, d-2, ...: widen from registers, rank from the kept lines; the
-                // first t whose extension is non-empty is the reference's t*
-                uint32_t Lp = ql, Rp = qr, t = d, tested = 0;
-                bool known = true;
-                NTC_STAT(9);
-                while (known && t > 1 && d - t < kSpecSpan) {
-                    t--;
-                    while (Lp > 0) {
-                        if (!wl.has(Lp)) { known = false; break; }
-                        if (wl.at(Lp) < t) break;
-                        Lp--;
-                    }
-                    while (known && Rp < ix.n) {
-                        if (!wr.has(Rp)) { known = false; break; }
-                        if (wr.at(Rp) < t) break;
-                        Rp++;
-                    }
-                    if (!known) break;
-                    const uint32_t lb = Lp / kRankBlock, rb = Rp / kRankBlock;
-                    if ((lb != li && lb != ri) || (rb != li && rb != ri)) { known = false; break; }
-                    const uint32_t a = ix.C[c] + rank_in(lb == li ? A : B, Lp - lb * kRankBlock);
-                    const uint32_t b = ix.C[c] + rank_in(rb == li ? A : B, Rp - rb * kRankBlock);
-                    if (a < b) {
-                        NTC_STAT(10);
-                        commit = true; nl = a; nr = b; nd = t + 1;
-                        break;
-                    }
-                    hi = t; cl = Lp; cr = Rp;  // extension fails at t, interval I_t
-                    tested++;
-                }
-                if (!commit) {
-                    if (tested == 0) {  // nothing decided: ordinary P1 probe next
-                        hi = d - 1; mode = kModeP1;
-                    } else {  // every t in [hi, d-1] fails; search below hi from I_hi
-                        l1 = cl; r1 = cr;
-                        mode = hi > tj + 1 ? kModeTj : kModeLin;
-                    }
-                }
+        if (mode == kModeScan) {
+            // find the first pair of consecutive long positions at or after p (position
+            // p - 1 is short, or p = 0); positions < U - 1 are short by length
+            if (p < U - 1) p = U - 1;
+            if (p + 1 >= len) { p = len; return 1; }
+            if (!covers(p + 1 - U, p + 1)) window(p + 1 - U);
+            uint32_t W = qb + 32 - p;
+            if (W > kScanW) W = kScanW;
+            if (W > len - p) W = len - p;
+            const uint2 *lvl = ix.tab + tab_base(U);
+            uint32_t longm = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < kScanW; i++)
+                if (i < W) longm |= (uint32_t)(lvl[key_at(p + i, U)].y < kTabShort) << i;
+            const uint32_t pairs = longm & (longm >> 1);
+            if (pairs == 0) {
+                if (p + W >= len) { p = len; return 1; }
+                p += W - ((longm >> (W - 1)) & 1u);  // keep a long last position
+                return 0;
             }
-            else { hi = d - 1; mode = kModeP1; }
-        } else if (mode == kModeP1) {
-            l1 = ql; r1 = qr;
-            if (ok) { commit = true; nl = el; nr = er; nd = hi + 1; }
-            else if (hi > tj + 1) mode = kModeTj;
-            else if (hi == 0) return -kErrInvalidBase;
-            else { cl = ql; cr = qr; mode = kModeLin; }
-        } else if (mode == kModeTj) {
-            if (ok) {
-                lo = tj; bl = el; bR = er;
-                if (hi - lo > 1) mode = kModeBs;
-                else { commit = true; nl = bl; nr = bR; nd = lo + 1; }
-            } else { hi = tj; cl = ql; cr = qr; mode = kModeLin; }
-        } else if (mode == kModeBs) {
-            if (ok) { lo = t; bl = el; bR = er; } else hi = t;
-            if (hi - lo <= 1) { commit = true; nl = bl; nr = bR; nd = lo + 1; }
-        } else {
-            cl = ql; cr = qr;
-            if (ok) { commit = true; nl = el; nr = er; nd = t + 1; }
-            else if (t == 0) return -kErrInvalidBase;
-            else hi = t;
-        }
-        if (commit) {
-            l = nl; r = nr; d = nd;
-            uint32_t flag = 0;
-            if (d == k) flag = (ix.uniq[l >> 5] >> (l & 31)) & 1u;
-            store_entry(E, ne++, p, l, 1u, d | (flag << 8));
-            p++;
+            const uint32_t x = p + (uint32_t)__builtin_ctz(pairs);  // long, short predecessor
+            const uint2 te = load2(lvl + key_at(x, U));
+            l = te.x; r = te.y; d = U;
+            p = x + 1;
             mode = kModeExt;
             note_single(ix);
-            return p >= len ? 1 : 0;
+            return 0;
         }
+        if (!covers(p + 1 - U, p)) window(p + 1 - U);
+        const int c = (int)((qw >> (2 * (p - qb))) & 3u);
+        if (mode == kModeExt) {
+            const uint2 te = load2(ix.tab + tab_base(U) + key_at(p, U));  // for a failure
+            uint32_t nl, nr;
+            extend(ix, c, l, r, nl, nr);
+            if (nl < nr) return commit(ix, nl, nr, d + 1 < k ? d + 1 : k);
+            if (!tab_long(te)) {  // p is short: table-determined, scan on
+                p++;
+                mode = kModeScan;
+                return p >= len ? 1 : 0;
+            }
+            if (d == U) return commit(ix, te.x, te.y, U);  // t* = U - 1
+            lo = U - 1; bl = te.x; bR = te.y;  // ext(I_{U-1}, c) = the U-mer's interval
+            hi = d - 1;
+            mode = kModeP1;
+            return 0;
+        }
+        // kModeP1: probe t = d - 1 from I_d; kModeBs: t = mid from I_hi (l1, r1)
+        const bool p1 = mode == kModeP1;
+        const uint32_t t = p1 ? hi : (lo + hi) >> 1;
+        uint32_t ql = p1 ? l : l1, qr = p1 ? r : r1;
+        widen(ix, ql, qr, t);
+        uint32_t el, er;
+        extend(ix, c, ql, qr, el, er);
+        if (el < er) {
+            if (p1) return commit(ix, el, er, t + 1);
+            lo = t; bl = el; bR = er;
+        } else {
+            hi = t; l1 = ql; r1 = qr;
+        }
+        if (hi - lo <= 1) return commit(ix, bl, bR, lo + 1);
+        mode = kModeBs;
         return 0;
     }
 };
+
+// (d, S) of every position of one read (diagnostics: ntc_debug_matching_statistics)
+NTC_HD void read_ms(const DevIndex &ix, const uint64_t *Q, uint64_t qo, const Entry *E, uint32_t ne,
+                    uint32_t len, uint32_t *d_out, uint32_t *s_out) {
+    EntryView ev{E, &ix, Q, qo, ix.k, -1};
+    uint32_t x = 0;
+    for (uint32_t i = 0; i <= ne && x < len; i++) {
+        const uint32_t until = i < ne ? E[i].p : len;
+        for (; x < until && x < len; x++) tab_ds(ix, Q, qo, x, d_out[x], s_out[x]);
+        if (i == ne) break;
+        for (uint32_t t = 0; t < E[i].m && x < len; t++, x++) {
+            d_out[x] = ev.dval(E[i], x);
+            s_out[x] = ev.sval(E[i], x);
+        }
+    }
+}
 
 // greedy right-to-left parse over the entries, lib.rs:175-218 (+ encode.rs:144-158)
 NTC_HD int parse_read(const DevIndex &ix, const uint64_t *Q, uint64_t qo, const Entry *E, uint32_t ne,
                       uint32_t len, uint64_t *R) {
     const uint32_t k = ix.k;
-    if (ne == 0) return -kErrFormat;
-    EntryView ev{E, &ix, k, (int32_t)ne - 1};
+    EntryView ev{E, &ix, Q, qo, k, (int32_t)ne - 1};
     uint32_t i = len;
     int nrec = 0;
     while (i > 0) {
@@ -767,6 +782,7 @@ NTC_HD int parse_read(const DevIndex &ix, const uint64_t *Q, uint64_t qo, const 
             seglen = L - (m - 1);
             i = pp;
         } else {
+            if (di == 0) return -kErrFormat;
             seglen = di;
             if (i > di) i -= di - 1;
             else i = 0;

@@ -73,6 +73,7 @@ __global__ __launch_bounds__(256) void k_pack(Enc4Args a, uint64_t total) {
     const uint32_t n = total - x0 < 32 ? (uint32_t)(total - x0) : 32u;
     uint64_t acc = 0;
     bool bad = false;
+    const uint32_t absent = a.ix.absent;
 #pragma unroll
     for (uint32_t t = 0; t < 32; t++) {
         const uint32_t o = sh + t;  // byte index into w (static after unrolling but sh)
@@ -82,14 +83,14 @@ __global__ __launch_bounds__(256) void k_pack(Enc4Args a, uint64_t total) {
         for (uint32_t q = 1; q < 12; q++) wv = (word == q) ? w[q] : wv;
         const uint32_t ch = (wv >> (8 * (o & 3))) & 0xFFu;
         if (t < n) {
-            bad |= !is_acgt(ch);
+            bad |= !is_acgt(ch) || ((absent >> fast_code(ch)) & 1u);
             acc |= (uint64_t)fast_code(ch) << (2 * t);
         }
     }
     a.Q[b] = acc;
     if (bad) {
         for (uint32_t t = 0; t < n; t++) {
-            if (!is_acgt(B[x0 + t])) {  // the read holding the first bad byte
+            if (!is_acgt(B[x0 + t]) || ((absent >> fast_code(B[x0 + t])) & 1u)) {  // its read
                 uint64_t lo = 0, hi = a.n_reads;
                 const uint64_t pos = a.offs[0] + x0 + t;
                 while (hi - lo > 1) {
@@ -135,7 +136,7 @@ __global__ __launch_bounds__(256) void k_ms4(Enc4Args a) {
                 idle = false;
                 const uint64_t b = a.offs[rd], e = a.offs[rd + 1];
                 const uint64_t P = b - o0;
-                st.start(a.ix, a.Q, P, a.E + P, (uint32_t)(e - b), a.use_prefix != 0);
+                st.start(a.ix, a.Q, P, a.E + P, (uint32_t)(e - b));
                 if (e <= b) {  // empty read (EncodeError, encode.rs:133-135) or bad offsets
                     atomicMin(a.status, (unsigned long long)((rd << 8) | (uint64_t)(e == b ? kErrEmptyRead : kErrFormat)));
                     a.ne[rd] = 0;
@@ -424,14 +425,21 @@ __global__ __launch_bounds__(256) void k_debug_gather4(Enc4Args a, uint32_t *d_o
     if (r >= a.n_reads) return;
     const uint64_t o0 = a.offs[0], b = a.offs[r], e = a.offs[r + 1];
     const uint64_t P = b - o0;
-    EntryView ev{a.E + P, &a.ix, a.ix.k, 0};
-    uint32_t p = 0;
-    for (uint32_t i = 0; i < a.ne[r] && p < e - b; i++) {
-        const Entry &en = ev.E[i];
-        for (uint32_t t = 0; t < en.m && p < e - b; t++, p++) {
-            d_out[P + p] = ev.dval(en, p);
-            s_out[P + p] = (en.dk & kRunTag) ? (a.ix.colex_at[en.v + t] & 0x7FFFFFFFu) : en.v;
-        }
+    read_ms(a.ix, a.Q, P, a.E + P, a.ne[r], (uint32_t)(e - b), d_out + P, s_out + P);
+}
+
+// suffix table level u (4^u entries) from level u - 1
+__global__ __launch_bounds__(256) void k_tab_level(DevIndex ix, uint32_t u, const uint2 *prev, uint2 *cur) {
+    const uint64_t key = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (key >> (2 * u)) return;
+    cur[key] = tab_make(ix, u, key, prev);
+}
+
+void launch_tab_build(const DevIndex &ix, uint32_t U, uint2 *tab, hipStream_t s) {
+    for (uint32_t u = 1; u <= U; u++) {
+        const uint64_t cnt = 1ULL << (2 * u);
+        hipLaunchKernelGGL(k_tab_level, grid_for(cnt), dim3(256), 0, s, ix, u, u > 1 ? tab + tab_base(u - 1) : tab,
+                           tab + tab_base(u));
     }
 }
 

@@ -3,6 +3,7 @@
 // the CPU, one read at a time, with the kernels' [tile][position][lane] scratch layout.
 // It lets the -m "not gpu" suite check the kernel ALGORITHM against the oracle on a
 // machine without a GPU.  It is not part of libntcomp_gpu.so and no product path loads it.
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -13,7 +14,8 @@
 using namespace ntc;
 
 namespace {
-bool load(const ntc_index_view *v, HostIndex &hx, Derived &dv, std::vector<WalkEntry> &walk, DevIndex &d) {
+bool load(const ntc_index_view *v, HostIndex &hx, Derived &dv, std::vector<WalkEntry> &walk, DevIndex &d,
+          std::vector<uint2> &tab, uint32_t tab_u = 0) {
     hx.n = v->n_nodes;
     hx.k = v->k;
     uint64_t nw = (hx.n + 63) / 64;
@@ -27,20 +29,24 @@ bool load(const ntc_index_view *v, HostIndex &hx, Derived &dv, std::vector<WalkE
     if (!build_derived(hx, dv, err, 1)) return false;
     build_walk_host(dv, hx.n, walk);
     d = host_dev_index(hx, dv, walk);
+    const uint32_t U = tab_u ? std::min<uint32_t>(tab_u, std::min<uint32_t>(hx.k, kTabMaxU)) : default_tab_u(hx.n, hx.k);
+    build_tab_host(d, U, tab);
+    d.tab = tab.data();
+    d.tab_u = U;
     return true;
 }
 }  // namespace
 
 extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const uint64_t *offs, uint64_t n_reads,
                           uint64_t *rec_out, uint64_t cap, uint64_t *rec_offsets, int64_t *bad, uint32_t *d_out,
-                          uint32_t *s_out, int variant, int use_paths, int use_prefix) {
+                          uint32_t *s_out, int variant, int use_paths, int tab_u) {
     HostIndex hx;
     Derived dv;
     std::vector<WalkEntry> walk;
+    std::vector<uint2> tab;
     DevIndex d;
-    if (!load(v, hx, dv, walk, d)) return NTC_ERR_FORMAT;
+    if (!load(v, hx, dv, walk, d, tab, (uint32_t)tab_u)) return NTC_ERR_FORMAT;
     if (!use_paths) d.has_paths = 0;
-    if (!use_prefix) d.prefix_len = 0;
     *bad = -1;
     uint64_t tiles = (n_reads + 63) / 64, total = 0;
     rec_offsets[0] = 0;
@@ -59,11 +65,11 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
                 std::vector<uint64_t> Q(len / 32 + 3, 0);
                 std::vector<Entry> E4(len + 1);
                 std::vector<uint64_t> R4(len + 1);
-                rc = pack_read(bases + offs[r], len, Q.data());
+                rc = pack_read(bases + offs[r], len, Q.data(), d.absent);
                 MsLane ms;
                 uint32_t ne = 0;
                 if (rc == 0) {
-                    ms.start(d, Q.data(), 0, E4.data(), len, use_prefix != 0);
+                    ms.start(d, Q.data(), 0, E4.data(), len);
                     for (;;) {
                         int st = ms.step(d);
                         if (st < 0) { rc = st; break; }
@@ -72,18 +78,8 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
                     ne = ms.ne;
                 }
                 if (rc == 0) rc = parse_read(d, Q.data(), 0, E4.data(), ne, len, R4.data());
-                if (d_out && rc >= 0) {
-                    uint32_t p = 0;
-                    EntryView ev{E4.data(), &d, d.k, 0};
-                    for (uint32_t ei = 0; ei < ne && p < len; ei++) {
-                        const Entry &en = E4[ei];
-                        for (uint32_t t = 0; t < en.m && p < len; t++, p++) {
-                            d_out[offs[r] - offs[0] + p] = ev.dval(en, p);
-                            s_out[offs[r] - offs[0] + p] =
-                                (en.dk & kRunTag) ? (d.colex_at[en.v + t] & 0x7FFFFFFFu) : en.v;
-                        }
-                    }
-                }
+                if (d_out && rc >= 0)
+                    read_ms(d, Q.data(), 0, E4.data(), ne, len, d_out + (offs[r] - offs[0]), s_out + (offs[r] - offs[0]));
                 if (rc >= 0) {
                     if (total + (uint64_t)rc > cap) return NTC_ERR_CAPACITY;
                     for (int jj = 0; jj < rc; jj++) rec_out[total + jj] = R4[jj];
@@ -119,8 +115,9 @@ extern "C" int emu_decode(const ntc_index_view *v, const uint64_t *recs, uint64_
     HostIndex hx;
     Derived dv;
     std::vector<WalkEntry> walk;
+    std::vector<uint2> tab;
     DevIndex d;
-    if (!load(v, hx, dv, walk, d)) return NTC_ERR_FORMAT;
+    if (!load(v, hx, dv, walk, d, tab, 1)) return NTC_ERR_FORMAT;
     std::vector<uint64_t> starts;
     uint64_t total = 0;
     for (uint64_t r = 0; r < n; r++) {

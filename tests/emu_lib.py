@@ -47,7 +47,7 @@ def make_view(n, k, rows, C, lcs):
     return v, keep
 
 
-def emu_encode(n, k, rows, C, lcs, bases, offs, want_ms=False, variant=4, use_paths=True, use_prefix=None):
+def emu_encode(n, k, rows, C, lcs, bases, offs, want_ms=False, variant=4, use_paths=True, tab_u=0):
     v, keep = make_view(n, k, rows, C, lcs)
     bases = np.ascontiguousarray(bases, dtype=np.uint8)
     offs = np.ascontiguousarray(offs, dtype=np.uint64)
@@ -59,7 +59,7 @@ def emu_encode(n, k, rows, C, lcs, bases, offs, want_ms=False, variant=4, use_pa
     s = np.zeros(total + 1, dtype=np.uint32)
     rc = emu_lib().emu_encode(ctypes.byref(v), _p(bases), _p(offs), len(offs) - 1, _p(recs), len(recs), _p(roff),
                               ctypes.byref(bad), _p(d) if want_ms else None, _p(s) if want_ms else None,
-                              variant, int(use_paths), int((not want_ms) if use_prefix is None else use_prefix))
+                              variant, int(use_paths), int(tab_u))
     if rc:
         raise RuntimeError(f"emu_encode rc={rc} bad={bad.value}")
     out = (recs[: int(roff[-1])], roff)

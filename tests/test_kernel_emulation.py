@@ -92,13 +92,32 @@ def test_emulated_v2_ms_on_repetitive_genome(k):
 
 
 @pytest.mark.parametrize("k", [12, 31, 91])
-def test_emulated_prefix_table_records_identical(k):
+def test_emulated_suffix_table_depth_is_invisible(k):
+    """Records and matching statistics do not depend on the suffix-table depth U (U = 1
+    walks every position through the SBWT; larger U reads more positions off the table)."""
     genome = nt.synth_genome(300 + k, 80_000)
     ix = nt.Index.build([genome.tobytes()], k)
-    reads = nt.synth_reads(genome, 3, 0, 1000, 150, 10_000)
-    offs = np.arange(0, 1000 * 150 + 1, 150, dtype=np.uint64)
-    a, ao = emu_encode(ix.n, k, ix.rows, ix.C, ix.lcs, reads, offs, use_prefix=True)
-    b, bo = emu_encode(ix.n, k, ix.rows, ix.C, ix.lcs, reads, offs, use_prefix=False)
-
+    reads = nt.synth_reads(genome, 3, 0, 500, 150, 20_000)
+    offs = np.arange(0, 500 * 150 + 1, 150, dtype=np.uint64)
     exp, eoff = OracleIndex(ix.n, k, ix.rows, ix.C, ix.lcs).encode(reads, offs)
-    assert np.array_equal(a, exp) and np.array_equal(b, exp) and np.array_equal(ao, eoff)
+    base = None
+    for u in (1, 2, 5, 9, 12, 14, 0):
+        got, goff, d, s = emu_encode(ix.n, k, ix.rows, ix.C, ix.lcs, reads, offs, want_ms=True, tab_u=u)
+        assert np.array_equal(got, exp) and np.array_equal(goff, eoff), u
+        if base is None:
+            base = (d, s)
+        assert np.array_equal(d, base[0]) and np.array_equal(s, base[1]), u
+
+
+def test_emulated_absent_character_is_an_invalid_base():
+    # genome without 'T': a read holding T has d = 0 there (the reference never
+    # terminates, lib.rs:207); the kernels report NTC_ERR_INVALID_BASE for that read
+    ix = nt.Index.build(["ACGACGGACCAGACGAGGCAACGAGCACCGA" * 3], 7, add_revcomp=False)
+    reads = [b"ACGACGGAC", b"ACGACGGACCAGACGAGG", b"ACGT"]
+    bases, offs = pack_reads(reads)
+    with pytest.raises(RuntimeError, match="rc=2 bad=2"):
+        emu_encode(ix.n, 7, ix.rows, ix.C, ix.lcs, bases, offs)
+    b2, o2 = pack_reads(reads[:2])
+    got, goff = emu_encode(ix.n, 7, ix.rows, ix.C, ix.lcs, b2, o2)
+    out, oo = emu_decode(ix.n, 7, ix.rows, ix.C, ix.lcs, got)
+    assert np.array_equal(out, b2) and np.array_equal(oo, o2)
