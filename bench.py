@@ -147,7 +147,7 @@ def main():
     main_ms = sum(mains) / len(mains)
     if args.mode == "encode":
         alg_bytes = total_bases * (1 + 2 * 64) + 8 * n_recs  # SURVEY.md 8(d) B_enc
-        kname = "k_encode"
+        kname = "k_ms4" if args.variant == 4 else "k_encode"
     else:
         n_long_bases = None
         alg_bytes = None
@@ -170,7 +170,12 @@ def main():
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                 "kernel": kname, "kernel_ms": round(main_ms, 3),
-                "alg_bytes_per_launch": int(alg_bytes)}
+                "alg_bytes_per_launch": int(alg_bytes),
+                "note": "achieved = SURVEY 8(d) algorithmic bytes (the reference's two 64 B rank-line reads "
+                        "per base) / kernel time; the suffix table and path runs skip most of those reads, "
+                        "so frac can exceed 1. traffic = measured HBM bytes per launch (rocprofv3 PMC)"}
+    if traffic:
+        roofline["traffic_frac"] = round(traffic / (main_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
 
     cpu = None
     parity = None

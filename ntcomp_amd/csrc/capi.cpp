@@ -356,14 +356,14 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     };
     void *d_lines, *d_lcs, *d_uniq, *d_walk_a, *d_walk_b, *d_pred, *d_code;
     int rc;
-    if ((rc = dalloc(dv.lines.size() * sizeof(RankLine), &d_lines))) return rc;
+    if ((rc = dalloc(dv.rank.size() * sizeof(uint2), &d_lines))) return rc;
     if ((rc = dalloc(n + 256, &d_lcs))) return rc;
     if ((rc = dalloc(dv.uniq.size() * 4, &d_uniq))) return rc;
     if ((rc = dalloc(n * sizeof(WalkEntry), &d_walk_a))) return rc;
     HIP_TRY(ctx, hipMalloc(&d_walk_b, n * sizeof(WalkEntry)));
     HIP_TRY(ctx, hipMalloc(&d_pred, n * 4));
     HIP_TRY(ctx, hipMalloc(&d_code, n + 64));
-    HIP_TRY(ctx, hipMemcpy(d_lines, dv.lines.data(), dv.lines.size() * sizeof(RankLine), hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(d_lines, dv.rank.data(), dv.rank.size() * sizeof(uint2), hipMemcpyHostToDevice));
     HIP_TRY(ctx, hipMemset(d_lcs, 0, n + 256));
     HIP_TRY(ctx, hipMemcpy(d_lcs, hx.lcs.data(), n, hipMemcpyHostToDevice));
     HIP_TRY(ctx, hipMemcpy(d_uniq, dv.uniq.data(), dv.uniq.size() * 4, hipMemcpyHostToDevice));
@@ -394,11 +394,11 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     HIP_TRY(ctx, hipFree(d_pred));
     HIP_TRY(ctx, hipFree(d_code));
     DevIndex &d = ctx->dix;
-    d.lines = (const RankLine *)d_lines;
+    d.rank = (const uint2 *)d_lines;
     d.lcs = (const uint8_t *)d_lcs;
     d.uniq = (const uint32_t *)d_uniq;
     d.walk = (const WalkEntry *)d_walk_a;
-    d.nlines = dv.nlines;
+    d.rwords = dv.rwords;
     d.n = (uint32_t)n;
     d.k = hx.k;
     d.t_jump = dv.t_jump;
@@ -413,11 +413,13 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     // suffix table, levels 1..U, built on the device from the rank lines
     uint32_t U = ctx->tab_u_opt ? std::min<uint32_t>(ctx->tab_u_opt, std::min<uint32_t>(hx.k, kTabMaxU))
                                 : default_tab_u(n, hx.k);
-    void *d_tab;
+    void *d_tab, *d_bits;
     if ((rc = dalloc(tab_base(U + 1) * sizeof(uint2), &d_tab))) return rc;
+    if ((rc = dalloc(tab_bits_words(U) * 4, &d_bits))) return rc;
     d.tab = (const uint2 *)d_tab;
+    d.tab_bits = (const uint32_t *)d_bits;
     d.tab_u = U;
-    launch_tab_build(d, U, (uint2 *)d_tab, ctx->stream);
+    launch_tab_build(d, U, (uint2 *)d_tab, (uint32_t *)d_bits, ctx->stream);
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     ctx->n_paths = dv.n_paths;

@@ -30,29 +30,14 @@ bool build_derived(const HostIndex &ix, Derived &out, std::string &err, int thre
         err = "LCS array shorter than n";
         return false;
     }
-    // rank lines: 448 positions = 7 words, so line li holds row words [7li, 7li+7)
-    const uint64_t nlines = n / kRankBlock + 1;
-    out.nlines = (uint32_t)nlines;
-    out.lines.assign(4 * nlines, RankLine{});
-    uint64_t ones[4] = {0, 0, 0, 0};
-    for (int c = 0; c < 4; c++) {
-        const uint64_t *row = ix.rows[c].data();
-        uint64_t cnt = 0;
-        for (uint64_t li = 0; li < nlines; li++) {
-            RankLine &L = out.lines[c * nlines + li];
-            L.count = (uint32_t)cnt;
-            L.pad = 0;
-            for (int j = 0; j < 7; j++) {
-                uint64_t wi = li * 7 + j;
-                uint64_t w = wi < nw ? row[wi] : 0;
-                if (wi == nw - 1 && (n & 63)) w &= (1ULL << (n & 63)) - 1;
-                L.w[j] = w;
-                cnt += (uint64_t)__builtin_popcountll(w);
-            }
-        }
-        ones[c] = cnt;
-    }
     // C array must agree with the rows: C[c] = 1 + #labels < c, and n = 1 + #labels
+    uint64_t ones[4] = {0, 0, 0, 0};
+    for (int c = 0; c < 4; c++)
+        for (uint64_t wi = 0; wi < nw; wi++) {
+            uint64_t w = ix.rows[c][wi];
+            if (wi == nw - 1 && (n & 63)) w &= (1ULL << (n & 63)) - 1;
+            ones[c] += (uint64_t)__builtin_popcountll(w);
+        }
     uint64_t acc = 1;
     for (int c = 0; c < 4; c++) {
         if (ix.C[c] != acc) {
@@ -65,6 +50,21 @@ bool build_derived(const HostIndex &ix, Derived &out, std::string &err, int thre
     if (acc != n) {
         err = "label count != n - 1 (not an SBWT: every non-root node needs one in-edge)";
         return false;
+    }
+    // rank words: 32 positions each, x = C[c] + ones before the word
+    const uint64_t rw = n / 32 + 2;
+    out.rwords = (uint32_t)rw;
+    out.rank.assign(4 * rw, mk2(0, 0));
+    for (int c = 0; c < 4; c++) {
+        uint64_t cnt = out.C[c];
+        for (uint64_t i = 0; i < rw; i++) {
+            const uint64_t wi = i >> 1;
+            uint64_t w = wi < nw ? ix.rows[c][wi] : 0;
+            if (wi == nw - 1 && (n & 63)) w &= (1ULL << (n & 63)) - 1;
+            const uint32_t bits = (uint32_t)(w >> (32 * (i & 1)));
+            out.rank[c * rw + i] = mk2((uint32_t)cnt, bits);
+            cnt += (uint64_t)__builtin_popcount(bits);
+        }
     }
     out.C[4] = (uint32_t)n;
     for (uint64_t i = 0; i < n; i++)
@@ -117,7 +117,7 @@ uint32_t default_tab_u(uint64_t n, uint32_t k) {
     return std::max<uint32_t>(1u, std::min<uint32_t>(u, k));
 }
 
-void build_tab_host(const DevIndex &d, uint32_t U, std::vector<uint2> &tab) {
+void build_tab_host(const DevIndex &d, uint32_t U, std::vector<uint2> &tab, std::vector<uint32_t> &bits) {
     tab.assign(tab_base(U + 1), mk2(0, 0));
     for (uint32_t u = 1; u <= U; u++) {
         uint2 *cur = tab.data() + tab_base(u);
@@ -125,20 +125,21 @@ void build_tab_host(const DevIndex &d, uint32_t U, std::vector<uint2> &tab) {
         const uint64_t cnt = 1ULL << (2 * u);
         for (uint64_t key = 0; key < cnt; key++) cur[key] = tab_make(d, u, key, prev);
     }
+    const uint64_t nb = tab_bits_words(U);
+    bits.assign(nb, 0);
+    const uint64_t full = (1ULL << (2 * U)) / 32;
+    for (uint64_t w = 0; w < full; w++) bits[w] = tab_bits_word(tab.data() + tab_base(U), w);
+    for (uint64_t key = full * 32; key < (1ULL << (2 * U)); key++)  // U < 3: fewer than 32 keys
+        bits[0] |= (uint32_t)tab_long(tab[tab_base(U) + key]) << key;
 }
 
 namespace {
-inline uint32_t host_rank(const Derived &dv, int c, uint64_t i) {
-    LineRegs L;
-    const uint64_t li = i / kRankBlock;
-    load_line(&dv.lines[(uint64_t)c * dv.nlines + li], L);
-    return rank_in(L, (uint32_t)(i - li * kRankBlock));
+inline uint32_t host_rank(const Derived &dv, int c, uint64_t i) {  // rank_c(i), without C[c]
+    return rank_word(dv.rank[(uint64_t)c * dv.rwords + (i >> 5)], (uint32_t)i) - dv.C[c];
 }
 inline uint32_t labels_of(const Derived &dv, uint64_t g) {  // 4-bit label set of node g
-    const uint64_t li = g / kRankBlock, off = g - li * kRankBlock;
     uint32_t m = 0;
-    for (int c = 0; c < 4; c++)
-        m |= (uint32_t)((dv.lines[(uint64_t)c * dv.nlines + li].w[off >> 6] >> (off & 63)) & 1) << c;
+    for (int c = 0; c < 4; c++) m |= ((dv.rank[(uint64_t)c * dv.rwords + (g >> 5)].y >> (g & 31)) & 1u) << c;
     return m;
 }
 }  // namespace
@@ -280,11 +281,11 @@ void build_walk_host(const Derived &dv, uint64_t n, std::vector<WalkEntry> &walk
 
 DevIndex host_dev_index(const HostIndex &ix, const Derived &dv, const std::vector<WalkEntry> &walk) {
     DevIndex d{};
-    d.lines = dv.lines.data();
+    d.rank = dv.rank.data();
     d.lcs = ix.lcs.data();
     d.uniq = dv.uniq.data();
     d.walk = walk.data();
-    d.nlines = dv.nlines;
+    d.rwords = dv.rwords;
     d.n = (uint32_t)ix.n;
     d.k = ix.k;
     d.t_jump = dv.t_jump;

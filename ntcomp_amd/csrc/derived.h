@@ -9,8 +9,8 @@
 namespace ntc {
 
 struct Derived {
-    uint32_t nlines = 0;
-    std::vector<RankLine> lines;  // [4][nlines]
+    uint32_t rwords = 0;
+    std::vector<uint2> rank;      // [4][rwords] rank words (encode_core.h)
     std::vector<uint32_t> uniq;   // ceil(n/32) (+1) words
     std::vector<uint32_t> pred;   // inverse-walk predecessor (select), pred[0] = 0
     std::vector<uint8_t> code;    // last character of each node (root: 0)
@@ -36,7 +36,7 @@ void build_paths(const HostIndex &ix, Derived &dv);
 // Suffix-table depth U for an index of n nodes (encode_core.h "Suffix table").
 uint32_t default_tab_u(uint64_t n, uint32_t k);
 // Host build of the suffix table levels 1..U (test emulation; the GPU builds it on device).
-void build_tab_host(const DevIndex &d, uint32_t U, std::vector<uint2> &tab);
+void build_tab_host(const DevIndex &d, uint32_t U, std::vector<uint2> &tab, std::vector<uint32_t> &bits);
 
 // Validates the index and fills rank lines, unique-predecessor bits, pred and code.
 bool build_derived(const HostIndex &ix, Derived &out, std::string &err, int threads);

@@ -29,15 +29,9 @@ inline void ntc_stat_add(int i, uint64_t v) { ntc_stats[i] += v; }
 NTC_HD void ntc_stat_add(int, uint64_t) {}
 #endif
 
-constexpr uint32_t kRankBlock = 448;  // positions per 64-byte rank line (7 x u64)
-
-// One row's rank line: the row's ones before the line + 448 bits of the row.  A rank is
-// ONE 64-byte load plus popcounts.  Lines of the 4 rows live in 4 separate arrays.
-struct alignas(64) RankLine {
-    uint32_t count;
-    uint32_t pad;
-    uint64_t w[7];
-};
+// Rank words: row c of the subset matrix as one 8-byte word per 32 positions, x = C[c] +
+// (ones of row c before the word), y = the 32 row bits.  extend = two 8-byte loads + two
+// popcounts (DESIGN.md "Data layout in HBM").  Rows live in 4 separate arrays of rwords.
 
 // Inverse-walk jump table: the 32 characters met by walking 32 steps backwards from node
 // j (text order, character t in bits 2t..2t+1) and the node reached.  Replaces 32
@@ -49,11 +43,11 @@ struct alignas(16) WalkEntry {
 };
 
 struct DevIndex {
-    const RankLine *lines;  // [4][nlines]
+    const uint2 *rank;      // [4][rwords] rank words
     const uint8_t *lcs;     // [n]
     const uint32_t *uniq;   // bit z: node z's (k-1)-suffix group is {z}
     const WalkEntry *walk;  // [n]
-    uint32_t nlines;
+    uint32_t rwords;        // n / 32 + 2
     uint32_t n;
     uint32_t k;
     uint32_t t_jump;        // first contraction probe below d-1 (see ms_step)
@@ -66,6 +60,7 @@ struct DevIndex {
     const uint64_t *pvalid;       // bit j: colex_at[j] holds a node (encode v3)
     const uint64_t *puniq;        // bit j: that node's (k-1)-suffix group is a singleton
     const uint2 *tab;             // suffix table, levels 1..tab_u (see tab_make)
+    const uint32_t *tab_bits;     // bit key of level tab_u: that U-mer is present (long)
     uint32_t tab_u;               // U: longest tabulated length (1 <= U <= min(k, 14))
     uint32_t absent;              // bit c: no node ends with character c
 };
@@ -94,64 +89,35 @@ NTC_HD uint8_t base_char(uint32_t c) { return (uint8_t)(0x54474341u >> (8 * (c &
 
 NTC_HD uint32_t clz32(uint32_t x) { return x ? (uint32_t)__builtin_clz(x) : 32u; }
 
-struct LineRegs {
-    uint32_t count;
-    uint64_t w[7];
-};
-
-NTC_HD void load_line(const RankLine *L, LineRegs &o) {
+NTC_HD uint2 mk2(uint32_t x, uint32_t y) {
+    uint2 v;
+    v.x = x;
+    v.y = y;
+    return v;
+}
+NTC_HD uint2 load2(const uint2 *p) {
 #ifdef __HIP_DEVICE_COMPILE__
-    const uint4 *p = reinterpret_cast<const uint4 *>(L);
-    uint4 a = p[0], b = p[1], c = p[2], d = p[3];
-    o.count = a.x;
-    o.w[0] = (uint64_t)a.z | ((uint64_t)a.w << 32);
-    o.w[1] = (uint64_t)b.x | ((uint64_t)b.y << 32);
-    o.w[2] = (uint64_t)b.z | ((uint64_t)b.w << 32);
-    o.w[3] = (uint64_t)c.x | ((uint64_t)c.y << 32);
-    o.w[4] = (uint64_t)c.z | ((uint64_t)c.w << 32);
-    o.w[5] = (uint64_t)d.x | ((uint64_t)d.y << 32);
-    o.w[6] = (uint64_t)d.z | ((uint64_t)d.w << 32);
+    return *p;
 #else
-    o.count = L->count;
-    for (int j = 0; j < 7; j++) o.w[j] = L->w[j];
+    return mk2(p->x, p->y);
 #endif
 }
-
-// ones in the line's positions [0, off), off < 448
-NTC_HD uint32_t rank_in(const LineRegs &L, uint32_t off) {
-    const uint32_t wi = off >> 6, bi = off & 63;
-    uint32_t s = L.count;
-#pragma unroll
-    for (uint32_t j = 0; j < 7; j++) {
-        uint64_t m = (j < wi) ? ~0ULL : ((j == wi) ? ((1ULL << bi) - 1) : 0ULL);
-        s += (uint32_t)__builtin_popcountll(L.w[j] & m);
-    }
-    return s;
+NTC_HD uint32_t rank_word(uint2 w, uint32_t x) {  // C[c] + rank_c(x) from x's word
+    return w.x + (uint32_t)__builtin_popcount(w.y & ((1u << (x & 31)) - 1u));
 }
 
 // extend_right(I, c) = [C[c] + rank_c(l), C[c] + rank_c(r))
 NTC_HD void extend(const DevIndex &ix, int c, uint32_t l, uint32_t r, uint32_t &nl, uint32_t &nr) {
-    const RankLine *rows = ix.lines + (uint64_t)c * ix.nlines;
-    const uint32_t li = l / kRankBlock, ri = r / kRankBlock;
-    LineRegs A;
-    load_line(rows + li, A);
-    const uint32_t rl = rank_in(A, l - li * kRankBlock);
-    uint32_t rr;
-    if (ri == li) {
-        rr = rank_in(A, r - li * kRankBlock);
-    } else {
-        LineRegs B;
-        load_line(rows + ri, B);
-        rr = rank_in(B, r - ri * kRankBlock);
-    }
-    nl = ix.C[c] + rl;
-    nr = ix.C[c] + rr;
+    const uint2 *row = ix.rank + (uint64_t)c * ix.rwords;
+    const uint2 a = load2(row + (l >> 5)), b = load2(row + (r >> 5));
+    nl = rank_word(a, l);
+    nr = rank_word(b, r);
 }
 
 // contract_left(I, t) [ext sbwt]: widen I to all nodes sharing the last t characters.
 NTC_HD void widen(const DevIndex &ix, uint32_t &l, uint32_t &r, uint32_t t) {
-    while (l > 0 && ix.lcs[l] >= t) l--;
-    while (r < ix.n && ix.lcs[r] >= t) r++;
+    while (l > 0 && ix.lcs[l] >= t) { NTC_STAT(13); l--; }
+    while (r < ix.n && ix.lcs[r] >= t) { NTC_STAT(13); r++; }
 }
 
 // One character of k-bounded matching statistics.  State (d, [l, r)) = length and colex
@@ -348,11 +314,12 @@ constexpr uint32_t kTabMaxU = 14;            // 4^14 entries x 8 B at the top le
 
 NTC_HD uint64_t tab_base(uint32_t u) { return ((1ULL << (2 * u)) - 4) / 3; }
 NTC_HD bool tab_long(uint2 e) { return e.y < kTabShort; }
-NTC_HD uint2 mk2(uint32_t x, uint32_t y) {
-    uint2 v;
-    v.x = x;
-    v.y = y;
-    return v;
+NTC_HD uint64_t tab_bits_words(uint32_t U) { return U >= 3 ? (1ULL << (2 * U)) / 32 : 1; }
+// presence bits of the top level: bit key of word key / 32
+NTC_HD uint32_t tab_bits_word(const uint2 *top, uint64_t w) {
+    uint32_t b = 0;
+    for (uint32_t i = 0; i < 32; i++) b |= (uint32_t)tab_long(top[32 * w + i]) << i;
+    return b;
 }
 
 // entry of u-mer `key` from level u-1 (`prev`; unused for u = 1): the u-mer is present
@@ -402,7 +369,8 @@ struct BaseReader {
 };
 
 enum : uint32_t { kModeScan = 0, kModeExt = 1, kModeP1 = 2, kModeBs = 3 };
-constexpr uint32_t kScanW = 16;  // suffix-table probes per SCAN unit (U + kScanW - 1 <= 32)
+constexpr uint32_t kScanW = 16;      // presence probes per SCAN unit (U + kScanW - 1 <= 32)
+constexpr uint32_t kScanFirstW = 4;  // first SCAN of a read: error-free starts pair at once
 
 // ======================================================================================
 // Matching statistics as RUN-LENGTH entries.  Positions whose U-mer is absent ("short")
@@ -590,14 +558,6 @@ NTC_HD void store_entry(Entry *E, uint32_t i, uint32_t p, uint32_t v, uint32_t m
 #endif
 }
 
-NTC_HD uint2 load2(const uint2 *p) {
-#ifdef __HIP_DEVICE_COMPILE__
-    return *p;
-#else
-    return mk2(p->x, p->y);
-#endif
-}
-
 struct MsLane {
     const uint64_t *Q;  // packed query stream; this read starts at character qo
     Entry *E;
@@ -615,7 +575,8 @@ struct MsLane {
         qw = 0;
         qb = 0xFFFFFFFFu;
         p = 0; d = 0; l = 0; r = ix.n; j = 0xFFFFFFFFu; ne = 0;
-        mode = kModeScan; hi = lo = l1 = r1 = bl = bR = 0;
+        mode = kModeScan; lo = l1 = r1 = bl = bR = 0;
+        hi = kScanFirstW;  // SCAN width cap (hi is free while scanning)
         try_run = false;
     }
     NTC_HD void window(uint32_t from) {
@@ -630,6 +591,7 @@ struct MsLane {
     NTC_HD void note_single(const DevIndex &ix) {
         j = 0xFFFFFFFFu;
         if (ix.has_paths && r == l + 1 && d >= ix.t_jump) {
+            NTC_STAT(15);
             j = ix.pos_of_node[l];
             try_run = j != 0xFFFFFFFFu;
         }
@@ -646,10 +608,13 @@ struct MsLane {
     NTC_HD int step(const DevIndex &ix) {
         const uint32_t k = ix.k, U = ix.tab_u;
         if (p >= len) return 1;
+        NTC_STAT(0);
         if (try_run) {
             try_run = false;
             uint32_t m = 0;
+            NTC_STAT(1);
             for (;;) {
+                NTC_STAT(4);
                 const uint64_t x = window2(Q, qo + p + m) ^ window2(ix.ptext, j + k + m);
                 uint32_t lim = x ? ctz64(x) >> 1 : 32u;
                 const uint32_t inv = ctz64(~window1(ix.pvalid, j + 1 + m));
@@ -659,6 +624,8 @@ struct MsLane {
                 if (lim < 32) break;
             }
             if (m > 0) {
+                NTC_STAT(2);
+                ntc_stat_add(3, m);
                 store_entry(E, ne++, p, j + 1, m, (d + 1 < k ? d + 1 : k) | kRunTag);
                 p += m;
                 j += m;
@@ -677,19 +644,26 @@ struct MsLane {
             if (p + 1 >= len) { p = len; return 1; }
             if (!covers(p + 1 - U, p + 1)) window(p + 1 - U);
             uint32_t W = qb + 32 - p;
-            if (W > kScanW) W = kScanW;
+            if (W > hi) W = hi;
             if (W > len - p) W = len - p;
-            const uint2 *lvl = ix.tab + tab_base(U);
+            hi = kScanW;
             uint32_t longm = 0;
+            NTC_STAT(5);
+            ntc_stat_add(6, W);
 #pragma unroll
             for (uint32_t i = 0; i < kScanW; i++)
-                if (i < W) longm |= (uint32_t)(lvl[key_at(p + i, U)].y < kTabShort) << i;
+                if (i < W) {
+                    const uint64_t key = key_at(p + i, U);
+                    longm |= ((ix.tab_bits[key >> 5] >> (key & 31)) & 1u) << i;
+                }
             const uint32_t pairs = longm & (longm >> 1);
             if (pairs == 0) {
                 if (p + W >= len) { p = len; return 1; }
                 p += W - ((longm >> (W - 1)) & 1u);  // keep a long last position
                 return 0;
             }
+            const uint2 *lvl = ix.tab + tab_base(U);
+            NTC_STAT(7);
             const uint32_t x = p + (uint32_t)__builtin_ctz(pairs);  // long, short predecessor
             const uint2 te = load2(lvl + key_at(x, U));
             l = te.x; r = te.y; d = U;
@@ -703,13 +677,18 @@ struct MsLane {
         if (mode == kModeExt) {
             const uint2 te = load2(ix.tab + tab_base(U) + key_at(p, U));  // for a failure
             uint32_t nl, nr;
+            NTC_STAT(8);
             extend(ix, c, l, r, nl, nr);
-            if (nl < nr) return commit(ix, nl, nr, d + 1 < k ? d + 1 : k);
+            if (nl < nr) { NTC_STAT(9); return commit(ix, nl, nr, d + 1 < k ? d + 1 : k); }
+            NTC_STAT(10);
             if (!tab_long(te)) {  // p is short: table-determined, scan on
-                p++;
+                // d_{p+i} <= m + i, so p+1 .. p+U-1-m are short as well
+                p += U - (te.y & 0xFFu);
                 mode = kModeScan;
+                hi = kScanW;
                 return p >= len ? 1 : 0;
             }
+            NTC_STAT(11);
             if (d == U) return commit(ix, te.x, te.y, U);  // t* = U - 1
             lo = U - 1; bl = te.x; bR = te.y;  // ext(I_{U-1}, c) = the U-mer's interval
             hi = d - 1;
@@ -717,6 +696,7 @@ struct MsLane {
             return 0;
         }
         // kModeP1: probe t = d - 1 from I_d; kModeBs: t = mid from I_hi (l1, r1)
+        NTC_STAT(12);
         const bool p1 = mode == kModeP1;
         const uint32_t t = p1 ? hi : (lo + hi) >> 1;
         uint32_t ql = p1 ? l : l1, qr = p1 ? r : r1;

@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void k_pack(Enc4Args a, uint64_t total) {
 
 constexpr uint32_t kPoolChunk = 64;
 
-__global__ __launch_bounds__(256) void k_ms4(Enc4Args a) {
+__global__ __launch_bounds__(256, 8) void k_ms4(Enc4Args a) {
     const uint32_t lane = threadIdx.x & 63;
     if (*a.status != ~0ull) return;  // a read failed to pack: nothing to do
     const uint64_t o0 = a.offs[0];
@@ -435,12 +435,26 @@ __global__ __launch_bounds__(256) void k_tab_level(DevIndex ix, uint32_t u, cons
     cur[key] = tab_make(ix, u, key, prev);
 }
 
-void launch_tab_build(const DevIndex &ix, uint32_t U, uint2 *tab, hipStream_t s) {
+__global__ __launch_bounds__(256) void k_tab_bits(const uint2 *top, uint32_t U, uint32_t *bits) {
+    const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (w >= tab_bits_words(U)) return;
+    if (U >= 3) {
+        bits[w] = tab_bits_word(top, w);
+    } else {
+        uint32_t b = 0;
+        for (uint32_t key = 0; key < (1u << (2 * U)); key++) b |= (uint32_t)tab_long(top[key]) << key;
+        bits[0] = b;
+    }
+}
+
+void launch_tab_build(const DevIndex &ix, uint32_t U, uint2 *tab, uint32_t *bits, hipStream_t s) {
     for (uint32_t u = 1; u <= U; u++) {
         const uint64_t cnt = 1ULL << (2 * u);
         hipLaunchKernelGGL(k_tab_level, grid_for(cnt), dim3(256), 0, s, ix, u, u > 1 ? tab + tab_base(u - 1) : tab,
                            tab + tab_base(u));
     }
+    hipLaunchKernelGGL(k_tab_bits, grid_for(tab_bits_words(U)), dim3(256), 0, s, (const uint2 *)(tab + tab_base(U)),
+                       U, bits);
 }
 
 void launch_debug_gather4(const Enc4Args &a, uint32_t *d_out, uint32_t *s_out, hipStream_t s) {
