@@ -21,7 +21,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libntcomp_gpu.so")
+# NTC_GPU_LIB: an alternative in-tree build (A/B experiments, ntcomp_amd/csrc/Makefile)
+LIB_PATH = os.environ.get("NTC_GPU_LIB") or os.path.join(_HERE, "libntcomp_gpu.so")
 
 NTC_OK = 0
 STATUS = {

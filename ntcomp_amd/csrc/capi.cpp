@@ -413,13 +413,17 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     // suffix table, levels 1..U, built on the device from the rank lines
     uint32_t U = ctx->tab_u_opt ? std::min<uint32_t>(ctx->tab_u_opt, std::min<uint32_t>(hx.k, kTabMaxU))
                                 : default_tab_u(n, hx.k);
-    void *d_tab, *d_bits;
+    const uint32_t F = filter_level(U);
+    void *d_tab, *d_bits, *d_fbits = nullptr;
     if ((rc = dalloc(tab_base(U + 1) * sizeof(uint2), &d_tab))) return rc;
     if ((rc = dalloc(tab_bits_words(U) * 4, &d_bits))) return rc;
+    if (F && (rc = dalloc(tab_bits_words(F) * 4, &d_fbits))) return rc;
     d.tab = (const uint2 *)d_tab;
     d.tab_bits = (const uint32_t *)d_bits;
+    d.filt_bits = (const uint32_t *)d_fbits;
+    d.filt_f = F;
     d.tab_u = U;
-    launch_tab_build(d, U, (uint2 *)d_tab, (uint32_t *)d_bits, ctx->stream);
+    launch_tab_build(d, U, (uint2 *)d_tab, (uint32_t *)d_bits, F, (uint32_t *)d_fbits, ctx->stream);
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     ctx->n_paths = dv.n_paths;

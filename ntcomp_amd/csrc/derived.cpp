@@ -117,7 +117,22 @@ uint32_t default_tab_u(uint64_t n, uint32_t k) {
     return std::max<uint32_t>(1u, std::min<uint32_t>(u, k));
 }
 
-void build_tab_host(const DevIndex &d, uint32_t U, std::vector<uint2> &tab, std::vector<uint32_t> &bits) {
+// presence bits of level u of a host table
+static void level_bits(const std::vector<uint2> &tab, uint32_t u, std::vector<uint32_t> &bits) {
+    bits.assign(tab_bits_words(u), 0);
+    const uint2 *lv = tab.data() + tab_base(u);
+    const uint64_t cnt = 1ULL << (2 * u);
+    if (cnt >= 32) {
+        for (uint64_t w = 0; w < cnt / 32; w++) bits[w] = tab_bits_word(lv, w);
+    } else {
+        for (uint64_t key = 0; key < cnt; key++) bits[0] |= (uint32_t)tab_long(lv[key]) << key;
+    }
+}
+
+uint32_t filter_level(uint32_t U) { return U >= kFiltMinU ? U - kFiltGap : 0; }
+
+void build_tab_host(const DevIndex &d, uint32_t U, std::vector<uint2> &tab, std::vector<uint32_t> &bits,
+                    std::vector<uint32_t> &fbits) {
     tab.assign(tab_base(U + 1), mk2(0, 0));
     for (uint32_t u = 1; u <= U; u++) {
         uint2 *cur = tab.data() + tab_base(u);
@@ -125,12 +140,9 @@ void build_tab_host(const DevIndex &d, uint32_t U, std::vector<uint2> &tab, std:
         const uint64_t cnt = 1ULL << (2 * u);
         for (uint64_t key = 0; key < cnt; key++) cur[key] = tab_make(d, u, key, prev);
     }
-    const uint64_t nb = tab_bits_words(U);
-    bits.assign(nb, 0);
-    const uint64_t full = (1ULL << (2 * U)) / 32;
-    for (uint64_t w = 0; w < full; w++) bits[w] = tab_bits_word(tab.data() + tab_base(U), w);
-    for (uint64_t key = full * 32; key < (1ULL << (2 * U)); key++)  // U < 3: fewer than 32 keys
-        bits[0] |= (uint32_t)tab_long(tab[tab_base(U) + key]) << key;
+    level_bits(tab, U, bits);
+    fbits.clear();
+    if (filter_level(U)) level_bits(tab, filter_level(U), fbits);
 }
 
 namespace {

@@ -36,7 +36,11 @@ void build_paths(const HostIndex &ix, Derived &dv);
 // Suffix-table depth U for an index of n nodes (encode_core.h "Suffix table").
 uint32_t default_tab_u(uint64_t n, uint32_t k);
 // Host build of the suffix table levels 1..U (test emulation; the GPU builds it on device).
-void build_tab_host(const DevIndex &d, uint32_t U, std::vector<uint2> &tab, std::vector<uint32_t> &bits);
+// (bits: presence of level U; fbits: presence of the filter level, or empty).
+void build_tab_host(const DevIndex &d, uint32_t U, std::vector<uint2> &tab, std::vector<uint32_t> &bits,
+                    std::vector<uint32_t> &fbits);
+// Level of the SCAN pre-filter bitmap for depth U (0 = none).
+uint32_t filter_level(uint32_t U);
 
 // Validates the index and fills rank lines, unique-predecessor bits, pred and code.
 bool build_derived(const HostIndex &ix, Derived &out, std::string &err, int threads);

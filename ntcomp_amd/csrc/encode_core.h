@@ -61,6 +61,8 @@ struct DevIndex {
     const uint64_t *puniq;        // bit j: that node's (k-1)-suffix group is a singleton
     const uint2 *tab;             // suffix table, levels 1..tab_u (see tab_make)
     const uint32_t *tab_bits;     // bit key of level tab_u: that U-mer is present (long)
+    const uint32_t *filt_bits;    // presence bits of level filt_f = U - 2 (L2-resident), or null
+    uint32_t filt_f;              // 0: no filter
     uint32_t tab_u;               // U: longest tabulated length (1 <= U <= min(k, 14))
     uint32_t absent;              // bit c: no node ends with character c
 };
@@ -315,7 +317,9 @@ constexpr uint32_t kTabMaxU = 14;            // 4^14 entries x 8 B at the top le
 NTC_HD uint64_t tab_base(uint32_t u) { return ((1ULL << (2 * u)) - 4) / 3; }
 NTC_HD bool tab_long(uint2 e) { return e.y < kTabShort; }
 NTC_HD uint64_t tab_bits_words(uint32_t U) { return U >= 3 ? (1ULL << (2 * U)) / 32 : 1; }
-// presence bits of the top level: bit key of word key / 32
+constexpr uint32_t kFiltGap = 2;   // filter level F = U - kFiltGap
+constexpr uint32_t kFiltMinU = 12; // below this the level-U bitmap is small enough alone
+// presence bits of one level: bit key of word key / 32
 NTC_HD uint32_t tab_bits_word(const uint2 *top, uint64_t w) {
     uint32_t b = 0;
     for (uint32_t i = 0; i < 32; i++) b |= (uint32_t)tab_long(top[32 * w + i]) << i;
@@ -368,7 +372,7 @@ struct BaseReader {
     }
 };
 
-enum : uint32_t { kModeScan = 0, kModeExt = 1, kModeP1 = 2, kModeBs = 3 };
+enum : uint32_t { kModeScan = 0, kModeExt = 1, kModeP1 = 2, kModeBs = 3, kModeBrk = 4 };
 constexpr uint32_t kScanW = 16;      // presence probes per SCAN unit (U + kScanW - 1 <= 32)
 constexpr uint32_t kScanFirstW = 4;  // first SCAN of a read: error-free starts pair at once
 
@@ -630,10 +634,10 @@ struct MsLane {
                 p += m;
                 j += m;
                 d = d + m < k ? d + m : k;
-                l = ix.colex_at[j] & 0x7FFFFFFFu;
-                r = l + 1;
                 if (p >= len) return 1;
-                window(p + 1 - U);  // issued with the colex_at load
+                // the run broke at p (mostly a sequencing error): table first
+                window(p + 1 - U);
+                mode = kModeBrk;
                 return 0;
             }
         }
@@ -647,12 +651,27 @@ struct MsLane {
             if (W > hi) W = hi;
             if (W > len - p) W = len - p;
             hi = kScanW;
-            uint32_t longm = 0;
             NTC_STAT(5);
-            ntc_stat_add(6, W);
+            // a present U-mer has present F-mer prefix and suffix (F = U - 2): test those
+            // in the small level-F bitmap first; the F-mer suffix of position y's U-mer is
+            // the F-mer prefix of y + 2's, so W + 2 filter bits cover W positions
+            uint32_t cand = (1u << W) - 1u;
+            if (ix.filt_f) {
+                const uint32_t F = ix.filt_f;
+                uint32_t fm = 0;  // bit i: F-mer ending at p - 2 + i is present
+#pragma unroll
+                for (uint32_t i = 0; i < kScanW + kFiltGap; i++)
+                    if (i < W + kFiltGap) {
+                        const uint64_t fk = (qw >> (2 * (p + 1 - U + i - qb))) & ((1ULL << (2 * F)) - 1);
+                        fm |= ((ix.filt_bits[fk >> 5] >> (fk & 31)) & 1u) << i;
+                    }
+                cand &= fm & (fm >> kFiltGap);
+            }
+            uint32_t longm = 0;
 #pragma unroll
             for (uint32_t i = 0; i < kScanW; i++)
-                if (i < W) {
+                if ((cand >> i) & 1u) {
+                    NTC_STAT(6);
                     const uint64_t key = key_at(p + i, U);
                     longm |= ((ix.tab_bits[key >> 5] >> (key & 31)) & 1u) << i;
                 }
@@ -673,6 +692,21 @@ struct MsLane {
             return 0;
         }
         if (!covers(p + 1 - U, p)) window(p + 1 - U);
+        if (mode == kModeBrk) {
+            NTC_STAT(14);
+            const uint2 te = load2(ix.tab + tab_base(U) + key_at(p, U));
+            const uint32_t v = ix.colex_at[j] & 0x7FFFFFFFu;  // node before p, for a long p
+            if (!tab_long(te)) {
+                p += U - (te.y & 0xFFu);
+                mode = kModeScan;
+                hi = kScanW;
+                return p >= len ? 1 : 0;
+            }
+            l = v;
+            r = v + 1;
+            mode = kModeExt;
+            return 0;
+        }
         const int c = (int)((qw >> (2 * (p - qb))) & 3u);
         if (mode == kModeExt) {
             const uint2 te = load2(ix.tab + tab_base(U) + key_at(p, U));  // for a failure

@@ -435,7 +435,7 @@ __global__ __launch_bounds__(256) void k_tab_level(DevIndex ix, uint32_t u, cons
     cur[key] = tab_make(ix, u, key, prev);
 }
 
-__global__ __launch_bounds__(256) void k_tab_bits(const uint2 *top, uint32_t U, uint32_t *bits) {
+__global__ __launch_bounds__(256) void k_tab_bits(const uint2 *top, uint32_t U, uint32_t *bits) {  // level U
     const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (w >= tab_bits_words(U)) return;
     if (U >= 3) {
@@ -447,7 +447,8 @@ __global__ __launch_bounds__(256) void k_tab_bits(const uint2 *top, uint32_t U, 
     }
 }
 
-void launch_tab_build(const DevIndex &ix, uint32_t U, uint2 *tab, uint32_t *bits, hipStream_t s) {
+void launch_tab_build(const DevIndex &ix, uint32_t U, uint2 *tab, uint32_t *bits, uint32_t F, uint32_t *fbits,
+                      hipStream_t s) {
     for (uint32_t u = 1; u <= U; u++) {
         const uint64_t cnt = 1ULL << (2 * u);
         hipLaunchKernelGGL(k_tab_level, grid_for(cnt), dim3(256), 0, s, ix, u, u > 1 ? tab + tab_base(u - 1) : tab,
@@ -455,6 +456,9 @@ void launch_tab_build(const DevIndex &ix, uint32_t U, uint2 *tab, uint32_t *bits
     }
     hipLaunchKernelGGL(k_tab_bits, grid_for(tab_bits_words(U)), dim3(256), 0, s, (const uint2 *)(tab + tab_base(U)),
                        U, bits);
+    if (F)
+        hipLaunchKernelGGL(k_tab_bits, grid_for(tab_bits_words(F)), dim3(256), 0, s,
+                           (const uint2 *)(tab + tab_base(F)), F, fbits);
 }
 
 void launch_debug_gather4(const Enc4Args &a, uint32_t *d_out, uint32_t *s_out, hipStream_t s) {

@@ -15,7 +15,7 @@ using namespace ntc;
 
 namespace {
 bool load(const ntc_index_view *v, HostIndex &hx, Derived &dv, std::vector<WalkEntry> &walk, DevIndex &d,
-          std::vector<uint2> &tab, std::vector<uint32_t> &bits, uint32_t tab_u = 0) {
+          std::vector<uint2> &tab, std::vector<uint32_t> &bits, std::vector<uint32_t> &fbits, uint32_t tab_u = 0) {
     hx.n = v->n_nodes;
     hx.k = v->k;
     uint64_t nw = (hx.n + 63) / 64;
@@ -30,9 +30,11 @@ bool load(const ntc_index_view *v, HostIndex &hx, Derived &dv, std::vector<WalkE
     build_walk_host(dv, hx.n, walk);
     d = host_dev_index(hx, dv, walk);
     const uint32_t U = tab_u ? std::min<uint32_t>(tab_u, std::min<uint32_t>(hx.k, kTabMaxU)) : default_tab_u(hx.n, hx.k);
-    build_tab_host(d, U, tab, bits);
+    build_tab_host(d, U, tab, bits, fbits);
     d.tab = tab.data();
     d.tab_bits = bits.data();
+    d.filt_f = fbits.empty() ? 0u : filter_level(U);
+    d.filt_bits = fbits.empty() ? nullptr : fbits.data();
     d.tab_u = U;
     return true;
 }
@@ -45,9 +47,9 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
     Derived dv;
     std::vector<WalkEntry> walk;
     std::vector<uint2> tab;
-    std::vector<uint32_t> bits;
+    std::vector<uint32_t> bits, fbits;
     DevIndex d;
-    if (!load(v, hx, dv, walk, d, tab, bits, (uint32_t)tab_u)) return NTC_ERR_FORMAT;
+    if (!load(v, hx, dv, walk, d, tab, bits, fbits, (uint32_t)tab_u)) return NTC_ERR_FORMAT;
     if (!use_paths) d.has_paths = 0;
     *bad = -1;
     uint64_t tiles = (n_reads + 63) / 64, total = 0;
@@ -118,9 +120,9 @@ extern "C" int emu_decode(const ntc_index_view *v, const uint64_t *recs, uint64_
     Derived dv;
     std::vector<WalkEntry> walk;
     std::vector<uint2> tab;
-    std::vector<uint32_t> bits;
+    std::vector<uint32_t> bits, fbits;
     DevIndex d;
-    if (!load(v, hx, dv, walk, d, tab, bits, 1)) return NTC_ERR_FORMAT;
+    if (!load(v, hx, dv, walk, d, tab, bits, fbits, 1)) return NTC_ERR_FORMAT;
     std::vector<uint64_t> starts;
     uint64_t total = 0;
     for (uint64_t r = 0; r < n; r++) {
