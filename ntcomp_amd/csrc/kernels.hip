@@ -46,15 +46,64 @@ __global__ __launch_bounds__(256) void k_encode(EncodeArgs a) {
     }
 }
 
-// ---- v4 ---------------------------------------------------------------------------
-// pack the batch's bases (position space: character x = batch position x) 32 per thread:
-// consecutive threads read consecutive 32-byte chunks (coalesced); bad bytes report the
-// read that holds them.
-__global__ __launch_bounds__(256) void k_pack(Enc4Args a, uint64_t total) {
+// ---- encode pipeline --------------------------------------------------------------
+// The batch's bases as 2-bit codes (position space: character x = batch position x), 32
+// per thread.  Bad bytes (non-ACGT or a character no node ends with) report the read that
+// holds them.
+__device__ __forceinline__ void pack_report_bad(const Enc4Args &a, const uint8_t *B, uint64_t x0, uint32_t n,
+                                                uint32_t absent) {
+    for (uint32_t t = 0; t < n; t++) {
+        if (!is_acgt(B[x0 + t]) || ((absent >> fast_code(B[x0 + t])) & 1u)) {  // its read
+            uint64_t lo = 0, hi = a.n_reads;
+            const uint64_t pos = a.offs[0] + x0 + t;
+            while (hi - lo > 1) {
+                const uint64_t mid = (lo + hi) >> 1;
+                if (a.offs[mid] <= pos) lo = mid; else hi = mid;
+            }
+            atomicMin(a.status, (unsigned long long)((lo << 8) | (uint64_t)kErrInvalidBase));
+            return;
+        }
+    }
+}
+
+// 4 ASCII bases -> 8 bits of 2-bit codes (SWAR); ok = all four are A/C/G/T present in the index
+__device__ __forceinline__ uint32_t pack4(uint32_t w, uint32_t absent_tab, bool &ok) {
+    const uint32_t t = ((w >> 1) ^ (w >> 2)) & 0x03030303u;  // A,C,G,T -> 0,1,2,3 per byte
+    ok &= __builtin_amdgcn_perm(0u, 0x54474341u, t) == w;     // code -> "ACGT"[code] round trip
+    ok &= __builtin_amdgcn_perm(0u, absent_tab, t) == 0u;     // absent characters
+    const uint32_t u = t | (t >> 6);
+    return (u | (u >> 12)) & 0xFFu;
+}
+
+// Thread b packs characters [32b, 32b + 32).  `bound` (>= the batch's bases) only sizes
+// the grid; the true count is offs[n] - offs[0].  A 16-byte aligned batch start (uniform
+// over the grid) takes the fast path: two aligned uint4 loads, consecutive lanes reading
+// consecutive 32-byte chunks; otherwise three aligned loads are realigned per byte.
+__global__ __launch_bounds__(256) void k_pack(Enc4Args a, uint64_t bound) {
     const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     const uint64_t x0 = b * 32;
+    if (x0 >= bound) return;
+    const uint64_t total = a.offs[a.n_reads] - a.offs[0];
     if (x0 >= total) return;
     const uint8_t *B = a.bases + a.offs[0];
+    const uint32_t absent = a.ix.absent;
+    const uint32_t n = total - x0 < 32 ? (uint32_t)(total - x0) : 32u;
+    if ((((uintptr_t)B) & 15) == 0 && n == 32) {
+        const uint32_t absent_tab = (absent & 1u) | ((absent >> 1) & 1u) << 8 | ((absent >> 2) & 1u) << 16 |
+                                    ((absent >> 3) & 1u) << 24;
+        const uint4 v0 = *reinterpret_cast<const uint4 *>(B + x0);
+        const uint4 v1 = *reinterpret_cast<const uint4 *>(B + x0 + 16);
+        bool ok = true;
+        const uint32_t lo = pack4(v0.x, absent_tab, ok) | pack4(v0.y, absent_tab, ok) << 8 |
+                            pack4(v0.z, absent_tab, ok) << 16 | pack4(v0.w, absent_tab, ok) << 24;
+        const uint32_t hi = pack4(v1.x, absent_tab, ok) | pack4(v1.y, absent_tab, ok) << 8 |
+                            pack4(v1.z, absent_tab, ok) << 16 | pack4(v1.w, absent_tab, ok) << 24;
+        a.Q[b] = (uint64_t)lo | ((uint64_t)hi << 32);
+        if (!ok) pack_report_bad(a, B, x0, 32, absent);
+        return;
+    }
+    // unaligned start or the last partial chunk: 16-byte blocks never cross a page, so
+    // reading a whole block that holds the batch's last byte stays inside its allocation
     const uint8_t *end = B + total;
     const uint8_t *p = B + x0;
     const uintptr_t al = (uintptr_t)p & ~(uintptr_t)15;
@@ -70,13 +119,11 @@ __global__ __launch_bounds__(256) void k_pack(Enc4Args a, uint64_t total) {
             w[4 * q] = w[4 * q + 1] = w[4 * q + 2] = w[4 * q + 3] = 0x41414141u;
         }
     }
-    const uint32_t n = total - x0 < 32 ? (uint32_t)(total - x0) : 32u;
     uint64_t acc = 0;
     bool bad = false;
-    const uint32_t absent = a.ix.absent;
 #pragma unroll
     for (uint32_t t = 0; t < 32; t++) {
-        const uint32_t o = sh + t;  // byte index into w (static after unrolling but sh)
+        const uint32_t o = sh + t;
         const uint32_t word = o >> 2;
         uint32_t wv = w[0];
 #pragma unroll
@@ -88,20 +135,7 @@ __global__ __launch_bounds__(256) void k_pack(Enc4Args a, uint64_t total) {
         }
     }
     a.Q[b] = acc;
-    if (bad) {
-        for (uint32_t t = 0; t < n; t++) {
-            if (!is_acgt(B[x0 + t]) || ((absent >> fast_code(B[x0 + t])) & 1u)) {  // its read
-                uint64_t lo = 0, hi = a.n_reads;
-                const uint64_t pos = a.offs[0] + x0 + t;
-                while (hi - lo > 1) {
-                    const uint64_t mid = (lo + hi) >> 1;
-                    if (a.offs[mid] <= pos) lo = mid; else hi = mid;
-                }
-                atomicMin(a.status, (unsigned long long)((lo << 8) | (uint64_t)kErrInvalidBase));
-                break;
-            }
-        }
-    }
+    if (bad) pack_report_bad(a, B, x0, n, absent);
 }
 
 constexpr uint32_t kPoolChunk = 64;

@@ -187,3 +187,38 @@ def test_gpu_full_scale_roundtrip_c91():
     exp, eoff = orc.encode(reads[: m * L], offs[: m + 1])
     assert np.array_equal(recs[: int(roff[m])], exp)
     ctx.close()
+
+
+@pytest.mark.parametrize("lead", [0, 3, 16, 37])
+def test_gpu_device_api_unaligned_ragged(ctx, lead):
+    """Batch starting `lead` bytes into the caller's buffer (offs[0] = lead), ragged reads and
+    an over-estimated max_read_len: records equal the host API's, nothing read past the end."""
+    genome = nt.synth_genome(12, 200_000)
+    ix = nt.Index.build([genome.tobytes()], 31)
+    ctx.upload(ix)
+    rng = np.random.default_rng(lead)
+    g = genome.tobytes()
+    reads = []
+    for _ in range(3000):
+        L = int(rng.integers(1, 300))
+        st = int(rng.integers(0, len(g) - L))
+        reads.append(g[st:st + L])
+    bases, offs = pack_reads(reads)
+    exp, eoff = ctx.encode(bases, offs)
+    buf = np.concatenate([np.frombuffer(b"N" * lead, dtype=np.uint8), bases])
+    offs_l = offs + np.uint64(lead)
+    n = len(reads)
+    db, do = ctx.alloc(buf.nbytes), ctx.alloc(offs_l.nbytes)
+    dr, dro = ctx.alloc(len(bases) * 8 + 64), ctx.alloc(offs_l.nbytes)
+    try:
+        ctx.h2d(db, buf)
+        ctx.h2d(do, offs_l)
+        for max_len in (400, 0):
+            ctx.encode_device(db, do, n, max_len, dr, len(bases) + 8, dro)
+            nrec = ctx.encode_status()
+            got = ctx.d2h(np.zeros(nrec, dtype=np.uint64), dr)
+            gro = ctx.d2h(np.zeros(n + 1, dtype=np.uint64), dro)
+            assert np.array_equal(got, exp) and np.array_equal(gro, eoff)
+    finally:
+        for p in (db, do, dr, dro):
+            ctx.free(p)
