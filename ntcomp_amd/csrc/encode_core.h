@@ -441,6 +441,15 @@ NTC_HD uint32_t ones_down(const uint64_t *w, uint32_t a, uint32_t maxn) {
     return cnt < maxn ? cnt : maxn;
 }
 
+NTC_HD Entry load_entry(const Entry *E, int32_t i) {
+#ifdef __HIP_DEVICE_COMPILE__
+    const uint4 v = *reinterpret_cast<const uint4 *>(E + i);
+    return Entry{v.x, v.y, v.z, v.w};
+#else
+    return E[i];
+#endif
+}
+
 // Right-to-left reader of one read's entries (+ suffix table for uncovered positions).
 struct EntryView {
     const Entry *E;
@@ -449,19 +458,29 @@ struct EntryView {
     uint64_t qo;
     uint32_t k;
     int32_t e;  // cursor (-1: the read has no entries); moves left only
+    Entry cur;  // E[e]
+    NTC_HD EntryView(const Entry *E_, const DevIndex *ix_, const uint64_t *Q_, uint64_t qo_, uint32_t k_, int32_t e_)
+        : E(E_), ix(ix_), Q(Q_), qo(qo_), k(k_), e(e_), cur{0, 0, 0, 0} {
+        if (e >= 0) cur = load_entry(E, e);
+    }
     NTC_HD void seek(uint32_t x) {  // last entry with p <= x, or entry 0
-        if (e <= 0) return;
-        const uint32_t pe = E[e].p;
-        if (pe <= x) return;
-        // every entry covers >= 1 position, so entry e - (pe - x) starts at or before x
-        int32_t g = e - (int32_t)(pe - x);
+        if (e <= 0 || cur.p <= x) return;
+        // every entry covers >= 1 position, so entry e - (p - x) starts at or before x
+        int32_t g = e - (int32_t)(cur.p - x);
         if (g < 0) g = 0;
-        while (g + 1 < e && E[g + 1].p <= x) g++;
+        Entry eg = load_entry(E, g);
+        while (g + 1 < e) {
+            const Entry nx = load_entry(E, g + 1);
+            if (nx.p > x) break;
+            g++;
+            eg = nx;
+        }
         e = g;
+        cur = eg;
     }
     NTC_HD bool covered(uint32_t x) {
         seek(x);
-        return e >= 0 && E[e].p <= x && x < E[e].p + E[e].m;
+        return e >= 0 && cur.p <= x && x < cur.p + cur.m;
     }
     NTC_HD uint32_t dval(const Entry &en, uint32_t x) const {
         const uint32_t d0 = en.dk & 0xFFu;
@@ -472,16 +491,19 @@ struct EntryView {
         return (en.dk & kRunTag) ? (ix->colex_at[en.v + (x - en.p)] & 0x7FFFFFFFu) : en.v;
     }
     NTC_HD uint32_t D(uint32_t x) {
-        if (covered(x)) return dval(E[e], x);
+        if (covered(x)) return dval(cur, x);
         uint32_t d, s;
         tab_ds(*ix, Q, qo, x, d, s);
         return d;
     }
-    NTC_HD uint32_t S(uint32_t x) {
-        if (covered(x)) return sval(E[e], x);
-        uint32_t d, s;
-        tab_ds(*ix, Q, qo, x, d, s);
-        return s;
+    // d at x, and S at x when S is needed for a record (d > 11 or d = k)
+    NTC_HD void DS(uint32_t x, uint32_t &d, uint32_t &s) {
+        if (covered(x)) {
+            d = dval(cur, x);
+            s = (d > 11 || d == k) ? sval(cur, x) : 0u;
+        } else {
+            tab_ds(*ix, Q, qo, x, d, s);
+        }
     }
     // consecutive positions x, x-1, ... with d = k and a singleton (k-1)-suffix group
     // (left_extend_kmer's per-step test)
@@ -489,9 +511,10 @@ struct EntryView {
         int32_t c = e;
         uint32_t cnt = 0;
         int64_t pos = x;
+        Entry en = cur;
         while (cnt < cap && pos >= 0) {
-            while (c > 0 && E[c].p > (uint32_t)pos) c--;
-            if (!(c >= 0 && E[c].p <= (uint32_t)pos && (uint32_t)pos < E[c].p + E[c].m)) {
+            while (c > 0 && en.p > (uint32_t)pos) en = load_entry(E, --c);
+            if (!(c >= 0 && en.p <= (uint32_t)pos && (uint32_t)pos < en.p + en.m)) {
                 // uncovered: d = min(pos + 1, U), = k only for U = k and a long position
                 if (ix->tab_u != k || (uint32_t)pos + 1 < k) break;
                 uint32_t d, s;
@@ -501,7 +524,6 @@ struct EntryView {
                 pos--;
                 continue;
             }
-            const Entry &en = E[c];
             const uint32_t d0 = en.dk & 0xFFu;
             if (!(en.dk & kRunTag)) {
                 if (d0 != k || !uniq_bit(*ix, en.v)) break;
@@ -752,7 +774,7 @@ struct MsLane {
 // (d, S) of every position of one read (diagnostics: ntc_debug_matching_statistics)
 NTC_HD void read_ms(const DevIndex &ix, const uint64_t *Q, uint64_t qo, const Entry *E, uint32_t ne,
                     uint32_t len, uint32_t *d_out, uint32_t *s_out) {
-    EntryView ev{E, &ix, Q, qo, ix.k, -1};
+    EntryView ev(E, &ix, Q, qo, ix.k, -1);
     uint32_t x = 0;
     for (uint32_t i = 0; i <= ne && x < len; i++) {
         const uint32_t until = i < ne ? E[i].p : len;
@@ -769,16 +791,15 @@ NTC_HD void read_ms(const DevIndex &ix, const uint64_t *Q, uint64_t qo, const En
 NTC_HD int parse_read(const DevIndex &ix, const uint64_t *Q, uint64_t qo, const Entry *E, uint32_t ne,
                       uint32_t len, uint64_t *R) {
     const uint32_t k = ix.k;
-    EntryView ev{E, &ix, Q, qo, k, (int32_t)ne - 1};
+    EntryView ev(E, &ix, Q, qo, k, (int32_t)ne - 1);
     uint32_t i = len;
     int nrec = 0;
     while (i > 0) {
         const uint32_t x = i - 1;
-        const uint32_t di = ev.D(x);
+        uint32_t di, st;
+        ev.DS(x, di, st);
         const uint32_t segend = i;
         uint32_t seglen;
-        uint32_t st = 0;
-        if (di > 11 || di == k) st = ev.S(x);
         if (di == k && i > k + 1) {
             const uint32_t ext = ev.run_from(i - 2, i - k - 1);
             const uint32_t L = k + ext;
