@@ -376,16 +376,14 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     if (result != (WalkEntry *)d_walk_a)
         HIP_TRY(ctx, hipMemcpyAsync(d_walk_a, result, n * sizeof(WalkEntry), hipMemcpyDeviceToDevice,
                                     ctx->stream));
-    void *d_ptext = nullptr, *d_colex_at = nullptr, *d_pos = nullptr, *d_pvalid = nullptr, *d_puniq = nullptr;
+    void *d_pstream = nullptr, *d_colex_at = nullptr, *d_pos = nullptr, *d_puniq = nullptr;
     if (dv.has_paths) {
-        if ((rc = dalloc(dv.pvalid.size() * 8, &d_pvalid))) return rc;
         if ((rc = dalloc(dv.puniq.size() * 8, &d_puniq))) return rc;
-        HIP_TRY(ctx, hipMemcpy(d_pvalid, dv.pvalid.data(), dv.pvalid.size() * 8, hipMemcpyHostToDevice));
         HIP_TRY(ctx, hipMemcpy(d_puniq, dv.puniq.data(), dv.puniq.size() * 8, hipMemcpyHostToDevice));
-        if ((rc = dalloc(dv.ptext.size() * 8, &d_ptext))) return rc;
+        if ((rc = dalloc(dv.pstream.size() * 16, &d_pstream))) return rc;
         if ((rc = dalloc(dv.colex_at.size() * 4 + 64, &d_colex_at))) return rc;
         if ((rc = dalloc(dv.pos_of_node.size() * 4, &d_pos))) return rc;
-        HIP_TRY(ctx, hipMemcpy(d_ptext, dv.ptext.data(), dv.ptext.size() * 8, hipMemcpyHostToDevice));
+        HIP_TRY(ctx, hipMemcpy(d_pstream, dv.pstream.data(), dv.pstream.size() * 16, hipMemcpyHostToDevice));
         HIP_TRY(ctx, hipMemcpy(d_colex_at, dv.colex_at.data(), dv.colex_at.size() * 4, hipMemcpyHostToDevice));
         HIP_TRY(ctx, hipMemcpy(d_pos, dv.pos_of_node.data(), dv.pos_of_node.size() * 4, hipMemcpyHostToDevice));
     }
@@ -404,10 +402,9 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     d.t_jump = dv.t_jump;
     for (int c = 0; c < 5; c++) d.C[c] = dv.C[c];
     d.has_paths = dv.has_paths ? 1u : 0u;
-    d.ptext = (const uint64_t *)d_ptext;
+    d.pstream = (const uint4 *)d_pstream;
     d.colex_at = (const uint32_t *)d_colex_at;
     d.pos_of_node = (const uint32_t *)d_pos;
-    d.pvalid = (const uint64_t *)d_pvalid;
     d.puniq = (const uint64_t *)d_puniq;
     d.absent = dv.absent;
     // suffix table, levels 1..U, built on the device from the rank lines
@@ -423,6 +420,7 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     d.filt_bits = (const uint32_t *)d_fbits;
     d.filt_f = F;
     d.tab_u = U;
+    d.tab_pos = (dv.has_paths && U >= dv.t_jump && n < (1ULL << 31)) ? 1u : 0u;
     launch_tab_build(d, U, (uint2 *)d_tab, (uint32_t *)d_bits, F, (uint32_t *)d_fbits, ctx->stream);
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));

@@ -138,7 +138,7 @@ void build_tab_host(const DevIndex &d, uint32_t U, std::vector<uint2> &tab, std:
         uint2 *cur = tab.data() + tab_base(u);
         const uint2 *prev = u > 1 ? tab.data() + tab_base(u - 1) : nullptr;
         const uint64_t cnt = 1ULL << (2 * u);
-        for (uint64_t key = 0; key < cnt; key++) cur[key] = tab_make(d, u, key, prev);
+        for (uint64_t key = 0; key < cnt; key++) cur[key] = tab_make(d, u, key, prev, d.tab_pos && u == U);
     }
     level_bits(tab, U, bits);
     fbits.clear();
@@ -239,10 +239,15 @@ void build_paths(const HostIndex &ix, Derived &dv) {
     if (tlen + 64 >= (1ULL << 31)) return;
     dv.colex_at.assign(tlen + 8, kNoNode);
     dv.pos_of_node.assign(n, kNoNode);
-    dv.ptext.assign(tlen / 32 + k / 32 + 8, 0);  // windows read up to k + 64 chars past a node
-    dv.pvalid.assign(tlen / 64 + 4, 0);
+    // groups read up to k + 64 characters past a node's position
+    dv.pstream.assign((tlen + k) / 32 + 8, uint4{0, 0, 0, 0});
     dv.puniq.assign(tlen / 64 + 4, 0);
-    auto put = [&](uint64_t t, uint32_t c) { dv.ptext[t >> 5] |= (uint64_t)(c & 3) << (2 * (t & 31)); };
+    auto put = [&](uint64_t t, uint32_t c) {
+        uint4 &g = dv.pstream[t >> 5];
+        const uint32_t o = (uint32_t)(t & 31);
+        if (o < 16) g.x |= (c & 3u) << (2 * o);
+        else g.y |= (c & 3u) << (2 * (o - 16));
+    };
     uint64_t b = 0;
     std::vector<uint8_t> first(k);
     for (uint64_t p = 0; p < np; p++) {
@@ -261,7 +266,8 @@ void build_paths(const HostIndex &ix, Derived &dv) {
             const uint32_t u = (dv.uniq[node >> 5] >> (node & 31)) & 1u;
             dv.colex_at[pos] = node | (u << 31);
             dv.pos_of_node[node] = (uint32_t)pos;
-            dv.pvalid[pos >> 6] |= 1ULL << (pos & 63);
+            const uint64_t end = pos + k - 1;  // the node's k-mer ends at text position end
+            dv.pstream[end >> 5].z |= 1u << (end & 31);
             if (u) dv.puniq[pos >> 6] |= 1ULL << (pos & 63);
         }
         b += (e - a) + k;  // last node at b+(e-a)-1; positions up to b+(e-a)+k-1 hold no node
@@ -303,10 +309,9 @@ DevIndex host_dev_index(const HostIndex &ix, const Derived &dv, const std::vecto
     d.t_jump = dv.t_jump;
     for (int c = 0; c < 5; c++) d.C[c] = dv.C[c];
     d.has_paths = dv.has_paths ? 1u : 0u;
-    d.ptext = dv.ptext.empty() ? nullptr : dv.ptext.data();
+    d.pstream = dv.pstream.empty() ? nullptr : dv.pstream.data();
     d.colex_at = dv.colex_at.empty() ? nullptr : dv.colex_at.data();
     d.pos_of_node = dv.pos_of_node.empty() ? nullptr : dv.pos_of_node.data();
-    d.pvalid = dv.pvalid.empty() ? nullptr : dv.pvalid.data();
     d.puniq = dv.puniq.empty() ? nullptr : dv.puniq.data();
     d.absent = dv.absent;
     d.tab = nullptr;  // see build_tab_host

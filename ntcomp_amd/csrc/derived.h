@@ -20,10 +20,9 @@ struct Derived {
     // sits at one position of a path text; consecutive positions are graph edges.
     bool has_paths = false;
     uint64_t tlen = 0;               // path text length (characters)
-    std::vector<uint64_t> ptext;     // 2-bit, char t at bits 2(t%32) of word t/32
+    std::vector<uint4> pstream;      // per 32 text chars: {chars lo, chars hi, end bits, 0}
     std::vector<uint32_t> colex_at;  // per text position: node | uniq << 31, or kNoNode
     std::vector<uint32_t> pos_of_node;  // per node: text position of its k-mer, or kNoNode
-    std::vector<uint64_t> pvalid;       // bit j: colex_at[j] != kNoNode
     std::vector<uint64_t> puniq;        // bit j: colex_at[j]'s group is a singleton
     uint64_t n_paths = 0;
     uint32_t absent = 0;                // bit c: C[c+1] == C[c] (no node ends with c)

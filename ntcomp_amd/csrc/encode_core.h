@@ -54,15 +54,15 @@ struct DevIndex {
     uint32_t C[5];          // C[4] = n
     // path walk (encode v2): a path cover of the de Bruijn graph, see derived.cpp
     uint32_t has_paths;
-    const uint64_t *ptext;        // path text, 2-bit, char t at bits 2(t%32) of word t/32
+    const uint4 *pstream;         // path text in 32-char groups: {chars (2-bit, u64), end bits, 0}
     const uint32_t *colex_at;     // node | uniq << 31 at each k-mer start, 0xFFFFFFFF elsewhere
     const uint32_t *pos_of_node;  // text position of each real node's k-mer, or 0xFFFFFFFF
-    const uint64_t *pvalid;       // bit j: colex_at[j] holds a node (encode v3)
     const uint64_t *puniq;        // bit j: that node's (k-1)-suffix group is a singleton
     const uint2 *tab;             // suffix table, levels 1..tab_u (see tab_make)
     const uint32_t *tab_bits;     // bit key of level tab_u: that U-mer is present (long)
     const uint32_t *filt_bits;    // presence bits of level filt_f = U - 2 (L2-resident), or null
     uint32_t filt_f;              // 0: no filter
+    uint32_t tab_pos;             // 1: top-level singleton entries carry the path position
     uint32_t tab_u;               // U: longest tabulated length (1 <= U <= min(k, 14))
     uint32_t absent;              // bit c: no node ends with character c
 };
@@ -312,6 +312,8 @@ NTC_HD int encode_lane(const DevIndex &ix, const uint8_t *q, uint32_t len, uint3
 // entries at tab_base(u); key = the u 2-bit codes, first character in the low bits.
 // ======================================================================================
 constexpr uint32_t kTabShort = 0xFFFFFF00u;  // y >= kTabShort: absent, m = y & 0xFF
+constexpr uint32_t kTabPos = 0x80000000u;    // top level, tab_pos: y = kTabPos | path position
+                                             // of the single node x (interval [x, x + 1))
 constexpr uint32_t kTabMaxU = 14;            // 4^14 entries x 8 B at the top level
 
 NTC_HD uint64_t tab_base(uint32_t u) { return ((1ULL << (2 * u)) - 4) / 3; }
@@ -319,6 +321,18 @@ NTC_HD bool tab_long(uint2 e) { return e.y < kTabShort; }
 NTC_HD uint64_t tab_bits_words(uint32_t U) { return U >= 3 ? (1ULL << (2 * U)) / 32 : 1; }
 constexpr uint32_t kFiltGap = 2;   // filter level F = U - kFiltGap
 constexpr uint32_t kFiltMinU = 12; // below this the level-U bitmap is small enough alone
+// interval of a present top-level entry (+ path position of a single node, or ~0)
+NTC_HD void tab_interval(const DevIndex &ix, uint2 te, uint32_t &l, uint32_t &r, uint32_t &j) {
+    l = te.x;
+    if (ix.tab_pos && (te.y & kTabPos)) {
+        r = l + 1;
+        j = te.y & ~kTabPos;
+    } else {
+        r = te.y;
+        j = 0xFFFFFFFFu;
+    }
+}
+
 // presence bits of one level: bit key of word key / 32
 NTC_HD uint32_t tab_bits_word(const uint2 *top, uint64_t w) {
     uint32_t b = 0;
@@ -329,7 +343,7 @@ NTC_HD uint32_t tab_bits_word(const uint2 *top, uint64_t w) {
 // entry of u-mer `key` from level u-1 (`prev`; unused for u = 1): the u-mer is present
 // iff its (u-1)-prefix is and extends by its last character; else it inherits the
 // longest present suffix of its (u-1)-suffix.
-NTC_HD uint2 tab_make(const DevIndex &ix, uint32_t u, uint64_t key, const uint2 *prev) {
+NTC_HD uint2 tab_make(const DevIndex &ix, uint32_t u, uint64_t key, const uint2 *prev, bool with_pos = false) {
     const int c = (int)((key >> (2 * (u - 1))) & 3u);
     if (u == 1) {
         const uint32_t a = ix.C[c], b = ix.C[c + 1];
@@ -340,7 +354,11 @@ NTC_HD uint2 tab_make(const DevIndex &ix, uint32_t u, uint64_t key, const uint2 
     if (tab_long(pre)) {
         uint32_t nl, nr;
         extend(ix, c, pre.x, pre.y, nl, nr);
-        if (nl < nr) return mk2(nl, nr);
+        if (nl < nr) {
+            if (with_pos && nr == nl + 1 && ix.pos_of_node[nl] != 0xFFFFFFFFu)
+                return mk2(nl, kTabPos | ix.pos_of_node[nl]);
+            return mk2(nl, nr);
+        }
     }
     const uint2 suf = prev[key >> 2];
     return tab_long(suf) ? mk2(suf.x, kTabShort | (u - 1)) : suf;
@@ -641,9 +659,18 @@ struct MsLane {
             NTC_STAT(1);
             for (;;) {
                 NTC_STAT(4);
-                const uint64_t x = window2(Q, qo + p + m) ^ window2(ix.ptext, j + k + m);
+                // path characters after node j's k-mer, and whether the k-mer ending at
+                // each of them is a node, from the interleaved 32-char groups
+                const uint64_t T = (uint64_t)j + k + m;
+                const uint4 g0 = ix.pstream[T >> 5], g1 = ix.pstream[(T >> 5) + 1];
+                const uint32_t sh = (uint32_t)(T & 31);
+                const uint64_t c0 = (uint64_t)g0.x | ((uint64_t)g0.y << 32);
+                const uint64_t c1 = (uint64_t)g1.x | ((uint64_t)g1.y << 32);
+                const uint64_t pc = sh ? ((c0 >> (2 * sh)) | (c1 << (64 - 2 * sh))) : c0;
+                const uint32_t pv = sh ? ((g0.z >> sh) | (g1.z << (32 - sh))) : g0.z;
+                const uint64_t x = window2(Q, qo + p + m) ^ pc;
                 uint32_t lim = x ? ctz64(x) >> 1 : 32u;
-                const uint32_t inv = ctz64(~window1(ix.pvalid, j + 1 + m));
+                const uint32_t inv = ~pv ? (uint32_t)__builtin_ctz(~pv) : 32u;
                 if (inv < lim) lim = inv;
                 if (len - p - m < lim) lim = len - p - m;
                 m += lim;
@@ -707,10 +734,17 @@ struct MsLane {
             NTC_STAT(7);
             const uint32_t x = p + (uint32_t)__builtin_ctz(pairs);  // long, short predecessor
             const uint2 te = load2(lvl + key_at(x, U));
-            l = te.x; r = te.y; d = U;
+            uint32_t jj;
+            tab_interval(ix, te, l, r, jj);
+            d = U;
             p = x + 1;
             mode = kModeExt;
-            note_single(ix);
+            if (ix.tab_pos) {  // the table already holds the path position (d = U >= t_jump)
+                j = jj;
+                try_run = jj != 0xFFFFFFFFu;
+            } else {
+                note_single(ix);
+            }
             return 0;
         }
         if (!covers(p + 1 - U, p)) window(p + 1 - U);
@@ -745,8 +779,10 @@ struct MsLane {
                 return p >= len ? 1 : 0;
             }
             NTC_STAT(11);
-            if (d == U) return commit(ix, te.x, te.y, U);  // t* = U - 1
-            lo = U - 1; bl = te.x; bR = te.y;  // ext(I_{U-1}, c) = the U-mer's interval
+            uint32_t tl, tr, tj;
+            tab_interval(ix, te, tl, tr, tj);
+            if (d == U) return commit(ix, tl, tr, U);  // t* = U - 1
+            lo = U - 1; bl = tl; bR = tr;  // ext(I_{U-1}, c) = the U-mer's interval
             hi = d - 1;
             mode = kModeP1;
             return 0;

@@ -466,7 +466,7 @@ __global__ __launch_bounds__(256) void k_debug_gather4(Enc4Args a, uint32_t *d_o
 __global__ __launch_bounds__(256) void k_tab_level(DevIndex ix, uint32_t u, const uint2 *prev, uint2 *cur) {
     const uint64_t key = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (key >> (2 * u)) return;
-    cur[key] = tab_make(ix, u, key, prev);
+    cur[key] = tab_make(ix, u, key, prev, ix.tab_pos && u == ix.tab_u);
 }
 
 __global__ __launch_bounds__(256) void k_tab_bits(const uint2 *top, uint32_t U, uint32_t *bits) {  // level U

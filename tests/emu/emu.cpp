@@ -30,6 +30,8 @@ bool load(const ntc_index_view *v, HostIndex &hx, Derived &dv, std::vector<WalkE
     build_walk_host(dv, hx.n, walk);
     d = host_dev_index(hx, dv, walk);
     const uint32_t U = tab_u ? std::min<uint32_t>(tab_u, std::min<uint32_t>(hx.k, kTabMaxU)) : default_tab_u(hx.n, hx.k);
+    d.tab_u = U;
+    d.tab_pos = (dv.has_paths && U >= dv.t_jump && hx.n < (1ULL << 31)) ? 1u : 0u;
     build_tab_host(d, U, tab, bits, fbits);
     d.tab = tab.data();
     d.tab_bits = bits.data();
