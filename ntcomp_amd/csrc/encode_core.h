@@ -659,22 +659,38 @@ struct MsLane {
             NTC_STAT(1);
             for (;;) {
                 NTC_STAT(4);
-                // path characters after node j's k-mer, and whether the k-mer ending at
-                // each of them is a node, from the interleaved 32-char groups
+                // 64 path characters after node j's k-mer, and whether the k-mer ending at
+                // each of them is a node, from three interleaved 32-char groups
                 const uint64_t T = (uint64_t)j + k + m;
-                const uint4 g0 = ix.pstream[T >> 5], g1 = ix.pstream[(T >> 5) + 1];
+                const uint4 g0 = ix.pstream[T >> 5], g1 = ix.pstream[(T >> 5) + 1], g2 = ix.pstream[(T >> 5) + 2];
                 const uint32_t sh = (uint32_t)(T & 31);
                 const uint64_t c0 = (uint64_t)g0.x | ((uint64_t)g0.y << 32);
                 const uint64_t c1 = (uint64_t)g1.x | ((uint64_t)g1.y << 32);
-                const uint64_t pc = sh ? ((c0 >> (2 * sh)) | (c1 << (64 - 2 * sh))) : c0;
-                const uint32_t pv = sh ? ((g0.z >> sh) | (g1.z << (32 - sh))) : g0.z;
-                const uint64_t x = window2(Q, qo + p + m) ^ pc;
-                uint32_t lim = x ? ctz64(x) >> 1 : 32u;
-                const uint32_t inv = ~pv ? (uint32_t)__builtin_ctz(~pv) : 32u;
-                if (inv < lim) lim = inv;
+                const uint64_t c2 = (uint64_t)g2.x | ((uint64_t)g2.y << 32);
+                const uint64_t pa = sh ? ((c0 >> (2 * sh)) | (c1 << (64 - 2 * sh))) : c0;
+                const uint64_t pb = sh ? ((c1 >> (2 * sh)) | (c2 << (64 - 2 * sh))) : c1;
+                const uint32_t va = sh ? ((g0.z >> sh) | (g1.z << (32 - sh))) : g0.z;
+                const uint32_t vb = sh ? ((g1.z >> sh) | (g2.z << (32 - sh))) : g1.z;
+                const uint64_t q = qo + p + m;
+                const uint64_t qi = q >> 5;
+                const uint32_t qs = (uint32_t)(q & 31) * 2;
+                const uint64_t w0 = Q[qi], w1 = Q[qi + 1], w2 = Q[qi + 2];
+                const uint64_t qa = qs ? ((w0 >> qs) | (w1 << (64 - qs))) : w0;
+                const uint64_t qb2 = qs ? ((w1 >> qs) | (w2 << (64 - qs))) : w1;
+                const uint64_t xa = qa ^ pa, xb = qb2 ^ pb;
+                uint32_t la = xa ? ctz64(xa) >> 1 : 32u;
+                const uint32_t ia = ~va ? (uint32_t)__builtin_ctz(~va) : 32u;
+                if (ia < la) la = ia;
+                uint32_t lim = la;
+                if (la == 32) {
+                    uint32_t lb = xb ? ctz64(xb) >> 1 : 32u;
+                    const uint32_t ib = ~vb ? (uint32_t)__builtin_ctz(~vb) : 32u;
+                    if (ib < lb) lb = ib;
+                    lim = 32 + lb;
+                }
                 if (len - p - m < lim) lim = len - p - m;
                 m += lim;
-                if (lim < 32) break;
+                if (lim < 64) break;
             }
             if (m > 0) {
                 NTC_STAT(2);
