@@ -393,6 +393,7 @@ struct BaseReader {
 enum : uint32_t { kModeScan = 0, kModeExt = 1, kModeP1 = 2, kModeBs = 3, kModeBrk = 4 };
 constexpr uint32_t kScanW = 16;      // presence probes per SCAN unit (U + kScanW - 1 <= 32)
 constexpr uint32_t kScanFirstW = 4;  // first SCAN of a read: error-free starts pair at once
+constexpr uint32_t kScanExact = 4;   // filter candidates tested exactly per SCAN
 
 // ======================================================================================
 // Matching statistics as RUN-LENGTH entries.  Positions whose U-mer is absent ("short")
@@ -732,18 +733,29 @@ struct MsLane {
                     }
                 cand &= fm & (fm >> kFiltGap);
             }
+            // exact test of the first kScanExact candidates only: the pair is almost always
+            // among them, and positions past the last one tested are left to the next SCAN
+            uint32_t tested = cand, span = W;
+#pragma unroll
+            for (uint32_t t = 0; t < kScanExact; t++) tested &= tested - 1;  // drop the first few
+            if (tested) {
+                span = (uint32_t)__builtin_ctz(tested);  // first untested candidate
+                tested = cand & ((1u << span) - 1u);
+            } else {
+                tested = cand;
+            }
             uint32_t longm = 0;
 #pragma unroll
             for (uint32_t i = 0; i < kScanW; i++)
-                if ((cand >> i) & 1u) {
+                if ((tested >> i) & 1u) {
                     NTC_STAT(6);
                     const uint64_t key = key_at(p + i, U);
                     longm |= ((ix.tab_bits[key >> 5] >> (key & 31)) & 1u) << i;
                 }
             const uint32_t pairs = longm & (longm >> 1);
             if (pairs == 0) {
-                if (p + W >= len) { p = len; return 1; }
-                p += W - ((longm >> (W - 1)) & 1u);  // keep a long last position
+                if (p + span >= len) { p = len; return 1; }
+                p += span - ((longm >> (span - 1)) & 1u);  // keep a long last position
                 return 0;
             }
             const uint2 *lvl = ix.tab + tab_base(U);
