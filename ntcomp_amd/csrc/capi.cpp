@@ -41,7 +41,7 @@ struct ntc_ctx {
     std::vector<void *> index_mem;
     uint64_t index_bytes = 0;
     // workspace buffers (grown, never shrunk)
-    DevBuf ws[20];
+    DevBuf ws[24];
     unsigned long long *d_status = nullptr;
     // last call
     CallKind last = kNone;
@@ -62,7 +62,7 @@ namespace {
 enum WsSlot {
     WS_D = 0, WS_S, WS_F, WS_R, WS_RECCOUNT, WS_SCANTMP, WS_TILEBASE, WS_TILEROWS,
     WS_STAGE_BASES, WS_STAGE_OFFS, WS_STAGE_RECS, WS_E, WS_DEC_A, WS_DEC_B, WS_DEC_C,
-    WS_DEC_D, WS_Q, WS_E3, WS_NE, WS_COUNTER
+    WS_DEC_D, WS_Q, WS_E3, WS_NE, WS_COUNTER, WS_R2
 };
 
 #define HIP_TRY(ctx, expr)                                                                   \
@@ -153,6 +153,8 @@ int encode4_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, u
     a.ne = (uint32_t *)p;
     if ((rc = ensure(ctx, WS_R, (total_bases + 1) * 8, &p))) return rc;
     a.R = (uint64_t *)p;
+    if ((rc = ensure(ctx, WS_R2, (n_reads + 1) * kRecSlot * 8, &p))) return rc;
+    a.R2 = (uint64_t *)p;
     if ((rc = ensure(ctx, WS_RECCOUNT, (n_reads + 1) * 4, &p))) return rc;
     a.rec_count = (uint32_t *)p;
     if ((rc = ensure(ctx, WS_COUNTER, 64, &p))) return rc;

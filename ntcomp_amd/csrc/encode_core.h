@@ -851,9 +851,12 @@ NTC_HD void read_ms(const DevIndex &ix, const uint64_t *Q, uint64_t qo, const En
     }
 }
 
-// greedy right-to-left parse over the entries, lib.rs:175-218 (+ encode.rs:144-158)
+constexpr uint32_t kRecSlot = 8;  // records per read in the dense slot; more spill
+
+// greedy right-to-left parse over the entries, lib.rs:175-218 (+ encode.rs:144-158).
+// Record j goes to slot[j] (j < kRecSlot) or spill[j].
 NTC_HD int parse_read(const DevIndex &ix, const uint64_t *Q, uint64_t qo, const Entry *E, uint32_t ne,
-                      uint32_t len, uint64_t *R) {
+                      uint32_t len, uint64_t *slot, uint64_t *spill) {
     const uint32_t k = ix.k;
     EntryView ev(E, &ix, Q, qo, k, (int32_t)ne - 1);
     uint32_t i = len;
@@ -895,7 +898,8 @@ NTC_HD int parse_read(const DevIndex &ix, const uint64_t *Q, uint64_t qo, const 
             const uint64_t bits = window2(Q, qo + segend - seglen);
             w = (bits & ((1ULL << (2 * seglen)) - 1)) | ((uint64_t)((first + 2) | (seglen << 2)) << 56);
         }
-        R[nrec] = w;
+        if (nrec < (int)kRecSlot) slot[nrec] = w;
+        else spill[nrec] = w;
         nrec++;
         if (i > 0) i -= 1;
         else break;

@@ -31,7 +31,8 @@ struct Enc4Args {
     uint64_t *Q;                 // packed bases, position space (2 bits, 32 per word)
     Entry *E;                    // entries, position space
     uint32_t *ne;                // entries per read
-    uint64_t *R;                 // records, position space
+    uint64_t *R;                 // records past kRecSlot, position space
+    uint64_t *R2;                // first kRecSlot records of each read (dense slots)
     uint32_t *rec_count;
     unsigned long long *status;
     unsigned long long *counter; // work queue head (zeroed per call)

@@ -206,7 +206,7 @@ __global__ __launch_bounds__(256) void k_parse4(Enc4Args a) {
     }
     const uint64_t o0 = a.offs[0], b = a.offs[r], e = a.offs[r + 1];
     const uint64_t P = b - o0;
-    const int rc = parse_read(a.ix, a.Q, P, a.E + P, a.ne[r], (uint32_t)(e - b), a.R + P);
+    const int rc = parse_read(a.ix, a.Q, P, a.E + P, a.ne[r], (uint32_t)(e - b), a.R2 + r * kRecSlot, a.R + P);
     if (rc < 0) {
         atomicMin(a.status, (unsigned long long)((r << 8) | (uint64_t)(-rc)));
         a.rec_count[r] = 0;
@@ -225,8 +225,13 @@ __global__ __launch_bounds__(256) void k_emit4(Enc4Args a, const uint64_t *rec_o
         atomicMin(a.status, (unsigned long long)((r << 8) | (uint64_t)kErrCapacity));
         return;
     }
-    const uint64_t *src = a.R + (a.offs[r] - a.offs[0]);
-    for (uint32_t j = 0; j < cnt; j++) out[off + j] = src[j];
+    const uint64_t *slot = a.R2 + r * kRecSlot;
+    const uint32_t ns = cnt < kRecSlot ? cnt : kRecSlot;
+    for (uint32_t j = 0; j < ns; j++) out[off + j] = slot[j];
+    if (cnt > kRecSlot) {
+        const uint64_t *spill = a.R + (a.offs[r] - a.offs[0]);
+        for (uint32_t j = kRecSlot; j < cnt; j++) out[off + j] = spill[j];
+    }
 }
 
 // rows of scratch a tile of 64 reads needs = longest read, rounded up to 32

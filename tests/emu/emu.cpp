@@ -83,7 +83,7 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
                     }
                     ne = ms.ne;
                 }
-                if (rc == 0) rc = parse_read(d, Q.data(), 0, E4.data(), ne, len, R4.data());
+                if (rc == 0) rc = parse_read(d, Q.data(), 0, E4.data(), ne, len, R4.data(), R4.data());
                 if (d_out && rc >= 0)
                     read_ms(d, Q.data(), 0, E4.data(), ne, len, d_out + (offs[r] - offs[0]), s_out + (offs[r] - offs[0]));
                 if (rc >= 0) {
