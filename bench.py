@@ -171,9 +171,13 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                 "kernel": kname, "kernel_ms": round(main_ms, 3),
                 "alg_bytes_per_launch": int(alg_bytes),
-                "note": "achieved = SURVEY 8(d) algorithmic bytes (the reference's two 64 B rank-line reads "
-                        "per base) / kernel time; the suffix table and path runs skip most of those reads, "
-                        "so frac can exceed 1. traffic = measured HBM bytes per launch (rocprofv3 PMC)"}
+                "note": ("achieved = SURVEY 8(d) algorithmic bytes (B_enc: the reference's two 64 B rank-line "
+                         "reads per base) / kernel time; the suffix table and path runs skip most of those "
+                         "reads, so frac can exceed 1" if args.mode == "encode" else
+                         "achieved = SURVEY 8(d) B_dec (one 64 B select line per walked base) / kernel time; "
+                         "the walk table reads 32 bases per 16 B entry, so frac can exceed 1") +
+                        ". traffic = HBM bytes per launch from rocprofv3 PMC (2*FETCH_SIZE + WRITE_SIZE, "
+                        "profiles/pmc_traffic.json); traffic_frac = traffic / kernel time / peak"}
     if traffic:
         roofline["traffic_frac"] = round(traffic / (main_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
 

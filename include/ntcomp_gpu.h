@@ -74,7 +74,7 @@ typedef struct ntc_index_view {
 /* Per-call device timings (milliseconds, HIP events on the context's stream). */
 typedef struct ntc_timing {
     double total_ms;      /* first launch -> last launch of the call           */
-    double main_ms;       /* the dominant kernel: encode MS+parse / decode walk */
+    double main_ms;       /* the dominant kernel: encode k_ms4 / decode walk     */
     double aux_ms;        /* everything else (tiling, scans, record emit)       */
     uint64_t units;       /* bases processed (encode: input, decode: output)   */
     uint64_t records;     /* records produced (encode) / consumed (decode)     */
@@ -88,16 +88,20 @@ const char *ntc_last_error(const ntc_ctx *ctx);
 /* Optional: launch on a caller-owned hipStream_t (passed as void*); NULL = own stream. */
 int ntc_ctx_set_stream(ntc_ctx *ctx, void *hip_stream);
 int ntc_ctx_synchronize(ntc_ctx *ctx);
-/* Tuning / diagnostics.  "encode_variant": 4 (default: packed bases, persistent MS kernel
- * with dynamic read assignment, path runs, speculative contraction, separate parse) or 1
- * (the first design: phase-synchronous lanes, kept for A/B).  Read-only: "n_paths",
- * "path_text_len" (the path cover built at upload).  Env NTC_ENCODE_VARIANT sets the
- * default at ntc_ctx_create.                                                          */
+/* Tuning / diagnostics.  "encode_variant": 4 (default: packed bases, suffix table for
+ * positions whose U-mer is absent, persistent matching-statistics kernel with dynamic
+ * read assignment and path runs, separate parse) or 1 (the first design: one lane per
+ * read walking every position, kept for A/B).  "tab_u": suffix-table depth U for the
+ * NEXT ntc_index_upload (0 = default ceil(log4 n) + 2 capped at min(k, 14); results
+ * never depend on it).  Read-only: "n_paths", "path_text_len" (the path cover built at
+ * upload), "tab_u" (after an upload: the depth in use).  Env NTC_ENCODE_VARIANT sets the
+ * default variant at ntc_ctx_create.                                                 */
 int ntc_ctx_set_option(ntc_ctx *ctx, const char *key, int64_t value);
 int ntc_ctx_get_option(const ntc_ctx *ctx, const char *key, int64_t *value);
 
-/* Upload the index once; builds the device-side rank lines, the unique-predecessor
- * bitvector and the inverse-walk jump table in HBM (DESIGN.md "Data layout"). */
+/* Upload the index once; builds the device-side rank words, the unique-predecessor
+ * bitvector, the path cover, the suffix table (+ presence bitmaps) and the inverse-walk
+ * jump table in HBM (DESIGN.md "Data layout in HBM").  About 3 GB at n = 10 M, k = 91. */
 int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *ix);
 int ntc_index_info(const ntc_ctx *ctx, uint64_t *n_nodes, uint32_t *k, uint64_t *device_bytes);
 
