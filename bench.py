@@ -67,6 +67,7 @@ def main():
         torch.cuda.set_device(local)
 
     import ntcomp_amd as nt
+    from ntcomp_amd import shard
 
     def barrier():
         if dist is not None:
@@ -94,7 +95,7 @@ def main():
         f"{ctx.get_option('n_paths')} paths, text {ctx.get_option('path_text_len')}")
 
     n, L = args.reads_per_gpu, args.read_len
-    first = rank * n
+    first, n = shard.read_range(rank, world, n)
     t0 = time.time()
     reads = nt.synth_reads(genome, 2, first, n, L, args.err_ppm, threads=nthreads)
     offs = np.arange(0, n * L + 1, L, dtype=np.uint64)
@@ -136,10 +137,7 @@ def main():
     sync(ctx)
     elapsed = time.perf_counter() - tt
     barrier()
-    if dist is not None:
-        tm = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
-        elapsed = float(tm.item())
+    elapsed = shard.max_over_ranks(elapsed, dist)
     ms_per_step = elapsed / args.steps * 1e3
     units_all = total_bases * world * args.steps
     value = units_all / elapsed / 1e6  # Mbases/s, whole job
