@@ -390,9 +390,8 @@ struct BaseReader {
     }
 };
 
-enum : uint32_t { kModeScan = 0, kModeExt = 1, kModeP1 = 2, kModeBs = 3, kModeBrk = 4 };
+enum : uint32_t { kModeScan = 0, kModeExt = 1, kModeP1 = 2, kModeBs = 3, kModeBrk = 4, kModeFirst = 5 };
 constexpr uint32_t kScanW = 16;      // presence probes per SCAN unit (U + kScanW - 1 <= 32)
-constexpr uint32_t kScanFirstW = 4;  // first SCAN of a read: error-free starts pair at once
 constexpr uint32_t kScanExact = 4;   // filter candidates tested exactly per SCAN
 
 // ======================================================================================
@@ -620,8 +619,8 @@ struct MsLane {
         qw = 0;
         qb = 0xFFFFFFFFu;
         p = 0; d = 0; l = 0; r = ix.n; j = 0xFFFFFFFFu; ne = 0;
-        mode = kModeScan; lo = l1 = r1 = bl = bR = 0;
-        hi = kScanFirstW;  // SCAN width cap (hi is free while scanning)
+        mode = kModeFirst; lo = l1 = r1 = bl = bR = 0;
+        hi = kScanW;  // SCAN width cap (hi is free while scanning)
         try_run = false;
     }
     NTC_HD void window(uint32_t from) {
@@ -648,6 +647,29 @@ struct MsLane {
         mode = kModeExt;
         note_single(ix);
         return p >= len ? 1 : 0;
+    }
+    // position p is short with table value m: d_{p+i} <= m + i, so p+1 .. p+U-1-m are
+    // short too.  A lone error at p leaves the pair (p + U, p + U + 1): the next SCAN
+    // needs m + 2 positions to reach it.
+    NTC_HD void skip_short(uint32_t m, uint32_t U) {
+        p += U - m;
+        mode = kModeScan;
+        hi = m + 2 < kScanW ? m + 2 : kScanW;
+    }
+    // x and x + 1 are long, x's predecessor short: walk from x (d = U, table interval)
+    NTC_HD int enter_pair(const DevIndex &ix, uint32_t x, uint2 te) {
+        uint32_t jj;
+        tab_interval(ix, te, l, r, jj);
+        d = ix.tab_u;
+        p = x + 1;
+        mode = kModeExt;
+        if (ix.tab_pos) {  // the table already holds the path position (d = U >= t_jump)
+            j = jj;
+            try_run = jj != 0xFFFFFFFFu;
+        } else {
+            note_single(ix);
+        }
+        return 0;
     }
     // one unit of work: 1 = read finished, 0 = continue, < 0 = error
     NTC_HD int step(const DevIndex &ix) {
@@ -707,6 +729,26 @@ struct MsLane {
                 return 0;
             }
         }
+        if (mode == kModeFirst) {
+            // read start: positions < U - 1 are short by length; error-free starts have the
+            // pair (U - 1, U), so test it directly with U - 1's full entry
+            mode = kModeScan;
+            if (len >= U + 1) {
+                window(0);
+                const uint2 te = load2(ix.tab + tab_base(U) + key_at(U - 1, U));
+                const uint64_t k2 = key_at(U, U);
+                const uint32_t b2 = (ix.tab_bits[k2 >> 5] >> (k2 & 31)) & 1u;
+                if (!tab_long(te)) {
+                    p = U - 1 + U - (te.y & 0xFFu);  // d_{U-1+i} <= m + i
+                    return p >= len ? 1 : 0;
+                }
+                if (!b2) {
+                    p = U + 1;  // U is short
+                    return p >= len ? 1 : 0;
+                }
+                return enter_pair(ix, U - 1, te);
+            }
+        }
         if (mode == kModeScan) {
             // find the first pair of consecutive long positions at or after p (position
             // p - 1 is short, or p = 0); positions < U - 1 are short by length
@@ -758,22 +800,9 @@ struct MsLane {
                 p += span - ((longm >> (span - 1)) & 1u);  // keep a long last position
                 return 0;
             }
-            const uint2 *lvl = ix.tab + tab_base(U);
             NTC_STAT(7);
             const uint32_t x = p + (uint32_t)__builtin_ctz(pairs);  // long, short predecessor
-            const uint2 te = load2(lvl + key_at(x, U));
-            uint32_t jj;
-            tab_interval(ix, te, l, r, jj);
-            d = U;
-            p = x + 1;
-            mode = kModeExt;
-            if (ix.tab_pos) {  // the table already holds the path position (d = U >= t_jump)
-                j = jj;
-                try_run = jj != 0xFFFFFFFFu;
-            } else {
-                note_single(ix);
-            }
-            return 0;
+            return enter_pair(ix, x, load2(ix.tab + tab_base(U) + key_at(x, U)));
         }
         if (!covers(p + 1 - U, p)) window(p + 1 - U);
         if (mode == kModeBrk) {
@@ -781,9 +810,7 @@ struct MsLane {
             const uint2 te = load2(ix.tab + tab_base(U) + key_at(p, U));
             const uint32_t v = ix.colex_at[j] & 0x7FFFFFFFu;  // node before p, for a long p
             if (!tab_long(te)) {
-                p += U - (te.y & 0xFFu);
-                mode = kModeScan;
-                hi = kScanW;
+                skip_short(te.y & 0xFFu, U);
                 return p >= len ? 1 : 0;
             }
             l = v;
@@ -800,10 +827,7 @@ struct MsLane {
             if (nl < nr) { NTC_STAT(9); return commit(ix, nl, nr, d + 1 < k ? d + 1 : k); }
             NTC_STAT(10);
             if (!tab_long(te)) {  // p is short: table-determined, scan on
-                // d_{p+i} <= m + i, so p+1 .. p+U-1-m are short as well
-                p += U - (te.y & 0xFFu);
-                mode = kModeScan;
-                hi = kScanW;
+                skip_short(te.y & 0xFFu, U);
                 return p >= len ? 1 : 0;
             }
             NTC_STAT(11);
