@@ -118,8 +118,8 @@ NTC_HD void extend(const DevIndex &ix, int c, uint32_t l, uint32_t r, uint32_t &
 
 // contract_left(I, t) [ext sbwt]: widen I to all nodes sharing the last t characters.
 NTC_HD void widen(const DevIndex &ix, uint32_t &l, uint32_t &r, uint32_t t) {
-    while (l > 0 && ix.lcs[l] >= t) { NTC_STAT(13); l--; }
-    while (r < ix.n && ix.lcs[r] >= t) { NTC_STAT(13); r++; }
+    while (l > 0 && ix.lcs[l] >= t) l--;
+    while (r < ix.n && ix.lcs[r] >= t) r++;
 }
 
 // One character of k-bounded matching statistics.  State (d, [l, r)) = length and colex
@@ -635,7 +635,6 @@ struct MsLane {
     NTC_HD void note_single(const DevIndex &ix) {
         j = 0xFFFFFFFFu;
         if (ix.has_paths && r == l + 1 && d >= ix.t_jump) {
-            NTC_STAT(15);
             j = ix.pos_of_node[l];
             try_run = j != 0xFFFFFFFFu;
         }
@@ -675,13 +674,10 @@ struct MsLane {
     NTC_HD int step(const DevIndex &ix) {
         const uint32_t k = ix.k, U = ix.tab_u;
         if (p >= len) return 1;
-        NTC_STAT(0);
         if (try_run) {
             try_run = false;
             uint32_t m = 0;
-            NTC_STAT(1);
             for (;;) {
-                NTC_STAT(4);
                 // 64 path characters after node j's k-mer, and whether the k-mer ending at
                 // each of them is a node, from three interleaved 32-char groups
                 const uint64_t T = (uint64_t)j + k + m;
@@ -716,8 +712,6 @@ struct MsLane {
                 if (lim < 64) break;
             }
             if (m > 0) {
-                NTC_STAT(2);
-                ntc_stat_add(3, m);
                 store_entry(E, ne++, p, j + 1, m, (d + 1 < k ? d + 1 : k) | kRunTag);
                 p += m;
                 j += m;
@@ -759,7 +753,6 @@ struct MsLane {
             if (W > hi) W = hi;
             if (W > len - p) W = len - p;
             hi = kScanW;
-            NTC_STAT(5);
             // a present U-mer has present F-mer prefix and suffix (F = U - 2): test those
             // in the small level-F bitmap first; the F-mer suffix of position y's U-mer is
             // the F-mer prefix of y + 2's, so W + 2 filter bits cover W positions
@@ -790,7 +783,6 @@ struct MsLane {
 #pragma unroll
             for (uint32_t i = 0; i < kScanW; i++)
                 if ((tested >> i) & 1u) {
-                    NTC_STAT(6);
                     const uint64_t key = key_at(p + i, U);
                     longm |= ((ix.tab_bits[key >> 5] >> (key & 31)) & 1u) << i;
                 }
@@ -800,13 +792,11 @@ struct MsLane {
                 p += span - ((longm >> (span - 1)) & 1u);  // keep a long last position
                 return 0;
             }
-            NTC_STAT(7);
             const uint32_t x = p + (uint32_t)__builtin_ctz(pairs);  // long, short predecessor
             return enter_pair(ix, x, load2(ix.tab + tab_base(U) + key_at(x, U)));
         }
         if (!covers(p + 1 - U, p)) window(p + 1 - U);
         if (mode == kModeBrk) {
-            NTC_STAT(14);
             const uint2 te = load2(ix.tab + tab_base(U) + key_at(p, U));
             const uint32_t v = ix.colex_at[j] & 0x7FFFFFFFu;  // node before p, for a long p
             if (!tab_long(te)) {
@@ -822,15 +812,12 @@ struct MsLane {
         if (mode == kModeExt) {
             const uint2 te = load2(ix.tab + tab_base(U) + key_at(p, U));  // for a failure
             uint32_t nl, nr;
-            NTC_STAT(8);
             extend(ix, c, l, r, nl, nr);
-            if (nl < nr) { NTC_STAT(9); return commit(ix, nl, nr, d + 1 < k ? d + 1 : k); }
-            NTC_STAT(10);
+            if (nl < nr) return commit(ix, nl, nr, d + 1 < k ? d + 1 : k);
             if (!tab_long(te)) {  // p is short: table-determined, scan on
                 skip_short(te.y & 0xFFu, U);
                 return p >= len ? 1 : 0;
             }
-            NTC_STAT(11);
             uint32_t tl, tr, tj;
             tab_interval(ix, te, tl, tr, tj);
             if (d == U) return commit(ix, tl, tr, U);  // t* = U - 1
@@ -840,7 +827,6 @@ struct MsLane {
             return 0;
         }
         // kModeP1: probe t = d - 1 from I_d; kModeBs: t = mid from I_hi (l1, r1)
-        NTC_STAT(12);
         const bool p1 = mode == kModeP1;
         const uint32_t t = p1 ? hi : (lo + hi) >> 1;
         uint32_t ql = p1 ? l : l1, qr = p1 ? r : r1;
