@@ -17,6 +17,11 @@
 #include <cstdint>
 
 #define NTC_HD __host__ __device__ __forceinline__
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+#ifndef NTC_NT
+#define NTC_NT 1  // streaming (nontemporal) hints, bit mask: 1 table entries + entry stores,
+                  // 2 exact presence bits, 4 path stream, 8 query words (k_ms4)
+#endif
 
 namespace ntc {
 
@@ -102,6 +107,33 @@ NTC_HD uint2 load2(const uint2 *p) {
     return *p;
 #else
     return mk2(p->x, p->y);
+#endif
+}
+template <int kBit, typename T>
+NTC_HD T ld_hint(const T *p) {
+#ifdef __HIP_DEVICE_COMPILE__
+    if constexpr ((NTC_NT & kBit) != 0) return __builtin_nontemporal_load(p);
+#endif
+    return *p;
+}
+template <int kBit>
+NTC_HD uint4 ld4(const uint4 *p) {
+#ifdef __HIP_DEVICE_COMPILE__
+    if constexpr ((NTC_NT & kBit) != 0) {
+        const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t *>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    }
+#endif
+    return *p;
+}
+// a load with no reuse (suffix-table entries: 2.9 GB, random): streaming hint, so that it
+// does not push the L2-resident filter bitmap out
+NTC_HD uint2 load2_stream(const uint2 *p) {
+#if defined(__HIP_DEVICE_COMPILE__) && (NTC_NT & 1)
+    const uint64_t v = __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(p));
+    return mk2((uint32_t)v, (uint32_t)(v >> 32));
+#else
+    return load2(p);
 #endif
 }
 NTC_HD uint32_t rank_word(uint2 w, uint32_t x) {  // C[c] + rank_c(x) from x's word
@@ -594,8 +626,12 @@ NTC_HD int pack_read(const uint8_t *q, uint32_t len, uint64_t *Q, uint32_t absen
 NTC_HD uint32_t fast_code(uint32_t b) { return ((b >> 1) ^ (b >> 2)) & 3u; }
 NTC_HD bool is_acgt(uint32_t b) { return b == 'A' || b == 'C' || b == 'G' || b == 'T'; }
 
+
 NTC_HD void store_entry(Entry *E, uint32_t i, uint32_t p, uint32_t v, uint32_t m, uint32_t dk) {
-#ifdef __HIP_DEVICE_COMPILE__
+#if defined(__HIP_DEVICE_COMPILE__) && (NTC_NT & 1)
+    u32x4_t x = {p, v, m, dk};
+    __builtin_nontemporal_store(x, reinterpret_cast<u32x4_t *>(E + i));
+#elif defined(__HIP_DEVICE_COMPILE__)
     *reinterpret_cast<uint4 *>(E + i) = make_uint4(p, v, m, dk);
 #else
     E[i] = Entry{p, v, m, dk};
@@ -681,7 +717,8 @@ struct MsLane {
                 // 64 path characters after node j's k-mer, and whether the k-mer ending at
                 // each of them is a node, from three interleaved 32-char groups
                 const uint64_t T = (uint64_t)j + k + m;
-                const uint4 g0 = ix.pstream[T >> 5], g1 = ix.pstream[(T >> 5) + 1], g2 = ix.pstream[(T >> 5) + 2];
+                const uint4 g0 = ld4<4>(ix.pstream + (T >> 5)), g1 = ld4<4>(ix.pstream + (T >> 5) + 1),
+                            g2 = ld4<4>(ix.pstream + (T >> 5) + 2);
                 const uint32_t sh = (uint32_t)(T & 31);
                 const uint64_t c0 = (uint64_t)g0.x | ((uint64_t)g0.y << 32);
                 const uint64_t c1 = (uint64_t)g1.x | ((uint64_t)g1.y << 32);
@@ -693,7 +730,7 @@ struct MsLane {
                 const uint64_t q = qo + p + m;
                 const uint64_t qi = q >> 5;
                 const uint32_t qs = (uint32_t)(q & 31) * 2;
-                const uint64_t w0 = Q[qi], w1 = Q[qi + 1], w2 = Q[qi + 2];
+                const uint64_t w0 = ld_hint<8>(Q + qi), w1 = ld_hint<8>(Q + qi + 1), w2 = ld_hint<8>(Q + qi + 2);
                 const uint64_t qa = qs ? ((w0 >> qs) | (w1 << (64 - qs))) : w0;
                 const uint64_t qb2 = qs ? ((w1 >> qs) | (w2 << (64 - qs))) : w1;
                 const uint64_t xa = qa ^ pa, xb = qb2 ^ pb;
@@ -729,7 +766,7 @@ struct MsLane {
             mode = kModeScan;
             if (len >= U + 1) {
                 window(0);
-                const uint2 te = load2(ix.tab + tab_base(U) + key_at(U - 1, U));
+                const uint2 te = load2_stream(ix.tab + tab_base(U) + key_at(U - 1, U));
                 const uint64_t k2 = key_at(U, U);
                 const uint32_t b2 = (ix.tab_bits[k2 >> 5] >> (k2 & 31)) & 1u;
                 if (!tab_long(te)) {
@@ -784,7 +821,7 @@ struct MsLane {
             for (uint32_t i = 0; i < kScanW; i++)
                 if ((tested >> i) & 1u) {
                     const uint64_t key = key_at(p + i, U);
-                    longm |= ((ix.tab_bits[key >> 5] >> (key & 31)) & 1u) << i;
+                    longm |= ((ld_hint<2>(ix.tab_bits + (key >> 5)) >> (key & 31)) & 1u) << i;
                 }
             const uint32_t pairs = longm & (longm >> 1);
             if (pairs == 0) {
@@ -793,11 +830,11 @@ struct MsLane {
                 return 0;
             }
             const uint32_t x = p + (uint32_t)__builtin_ctz(pairs);  // long, short predecessor
-            return enter_pair(ix, x, load2(ix.tab + tab_base(U) + key_at(x, U)));
+            return enter_pair(ix, x, load2_stream(ix.tab + tab_base(U) + key_at(x, U)));
         }
         if (!covers(p + 1 - U, p)) window(p + 1 - U);
         if (mode == kModeBrk) {
-            const uint2 te = load2(ix.tab + tab_base(U) + key_at(p, U));
+            const uint2 te = load2_stream(ix.tab + tab_base(U) + key_at(p, U));
             const uint32_t v = ix.colex_at[j] & 0x7FFFFFFFu;  // node before p, for a long p
             if (!tab_long(te)) {
                 skip_short(te.y & 0xFFu, U);
@@ -810,7 +847,7 @@ struct MsLane {
         }
         const int c = (int)((qw >> (2 * (p - qb))) & 3u);
         if (mode == kModeExt) {
-            const uint2 te = load2(ix.tab + tab_base(U) + key_at(p, U));  // for a failure
+            const uint2 te = load2_stream(ix.tab + tab_base(U) + key_at(p, U));  // for a failure
             uint32_t nl, nr;
             extend(ix, c, l, r, nl, nr);
             if (nl < nr) return commit(ix, nl, nr, d + 1 < k ? d + 1 : k);
