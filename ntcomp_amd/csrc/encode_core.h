@@ -790,9 +790,9 @@ struct MsLane {
             if (W > hi) W = hi;
             if (W > len - p) W = len - p;
             hi = kScanW;
-            // a present U-mer has present F-mer prefix and suffix (F = U - 2): test those
-            // in the small level-F bitmap first; the F-mer suffix of position y's U-mer is
-            // the F-mer prefix of y + 2's, so W + 2 filter bits cover W positions
+            // a present U-mer has its three F-mers (F = U - 2, at offsets 0, 1, 2) present:
+            // test them in the small level-F bitmap first; the F-mer ending at y is shared
+            // by the U-mers ending at y, y + 1 and y + 2, so W + 2 filter bits cover W positions
             uint32_t cand = (1u << W) - 1u;
             if (ix.filt_f) {
                 const uint32_t F = ix.filt_f;
@@ -803,7 +803,7 @@ struct MsLane {
                         const uint64_t fk = (qw >> (2 * (p + 1 - U + i - qb))) & ((1ULL << (2 * F)) - 1);
                         fm |= ((ix.filt_bits[fk >> 5] >> (fk & 31)) & 1u) << i;
                     }
-                cand &= fm & (fm >> kFiltGap);
+                cand &= fm & (fm >> 1) & (fm >> kFiltGap);  // all three F-mers of the U-mer
             }
             // exact test of the first kScanExact candidates only: the pair is almost always
             // among them, and positions past the last one tested are left to the next SCAN
