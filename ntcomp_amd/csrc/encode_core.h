@@ -19,8 +19,8 @@
 #define NTC_HD __host__ __device__ __forceinline__
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 #ifndef NTC_NT
-#define NTC_NT 1  // streaming (nontemporal) hints, bit mask: 1 table entries + entry stores,
-                  // 2 exact presence bits, 4 path stream, 8 query words (k_ms4)
+#define NTC_NT 17  // streaming (nontemporal) hints, bit mask: 1 table entries, 16 entry stores,
+                   // 2 exact presence bits, 4 path stream, 8 query words (k_ms4)
 #endif
 
 namespace ntc {
@@ -628,7 +628,7 @@ NTC_HD bool is_acgt(uint32_t b) { return b == 'A' || b == 'C' || b == 'G' || b =
 
 
 NTC_HD void store_entry(Entry *E, uint32_t i, uint32_t p, uint32_t v, uint32_t m, uint32_t dk) {
-#if defined(__HIP_DEVICE_COMPILE__) && (NTC_NT & 1)
+#if defined(__HIP_DEVICE_COMPILE__) && (NTC_NT & 16)
     u32x4_t x = {p, v, m, dk};
     __builtin_nontemporal_store(x, reinterpret_cast<u32x4_t *>(E + i));
 #elif defined(__HIP_DEVICE_COMPILE__)

@@ -140,7 +140,23 @@ __global__ __launch_bounds__(256) void k_pack(Enc4Args a, uint64_t bound) {
 
 constexpr uint32_t kPoolChunk = 64;
 
-__global__ __launch_bounds__(256, 8) void k_ms4(Enc4Args a) {
+// parse of read r (k_parse4's body)
+__device__ __forceinline__ void parse_one(const Enc4Args &a, uint64_t r) {
+    const uint64_t o0 = a.offs[0], b = a.offs[r], e = a.offs[r + 1];
+    const uint64_t P = b - o0;
+    const int rc = parse_read(a.ix, a.Q, P, a.E + P, a.ne[r], (uint32_t)(e - b), a.R2 + r * kRecSlot, a.R + P);
+    if (rc < 0) {
+        atomicMin(a.status, (unsigned long long)((r << 8) | (uint64_t)(-rc)));
+        a.rec_count[r] = 0;
+    } else {
+        a.rec_count[r] = (uint32_t)rc;
+    }
+}
+
+#ifndef NTC_MS_WAVES
+#define NTC_MS_WAVES 8  // waves per SIMD k_ms4 is compiled for (SGPR <= 80, VGPR <= 64)
+#endif
+__global__ __launch_bounds__(256, NTC_MS_WAVES) void k_ms4(Enc4Args a) {
     const uint32_t lane = threadIdx.x & 63;
     if (*a.status != ~0ull) return;  // a read failed to pack: nothing to do
     const uint64_t o0 = a.offs[0];
@@ -180,7 +196,8 @@ __global__ __launch_bounds__(256, 8) void k_ms4(Enc4Args a) {
             const uint64_t took = (uint64_t)__popcll(want);
             pool_lo += took < avail ? took : avail;
         }
-        if (__ballot(!idle) == 0 && exhausted) break;
+        const bool done = __ballot(!idle) == 0 && exhausted;
+        if (done) break;
         // ---- one unit of work per busy lane --------------------------------------------
         if (!idle) {
             const int rc = st.step(a.ix);
@@ -204,21 +221,14 @@ __global__ __launch_bounds__(256) void k_parse4(Enc4Args a) {
         a.rec_count[r] = 0;
         return;
     }
-    const uint64_t o0 = a.offs[0], b = a.offs[r], e = a.offs[r + 1];
-    const uint64_t P = b - o0;
-    const int rc = parse_read(a.ix, a.Q, P, a.E + P, a.ne[r], (uint32_t)(e - b), a.R2 + r * kRecSlot, a.R + P);
-    if (rc < 0) {
-        atomicMin(a.status, (unsigned long long)((r << 8) | (uint64_t)(-rc)));
-        a.rec_count[r] = 0;
-    } else {
-        a.rec_count[r] = (uint32_t)rc;
-    }
+    parse_one(a, r);
 }
 
 __global__ __launch_bounds__(256) void k_emit4(Enc4Args a, const uint64_t *rec_offsets, uint64_t *out,
                                                uint64_t capacity) {
     const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (r >= a.n_reads) return;
+    if (*a.status != ~0ull) return;  // a read failed: the call reports that, no output
     const uint32_t cnt = a.rec_count[r];
     const uint64_t off = rec_offsets[r];
     if (off + cnt > capacity) {
