@@ -149,7 +149,7 @@ def main():
     else:
         n_long_bases = None
         alg_bytes = None
-        kname = "k_dec_walk"
+        kname = "k_dec_rec"
     # decode: B_dec = 64 B per walked base + 1 B/base out + 8 B/record
     if args.mode == "decode":
         recs_h = ctx.d2h(np.zeros(n_recs, dtype=np.uint64), d_recs)

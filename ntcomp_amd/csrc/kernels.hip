@@ -326,15 +326,24 @@ __global__ __launch_bounds__(256) void k_dec_index(DecIndexArgs a) {
     }
 }
 
-__global__ __launch_bounds__(256) void k_dec_walk(DecWalkArgs a) {
-    const uint64_t rid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+// one lane per RECORD: records are independent once their output offsets are known.  A
+// read's records are consumed last to first (lib.rs:266), so record r of read rid (records
+// [rb, re)) lands at E[rb] + (E[re] - E[r + 1]) with E the exclusive scan of lengths.
+__global__ __launch_bounds__(256) void k_dec_rec(DecWalkArgs a) {
+    const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= a.n) return;
     if (*a.status != ~0ull) return;
-    const uint64_t nreads = a.fscan[a.n];
-    if (rid >= nreads) return;
+    const uint64_t rid = a.fscan[r + 1] - 1;  // record 0 is a first record (k_dec_index)
     const uint64_t rb = a.rec_start[rid], re = a.rec_start[rid + 1];
-    const uint64_t ob = a.E[rb], oe = a.E[re];
-    const int rc = decode_read(a.ix, a.recs, rb, re, a.out + ob, oe - ob);
-    if (rc < 0) atomicMin(a.status, (unsigned long long)((rid << 8) | (uint64_t)(-rc)));
+    uint8_t *out = a.out + a.E[rb] + (a.E[re] - a.E[r + 1]);
+    const uint64_t w = a.recs[r];
+    const uint32_t flag = (uint32_t)(w >> 56);
+    if (flag & 2) {
+        const uint32_t len = flag >> 2;
+        for (uint32_t j = 0; j < len; j++) out[j] = base_char((uint32_t)(w >> (2 * j)));
+    } else if (!walk_record(a.ix, (uint32_t)w, (uint32_t)(w >> 32) & 0xFFFFFFu, out)) {
+        atomicMin(a.status, (unsigned long long)((rid << 8) | (uint64_t)kErrFormat));
+    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -553,7 +562,7 @@ void launch_dec_index(const DecIndexArgs &a, hipStream_t s) {
     hipLaunchKernelGGL(k_dec_index, grid_for(a.n + 1), dim3(256), 0, s, a);
 }
 void launch_dec_walk(const DecWalkArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL(k_dec_walk, grid_for(a.n), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_dec_rec, grid_for(a.n), dim3(256), 0, s, a);
 }
 void launch_walk_build(const uint32_t *pred, const uint8_t *code, uint64_t n, WalkEntry *a, WalkEntry *b,
                        WalkEntry **result, hipStream_t s) {
