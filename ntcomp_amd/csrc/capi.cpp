@@ -41,7 +41,7 @@ struct ntc_ctx {
     std::vector<void *> index_mem;
     uint64_t index_bytes = 0;
     // workspace buffers (grown, never shrunk)
-    DevBuf ws[24];
+    DevBuf ws[28];
     unsigned long long *d_status = nullptr;
     // last call
     CallKind last = kNone;
@@ -54,6 +54,8 @@ struct ntc_ctx {
     int num_cus = 0;
     Enc4Args last4{};
     uint32_t tab_u_opt = 0;  // suffix-table depth for the next upload (0 = default_tab_u)
+    void *o2_zeroed = nullptr;  // WS_O2 buffer known to be all zero (k_dec_expand re-zeroes it)
+    uint64_t o2_zeroed_bytes = 0;
     uint64_t n_paths = 0, path_text_len = 0;
 };
 
@@ -62,7 +64,7 @@ namespace {
 enum WsSlot {
     WS_D = 0, WS_S, WS_F, WS_R, WS_RECCOUNT, WS_SCANTMP, WS_TILEBASE, WS_TILEROWS,
     WS_STAGE_BASES, WS_STAGE_OFFS, WS_STAGE_RECS, WS_E, WS_DEC_A, WS_DEC_B, WS_DEC_C,
-    WS_DEC_D, WS_Q, WS_E3, WS_NE, WS_COUNTER, WS_R2
+    WS_DEC_D, WS_Q, WS_E3, WS_NE, WS_COUNTER, WS_R2, WS_O2
 };
 
 #define HIP_TRY(ctx, expr)                                                                   \
@@ -596,6 +598,14 @@ int ntc_decode_batch_device(ntc_ctx *ctx, const uint64_t *d_recs, uint64_t n_rec
     E = (uint64_t *)fscan + (n + 1);
     if ((rc = ensure(ctx, WS_DEC_D, (n + 1) * 8, &rstart))) return rc;
     if ((rc = ensure(ctx, WS_SCANTMP, scan_tmp_words(n + 1) * 8, &tmp))) return rc;
+    void *o2;
+    if ((rc = ensure(ctx, WS_O2, (bases_capacity / 32 + 2) * 8, &o2))) return rc;
+    if (o2 != ctx->o2_zeroed || ctx->ws[WS_O2].bytes != ctx->o2_zeroed_bytes) {
+        // fresh buffer: zero once; every call leaves it zeroed
+        HIP_TRY(ctx, hipMemsetAsync(o2, 0, ctx->ws[WS_O2].bytes, ctx->stream));
+        ctx->o2_zeroed = o2;
+        ctx->o2_zeroed_bytes = ctx->ws[WS_O2].bytes;
+    }
     HIP_TRY(ctx, hipMemsetAsync(ctx->d_status, 0xFF, 8, ctx->stream));
     ctx->last = kDecode;
     ctx->last_n = n;
@@ -632,8 +642,11 @@ int ntc_decode_batch_device(ntc_ctx *ctx, const uint64_t *d_recs, uint64_t n_rec
     wa.E = (const uint64_t *)E;
     wa.rec_start = (const uint64_t *)rstart;
     wa.out = d_bases_out;
+    wa.O2 = (uint64_t *)o2;
     wa.status = ctx->d_status;
     launch_dec_walk(wa, ctx->stream);
+    launch_dec_expand((const uint64_t *)E, n, bases_capacity, (uint64_t *)o2, d_bases_out, ctx->d_status,
+                      ctx->stream);
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
     return NTC_OK;

@@ -282,7 +282,7 @@ void build_walk_host(const Derived &dv, uint64_t n, std::vector<WalkEntry> &walk
     for (uint64_t j = 0; j < n; j++) {
         a[j].chars = dv.code[j];
         a[j].jump = dv.pred[j];
-        a[j].pad = 0;
+        a[j].older = 0;
     }
     for (uint32_t m = 1; m < 32; m *= 2) {
         for (uint64_t j = 0; j < n; j++) {
@@ -290,9 +290,15 @@ void build_walk_host(const Derived &dv, uint64_t n, std::vector<WalkEntry> &walk
             const WalkEntry &y = a[x.jump];
             b[j].chars = y.chars | (x.chars << (2 * m));
             b[j].jump = y.jump;
-            b[j].pad = 0;
+            b[j].older = 0;
         }
         a.swap(b);
+    }
+    // a = 32-step entries, b = 16-step: extend to kWalkSpan = 48 steps
+    for (uint64_t j = 0; j < n; j++) {
+        const WalkEntry &y = b[a[j].jump];
+        a[j].older = (uint32_t)y.chars;
+        a[j].jump = y.jump;
     }
     walk.swap(a);
 }

@@ -42,10 +42,11 @@ NTC_HD void ntc_stat_add(int, uint64_t) {}
 // j (text order, character t in bits 2t..2t+1) and the node reached.  Replaces 32
 // dependent select()s of access_kmer by one 16-byte load.
 struct alignas(16) WalkEntry {
-    uint64_t chars;
-    uint32_t jump;
-    uint32_t pad;
+    uint64_t chars;  // the last 32 of the 48 characters (text order, oldest in the low bits)
+    uint32_t jump;   // the node kWalkSpan steps back
+    uint32_t older;  // the 16 characters before those
 };
+constexpr uint32_t kWalkSpan = 48;
 
 struct DevIndex {
     const uint2 *rank;      // [4][rwords] rank words
@@ -954,6 +955,91 @@ NTC_HD int parse_read(const DevIndex &ix, const uint64_t *Q, uint64_t qo, const 
     return nrec;
 }
 
+// ASCII of n <= 32 two-bit codes (code t at bits 2t) to out[0..n): aligned 4-byte stores
+// (four codes -> "ACGT" bytes with one byte permute), single bytes at the ends
+NTC_HD void store_codes(uint8_t *out, uint64_t codes, uint32_t n) {
+    uint32_t i = 0;
+    while (i < n && (((uintptr_t)(out + i)) & 3u)) {
+        out[i] = base_char((uint32_t)(codes >> (2 * i)));
+        i++;
+    }
+    for (; i + 4 <= n; i += 4) {
+        const uint32_t x = (uint32_t)(codes >> (2 * i)) & 0xFFu;
+        const uint32_t spread = (x & 3u) | ((x & 0xCu) << 6) | ((x & 0x30u) << 12) | ((x & 0xC0u) << 18);
+#ifdef __HIP_DEVICE_COMPILE__
+        *reinterpret_cast<uint32_t *>(out + i) = __builtin_amdgcn_perm(0u, 0x54474341u, spread);
+#else
+        for (uint32_t b = 0; b < 4; b++) out[i + b] = base_char(spread >> (8 * b));
+#endif
+    }
+    for (; i < n; i++) out[i] = base_char((uint32_t)(codes >> (2 * i)));
+}
+
+// 2-bit output writer for the decode walk: pieces arrive right to left; one word is
+// accumulated in registers and written when the writer moves left of it -- a plain store
+// when the word lies inside this record's range [lo, hi) (in characters), atomicOr for
+// the (at most two) boundary words shared with neighbouring records.
+struct CodeWriter {
+    uint64_t *O;        // zeroed 2-bit output, character g at bits 2(g%32) of word g/32
+    uint64_t lo, hi;    // this record's characters
+    uint64_t w;         // word being accumulated (~0: none)
+    uint64_t acc;
+    NTC_HD void flush() {
+        if (w == ~0ULL) return;
+        if (w * 32 >= lo && w * 32 + 32 <= hi) {
+            O[w] = acc;
+        } else {
+#ifdef __HIP_DEVICE_COMPILE__
+            atomicOr(reinterpret_cast<unsigned long long *>(O + w), (unsigned long long)acc);
+#else
+            O[w] |= acc;
+#endif
+        }
+    }
+    NTC_HD void put_word_part(uint64_t word, uint64_t bits) {
+        if (word != w) {
+            flush();
+            w = word;
+            acc = 0;
+        }
+        acc |= bits;
+    }
+    // n <= 32 codes (code t at bits 2t) for characters [g, g + n)
+    NTC_HD void put(uint64_t g, uint64_t codes, uint32_t n) {
+        if (n == 0) return;
+        if (n < 32) codes &= (1ULL << (2 * n)) - 1;
+        const uint64_t w0 = g >> 5, w1 = (g + n - 1) >> 5;
+        const uint32_t sh = (uint32_t)(g & 31) * 2;
+        if (w1 != w0) put_word_part(w1, codes >> (64 - sh));  // right part first
+        put_word_part(w0, codes << sh);
+    }
+};
+
+// The L characters of the L-step inverse walk from node j, to output characters
+// [g0, g0 + L) of a CodeWriter; false on a malformed record.
+NTC_HD bool walk_record_codes(const DevIndex &ix, uint32_t j, uint32_t L, uint64_t g0, CodeWriter &cw) {
+    uint32_t end = L, cur = j;
+    while (end > 0) {
+        if (cur >= ix.n) return false;
+#ifdef __HIP_DEVICE_COMPILE__
+        const uint4 e4 = *reinterpret_cast<const uint4 *>(ix.walk + cur);
+        const uint64_t chars = (uint64_t)e4.x | ((uint64_t)e4.y << 32);
+        const uint32_t jump = e4.z, older = e4.w;
+#else
+        const uint64_t chars = ix.walk[cur].chars;
+        const uint32_t jump = ix.walk[cur].jump, older = ix.walk[cur].older;
+#endif
+        const uint32_t take = end < kWalkSpan ? end : kWalkSpan;
+        const uint32_t t32 = take < 32 ? take : 32;
+        cw.put(g0 + end - t32, t32 ? chars >> (2 * (32 - t32)) : 0, t32);
+        const uint32_t t16 = take - t32;
+        if (t16) cw.put(g0 + end - take, (uint64_t)(older >> (2 * (16 - t16))), t16);
+        end -= take;
+        cur = jump;
+    }
+    return true;
+}
+
 // Writes the L characters of the L-step inverse walk from node j into out[0..L).
 NTC_HD bool walk_record(const DevIndex &ix, uint32_t j, uint32_t L, uint8_t *out) {
     uint32_t end = L, cur = j;
@@ -962,15 +1048,16 @@ NTC_HD bool walk_record(const DevIndex &ix, uint32_t j, uint32_t L, uint8_t *out
 #ifdef __HIP_DEVICE_COMPILE__
         const uint4 e4 = *reinterpret_cast<const uint4 *>(ix.walk + cur);
         const uint64_t chars = (uint64_t)e4.x | ((uint64_t)e4.y << 32);
-        const uint32_t jump = e4.z;
+        const uint32_t jump = e4.z, older = e4.w;
 #else
         const uint64_t chars = ix.walk[cur].chars;
-        const uint32_t jump = ix.walk[cur].jump;
+        const uint32_t jump = ix.walk[cur].jump, older = ix.walk[cur].older;
 #endif
-        const uint32_t take = end < 32 ? end : 32;
-        const uint32_t sh = 32 - take;
-        for (uint32_t u = 0; u < take; u++)
-            out[end - take + u] = base_char((uint32_t)(chars >> (2 * (sh + u))));
+        const uint32_t take = end < kWalkSpan ? end : kWalkSpan;
+        const uint32_t t32 = take < 32 ? take : 32;  // from `chars`
+        store_codes(out + end - t32, t32 ? chars >> (2 * (32 - t32)) : 0, t32);
+        const uint32_t t16 = take - t32;  // from `older`
+        if (t16) store_codes(out + end - take, (uint64_t)(older >> (2 * (16 - t16))), t16);
         end -= take;
         cur = jump;
     }

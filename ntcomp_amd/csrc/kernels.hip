@@ -329,21 +329,52 @@ __global__ __launch_bounds__(256) void k_dec_index(DecIndexArgs a) {
 // one lane per RECORD: records are independent once their output offsets are known.  A
 // read's records are consumed last to first (lib.rs:266), so record r of read rid (records
 // [rb, re)) lands at E[rb] + (E[re] - E[r + 1]) with E the exclusive scan of lengths.
+// Characters go to the zeroed 2-bit array O2 (CodeWriter); k_dec_expand writes ASCII.
 __global__ __launch_bounds__(256) void k_dec_rec(DecWalkArgs a) {
     const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (r >= a.n) return;
     if (*a.status != ~0ull) return;
     const uint64_t rid = a.fscan[r + 1] - 1;  // record 0 is a first record (k_dec_index)
     const uint64_t rb = a.rec_start[rid], re = a.rec_start[rid + 1];
-    uint8_t *out = a.out + a.E[rb] + (a.E[re] - a.E[r + 1]);
+    const uint64_t g0 = a.E[rb] + (a.E[re] - a.E[r + 1]);
     const uint64_t w = a.recs[r];
     const uint32_t flag = (uint32_t)(w >> 56);
+    const uint32_t L = (flag & 2) ? (flag >> 2) : ((uint32_t)(w >> 32) & 0xFFFFFFu);
+    CodeWriter cw{a.O2, g0, g0 + L, ~0ULL, 0};
     if (flag & 2) {
-        const uint32_t len = flag >> 2;
-        for (uint32_t j = 0; j < len; j++) out[j] = base_char((uint32_t)(w >> (2 * j)));
-    } else if (!walk_record(a.ix, (uint32_t)w, (uint32_t)(w >> 32) & 0xFFFFFFu, out)) {
+        cw.put(g0, w, L);
+    } else if (!walk_record_codes(a.ix, (uint32_t)w, L, g0, cw)) {
         atomicMin(a.status, (unsigned long long)((rid << 8) | (uint64_t)kErrFormat));
+        return;
     }
+    cw.flush();
+}
+
+// 2-bit output -> ASCII, 32 characters per thread (two 16-byte stores when the output is
+// 16-byte aligned, the common case), then re-zero the word for the next call
+__global__ __launch_bounds__(256) void k_dec_expand(const uint64_t *E, uint64_t n, uint64_t *O2, uint8_t *out,
+                                                    const unsigned long long *status) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t total = E[n];
+    if (t * 32 >= total) return;
+    const uint64_t codes = O2[t];
+    O2[t] = 0;
+    if (*status != ~0ull) return;
+    const uint32_t cnt = total - t * 32 < 32 ? (uint32_t)(total - t * 32) : 32u;
+    uint8_t *o = out + t * 32;
+    if (cnt == 32 && (((uintptr_t)out) & 15) == 0) {
+        uint32_t v[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const uint32_t x = (uint32_t)(codes >> (8 * q)) & 0xFFu;
+            const uint32_t spread = (x & 3u) | ((x & 0xCu) << 6) | ((x & 0x30u) << 12) | ((x & 0xC0u) << 18);
+            v[q] = __builtin_amdgcn_perm(0u, 0x54474341u, spread);
+        }
+        reinterpret_cast<uint4 *>(o)[0] = make_uint4(v[0], v[1], v[2], v[3]);
+        reinterpret_cast<uint4 *>(o)[1] = make_uint4(v[4], v[5], v[6], v[7]);
+        return;
+    }
+    for (uint32_t i = 0; i < cnt; i++) o[i] = base_char((uint32_t)(codes >> (2 * i)));
 }
 
 // ---------------------------------------------------------------------------------
@@ -356,7 +387,7 @@ __global__ __launch_bounds__(256) void k_walk_init(const uint32_t *pred, const u
     WalkEntry e;
     e.chars = code[j];
     e.jump = pred[j];
-    e.pad = 0;
+    e.older = 0;
     w[j] = e;
 }
 
@@ -369,8 +400,19 @@ __global__ __launch_bounds__(256) void k_walk_double(const WalkEntry *a, WalkEnt
     WalkEntry o;
     o.chars = y.chars | (x.chars << (2 * m));
     o.jump = y.jump;
-    o.pad = 0;
+    o.older = 0;
     b[j] = o;
+}
+
+// 48-step entries: the 16 characters before the 32 of w32[j], from w16 at its jump
+__global__ __launch_bounds__(256) void k_walk_ext(WalkEntry *w32, const WalkEntry *w16, uint64_t n) {
+    const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    WalkEntry x = w32[j];
+    const WalkEntry y = w16[x.jump];
+    x.older = (uint32_t)y.chars;
+    x.jump = y.jump;
+    w32[j] = x;
 }
 
 // ---------------------------------------------------------------------------------
@@ -564,6 +606,10 @@ void launch_dec_index(const DecIndexArgs &a, hipStream_t s) {
 void launch_dec_walk(const DecWalkArgs &a, hipStream_t s) {
     hipLaunchKernelGGL(k_dec_rec, grid_for(a.n), dim3(256), 0, s, a);
 }
+void launch_dec_expand(const uint64_t *E, uint64_t n, uint64_t max_bases, uint64_t *O2, uint8_t *out,
+                       const unsigned long long *status, hipStream_t s) {
+    hipLaunchKernelGGL(k_dec_expand, grid_for((max_bases + 31) / 32), dim3(256), 0, s, E, n, O2, out, status);
+}
 void launch_walk_build(const uint32_t *pred, const uint8_t *code, uint64_t n, WalkEntry *a, WalkEntry *b,
                        WalkEntry **result, hipStream_t s) {
     hipLaunchKernelGGL(k_walk_init, grid_for(n), dim3(256), 0, s, pred, code, n, a);
@@ -573,6 +619,8 @@ void launch_walk_build(const uint32_t *pred, const uint8_t *code, uint64_t n, Wa
         a = b;
         b = t;
     }
+    // a = 32-step entries, b = 16-step entries
+    hipLaunchKernelGGL(k_walk_ext, grid_for(n), dim3(256), 0, s, a, (const WalkEntry *)b, n);
     *result = a;
 }
 

@@ -125,29 +125,34 @@ extern "C" int emu_decode(const ntc_index_view *v, const uint64_t *recs, uint64_
     std::vector<uint32_t> bits, fbits;
     DevIndex d;
     if (!load(v, hx, dv, walk, d, tab, bits, fbits, 1)) return NTC_ERR_FORMAT;
-    std::vector<uint64_t> starts;
-    uint64_t total = 0;
+    // the kernels' decode: per record, 2-bit codes via CodeWriter, then ASCII (k_dec_rec +
+    // k_dec_expand); a read's records are consumed last to first (lib.rs:266)
+    std::vector<uint64_t> starts, lens(n), E(n + 1, 0);
     for (uint64_t r = 0; r < n; r++) {
-        uint32_t flag = (uint32_t)(recs[r] >> 56);
+        const uint32_t flag = (uint32_t)(recs[r] >> 56);
         if (flag & 1) starts.push_back(r);
-        total += (flag & 2) ? (flag >> 2) : ((uint32_t)(recs[r] >> 32) & 0xFFFFFF);
+        lens[r] = (flag & 2) ? (flag >> 2) : ((uint32_t)(recs[r] >> 32) & 0xFFFFFF);
+        E[r + 1] = E[r] + lens[r];
     }
+    const uint64_t total = E[n];
     if (total > cap || starts.size() + 1 > offcap) return NTC_ERR_CAPACITY;
     if (n && (starts.empty() || starts[0] != 0)) return NTC_ERR_FORMAT;
     starts.push_back(n);
-    uint64_t pos = 0;
+    std::vector<uint64_t> O2(total / 32 + 2, 0);
     offs[0] = 0;
     for (size_t i = 0; i + 1 < starts.size(); i++) {
-        uint64_t len = 0;
-        for (uint64_t r = starts[i]; r < starts[i + 1]; r++) {
-            uint32_t flag = (uint32_t)(recs[r] >> 56);
-            len += (flag & 2) ? (flag >> 2) : ((uint32_t)(recs[r] >> 32) & 0xFFFFFF);
+        const uint64_t rb = starts[i], re = starts[i + 1];
+        for (uint64_t r = rb; r < re; r++) {
+            const uint64_t g0 = E[rb] + (E[re] - E[r + 1]);
+            CodeWriter cw{O2.data(), g0, g0 + lens[r], ~0ULL, 0};
+            const uint64_t w = recs[r];
+            if ((w >> 56) & 2) cw.put(g0, w, (uint32_t)lens[r]);
+            else if (!walk_record_codes(d, (uint32_t)w, (uint32_t)lens[r], g0, cw)) return NTC_ERR_FORMAT;
+            cw.flush();
         }
-        int rc = decode_read(d, recs, starts[i], starts[i + 1], out + pos, len);
-        if (rc < 0) return -rc;
-        pos += len;
-        offs[i + 1] = pos;
+        offs[i + 1] = E[re];
     }
+    for (uint64_t g = 0; g < total; g++) out[g] = base_char((uint32_t)(O2[g >> 5] >> (2 * (g & 31))));
     *nreads = starts.size() - 1;
     return NTC_OK;
 }
