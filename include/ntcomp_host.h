@@ -36,6 +36,22 @@ int ntc_index_view_of(const ntc_index_host *ix, ntc_index_view *view);
 int ntc_index_save(const ntc_index_host *ix, const char *prefix);
 int ntc_index_load(const char *prefix, ntc_index_host **out);
 
+/* ---- FASTX ingest (CLI) -------------------------------------------------------------- */
+/* needletail::parse_fastx_file + SequenceRecord::normalize(true) as src/main.rs:51-62 and
+ * :158-163 use them: plain or gzip FASTA/FASTQ, sequences normalized (ACGTN- kept, lower
+ * case upper-cased, U -> T, IUPAC kept, whitespace dropped, anything else -> N), names
+ * dropped.  Batches hold up to max_reads reads / about max_bases bases; the buffers are
+ * owned by the reader and valid until the next call.  n_reads = 0 at end of input.    */
+typedef struct ntc_fastx ntc_fastx;
+int ntc_fastx_open(const char *path, ntc_fastx **out);
+int ntc_fastx_next_batch(ntc_fastx *fx, uint64_t max_reads, uint64_t max_bases, const uint8_t **bases,
+                         const uint64_t **offsets, uint64_t *n_reads);
+void ntc_fastx_close(ntc_fastx *fx);
+/* decode output (src/main.rs:203-209): ">seq.{first_id + r}\n{read r}\n" for each read;
+ * *out is freed with ntc_buffer_free (include/ntcomp_codec.h).                         */
+int ntc_fasta_format(const uint8_t *bases, const uint64_t *offsets, uint64_t n_reads, uint64_t first_id,
+                     uint8_t **out, uint64_t *out_len);
+
 /* ---- synthetic workload ------------------------------------------- */
 /* i.i.d. uniform ACGT genome from SplitMix64(seed). */
 int ntc_synth_genome(uint64_t seed, uint64_t length, uint8_t *out);

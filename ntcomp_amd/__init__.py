@@ -40,6 +40,7 @@ EXPORTED = [
     "ntc_memcpy_d2h", "ntc_debug_matching_statistics", "ntc_build_index", "ntc_index_free",
     "ntc_index_view_of", "ntc_index_save", "ntc_index_load", "ntc_synth_genome", "ntc_synth_reads",
     "ntc_file_header", "ntc_write_block", "ntc_read_block", "ntc_buffer_free",
+    "ntc_fastx_open", "ntc_fastx_next_batch", "ntc_fastx_close", "ntc_fasta_format",
 ]
 
 
@@ -114,6 +115,10 @@ def lib():
         "ntc_read_block": (I, [P, u64, ctypes.POINTER(u64), ctypes.POINTER(P), ctypes.POINTER(u64),
                                ctypes.POINTER(u64)]),
         "ntc_buffer_free": (None, [P]),
+        "ntc_fastx_open": (I, [ctypes.c_char_p, ctypes.POINTER(P)]),
+        "ntc_fastx_next_batch": (I, [P, u64, u64, ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(u64)]),
+        "ntc_fastx_close": (None, [P]),
+        "ntc_fasta_format": (I, [P, P, u64, u64, ctypes.POINTER(P), ctypes.POINTER(u64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -415,3 +420,61 @@ def read_block(data):
     finally:
         lib().ntc_buffer_free(recs)
     return arr, int(used.value), int(nrec.value)
+
+
+# ---- FASTX ingest ---------------------------------------------------------------------
+class FastxReader:
+    """needletail::parse_fastx_file + normalize(true) (src/main.rs:51-62, 158-163): plain or
+    gzip FASTA/FASTQ -> batches of (bases, read offsets) as numpy arrays (copies)."""
+
+    def __init__(self, path):
+        self.h = ctypes.c_void_p()
+        rc = lib().ntc_fastx_open(os.fsencode(path), ctypes.byref(self.h))
+        if rc:
+            raise NtcError(rc, f"ntc_fastx_open({path})")
+
+    def batch(self, max_reads=1 << 20, max_bases=1 << 28):
+        b, o, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+        rc = lib().ntc_fastx_next_batch(self.h, max_reads, max_bases, ctypes.byref(b), ctypes.byref(o), ctypes.byref(n))
+        if rc:
+            raise NtcError(rc, "ntc_fastx_next_batch")
+        if n.value == 0:
+            return None
+        offs = np.ctypeslib.as_array((ctypes.c_uint64 * (n.value + 1)).from_address(o.value)).copy()
+        total = int(offs[-1])
+        bases = (np.ctypeslib.as_array((ctypes.c_uint8 * total).from_address(b.value)).copy() if total
+                 else np.zeros(0, dtype=np.uint8))
+        return bases, offs
+
+    def __iter__(self):
+        while True:
+            x = self.batch()
+            if x is None:
+                return
+            yield x
+
+    def close(self):
+        if self.h:
+            lib().ntc_fastx_close(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def fasta_format(bases, offsets, first_id):
+    """Decode output lines (src/main.rs:203-209): '>seq.{first_id + r}' + read r."""
+    bases = np.ascontiguousarray(bases, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    out, n = ctypes.c_void_p(), ctypes.c_uint64()
+    b = bases if len(bases) else np.zeros(1, dtype=np.uint8)
+    rc = lib().ntc_fasta_format(_p(b), _p(offsets), len(offsets) - 1, first_id, ctypes.byref(out), ctypes.byref(n))
+    if rc:
+        raise NtcError(rc, "ntc_fasta_format")
+    try:
+        return ctypes.string_at(out.value, n.value)
+    finally:
+        lib().ntc_buffer_free(out)
