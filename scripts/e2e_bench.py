@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""End-to-end CLI timing: synthetic FASTQ -> `ntcomp encode` ->
+encoded.dat -> `ntcomp decode` -> FASTA, wall clock of each CLI process (index prebuilt
+and saved first; the input reads come from the same generator as bench.py)."""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reads", type=int, default=2_000_000)
+    ap.add_argument("--read-len", type=int, default=150)
+    ap.add_argument("--k", type=int, default=91)
+    ap.add_argument("--genome-bp", type=int, default=5_000_000)
+    ap.add_argument("--dir", default="/tmp/ntc_e2e")
+    ap.add_argument("--gzip", action="store_true", help="gzip the FASTQ (level 1)")
+    a = ap.parse_args()
+    import numpy as np
+    import ntcomp_amd as nt
+    os.makedirs(a.dir, exist_ok=True)
+    genome = nt.synth_genome(1, a.genome_bp)
+    ix = nt.Index.build([genome.tobytes()], a.k, threads=16)
+    prefix = os.path.join(a.dir, "idx")
+    ix.save(prefix)
+    L, n = a.read_len, a.reads
+    reads = nt.synth_reads(genome, 2, 0, n, L, 10_000, threads=16)
+    fq = os.path.join(a.dir, "reads.fq" + (".gz" if a.gzip else ""))
+    # FASTQ: @r<i> / read / + / constant quality (vectorised)
+    t0 = time.time()
+    body = reads.reshape(n, L)
+    qual = np.full((n, L), ord("I"), dtype=np.uint8)
+    nl = np.full((n, 1), 10, dtype=np.uint8)
+    plus = np.frombuffer(b"+\n", dtype=np.uint8)[None, :].repeat(n, 0)
+    head = np.frombuffer(b"@r\n", dtype=np.uint8)[None, :].repeat(n, 0)
+    rec = np.concatenate([head, body, nl, plus, qual, nl], axis=1).tobytes()
+    if a.gzip:
+        import gzip
+        with gzip.open(fq, "wb", compresslevel=1) as f:
+            f.write(rec)
+    else:
+        with open(fq, "wb") as f:
+            f.write(rec)
+    print(f"fastq {len(rec) / 1e9:.2f} GB written in {time.time() - t0:.1f}s", file=sys.stderr)
+    enc, dec = os.path.join(a.dir, "enc.dat"), os.path.join(a.dir, "dec.fa")
+    cmd = [sys.executable, "-m", "ntcomp_amd"]
+    t0 = time.time()
+    with open(enc, "wb") as f:
+        subprocess.run(cmd + ["encode", "-i", prefix, fq], stdout=f, check=True, cwd=REPO)
+    te = time.time() - t0
+    t0 = time.time()
+    with open(dec, "wb") as f:
+        subprocess.run(cmd + ["decode", "-i", prefix, enc], stdout=f, check=True, cwd=REPO)
+    td = time.time() - t0
+    ok = open(dec, "rb").read().split(b"\n")[1::2]
+    same = b"".join(ok) == reads.tobytes()
+    bases = n * L
+    print(json.dumps({"metric": "end-to-end CLI Mbases/s (process wall clock, incl. index load + upload)",
+                      "reads": n, "read_len": L, "k": a.k, "fastq_bytes": len(rec), "gzip": a.gzip,
+                      "encode_s": round(te, 3), "encode_mbases_s": round(bases / te / 1e6, 1),
+                      "encoded_bytes": os.path.getsize(enc), "bits_per_base": round(8 * os.path.getsize(enc) / bases, 4),
+                      "decode_s": round(td, 3), "decode_mbases_s": round(bases / td / 1e6, 1),
+                      "round_trip_exact": same}))
+
+
+if __name__ == "__main__":
+    main()
