@@ -63,8 +63,11 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")  # barrier + max of the timed region only
+    # one GPU per rank; on a box with fewer GPUs than ranks (a rehearsal), ranks share them
+    ndev = torch.cuda.device_count()
+    device = local % ndev if ndev else local
     if torch.cuda.is_available():
-        torch.cuda.set_device(local)
+        torch.cuda.set_device(device)
 
     import ntcomp_amd as nt
     from ntcomp_amd import shard
@@ -84,7 +87,7 @@ def main():
     genome = nt.synth_genome(1, args.genome_bp)
     index = nt.Index.build([genome.tobytes()], args.k, threads=nthreads)
     log(f"[rank {rank}] index k={args.k} n={index.n} built in {time.time() - t0:.1f}s")
-    ctx = nt.GpuContext(local)
+    ctx = nt.GpuContext(device)
     ctx.set_option("encode_variant", args.variant)
     for kv in args.opt:
         key, val = kv.split("=")
