@@ -222,3 +222,71 @@ def test_gpu_device_api_unaligned_ragged(ctx, lead):
     finally:
         for p in (db, do, dr, dro):
             ctx.free(p)
+
+
+def _repeat_genome(seed, units, unit_len, mut, spacer):
+    rng = np.random.default_rng(seed)
+    unit = nt.synth_genome(seed, unit_len).tobytes()
+    parts = []
+    for _ in range(units):
+        u = bytearray(unit)
+        for _ in range(mut):
+            u[int(rng.integers(0, len(u)))] = b"ACGT"[int(rng.integers(0, 4))]
+        parts.append(bytes(u) + nt.synth_genome(int(rng.integers(1, 1 << 30)), spacer).tobytes())
+    return np.frombuffer(b"".join(parts), dtype=np.uint8)
+
+
+@pytest.mark.parametrize("k,err_ppm,genome_kind,L", [
+    (31, 10_000, "random", 150), (91, 20_000, "random", 150), (63, 5_000, "repeats", 150),
+    (91, 10_000, "repeats", 250), (127, 10_000, "random", 300), (21, 50_000, "random", 100)])
+def test_gpu_parity_sweep(ctx, k, err_ppm, genome_kind, L):
+    """Larger sweep: 60k reads per config, bit-exact records and exact round trips, on
+    random genomes and on genomes of near-identical repeats (long LCS runs, branching
+    paths, contraction probes above U - 1 and binary searches)."""
+    genome = nt.synth_genome(70 + k, 2_000_000) if genome_kind == "random" else _repeat_genome(k, 600, 700, 4, 150)
+    ix = nt.Index.build([genome.tobytes()], k, threads=8)
+    ctx.upload(ix)
+    n = 60_000
+    reads = nt.synth_reads(genome, 31, 0, n, L, err_ppm, threads=8)
+    offs = np.arange(0, n * L + 1, L, dtype=np.uint64)
+    exp, eoff = OracleIndex(ix.n, k, ix.rows, ix.C, ix.lcs).encode(reads, offs)
+    got, goff = ctx.encode(reads, offs)
+    assert np.array_equal(goff, eoff) and np.array_equal(got, exp)
+    out, o2 = ctx.decode(got)
+    assert np.array_equal(out, reads) and np.array_equal(o2, offs)
+
+
+def test_gpu_reads_with_n_report_the_first_bad_read(ctx):
+    genome = nt.synth_genome(15, 100_000)
+    ctx.upload(nt.Index.build([genome.tobytes()], 31))
+    reads = bytearray(nt.synth_reads(genome, 3, 0, 5000, 150, 10_000).tobytes())
+    for r in (3210, 4000, 77):
+        reads[r * 150 + 40] = ord("N")
+    bases = np.frombuffer(bytes(reads), dtype=np.uint8)
+    offs = np.arange(0, 5000 * 150 + 1, 150, dtype=np.uint64)
+    with pytest.raises(nt.NtcError) as e:
+        ctx.encode(bases, offs)
+    assert e.value.code == 2 and e.value.bad_read == 77
+
+
+def test_gpu_long_reads(ctx):
+    """Nanopore-length reads (10-30 kb) at k = 31: many runs and errors per read."""
+    genome = nt.synth_genome(16, 400_000)
+    ix = nt.Index.build([genome.tobytes()], 31)
+    ctx.upload(ix)
+    rng = np.random.default_rng(8)
+    g = genome.tobytes()
+    reads = []
+    for _ in range(40):
+        L = int(rng.integers(10_000, 30_000))
+        st = int(rng.integers(0, len(g) - L))
+        s = bytearray(g[st:st + L])
+        for _ in range(L // 100):
+            s[int(rng.integers(0, L))] = b"ACGT"[int(rng.integers(0, 4))]
+        reads.append(bytes(s))
+    bases, offs = pack_reads(reads)
+    exp, eoff = OracleIndex(ix.n, 31, ix.rows, ix.C, ix.lcs).encode(bases, offs)
+    got, goff = ctx.encode(bases, offs)
+    assert np.array_equal(goff, eoff) and np.array_equal(got, exp)
+    out, o2 = ctx.decode(got)
+    assert np.array_equal(out, bases) and np.array_equal(o2, offs)
