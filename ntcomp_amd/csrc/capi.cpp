@@ -589,15 +589,14 @@ int ntc_decode_batch_device(ntc_ctx *ctx, const uint64_t *d_recs, uint64_t n_rec
     if (!ctx || (!d_recs && n_recs) || !d_read_offsets_out) return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument");
     if (!ctx->has_index) return set_err(ctx, NTC_ERR_NO_INDEX, "no index uploaded");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    void *first, *lens, *fscan, *E, *rstart, *tmp;
+    void *fscan, *E, *rstart, *tmp;
     int rc;
     const uint64_t n = n_recs;
-    if ((rc = ensure(ctx, WS_DEC_A, (n + 1) * 4, &first))) return rc;
-    if ((rc = ensure(ctx, WS_DEC_B, (n + 1) * 4, &lens))) return rc;
     if ((rc = ensure(ctx, WS_DEC_C, (n + 1) * 8 * 2, &fscan))) return rc;
     E = (uint64_t *)fscan + (n + 1);
     if ((rc = ensure(ctx, WS_DEC_D, (n + 1) * 8, &rstart))) return rc;
-    if ((rc = ensure(ctx, WS_SCANTMP, scan_tmp_words(n + 1) * 8, &tmp))) return rc;
+    if ((rc = ensure(ctx, WS_SCANTMP, (4 * (n / 2048 + 2) + scan_tmp_words(n / 2048 + 2)) * 8, &tmp)))
+        return rc;
     void *o2;
     if ((rc = ensure(ctx, WS_O2, (bases_capacity / 32 + 2) * 8, &o2))) return rc;
     if (o2 != ctx->o2_zeroed || ctx->ws[WS_O2].bytes != ctx->o2_zeroed_bytes) {
@@ -618,9 +617,6 @@ int ntc_decode_batch_device(ntc_ctx *ctx, const uint64_t *d_recs, uint64_t n_rec
         HIP_TRY(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
         return NTC_OK;
     }
-    launch_dec_prep(d_recs, n, (uint32_t *)first, (uint32_t *)lens, ctx->stream);
-    scan_excl_u32((const uint32_t *)first, n, (uint64_t *)fscan, (uint64_t *)tmp, ctx->stream);
-    scan_excl_u32((const uint32_t *)lens, n, (uint64_t *)E, (uint64_t *)tmp, ctx->stream);
     DecIndexArgs ia{};
     ia.recs = d_recs;
     ia.n = n;
@@ -631,7 +627,7 @@ int ntc_decode_batch_device(ntc_ctx *ctx, const uint64_t *d_recs, uint64_t n_rec
     ia.offs_capacity = offsets_capacity;
     ia.bases_capacity = bases_capacity;
     ia.status = ctx->d_status;
-    launch_dec_index(ia, ctx->stream);
+    launch_dec_index_fused(ia, (uint64_t *)fscan, (uint64_t *)E, (uint64_t *)tmp, ctx->stream);
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
     DecWalkArgs wa{};

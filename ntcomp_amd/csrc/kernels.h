@@ -97,8 +97,8 @@ void launch_tab_build(const DevIndex &ix, uint32_t U, uint2 *tab, uint32_t *bits
 void launch_tile_rows(const uint64_t *offs, uint64_t n_reads, uint32_t *tile_rows, hipStream_t s);
 void launch_emit(const EmitArgs &a, hipStream_t s);
 void launch_debug_gather(const DebugArgs &a, hipStream_t s);
-void launch_dec_prep(const uint64_t *recs, uint64_t n, uint32_t *first, uint32_t *lens, hipStream_t s);
-void launch_dec_index(const DecIndexArgs &a, hipStream_t s);
+// fscan + E + read starts/offsets in one reduce + apply pass (tmp: 4 * tiles + 2 + scan_tmp_words)
+void launch_dec_index_fused(const DecIndexArgs &a, uint64_t *fscan, uint64_t *E, uint64_t *tmp, hipStream_t s);
 void launch_dec_walk(const DecWalkArgs &a, hipStream_t s);
 void launch_dec_expand(const uint64_t *E, uint64_t n, uint64_t max_bases, uint64_t *O2, uint8_t *out,
                        const unsigned long long *status, hipStream_t s);

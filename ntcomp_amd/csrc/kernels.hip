@@ -295,37 +295,6 @@ __global__ __launch_bounds__(256) void k_debug_gather(DebugArgs a) {
 // ---------------------------------------------------------------------------------
 // decode
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_dec_prep(const uint64_t *recs, uint64_t n, uint32_t *first,
-                                                  uint32_t *lens) {
-    const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (r >= n) return;
-    const uint64_t w = recs[r];
-    const uint32_t flag = (uint32_t)(w >> 56);
-    first[r] = flag & 1;
-    lens[r] = (flag & 2) ? (flag >> 2) : ((uint32_t)(w >> 32) & 0xFFFFFFu);
-}
-
-__global__ __launch_bounds__(256) void k_dec_index(DecIndexArgs a) {
-    const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (r > a.n) return;
-    const uint64_t nreads = a.fscan[a.n];
-    if (r == a.n) {
-        a.rec_start[nreads] = a.n;
-        if (nreads + 1 > a.offs_capacity || a.E[a.n] > a.bases_capacity)
-            atomicMin(a.status, (unsigned long long)kErrCapacity);
-        else
-            a.offs_out[nreads] = a.E[a.n];
-        return;
-    }
-    const bool first = (a.recs[r] >> 56) & 1;
-    if (r == 0 && !first) atomicMin(a.status, (unsigned long long)kErrFormat);
-    if (first) {
-        const uint64_t rid = a.fscan[r];
-        a.rec_start[rid] = r;
-        if (rid < a.offs_capacity) a.offs_out[rid] = a.E[r];
-    }
-}
-
 // one lane per RECORD: records are independent once their output offsets are known.  A
 // read's records are consumed last to first (lib.rs:266), so record r of read rid (records
 // [rb, re)) lands at E[rb] + (E[re] - E[r + 1]) with E the exclusive scan of lengths.
@@ -334,7 +303,7 @@ __global__ __launch_bounds__(256) void k_dec_rec(DecWalkArgs a) {
     const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (r >= a.n) return;
     if (*a.status != ~0ull) return;
-    const uint64_t rid = a.fscan[r + 1] - 1;  // record 0 is a first record (k_dec_index)
+    const uint64_t rid = a.fscan[r + 1] - 1;  // record 0 is a first record (k_dec_apply)
     const uint64_t rb = a.rec_start[rid], re = a.rec_start[rid + 1];
     const uint64_t g0 = a.E[rb] + (a.E[re] - a.E[r + 1]);
     const uint64_t w = a.recs[r];
@@ -494,6 +463,132 @@ void scan_excl_t(const T *in, uint64_t n, uint64_t *out, uint64_t *tmp, hipStrea
                        (const uint64_t *)part_scan, out);
 }
 
+// ---- decode index: one pass over the record words --------------------------------------
+// Per record: fscan (exclusive count of first records = read id of the NEXT read) and E
+// (exclusive sum of segment lengths = output offset in record order).  The apply pass also
+// records each read's first record and its output offset.
+__device__ __forceinline__ void dec_desc(uint64_t w, uint64_t &f, uint64_t &len) {
+    const uint32_t flag = (uint32_t)(w >> 56);
+    f = flag & 1u;
+    len = (flag & 2u) ? (flag >> 2) : ((uint32_t)(w >> 32) & 0xFFFFFFu);
+}
+
+constexpr int kDecItems = 8;  // records per thread in the decode index scan
+constexpr uint64_t kDecTile = (uint64_t)kScanThreads * kDecItems;
+
+__global__ __launch_bounds__(kScanThreads) void k_dec_reduce(const uint64_t *recs, uint64_t n, uint64_t *pf,
+                                                             uint64_t *pl) {
+    const uint64_t base = (uint64_t)blockIdx.x * kDecTile + threadIdx.x;  // coalesced: order-free sums
+    uint64_t sf = 0, sl = 0;
+#pragma unroll
+    for (int j = 0; j < kDecItems; j++) {
+        const uint64_t r = base + (uint64_t)j * kScanThreads;
+        if (r < n) {
+            uint64_t f, l;
+            dec_desc(recs[r], f, l);
+            sf += f;
+            sl += l;
+        }
+    }
+    uint64_t tf, tl;
+    block_excl_scan(sf, tf);
+    block_excl_scan(sl, tl);
+    if (threadIdx.x == 0) {
+        pf[blockIdx.x] = tf;
+        pl[blockIdx.x] = tl;
+    }
+}
+
+// each wave scans its 512 records as 8 coalesced chunks of 64 (shuffle scan + carry),
+// then the 4 wave totals are combined once per block
+__global__ __launch_bounds__(kScanThreads) void k_dec_apply(DecIndexArgs a, const uint64_t *bf, const uint64_t *bl,
+                                                            uint64_t *fscan, uint64_t *E) {
+    __shared__ uint64_t s_wf[kScanThreads / 64], s_wl[kScanThreads / 64];
+    const uint64_t n = a.n;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t wbase = (uint64_t)blockIdx.x * kDecTile + (uint64_t)wave * 64 * kDecItems;
+    uint32_t exf[kDecItems];
+    uint64_t exl[kDecItems];
+    uint32_t firsts = 0, cf = 0;
+    uint64_t cl = 0;
+#pragma unroll
+    for (int j = 0; j < kDecItems; j++) {
+        const uint64_t r = wbase + (uint64_t)j * 64 + lane;
+        uint64_t f = 0, l = 0;
+        if (r < n) dec_desc(a.recs[r], f, l);
+        uint32_t incf = (uint32_t)f;
+        uint64_t incl = l;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t tf = __shfl_up(incf, o, 64);
+            const uint64_t tl = shfl_up64(incl, o);
+            if (lane >= (uint32_t)o) {
+                incf += tf;
+                incl += tl;
+            }
+        }
+        exf[j] = cf + incf - (uint32_t)f;
+        exl[j] = cl + incl - l;
+        firsts |= (uint32_t)f << j;
+        cf += __shfl(incf, 63, 64);
+        cl += (uint64_t)__shfl((uint32_t)incl, 63, 64) | ((uint64_t)__shfl((uint32_t)(incl >> 32), 63, 64) << 32);
+    }
+    if (lane == 0) {
+        s_wf[wave] = cf;
+        s_wl[wave] = cl;
+    }
+    __syncthreads();
+    uint64_t of = bf ? bf[blockIdx.x] : 0, ol = bl ? bl[blockIdx.x] : 0, tf = of, tl = ol;
+    for (uint32_t w = 0; w < kScanThreads / 64; w++) {
+        if (w < wave) {
+            of += s_wf[w];
+            ol += s_wl[w];
+        }
+        tf += s_wf[w];
+        tl += s_wl[w];
+    }
+#pragma unroll
+    for (int j = 0; j < kDecItems; j++) {
+        const uint64_t r = wbase + (uint64_t)j * 64 + lane;
+        if (r < n) {
+            const uint64_t rf = of + exf[j], rl = ol + exl[j];
+            fscan[r] = rf;
+            E[r] = rl;
+            if ((firsts >> j) & 1u) {  // first record of read rf
+                a.rec_start[rf] = r;
+                if (rf < a.offs_capacity) a.offs_out[rf] = rl;
+            } else if (r == 0) {
+                atomicMin(a.status, (unsigned long long)kErrFormat);  // records must start a read
+            }
+        }
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {  // totals (n is inside the last tile)
+        fscan[n] = tf;
+        E[n] = tl;
+        a.rec_start[tf] = n;
+        if (tf + 1 > a.offs_capacity || tl > a.bases_capacity)
+            atomicMin(a.status, (unsigned long long)kErrCapacity);
+        else
+            a.offs_out[tf] = tl;
+    }
+}
+
+void launch_dec_index_fused(const DecIndexArgs &a, uint64_t *fscan, uint64_t *E, uint64_t *tmp, hipStream_t s) {
+    const uint64_t n = a.n;
+    const uint64_t nb = (n + kDecTile - 1) / kDecTile;
+    if (nb <= 1) {
+        hipLaunchKernelGGL(k_dec_apply, dim3(1), dim3(kScanThreads), 0, s, a, (const uint64_t *)nullptr,
+                           (const uint64_t *)nullptr, fscan, E);
+        return;
+    }
+    uint64_t *pf = tmp, *pl = tmp + nb, *pfs = pl + nb, *pls = pfs + nb + 1, *t2 = pls + nb + 1;
+    hipLaunchKernelGGL(k_dec_reduce, dim3((uint32_t)nb), dim3(kScanThreads), 0, s, a.recs, n, pf, pl);
+    scan_excl_t<uint64_t>(pf, nb, pfs, t2, s);
+    scan_excl_t<uint64_t>(pl, nb, pls, t2, s);
+    hipLaunchKernelGGL(k_dec_apply, dim3((uint32_t)nb), dim3(kScanThreads), 0, s, a, (const uint64_t *)pfs,
+                       (const uint64_t *)pls, fscan, E);
+}
+
 uint64_t scan_tmp_words(uint64_t n) {
     uint64_t w = 0;
     while (true) {
@@ -596,12 +691,6 @@ void launch_emit(const EmitArgs &a, hipStream_t s) {
 }
 void launch_debug_gather(const DebugArgs &a, hipStream_t s) {
     hipLaunchKernelGGL(k_debug_gather, grid_for(a.n_reads), dim3(256), 0, s, a);
-}
-void launch_dec_prep(const uint64_t *recs, uint64_t n, uint32_t *first, uint32_t *lens, hipStream_t s) {
-    hipLaunchKernelGGL(k_dec_prep, grid_for(n), dim3(256), 0, s, recs, n, first, lens);
-}
-void launch_dec_index(const DecIndexArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL(k_dec_index, grid_for(a.n + 1), dim3(256), 0, s, a);
 }
 void launch_dec_walk(const DecWalkArgs &a, hipStream_t s) {
     hipLaunchKernelGGL(k_dec_rec, grid_for(a.n), dim3(256), 0, s, a);

@@ -7,7 +7,7 @@ set -u
 OUT=${OUT:-gpurun_out/prof}
 MODE=${MODE:-encode}
 BENCH="bench.py --mode $MODE"
-KRE=${KRE:-'k_encode|k_ms4|k_parse4|k_pack|k_emit4|k_dec_rec|k_dec_prep|k_dec_index'}
+KRE=${KRE:-'k_encode|k_ms4|k_parse4|k_pack|k_emit4|k_dec_rec|k_dec_reduce|k_dec_apply|k_dec_expand'}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 run() {  # name, limit, rocprof args...
