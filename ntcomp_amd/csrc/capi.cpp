@@ -589,12 +589,11 @@ int ntc_decode_batch_device(ntc_ctx *ctx, const uint64_t *d_recs, uint64_t n_rec
     if (!ctx || (!d_recs && n_recs) || !d_read_offsets_out) return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument");
     if (!ctx->has_index) return set_err(ctx, NTC_ERR_NO_INDEX, "no index uploaded");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    void *fscan, *E, *rstart, *tmp;
+    void *fscan, *E, *tmp;
     int rc;
     const uint64_t n = n_recs;
     if ((rc = ensure(ctx, WS_DEC_C, (n + 1) * 8 * 2, &fscan))) return rc;
     E = (uint64_t *)fscan + (n + 1);
-    if ((rc = ensure(ctx, WS_DEC_D, (n + 1) * 8, &rstart))) return rc;
     if ((rc = ensure(ctx, WS_SCANTMP, (4 * (n / 2048 + 2) + scan_tmp_words(n / 2048 + 2)) * 8, &tmp)))
         return rc;
     void *o2;
@@ -620,9 +619,6 @@ int ntc_decode_batch_device(ntc_ctx *ctx, const uint64_t *d_recs, uint64_t n_rec
     DecIndexArgs ia{};
     ia.recs = d_recs;
     ia.n = n;
-    ia.fscan = (const uint64_t *)fscan;
-    ia.E = (const uint64_t *)E;
-    ia.rec_start = (uint64_t *)rstart;
     ia.offs_out = d_read_offsets_out;
     ia.offs_capacity = offsets_capacity;
     ia.bases_capacity = bases_capacity;
@@ -636,7 +632,7 @@ int ntc_decode_batch_device(ntc_ctx *ctx, const uint64_t *d_recs, uint64_t n_rec
     wa.n = n;
     wa.fscan = (const uint64_t *)fscan;
     wa.E = (const uint64_t *)E;
-    wa.rec_start = (const uint64_t *)rstart;
+    wa.offs_out = d_read_offsets_out;
     wa.out = d_bases_out;
     wa.O2 = (uint64_t *)o2;
     wa.status = ctx->d_status;

@@ -64,9 +64,6 @@ struct DebugArgs {
 struct DecIndexArgs {
     const uint64_t *recs;
     uint64_t n;
-    const uint64_t *fscan;   // exclusive scan of first flags, [n+1]
-    const uint64_t *E;       // exclusive scan of segment lengths, [n+1]
-    uint64_t *rec_start;     // [n+1]
     uint64_t *offs_out;      // caller's read offsets
     uint64_t offs_capacity;
     uint64_t bases_capacity;
@@ -77,9 +74,9 @@ struct DecWalkArgs {
     DevIndex ix;
     const uint64_t *recs;
     uint64_t n;
-    const uint64_t *fscan;
+    const uint64_t *fscan;       // read id of each record
     const uint64_t *E;
-    const uint64_t *rec_start;
+    const uint64_t *offs_out;    // each read's output offset [nreads + 1]
     uint8_t *out;
     uint64_t *O2;                // zeroed 2-bit output (k_dec_rec -> k_dec_expand)
     unsigned long long *status;

@@ -296,19 +296,19 @@ __global__ __launch_bounds__(256) void k_debug_gather(DebugArgs a) {
 // decode
 // ---------------------------------------------------------------------------------
 // one lane per RECORD: records are independent once their output offsets are known.  A
-// read's records are consumed last to first (lib.rs:266), so record r of read rid (records
-// [rb, re)) lands at E[rb] + (E[re] - E[r + 1]) with E the exclusive scan of lengths.
+// read's records are consumed last to first (lib.rs:266), so record r of read rid lands at
+// start(rid) + (end(rid) - E[r + 1]), with E the exclusive scan of lengths in record order
+// and start/end(rid) the read's output range (offs_out, written by k_dec_apply).
 // Characters go to the zeroed 2-bit array O2 (CodeWriter); k_dec_expand writes ASCII.
 __global__ __launch_bounds__(256) void k_dec_rec(DecWalkArgs a) {
     const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (r >= a.n) return;
     if (*a.status != ~0ull) return;
-    const uint64_t rid = a.fscan[r + 1] - 1;  // record 0 is a first record (k_dec_apply)
-    const uint64_t rb = a.rec_start[rid], re = a.rec_start[rid + 1];
-    const uint64_t g0 = a.E[rb] + (a.E[re] - a.E[r + 1]);
+    const uint64_t rid = a.fscan[r];  // read id of record r (k_dec_apply)
     const uint64_t w = a.recs[r];
     const uint32_t flag = (uint32_t)(w >> 56);
     const uint32_t L = (flag & 2) ? (flag >> 2) : ((uint32_t)(w >> 32) & 0xFFFFFFu);
+    const uint64_t g0 = a.offs_out[rid] + (a.offs_out[rid + 1] - (a.E[r] + L));
     CodeWriter cw{a.O2, g0, g0 + L, ~0ULL, 0};
     if (flag & 2) {
         cw.put(g0, w, L);
@@ -552,10 +552,10 @@ __global__ __launch_bounds__(kScanThreads) void k_dec_apply(DecIndexArgs a, cons
         const uint64_t r = wbase + (uint64_t)j * 64 + lane;
         if (r < n) {
             const uint64_t rf = of + exf[j], rl = ol + exl[j];
-            fscan[r] = rf;
+            const bool first = (firsts >> j) & 1u;
+            fscan[r] = first ? rf : rf - 1;  // read id of record r
             E[r] = rl;
-            if ((firsts >> j) & 1u) {  // first record of read rf
-                a.rec_start[rf] = r;
+            if (first) {  // first record of read rf: its output offset
                 if (rf < a.offs_capacity) a.offs_out[rf] = rl;
             } else if (r == 0) {
                 atomicMin(a.status, (unsigned long long)kErrFormat);  // records must start a read
@@ -565,7 +565,6 @@ __global__ __launch_bounds__(kScanThreads) void k_dec_apply(DecIndexArgs a, cons
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {  // totals (n is inside the last tile)
         fscan[n] = tf;
         E[n] = tl;
-        a.rec_start[tf] = n;
         if (tf + 1 > a.offs_capacity || tl > a.bases_capacity)
             atomicMin(a.status, (unsigned long long)kErrCapacity);
         else
