@@ -4,8 +4,9 @@ Mirrors the reference CLI (src/cli.rs:27-93, src/main.rs:91-211) with the hot pa
 the GPU: FASTX ingest in C++ (needletail parse + normalize(true) restated), encode /
 decode through libntcomp_gpu.so, blocks of 65,536 reads (main.rs:152) in the encoded.dat
 layout (file header lib.rs:52-67, write_block_to lib.rs:232-252), decode output
-">seq.N" (main.rs:203-209).  Block compression runs on a thread pool (ctypes releases the
-GIL); blocks are written in order.
+">seq.N" (main.rs:203-209).  Pipelined: FASTX parse runs a batch ahead on its own
+thread, block compression / unzip and FASTA formatting on a thread pool (ctypes releases
+the GIL), each GPU context on its own driver thread; blocks are written in file order.
 
 Index files: <prefix>.sbwt / <prefix>.lcs in this library's own layout (the sbwt 0.3.11
 byte layout is unavailable offline -- DESIGN.md section 8).
@@ -22,6 +23,42 @@ BLOCK_READS = 65536  # main.rs:152
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+class _Stats:
+    """--stats: seconds spent per pipeline stage (summed over threads) and wall clock."""
+
+    def __init__(self, on):
+        import threading
+        import time
+        self.on, self.time, self.lock = on, time.perf_counter, threading.Lock()
+        self.t0 = self.time()
+        self.acc = {}
+
+    def wrap(self, name, fn):
+        if not self.on:
+            return fn
+
+        def run(*a, **k):
+            t = self.time()
+            try:
+                return fn(*a, **k)
+            finally:
+                with self.lock:
+                    self.acc[name] = self.acc.get(name, 0.0) + self.time() - t
+        return run
+
+    def report(self, **extra):
+        if self.on:
+            import json
+            d = {k: round(v, 3) for k, v in self.acc.items()}
+            try:  # interpreter start -> now, imports included
+                import psutil
+                import time
+                extra["process_s"] = round(time.time() - psutil.Process().create_time(), 3)
+            except Exception:
+                pass
+            log(json.dumps({"stats": d, "wall_s": round(self.time() - self.t0, 3), **extra}))
 
 
 def _read_list(path):
@@ -58,26 +95,30 @@ def cmd_build(args):
     ix.save(args.output_prefix)
 
 
-def _open_gpus(index, n):
+def _open_gpus(index, n, st=None):
+    """One context per GPU, each holding its own copy of the index."""
     import ntcomp_amd as nt
     ctxs = []
     for d in range(n):
-        c = nt.GpuContext(d)
-        c.upload(index)
+        c = (st.wrap("gpu_init", nt.GpuContext) if st else nt.GpuContext)(d)
+        (st.wrap("index_upload", c.upload) if st else c.upload)(index)
+        if st and st.on:
+            st.acc["upload_host_derive"] = st.acc.get("upload_host_derive", 0.0) + c.get_option("upload_host_us") / 1e6
         ctxs.append(c)
     return ctxs
 
 
 def cmd_encode(args):
     import ntcomp_amd as nt
+    st = _Stats(args.stats)
     log("Loading SBWT index...")
-    index = nt.Index.load(args.index_prefix)
-    ctxs = _open_gpus(index, args.gpus)
+    index = st.wrap("index_load", nt.Index.load)(args.index_prefix)
+    ctxs = _open_gpus(index, args.gpus, st)
     out = sys.stdout.buffer
     out.write(nt.file_header())
     log("Encoding fastX data...")
     pool = cf.ThreadPoolExecutor(max_workers=args.threads)
-    gpu_pool = cf.ThreadPoolExecutor(max_workers=len(ctxs))
+    gpu_pools = [cf.ThreadPoolExecutor(max_workers=1) for _ in ctxs]  # one driver thread per context
     pending = []  # compressed blocks, in file order
 
     def flush(wait_all=False):
@@ -86,9 +127,11 @@ def cmd_encode(args):
             if data is not None:
                 out.write(data)
 
+    write_block = st.wrap("compress", nt.write_block)
+
     def compress(recs, nreads):
         try:
-            return nt.write_block(recs, nreads)
+            return write_block(recs, nreads)
         except nt.NtcError as e:
             if e.code == 3:  # a stream with no records: write_block_to errs, the
                 log("warning: block dropped (no long or no short records; main.rs:170 ignores the error)")
@@ -98,16 +141,22 @@ def cmd_encode(args):
     carry_recs, carry_counts = [], []  # records of reads not yet in a full block
     rd = nt.FastxReader(args.query_file)
     batch_reads = BLOCK_READS * args.blocks_per_batch
-    batches = iter(lambda: rd.batch(max_reads=batch_reads, max_bases=batch_reads * 1024), None)
-    # encode batches on the GPUs (one worker per GPU), blocks in order
-    jobs = []
+    # FASTX parse runs one batch ahead on its own thread (the C reader releases the GIL)
+    reader = cf.ThreadPoolExecutor(max_workers=1)
 
-    def encode_on(ctx, bases, offs):
-        return ctx.encode(bases, offs)
+    next_batch = st.wrap("parse", lambda: rd.batch(max_reads=batch_reads, max_bases=batch_reads * 1024))
+    encode_on = st.wrap("gpu_encode", lambda ctx, bases, offs: ctx.encode(bases, offs))
 
+    jobs = []  # GPU encodes in flight, in file order
     gi = 0
-    for bases, offs in batches:
-        jobs.append(gpu_pool.submit(encode_on, ctxs[gi % len(ctxs)], bases, offs))
+    nxt = reader.submit(next_batch)
+    while True:
+        x = nxt.result()
+        if x is None:
+            break
+        nxt = reader.submit(next_batch)
+        bases, offs = x
+        jobs.append(gpu_pools[gi % len(ctxs)].submit(encode_on, ctxs[gi % len(ctxs)], bases, offs))
         gi += 1
         while len(jobs) > len(ctxs) or (jobs and jobs[0].done()):
             _emit(jobs.pop(0).result(), carry_recs, carry_counts, pool, pending, compress)
@@ -121,9 +170,11 @@ def cmd_encode(args):
         pending.append(pool.submit(compress, recs, len(counts)))
     flush(wait_all=True)
     out.flush()
+    reader.shutdown()
     rd.close()
     for c in ctxs:
         c.close()
+    st.report(command="encode", gpus=len(ctxs))
 
 
 def _emit(result, carry_recs, carry_counts, pool, pending, compress):
@@ -149,42 +200,88 @@ def _emit(result, carry_recs, carry_counts, pool, pending, compress):
         carry_counts.append(allc[rest:])
 
 
+def _block_extents(data, pos):
+    """Byte ranges of the blocks after the file header: each block is four
+    (32-byte BlockHeader, gzip payload) streams, payload length = the header's first u32
+    (lib.rs:37-50, 232-252).  A truncated tail ends the list, as it ends the reference's
+    read loop (main.rs:202)."""
+    out, n = [], len(data)
+    while pos < n:
+        p = pos
+        for _ in range(4):
+            if p + 32 > n:
+                return out
+            p += 32 + int(np.frombuffer(data[p:p + 4], dtype="<u4")[0])
+        if p > n:
+            return out
+        out.append((pos, p))
+        pos = p
+    return out
+
+
 def cmd_decode(args):
     import ntcomp_amd as nt
-    index = nt.Index.load(args.index_prefix)
-    ctxs = _open_gpus(index, 1)
-    ctx = ctxs[0]
+    st = _Stats(args.stats)
+    index = st.wrap("index_load", nt.Index.load)(args.index_prefix)
+    ctxs = _open_gpus(index, args.gpus, st)
+    read_block = st.wrap("unzip", nt.read_block)
+    fasta_format = st.wrap("format", nt.fasta_format)
+    gpu_decode = st.wrap("gpu_decode", lambda ctx, r: ctx.decode(r))
     data = np.memmap(args.input_path, dtype=np.uint8, mode="r") if os.path.getsize(args.input_path) else \
         np.zeros(0, dtype=np.uint8)
     out = sys.stdout.buffer
     log("Decoding encoded data...")
-    pos = 32  # file header (decode_file_header, main.rs:196-198)
+    # blocks unzip in parallel on the CPU pool, batches decode on the GPUs (round-robin),
+    # FASTA formatting runs on the pool, and everything is written in file order
+    extents = _block_extents(data, 32)  # after the file header (main.rs:196-198)
+    pool = cf.ThreadPoolExecutor(max_workers=args.threads)
+    gpu_pools = [cf.ThreadPoolExecutor(max_workers=1) for _ in ctxs]  # one driver thread per context
+    bpb = args.blocks_per_batch
+    unzip = [pool.submit(read_block, data[a:b]) for a, b in extents[:2 * bpb]]
+    submitted = len(unzip)
+    decodes = []  # (future of (bases, offs)) in file order
+    formats = []  # (future of bytes) in file order
     seq_id = 1
-    batch, nbatch = [], 0
+    stop = False
 
-    def decode_flush():
-        nonlocal seq_id, batch, nbatch
-        if not batch:
-            return
-        recs = np.concatenate(batch)
-        bases, offs = ctx.decode(recs)
-        out.write(nt.fasta_format(bases, offs, seq_id))
-        seq_id += len(offs) - 1
-        batch, nbatch = [], 0
+    def finish_decodes(keep):
+        nonlocal seq_id
+        while len(decodes) > keep:
+            bases, offs = decodes.pop(0).result()
+            formats.append(pool.submit(fasta_format, bases, offs, seq_id))
+            seq_id += len(offs) - 1
+            while formats and (formats[0].done() or len(formats) > 2):
+                out.write(formats.pop(0).result())
 
-    while True:
-        try:
-            recs, used, _ = nt.read_block(data[pos:])
-        except nt.NtcError:
-            break  # end of input or a damaged block ends the reference's loop too (main.rs:202)
-        pos += used
-        batch.append(recs)
-        nbatch += 1
-        if nbatch >= args.blocks_per_batch:
-            decode_flush()
-    decode_flush()
+    b0, gi = 0, 0
+    while b0 < len(extents) and not stop:
+        recs = []
+        for i in range(b0, min(b0 + bpb, len(extents))):
+            try:
+                recs.append(unzip[i].result()[0])
+            except nt.NtcError:
+                stop = True  # a damaged block ends the reference's loop (main.rs:202)
+                break
+        # keep about two batches of blocks unzipping ahead
+        while submitted < min(len(extents), b0 + 3 * bpb):
+            a, b = extents[submitted]
+            unzip.append(pool.submit(read_block, data[a:b]))
+            submitted += 1
+        for i in range(b0, min(b0 + bpb, len(extents))):
+            unzip[i] = None
+        b0 += bpb
+        if recs:
+            allr = np.concatenate(recs) if len(recs) > 1 else recs[0]
+            decodes.append(gpu_pools[gi % len(ctxs)].submit(gpu_decode, ctxs[gi % len(ctxs)], allr))
+            gi += 1
+        finish_decodes(len(ctxs))
+    finish_decodes(0)
+    for f in formats:
+        out.write(f.result())
     out.flush()
-    ctx.close()
+    for c in ctxs:
+        c.close()
+    st.report(command="decode", gpus=len(ctxs), blocks=len(extents))
 
 
 def main(argv=None):
@@ -208,10 +305,14 @@ def main(argv=None):
     e.add_argument("--gpus", type=int, default=1, help="GPUs to encode on (batches dealt round-robin).")
     e.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 4), help="block compression threads")
     e.add_argument("--blocks-per-batch", type=int, default=16, help="65,536-read blocks per GPU call")
+    e.add_argument("--stats", action="store_true", help="print per-stage seconds to stderr")
     d = sub.add_parser("decode", help="Decode data written with Encode")
     d.add_argument("input_path", help="File with encoded fastX data.")
     d.add_argument("-i", "--index", dest="index_prefix", required=True, help="Prefix for prebuilt <prefix>.sbwt and <prefix>.lcs")
+    d.add_argument("--gpus", type=int, default=1, help="GPUs to decode on (batches dealt round-robin).")
+    d.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 4), help="block unzip / format threads")
     d.add_argument("--blocks-per-batch", type=int, default=16, help="blocks per GPU call")
+    d.add_argument("--stats", action="store_true", help="print per-stage seconds to stderr")
     args = ap.parse_args(argv)
     if args.command == "build":
         cmd_build(args)

@@ -81,6 +81,14 @@ struct BitReader {
     const uint64_t *w;
     uint64_t nw, pos = 0;  // bit position
     BitReader(const uint64_t *words, uint64_t n) : w(words), nw(n) {}
+    // the next 64 bits from pos, MSB first (zero past the end)
+    uint64_t peek64() const {
+        const uint64_t i = pos >> 6, sh = pos & 63;
+        const uint64_t hi = i < nw ? w[i] : 0;
+        if (!sh) return hi;
+        const uint64_t lo = i + 1 < nw ? w[i + 1] : 0;
+        return (hi << sh) | (lo >> (64 - sh));
+    }
     bool bit(int &b) {
         if (pos >= nw * 64) return false;
         b = (int)((w[pos >> 6] >> (63 - (pos & 63))) & 1);
@@ -88,21 +96,29 @@ struct BitReader {
         return true;
     }
     bool get(int nbits, uint64_t &v) {
-        v = 0;
-        for (int i = 0; i < nbits; i++) {
-            int b;
-            if (!bit(b)) return false;
-            v = (v << 1) | (uint64_t)b;
+        if (nbits == 0) {
+            v = 0;
+            return true;
         }
+        if (pos + (uint64_t)nbits > nw * 64) return false;
+        v = peek64() >> (64 - nbits);
+        pos += (uint64_t)nbits;
         return true;
     }
-    bool unary(uint64_t &n) {
+    bool unary(uint64_t &n) {  // zeros up to and including the terminating one
         n = 0;
-        int b;
         for (;;) {
-            if (!bit(b)) return false;
-            if (b) return true;
-            n++;
+            if (pos >= nw * 64) return false;
+            const uint64_t x = peek64();
+            if (x) {
+                const int z = __builtin_clzll(x);
+                if (pos + (uint64_t)z >= nw * 64) return false;
+                n += (uint64_t)z;
+                pos += (uint64_t)z + 1;
+                return true;
+            }
+            n += 64;
+            pos += 64;
         }
     }
 };

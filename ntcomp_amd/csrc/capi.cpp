@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -57,6 +58,7 @@ struct ntc_ctx {
     void *o2_zeroed = nullptr;  // WS_O2 buffer known to be all zero (k_dec_expand re-zeroes it)
     uint64_t o2_zeroed_bytes = 0;
     uint64_t n_paths = 0, path_text_len = 0;
+    int64_t upload_host_us = 0, upload_total_us = 0;  // last ntc_index_upload: host derive / total
 };
 
 namespace {
@@ -333,6 +335,11 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     for (int c = 0; c < 4; c++)
         if (!v->rows[c]) return set_err(ctx, NTC_ERR_INVALID_ARG, "null subset-matrix row");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const auto t_start = std::chrono::steady_clock::now();
+    auto us_since = [&] {
+        return (int64_t)std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() -
+                                                                              t_start).count();
+    };
     HostIndex hx;
     hx.n = v->n_nodes;
     hx.k = v->k;
@@ -344,7 +351,8 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     hx.lcs.assign(v->lcs, v->lcs + v->n_nodes);
     Derived dv;
     std::string err;
-    if (!build_derived(hx, dv, err, 0)) return set_err(ctx, NTC_ERR_FORMAT, err);
+    if (!build_derived(hx, dv, err, false)) return set_err(ctx, NTC_ERR_FORMAT, err);
+    ctx->upload_host_us = us_since();
     // free a previous index
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     for (void *p : ctx->index_mem) HIP_TRY(ctx, hipFree(p));
@@ -380,16 +388,76 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     if (result != (WalkEntry *)d_walk_a)
         HIP_TRY(ctx, hipMemcpyAsync(d_walk_a, result, n * sizeof(WalkEntry), hipMemcpyDeviceToDevice,
                                     ctx->stream));
+    // path cover, built on the device (kernels.hip "path cover"; derived.cpp build_paths is
+    // the same cover on the host, for emulation)
     void *d_pstream = nullptr, *d_colex_at = nullptr, *d_pos = nullptr, *d_puniq = nullptr;
-    if (dv.has_paths) {
-        if ((rc = dalloc(dv.puniq.size() * 8, &d_puniq))) return rc;
-        HIP_TRY(ctx, hipMemcpy(d_puniq, dv.puniq.data(), dv.puniq.size() * 8, hipMemcpyHostToDevice));
-        if ((rc = dalloc(dv.pstream.size() * 16, &d_pstream))) return rc;
-        if ((rc = dalloc(dv.colex_at.size() * 4 + 64, &d_colex_at))) return rc;
-        if ((rc = dalloc(dv.pos_of_node.size() * 4, &d_pos))) return rc;
-        HIP_TRY(ctx, hipMemcpy(d_pstream, dv.pstream.data(), dv.pstream.size() * 16, hipMemcpyHostToDevice));
-        HIP_TRY(ctx, hipMemcpy(d_colex_at, dv.colex_at.data(), dv.colex_at.size() * 4, hipMemcpyHostToDevice));
-        HIP_TRY(ctx, hipMemcpy(d_pos, dv.pos_of_node.data(), dv.pos_of_node.size() * 4, hipMemcpyHostToDevice));
+    bool has_paths = false;
+    uint64_t tlen = 0, n_paths = 0;
+    if (n < (1ULL << 31)) {
+        const std::vector<uint8_t> dummy = dummy_nodes(hx, dv);
+        std::vector<uint32_t> dbits(n / 32 + 2, 0);
+        for (uint64_t z = 0; z < n; z++)
+            if (dummy[z]) dbits[z >> 5] |= 1u << (z & 31);
+        std::vector<void *> tmp;
+        auto talloc = [&](uint64_t bytes, void **p) -> int {
+            HIP_TRY(ctx, hipMalloc(p, bytes));
+            tmp.push_back(*p);
+            return NTC_OK;
+        };
+        auto free_tmp = [&]() {
+            (void)hipStreamSynchronize(ctx->stream);
+            for (void *p : tmp) (void)hipFree(p);
+            tmp.clear();
+        };
+        void *d_dummy, *d_prv, *d_sta, *d_stb, *d_len, *d_vals, *d_base, *d_stmp, *d_cnt;
+        if ((rc = talloc(dbits.size() * 4, &d_dummy)) || (rc = talloc(n * 4, &d_prv)) ||
+            (rc = talloc(n * 16, &d_sta)) || (rc = talloc(n * 16, &d_stb)) || (rc = talloc(n * 4, &d_len)) ||
+            (rc = talloc(n * 4, &d_vals)) || (rc = talloc((n + 1) * 8, &d_base)) ||
+            (rc = talloc(scan_tmp_words(n) * 8, &d_stmp)) || (rc = talloc(16, &d_cnt))) {
+            free_tmp();
+            return rc;
+        }
+        HIP_TRY(ctx, hipMemcpy(d_dummy, dbits.data(), dbits.size() * 4, hipMemcpyHostToDevice));
+        PathArgs pa{(const uint2 *)d_lines, dv.rwords, (uint32_t)n, hx.k, (const uint8_t *)d_lcs,
+                    (const uint32_t *)d_dummy, (const uint32_t *)d_pred, (const uint8_t *)d_code,
+                    (const uint32_t *)d_uniq};
+        uint32_t *prv = (uint32_t *)d_prv, *cnt = (uint32_t *)d_cnt;
+        HIP_TRY(ctx, hipMemsetAsync(prv, 0xFF, n * 4, ctx->stream));
+        HIP_TRY(ctx, hipMemsetAsync(cnt, 0, 16, ctx->stream));
+        launch_path_edges(pa, prv, ctx->stream);
+        const uint4 *st = launch_path_rank(prv, (uint32_t)n, (uint4 *)d_sta, (uint4 *)d_stb, ctx->stream);
+        launch_path_cut(pa, st, prv, cnt, ctx->stream);
+        uint32_t cut = 0;
+        HIP_TRY(ctx, hipMemcpyAsync(&cut, cnt, 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        if (cut) st = launch_path_rank(prv, (uint32_t)n, (uint4 *)d_sta, (uint4 *)d_stb, ctx->stream);
+        HIP_TRY(ctx, hipMemsetAsync(d_len, 0, n * 4, ctx->stream));
+        launch_path_lengths(pa, st, prv, (uint32_t *)d_len, (uint32_t *)d_vals, cnt + 1, ctx->stream);
+        scan_excl_u32((const uint32_t *)d_vals, n, (uint64_t *)d_base, (uint64_t *)d_stmp, ctx->stream);
+        uint32_t np32 = 0;
+        HIP_TRY(ctx, hipMemcpyAsync(&tlen, (uint64_t *)d_base + n, 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(&np32, cnt + 1, 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        HIP_TRY(ctx, hipGetLastError());
+        n_paths = np32;
+        if (tlen + 64 < (1ULL << 31)) {
+            // sizes as derived.cpp build_paths: groups read up to k + 64 characters past a node
+            const uint64_t n_groups = (tlen + hx.k) / 32 + 8, n_colex = tlen + 8, n_puniq = tlen / 64 + 4;
+            if ((rc = dalloc(n_puniq * 8, &d_puniq)) || (rc = dalloc(n_groups * 16, &d_pstream)) ||
+                (rc = dalloc(n_colex * 4 + 64, &d_colex_at)) || (rc = dalloc(n * 4, &d_pos))) {
+                free_tmp();
+                return rc;
+            }
+            HIP_TRY(ctx, hipMemsetAsync(d_puniq, 0, n_puniq * 8, ctx->stream));
+            HIP_TRY(ctx, hipMemsetAsync(d_pstream, 0, n_groups * 16, ctx->stream));
+            HIP_TRY(ctx, hipMemsetAsync(d_colex_at, 0xFF, n_colex * 4 + 64, ctx->stream));
+            HIP_TRY(ctx, hipMemsetAsync(d_pos, 0xFF, n * 4, ctx->stream));
+            launch_path_place(pa, st, prv, (const uint64_t *)d_base, (uint32_t *)d_colex_at, (uint32_t *)d_pos,
+                              (uint4 *)d_pstream, (uint64_t *)d_puniq, ctx->stream);
+            HIP_TRY(ctx, hipGetLastError());
+            has_paths = true;
+        }
+        free_tmp();
     }
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     HIP_TRY(ctx, hipFree(d_walk_b));
@@ -405,7 +473,7 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     d.k = hx.k;
     d.t_jump = dv.t_jump;
     for (int c = 0; c < 5; c++) d.C[c] = dv.C[c];
-    d.has_paths = dv.has_paths ? 1u : 0u;
+    d.has_paths = has_paths ? 1u : 0u;
     d.pstream = (const uint4 *)d_pstream;
     d.colex_at = (const uint32_t *)d_colex_at;
     d.pos_of_node = (const uint32_t *)d_pos;
@@ -424,13 +492,14 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     d.filt_bits = (const uint32_t *)d_fbits;
     d.filt_f = F;
     d.tab_u = U;
-    d.tab_pos = (dv.has_paths && U >= dv.t_jump && n < (1ULL << 31)) ? 1u : 0u;
+    d.tab_pos = (has_paths && U >= dv.t_jump && n < (1ULL << 31)) ? 1u : 0u;
     launch_tab_build(d, U, (uint2 *)d_tab, (uint32_t *)d_bits, F, (uint32_t *)d_fbits, ctx->stream);
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    ctx->n_paths = dv.n_paths;
-    ctx->path_text_len = dv.tlen;
+    ctx->n_paths = n_paths;
+    ctx->path_text_len = tlen;
     ctx->has_index = true;
+    ctx->upload_total_us = us_since();
     return NTC_OK;
 }
 
@@ -457,6 +526,22 @@ int ntc_ctx_get_option(const ntc_ctx *ctx, const char *key, int64_t *value) {
     else if (std::strcmp(key, "tab_u") == 0) *value = ctx->has_index ? ctx->dix.tab_u : ctx->tab_u_opt;
     else if (std::strcmp(key, "n_paths") == 0) *value = (int64_t)ctx->n_paths;
     else if (std::strcmp(key, "path_text_len") == 0) *value = (int64_t)ctx->path_text_len;
+    else if (std::strcmp(key, "path_hash") == 0) {  // test hook: derived.h path_cover_hash of the device cover
+        if (!ctx->has_index || !ctx->dix.has_paths) return NTC_ERR_NO_INDEX;
+        const uint64_t n = ctx->dix.n, k = ctx->dix.k, tlen = ctx->path_text_len;
+        std::vector<uint4> ps((tlen + k) / 32 + 8);
+        std::vector<uint32_t> ca(tlen + 8), pn(n);
+        std::vector<uint64_t> pu(tlen / 64 + 4);
+        if (hipSetDevice(ctx->device) != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess ||
+            hipMemcpy(ps.data(), ctx->dix.pstream, ps.size() * 16, hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(ca.data(), ctx->dix.colex_at, ca.size() * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(pn.data(), ctx->dix.pos_of_node, pn.size() * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(pu.data(), ctx->dix.puniq, pu.size() * 8, hipMemcpyDeviceToHost) != hipSuccess)
+            return NTC_ERR_HIP;
+        *value = (int64_t)path_cover_hash(ps.data(), ca.data(), pn.data(), pu.data(), n, (uint32_t)k, tlen);
+    }
+    else if (std::strcmp(key, "upload_host_us") == 0) *value = ctx->upload_host_us;
+    else if (std::strcmp(key, "upload_total_us") == 0) *value = ctx->upload_total_us;
     else return NTC_ERR_INVALID_ARG;
     return NTC_OK;
 }

@@ -8,8 +8,7 @@
 
 namespace ntc {
 
-bool build_derived(const HostIndex &ix, Derived &out, std::string &err, int threads) {
-    (void)threads;
+bool build_derived(const HostIndex &ix, Derived &out, std::string &err, bool host_paths) {
     const uint64_t n = ix.n;
     const uint32_t k = ix.k;
     if (n == 0 || n >= (uint64_t)kTabShort) {
@@ -101,7 +100,7 @@ bool build_derived(const HostIndex &ix, Derived &out, std::string &err, int thre
     double l4 = std::log((double)n) / std::log(4.0);
     uint32_t tj = (uint32_t)std::ceil(l4) + 2;
     out.t_jump = std::max<uint32_t>(1, tj);
-    build_paths(ix, out);
+    if (host_paths) build_paths(ix, out);
     out.absent = 0;
     for (int c = 0; c < 4; c++)
         if (out.C[c + 1] == out.C[c]) out.absent |= 1u << c;
@@ -156,80 +155,81 @@ inline uint32_t labels_of(const Derived &dv, uint64_t g) {  // 4-bit label set o
 }
 }  // namespace
 
-// Path cover: walk the de Bruijn graph from path starts (source k-mers, in-degree != 1,
-// or a predecessor with out-degree != 1), then from any still-unvisited node (cycles),
-// always moving to an unvisited successor.  Only speed depends on the cover; the kernel
-// uses a path step only when it provably equals the SBWT step (encode_core.h).
+std::vector<uint8_t> dummy_nodes(const HostIndex &ix, const Derived &dv) {
+    // dummies: BFS from the root through labels, depth < k
+    const uint64_t n = ix.n;
+    const uint32_t k = ix.k;
+    std::vector<uint8_t> dummy(n, 0);
+    std::vector<std::pair<uint32_t, uint32_t>> q;
+    q.push_back({0, 0});
+    dummy[0] = 1;
+    for (size_t h = 0; h < q.size(); h++) {
+        auto [v, dep] = q[h];
+        if (dep + 1 >= k) continue;
+        uint32_t m = labels_of(dv, v);
+        for (int c = 0; c < 4; c++)
+            if (m >> c & 1) {
+                uint32_t z = dv.C[c] + host_rank(dv, c, v);
+                if (!dummy[z]) {
+                    dummy[z] = 1;
+                    q.push_back({z, dep + 1});
+                }
+            }
+    }
+    return dummy;
+}
+
+uint32_t path_succ(const HostIndex &ix, const Derived &dv, const std::vector<uint8_t> &dummy, uint64_t z) {
+    const uint64_t n = ix.n;
+    const uint32_t k = ix.k;
+    if (dummy[z]) return kNoNode;
+    const bool head = k < 2 || ix.lcs[z] < k - 1;
+    const bool alone = k < 2 || z + 1 == n || ix.lcs[z + 1] < k - 1;
+    const uint32_t m = labels_of(dv, z);
+    if (!head || !alone || m == 0 || (m & (m - 1))) return kNoNode;
+    const int c = __builtin_ctz(m);
+    const uint32_t y = dv.C[c] + host_rank(dv, c, z);
+    return dummy[y] ? kNoNode : y;
+}
+
+// Path cover = the unitigs of the de Bruijn graph on real k-mers: edge z -> y when z is
+// alone in its (k-1)-suffix group, has exactly one successor y, and neither is a dummy
+// (y then has z as its only predecessor).  Paths start at real nodes without an in-edge;
+// a cycle starts at its smallest node.  Paths are laid out by start node, ascending.
+// The device builds the same cover in parallel (kernels.hip "path cover"); only speed
+// depends on it -- the kernel uses a path step only when it provably equals the SBWT step
+// (encode_core.h).
 void build_paths(const HostIndex &ix, Derived &dv) {
     const uint64_t n = ix.n;
     const uint32_t k = ix.k;
     dv.has_paths = false;
     if (n >= (1ULL << 31) || k < 1) return;
-    // dummies: BFS from the root through labels, depth < k
-    std::vector<uint8_t> dummy(n, 0);
-    {
-        std::vector<std::pair<uint32_t, uint32_t>> q;
-        q.push_back({0, 0});
-        dummy[0] = 1;
-        for (size_t h = 0; h < q.size(); h++) {
-            auto [v, dep] = q[h];
-            if (dep + 1 >= k) continue;
-            uint32_t m = labels_of(dv, v);
-            for (int c = 0; c < 4; c++)
-                if (m >> c & 1) {
-                    uint32_t z = dv.C[c] + host_rank(dv, c, v);
-                    if (!dummy[z]) {
-                        dummy[z] = 1;
-                        q.push_back({z, dep + 1});
-                    }
-                }
-        }
+    const std::vector<uint8_t> dummy = dummy_nodes(ix, dv);
+    std::vector<uint32_t> nxt(n), prv(n, kNoNode);
+    for (uint64_t z = 0; z < n; z++) {
+        nxt[z] = path_succ(ix, dv, dummy, z);
+        if (nxt[z] != kNoNode) prv[nxt[z]] = (uint32_t)z;
     }
-    auto group_first = [&](uint64_t z) {
-        while (z > 0 && k >= 2 && ix.lcs[z] >= k - 1) z--;
-        return z;
-    };
-    auto succ_mask = [&](uint64_t z) { return labels_of(dv, group_first(z)); };
-    auto group_size = [&](uint64_t g) {  // nodes sharing g's (k-1)-suffix, g group-first
-        uint64_t e = g + 1;
-        while (e < n && k >= 2 && ix.lcs[e] >= k - 1) e++;
-        return e - g;
-    };
-    std::vector<uint8_t> visited(n, 0);
-    std::vector<uint32_t> order;  // node sequence of all paths
-    std::vector<uint64_t> path_start;
-    order.reserve(n);
-    auto walk = [&](uint32_t z) {
-        path_start.push_back(order.size());
-        visited[z] = 1;
-        order.push_back(z);
-        for (;;) {
-            const uint64_t g = group_first(z);
-            const uint32_t m = labels_of(dv, g);
-            uint32_t next = kNoNode;
-            for (int c = 0; c < 4 && next == kNoNode; c++)
-                if (m >> c & 1) {
-                    uint32_t y = dv.C[c] + host_rank(dv, c, g);
-                    if (!visited[y] && !dummy[y]) next = y;
-                }
-            if (next == kNoNode) break;
-            visited[next] = 1;
-            order.push_back(next);
-            z = next;
-        }
-    };
-    for (uint64_t z = 1; z < n; z++) {
-        if (dummy[z]) continue;
-        const uint32_t pz = dv.pred[z];
-        bool start = dummy[pz] != 0;
-        if (!start) {
-            const uint64_t pg = group_first(pz);
-            start = group_size(pg) != 1 || __builtin_popcount(succ_mask(pz)) != 1;
-        }
-        if (start && !visited[z]) walk((uint32_t)z);
-    }
+    std::vector<uint8_t> start(n, 0), seen(n, 0);
     for (uint64_t z = 1; z < n; z++)
-        if (!dummy[z] && !visited[z]) walk((uint32_t)z);
+        if (!dummy[z] && prv[z] == kNoNode) {
+            start[z] = 1;
+            for (uint32_t y = (uint32_t)z; y != kNoNode; y = nxt[y]) seen[y] = 1;
+        }
+    for (uint64_t z = 1; z < n; z++)  // what is left lies on cycles: cut each at its minimum
+        if (!dummy[z] && !seen[z]) {
+            start[z] = 1;
+            for (uint32_t y = (uint32_t)z; !seen[y]; y = nxt[y]) seen[y] = 1;
+        }
+    std::vector<uint64_t> path_start;
+    std::vector<uint32_t> order;
+    order.reserve(n);
+    for (uint64_t z = 1; z < n; z++) {
+        if (!start[z]) continue;
+        path_start.push_back(order.size());
+        order.push_back((uint32_t)z);
+        for (uint32_t y = nxt[z]; y != kNoNode && !start[y]; y = nxt[y]) order.push_back(y);
+    }
     path_start.push_back(order.size());
     const uint64_t np = path_start.size() - 1;
     // text layout: per path k chars of its first k-mer, one char per further node, then

@@ -30,8 +30,26 @@ struct Derived {
 
 constexpr uint32_t kNoNode = 0xFFFFFFFFu;
 
-// Builds the path cover (fills has_paths, tlen, ptext, colex_at, pos_of_node).
+// Builds the path cover on the host (fills has_paths, tlen, pstream, colex_at,
+// pos_of_node, puniq); test emulation -- the upload builds the same cover on the device.
 void build_paths(const HostIndex &ix, Derived &dv);
+// FNV-1a over the path-cover arrays (pstream, colex_at, pos_of_node, puniq) at the sizes
+// build_paths gives them: lets a test compare the device-built cover with the host one.
+inline uint64_t path_cover_hash(const uint4 *pstream, const uint32_t *colex_at, const uint32_t *pos_of_node,
+                                const uint64_t *puniq, uint64_t n, uint32_t k, uint64_t tlen) {
+    uint64_t h = 1469598103934665603ULL;
+    auto mix = [&](const void *p, uint64_t bytes) {
+        const uint8_t *b = (const uint8_t *)p;
+        for (uint64_t i = 0; i < bytes; i++) h = (h ^ b[i]) * 1099511628211ULL;
+    };
+    mix(pstream, ((tlen + k) / 32 + 8) * 16);
+    mix(colex_at, (tlen + 8) * 4);
+    mix(pos_of_node, n * 4);
+    mix(puniq, (tlen / 64 + 4) * 8);
+    return h;
+}
+// dummy[z] = 1 when node z's k-mer contains '$' (BFS from the root, depth < k).
+std::vector<uint8_t> dummy_nodes(const HostIndex &ix, const Derived &dv);
 // Suffix-table depth U for an index of n nodes (encode_core.h "Suffix table").
 uint32_t default_tab_u(uint64_t n, uint32_t k);
 // Host build of the suffix table levels 1..U (test emulation; the GPU builds it on device).
@@ -41,8 +59,9 @@ void build_tab_host(const DevIndex &d, uint32_t U, std::vector<uint2> &tab, std:
 // Level of the SCAN pre-filter bitmap for depth U (0 = none).
 uint32_t filter_level(uint32_t U);
 
-// Validates the index and fills rank lines, unique-predecessor bits, pred and code.
-bool build_derived(const HostIndex &ix, Derived &out, std::string &err, int threads);
+// Validates the index and fills rank lines, unique-predecessor bits, pred and code; with
+// host_paths also the path cover (test emulation; the upload builds it on the device).
+bool build_derived(const HostIndex &ix, Derived &out, std::string &err, bool host_paths);
 // Host doubling of the walk table (the GPU builds the same table on device).
 void build_walk_host(const Derived &dv, uint64_t n, std::vector<WalkEntry> &walk);
 // DevIndex over host arrays (test emulation only).

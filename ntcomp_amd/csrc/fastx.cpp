@@ -8,13 +8,22 @@
 // upper case; t u U -> T; n -> N; . ~ -> -; IUPAC B D H V R Y S W K M kept (lower case
 // upper-cased); whitespace dropped; anything else -> N.  Record names are not kept (the
 // reference discards them on encode, main.rs:158-166).
+//
+// Feed rate: a producer thread inflates (or reads) 8 MiB chunks into a small ring while
+// the caller's thread scans records in place (memchr per line, branch-free table
+// normalisation into one growing buffer), so a gzip input is bound by inflate alone.
+#include <emmintrin.h>
 #include <zlib.h>
 
+#include <algorithm>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <string>
+#include <deque>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/ntcomp_host.h"
@@ -45,87 +54,208 @@ void init_norm() {
     norm_init = true;
 }
 
+constexpr size_t kChunk = 8u << 20;
+constexpr size_t kRing = 4;
+
+// Producer: gzread into chunks, bounded queue of kRing chunks.
+struct ChunkSource {
+    gzFile f;
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::vector<char>> full;
+    std::vector<std::vector<char>> spare;
+    bool done = false, stop = false, error = false;
+
+    explicit ChunkSource(gzFile file) : f(file) { th = std::thread([this] { run(); }); }
+    ~ChunkSource() {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            stop = true;
+        }
+        cv.notify_all();
+        th.join();
+    }
+    void run() {
+        for (;;) {
+            std::vector<char> c;
+            {
+                std::unique_lock<std::mutex> g(mu);
+                cv.wait(g, [&] { return stop || full.size() < kRing; });
+                if (stop) return;
+                if (!spare.empty()) {
+                    c.swap(spare.back());
+                    spare.pop_back();
+                }
+            }
+            c.resize(kChunk);
+            const int got = gzread(f, c.data(), (unsigned)kChunk);
+            std::lock_guard<std::mutex> g(mu);
+            if (got < 0) error = true;
+            if (got <= 0) {
+                done = true;
+                cv.notify_all();
+                return;
+            }
+            c.resize((size_t)got);
+            full.push_back(std::move(c));
+            cv.notify_all();
+        }
+    }
+    // next chunk into `out` (swapped); false at end of input
+    bool take(std::vector<char> &out, bool &err) {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return !full.empty() || done; });
+        err = error;
+        if (full.empty()) return false;
+        out.swap(full.front());
+        full.pop_front();
+        cv.notify_all();
+        return true;
+    }
+    void give_back(std::vector<char> &c) {
+        std::lock_guard<std::mutex> g(mu);
+        if (spare.size() < kRing) spare.push_back(std::move(c));
+    }
+};
+
 }  // namespace
 
 struct ntc_fastx {
     gzFile f = nullptr;
-    std::vector<char> buf;  // read-ahead
+    ChunkSource *src = nullptr;
+    std::vector<char> buf;  // unparsed bytes live in [pos, end)
+    std::vector<char> chunk;
     size_t pos = 0, end = 0;
-    bool eof = false;
-    int format = 0;  // 0 unknown, '>' FASTA, '@' FASTQ
+    bool eof = false, io_error = false;
+    int format = 0;  // '>' FASTA, '@' FASTQ
     bool have_pending = false;  // FASTA: the next record's '>' line was already consumed
     // current batch
     std::vector<uint8_t> bases;
+    size_t nb = 0;
     std::vector<uint64_t> offsets;
 
+    // append the next chunk behind the unparsed tail; false at end of input (a missing
+    // final newline is supplied once so the last line always ends in '\n')
     bool fill() {
         if (eof) return false;
-        if (pos > 0 && pos < end) std::memmove(buf.data(), buf.data() + pos, end - pos);
-        end -= pos;
-        pos = 0;
-        if (buf.size() < (1u << 22)) buf.resize(1u << 22);
-        if (end == buf.size()) buf.resize(buf.size() * 2);
-        const int got = gzread(f, buf.data() + end, (unsigned)(buf.size() - end));
-        if (got <= 0) {
+        const size_t tail = end - pos;
+        if (!src->take(chunk, io_error)) {
             eof = true;
-            return false;
-        }
-        end += (size_t)got;
-        return true;
-    }
-    // one line without its terminator; false at end of input
-    bool line(std::string &out) {
-        out.clear();
-        for (;;) {
-            const char *b = buf.data() + pos;
-            const char *nl = (const char *)std::memchr(b, '\n', end - pos);
-            if (nl) {
-                out.append(b, nl - b);
-                pos = (size_t)(nl - buf.data()) + 1;
-                if (!out.empty() && out.back() == '\r') out.pop_back();
+            if (tail && buf[end - 1] != '\n') {
+                if (end == buf.size()) buf.resize(buf.size() + 1);
+                buf[end++] = '\n';
                 return true;
             }
-            out.append(b, end - pos);
-            pos = end;
-            if (!fill()) return !out.empty();
+            return false;
         }
+        if (pos) std::memmove(buf.data(), buf.data() + pos, tail);
+        pos = 0;
+        end = tail;
+        if (buf.size() < end + chunk.size()) buf.resize(end + chunk.size() + (1u << 16));
+        std::memcpy(buf.data() + end, chunk.data(), chunk.size());
+        end += chunk.size();
+        src->give_back(chunk);
+        return true;
     }
-    void append_seq(const std::string &s) {
-        for (unsigned char c : s) {
-            const uint8_t v = norm_table[c];
-            if (v) bases.push_back(v);
+    const char *find_nl(size_t from) const {
+        return (const char *)std::memchr(buf.data() + from, '\n', end - from);
+    }
+    void append_seq(const char *s, size_t n) {
+        if (nb + n > bases.size()) bases.resize(std::max(bases.size() * 2, nb + n + (1u << 20)));
+        uint8_t *d = bases.data() + nb;
+        size_t i = 0, j = 0;
+        // fast path: 16 bytes at a time while every byte is already one of A C G T
+        const __m128i cA = _mm_set1_epi8('A'), cC = _mm_set1_epi8('C'), cG = _mm_set1_epi8('G'),
+                      cT = _mm_set1_epi8('T');
+        for (; i + 16 <= n; i += 16) {
+            const __m128i x = _mm_loadu_si128((const __m128i *)(s + i));
+            const __m128i ok = _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(x, cA), _mm_cmpeq_epi8(x, cC)),
+                                            _mm_or_si128(_mm_cmpeq_epi8(x, cG), _mm_cmpeq_epi8(x, cT)));
+            if (_mm_movemask_epi8(ok) == 0xFFFF) {
+                _mm_storeu_si128((__m128i *)(d + j), x);
+                j += 16;
+                continue;
+            }
+            for (size_t t = i; t < i + 16; t++) {  // this block holds something else
+                const uint8_t v = norm_table[(uint8_t)s[t]];
+                d[j] = v;
+                j += v != 0;
+            }
         }
+        for (; i < n; i++) {
+            const uint8_t v = norm_table[(uint8_t)s[i]];
+            d[j] = v;
+            j += v != 0;
+        }
+        nb += j;
     }
-    // next record's normalized sequence appended to `bases`; 0 = ok, 1 = end, <0 error
-    int next() {
-        std::string l;
-        if (format == '>') {
-            if (!have_pending) {
-                do {
-                    if (!line(l)) return 1;
-                } while (l.empty());
-                if (l[0] != '>') return -1;
+    // next FASTQ record's sequence appended; 0 ok, 1 end of input, <0 format error
+    int next_fastq() {
+        for (;;) {
+            while (pos < end && (buf[pos] == '\n' || buf[pos] == '\r')) pos++;
+            if (pos == end) {
+                if (!fill()) return 1;
+                continue;
             }
-            have_pending = false;
-            while (line(l)) {
-                if (!l.empty() && l[0] == '>') {
-                    have_pending = true;
-                    break;
-                }
-                append_seq(l);
+            if (buf[pos] != '@') return -1;
+            const char *h = find_nl(pos);
+            const char *se = h ? find_nl((size_t)(h - buf.data()) + 1) : nullptr;
+            const char *pe = se ? find_nl((size_t)(se - buf.data()) + 1) : nullptr;
+            const char *qe = pe ? find_nl((size_t)(pe - buf.data()) + 1) : nullptr;
+            if (!qe) {
+                if (!fill()) return -1;  // truncated record
+                continue;
             }
+            if (se[1] != '+') return -1;
+            append_seq(h + 1, (size_t)(se - h - 1));
+            pos = (size_t)(qe - buf.data()) + 1;
             return 0;
         }
-        // FASTQ
-        do {
-            if (!line(l)) return 1;
-        } while (l.empty());
-        if (l[0] != '@') return -1;
-        std::string seq, plus, qual;
-        if (!line(seq) || !line(plus) || plus.empty() || plus[0] != '+') return -1;
-        if (!line(qual)) return -1;
-        append_seq(seq);
-        return 0;
+    }
+    // next FASTA record's sequence (any number of lines) appended
+    int next_fasta() {
+        if (!have_pending) {
+            for (;;) {  // skip blank lines, then expect a header
+                while (pos < end && (buf[pos] == '\n' || buf[pos] == '\r')) pos++;
+                if (pos < end) break;
+                if (!fill()) return 1;
+            }
+            if (buf[pos] != '>') return -1;
+            for (;;) {
+                const char *h = find_nl(pos);
+                if (h) {
+                    pos = (size_t)(h - buf.data()) + 1;
+                    break;
+                }
+                pos = end;  // a header longer than the buffer: drop what we have
+                if (!fill()) return 0;
+            }
+        }
+        have_pending = false;
+        bool mid_line = false;  // a sequence line continues across a refill
+        for (;;) {
+            if (pos == end && !fill()) return 0;
+            if (!mid_line && buf[pos] == '>') {
+                // the next record's header: consume it now
+                for (;;) {
+                    const char *h = find_nl(pos);
+                    if (h) {
+                        pos = (size_t)(h - buf.data()) + 1;
+                        break;
+                    }
+                    pos = end;
+                    if (!fill()) break;
+                }
+                have_pending = true;
+                return 0;
+            }
+            const char *nl = find_nl(pos);
+            const size_t stop = nl ? (size_t)(nl - buf.data()) : end;
+            append_seq(buf.data() + pos, stop - pos);
+            pos = nl ? stop + 1 : end;
+            mid_line = !nl;
+        }
     }
 };
 
@@ -140,8 +270,8 @@ int ntc_fastx_open(const char *path, ntc_fastx **out) {
     gzbuffer(f, 1u << 20);
     auto *fx = new ntc_fastx();
     fx->f = f;
-    fx->buf.resize(1u << 22);
-    // detect the format from the first non-empty character
+    fx->src = new ChunkSource(f);
+    // detect the format from the first non-whitespace character
     for (;;) {
         if (fx->pos == fx->end && !fx->fill()) break;
         const char c = fx->buf[fx->pos];
@@ -152,10 +282,10 @@ int ntc_fastx_open(const char *path, ntc_fastx **out) {
         fx->format = c;
         break;
     }
-    if (fx->format != '>' && fx->format != '@' && !(fx->eof && fx->pos == fx->end)) {
-        gzclose(f);
-        delete fx;
-        return NTC_ERR_FORMAT;
+    if (fx->io_error || (fx->format != '>' && fx->format != '@' && fx->format != 0)) {
+        const int rc = fx->io_error ? NTC_ERR_IO : NTC_ERR_FORMAT;
+        ntc_fastx_close(fx);
+        return rc;
     }
     if (fx->format == 0) fx->format = '>';  // empty input
     *out = fx;
@@ -165,14 +295,16 @@ int ntc_fastx_open(const char *path, ntc_fastx **out) {
 int ntc_fastx_next_batch(ntc_fastx *fx, uint64_t max_reads, uint64_t max_bases, const uint8_t **bases,
                          const uint64_t **offsets, uint64_t *n_reads) {
     if (!fx || !bases || !offsets || !n_reads || max_reads == 0) return NTC_ERR_INVALID_ARG;
-    fx->bases.clear();
+    fx->nb = 0;
     fx->offsets.assign(1, 0);
-    while (fx->offsets.size() - 1 < max_reads && fx->bases.size() < max_bases) {
-        const int rc = fx->next();
+    fx->offsets.reserve(max_reads + 1);
+    while (fx->offsets.size() - 1 < max_reads && fx->nb < max_bases) {
+        const int rc = fx->format == '@' ? fx->next_fastq() : fx->next_fasta();
         if (rc == 1) break;
         if (rc < 0) return NTC_ERR_FORMAT;
-        fx->offsets.push_back(fx->bases.size());
+        fx->offsets.push_back(fx->nb);
     }
+    if (fx->io_error) return NTC_ERR_IO;
     *bases = fx->bases.data();
     *offsets = fx->offsets.data();
     *n_reads = fx->offsets.size() - 1;
@@ -205,6 +337,7 @@ int ntc_fasta_format(const uint8_t *bases, const uint64_t *offsets, uint64_t n_r
 
 void ntc_fastx_close(ntc_fastx *fx) {
     if (!fx) return;
+    delete fx->src;  // joins the producer before the file goes away
     if (fx->f) gzclose(fx->f);
     delete fx;
 }

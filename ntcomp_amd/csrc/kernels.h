@@ -102,6 +102,33 @@ void launch_dec_expand(const uint64_t *E, uint64_t n, uint64_t max_bases, uint64
 void launch_walk_build(const uint32_t *pred, const uint8_t *code, uint64_t n, WalkEntry *a, WalkEntry *b,
                        WalkEntry **result, hipStream_t s);
 uint64_t scan_tmp_words(uint64_t n);
+
+// Path cover on the device (derived.cpp build_paths, same cover): unitigs of the real
+// k-mers, laid out by start node.  Orchestrated by ntc_index_upload.
+struct PathArgs {
+    const uint2 *rank;       // rank words [4][rwords]
+    uint32_t rwords;
+    uint32_t n, k;
+    const uint8_t *lcs;
+    const uint32_t *dummy;   // bit z: node z is a dummy
+    const uint32_t *pred;    // inverse-walk predecessor
+    const uint8_t *code;     // last character of each node
+    const uint32_t *uniq;    // bit z: z's (k-1)-suffix group is {z}
+};
+// prv[y] = the path predecessor of y, or 0xFFFFFFFF (prv must be preset to all ones)
+void launch_path_edges(const PathArgs &a, uint32_t *prv, hipStream_t s);
+// list ranking by pointer jumping: st[z] = {start node, distance, min node on the way, 0};
+// returns the buffer (a or b) holding the result
+uint4 *launch_path_rank(const uint32_t *prv, uint32_t n, uint4 *a, uint4 *b, hipStream_t s);
+// cut every cycle at its smallest node (prv[min] = none); *flag = 1 if any was cut
+void launch_path_cut(const PathArgs &a, const uint4 *st, uint32_t *prv, uint32_t *flag, hipStream_t s);
+// len[start] = path length (len zeroed first); vals[z] = len + k at starts, else 0;
+// *n_paths += number of starts
+void launch_path_lengths(const PathArgs &a, const uint4 *st, const uint32_t *prv, uint32_t *len, uint32_t *vals,
+                         uint32_t *n_paths, hipStream_t s);
+// text, node-end bits, colex_at, pos_of_node, puniq (outputs preset: zeros / all ones)
+void launch_path_place(const PathArgs &a, const uint4 *st, const uint32_t *prv, const uint64_t *base,
+                       uint32_t *colex_at, uint32_t *pos_of_node, uint4 *pstream, uint64_t *puniq, hipStream_t s);
 void scan_excl_u32(const uint32_t *in, uint64_t n, uint64_t *out, uint64_t *tmp, hipStream_t s);
 void scan_excl_u64(const uint64_t *in, uint64_t n, uint64_t *out, uint64_t *tmp, hipStream_t s);
 

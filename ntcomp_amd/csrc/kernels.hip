@@ -712,4 +712,136 @@ void launch_walk_build(const uint32_t *pred, const uint8_t *code, uint64_t n, Wa
     *result = a;
 }
 
+
+// ---- path cover (derived.cpp build_paths, in parallel) ---------------------------------
+// Edge z -> y when z is alone in its (k-1)-suffix group with one label and neither node
+// is a dummy; every node then has at most one path in- and out-edge, so the components
+// are simple paths and cycles.  List ranking by pointer jumping gives each node its start
+// and distance; cycles are cut at their smallest node and ranked again.
+__device__ __forceinline__ bool path_dummy(const uint32_t *bits, uint32_t z) { return (bits[z >> 5] >> (z & 31)) & 1u; }
+
+__global__ __launch_bounds__(256) void k_path_edges(PathArgs a, uint32_t *prv) {
+    const uint32_t z = blockIdx.x * 256u + threadIdx.x;
+    if (z >= a.n || path_dummy(a.dummy, z)) return;
+    const bool head = a.k < 2 || a.lcs[z] < a.k - 1;
+    const bool alone = a.k < 2 || z + 1 == a.n || a.lcs[z + 1] < a.k - 1;
+    if (!head || !alone) return;
+    uint2 w[4];
+    uint32_t m = 0;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        w[c] = a.rank[(uint64_t)c * a.rwords + (z >> 5)];
+        m |= ((w[c].y >> (z & 31)) & 1u) << c;
+    }
+    if (m == 0 || (m & (m - 1))) return;
+    const int c = __builtin_ctz(m);
+    const uint32_t y = rank_word(w[c], z);
+    if (!path_dummy(a.dummy, y)) prv[y] = z;
+}
+
+__global__ __launch_bounds__(256) void k_path_rank_init(const uint32_t *prv, uint32_t n, uint4 *st) {
+    const uint32_t z = blockIdx.x * 256u + threadIdx.x;
+    if (z >= n) return;
+    const uint32_t p = prv[z];
+    st[z] = p == 0xFFFFFFFFu ? make_uint4(z, 0, z, 0) : make_uint4(p, 1, min(z, p), 0);
+}
+
+__global__ __launch_bounds__(256) void k_path_rank_step(const uint4 *in, uint32_t n, uint4 *out) {
+    const uint32_t z = blockIdx.x * 256u + threadIdx.x;
+    if (z >= n) return;
+    const uint4 e = in[z];
+    const uint4 f = in[e.x];
+    out[z] = make_uint4(f.x, e.y + f.y, min(e.z, f.z), 0);
+}
+
+__global__ __launch_bounds__(256) void k_path_cut(PathArgs a, const uint4 *st, uint32_t *prv, uint32_t *flag) {
+    const uint32_t z = blockIdx.x * 256u + threadIdx.x;
+    if (z == 0 || z >= a.n || path_dummy(a.dummy, z)) return;
+    const uint4 e = st[z];
+    // only z itself writes prv[z]; a node whose rank did not end at a start is on a cycle
+    if (e.z == z && prv[e.x] != 0xFFFFFFFFu) {
+        prv[z] = 0xFFFFFFFFu;
+        *flag = 1;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_path_len(PathArgs a, const uint4 *st, uint32_t *len) {
+    const uint32_t z = blockIdx.x * 256u + threadIdx.x;
+    if (z == 0 || z >= a.n || path_dummy(a.dummy, z)) return;
+    const uint4 e = st[z];
+    atomicMax(len + e.x, e.y + 1);
+}
+
+__global__ __launch_bounds__(256) void k_path_vals(PathArgs a, const uint32_t *prv, const uint32_t *len,
+                                                   uint32_t *vals, uint32_t *n_paths) {
+    const uint32_t z = blockIdx.x * 256u + threadIdx.x;
+    if (z >= a.n) return;
+    const bool start = z > 0 && !path_dummy(a.dummy, z) && prv[z] == 0xFFFFFFFFu;
+    vals[z] = start ? len[z] + a.k : 0;
+    const uint64_t ballot = __ballot(start);
+    if (start && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(ballot)) atomicAdd(n_paths, (uint32_t)__popcll(ballot));
+}
+
+__device__ __forceinline__ void path_put(uint4 *pstream, uint64_t t, uint32_t c) {
+    const uint32_t o = (uint32_t)(t & 31);
+    uint32_t *w = reinterpret_cast<uint32_t *>(pstream + (t >> 5)) + (o < 16 ? 0 : 1);
+    atomicOr(w, (c & 3u) << (2 * (o & 15)));
+}
+
+__global__ __launch_bounds__(256) void k_path_place(PathArgs a, const uint4 *st, const uint32_t *prv,
+                                                    const uint64_t *base, uint32_t *colex_at, uint32_t *pos_of_node,
+                                                    uint4 *pstream, uint64_t *puniq) {
+    const uint32_t z = blockIdx.x * 256u + threadIdx.x;
+    if (z == 0 || z >= a.n || path_dummy(a.dummy, z)) return;
+    const uint4 e = st[z];
+    const uint64_t pos = base[e.x] + e.y;
+    const uint32_t u = (a.uniq[z >> 5] >> (z & 31)) & 1u;
+    colex_at[pos] = z | (u << 31);
+    pos_of_node[z] = (uint32_t)pos;
+    const uint64_t end = pos + a.k - 1;  // the node's k-mer ends at text position end
+    atomicOr(reinterpret_cast<uint32_t *>(pstream + (end >> 5)) + 2, 1u << (end & 31));
+    if (u) atomicOr(reinterpret_cast<unsigned long long *>(puniq + (pos >> 6)), 1ull << (pos & 63));
+    if (prv[z] != 0xFFFFFFFFu) {
+        path_put(pstream, end, a.code[z]);
+    } else {  // a path start: all k characters of its k-mer, walking back k - 1 predecessors
+        uint32_t t = z;
+        for (int64_t i = (int64_t)a.k - 1; i >= 0; i--) {
+            path_put(pstream, pos + (uint64_t)i, a.code[t]);
+            t = a.pred[t];
+        }
+    }
+}
+
+void launch_path_edges(const PathArgs &a, uint32_t *prv, hipStream_t s) {
+    hipLaunchKernelGGL(k_path_edges, grid_for(a.n), dim3(256), 0, s, a, prv);
+}
+
+uint4 *launch_path_rank(const uint32_t *prv, uint32_t n, uint4 *a, uint4 *b, hipStream_t s) {
+    hipLaunchKernelGGL(k_path_rank_init, grid_for(n), dim3(256), 0, s, prv, n, a);
+    // 2^rounds >= n: every path is ranked to its start, every cycle's minimum is found
+    int rounds = 1;
+    while ((1ull << rounds) < (uint64_t)n) rounds++;
+    for (int r = 0; r < rounds; r++) {
+        hipLaunchKernelGGL(k_path_rank_step, grid_for(n), dim3(256), 0, s, (const uint4 *)a, n, b);
+        std::swap(a, b);
+    }
+    return a;
+}
+
+void launch_path_cut(const PathArgs &a, const uint4 *st, uint32_t *prv, uint32_t *flag, hipStream_t s) {
+    hipLaunchKernelGGL(k_path_cut, grid_for(a.n), dim3(256), 0, s, a, st, prv, flag);
+}
+
+void launch_path_lengths(const PathArgs &a, const uint4 *st, const uint32_t *prv, uint32_t *len, uint32_t *vals,
+                         uint32_t *n_paths, hipStream_t s) {
+    hipLaunchKernelGGL(k_path_len, grid_for(a.n), dim3(256), 0, s, a, st, len);
+    hipLaunchKernelGGL(k_path_vals, grid_for(a.n), dim3(256), 0, s, a, prv, (const uint32_t *)len, vals, n_paths);
+}
+
+void launch_path_place(const PathArgs &a, const uint4 *st, const uint32_t *prv, const uint64_t *base,
+                       uint32_t *colex_at, uint32_t *pos_of_node, uint4 *pstream, uint64_t *puniq, hipStream_t s) {
+    hipLaunchKernelGGL(k_path_place, grid_for(a.n), dim3(256), 0, s, a, st, prv, base, colex_at, pos_of_node, pstream,
+                       puniq);
+}
+
 }  // namespace ntc

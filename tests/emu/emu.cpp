@@ -26,7 +26,7 @@ bool load(const ntc_index_view *v, HostIndex &hx, Derived &dv, std::vector<WalkE
     hx.lcs.assign(v->lcs, v->lcs + hx.n);
     hx.lcs.resize(hx.n + 256, 0);
     std::string err;
-    if (!build_derived(hx, dv, err, 1)) return false;
+    if (!build_derived(hx, dv, err, true)) return false;
     build_walk_host(dv, hx.n, walk);
     d = host_dev_index(hx, dv, walk);
     const uint32_t U = tab_u ? std::min<uint32_t>(tab_u, std::min<uint32_t>(hx.k, kTabMaxU)) : default_tab_u(hx.n, hx.k);
@@ -41,6 +41,23 @@ bool load(const ntc_index_view *v, HostIndex &hx, Derived &dv, std::vector<WalkE
     return true;
 }
 }  // namespace
+
+// out[0] = path-cover hash, out[1] = text length, out[2] = paths (host build_paths)
+extern "C" int emu_path_cover(const ntc_index_view *v, uint64_t *out) {
+    HostIndex hx;
+    Derived dv;
+    std::vector<WalkEntry> walk;
+    DevIndex d{};
+    std::vector<uint2> tab;
+    std::vector<uint32_t> bits, fbits;
+    if (!load(v, hx, dv, walk, d, tab, bits, fbits, 1)) return 1;
+    if (!dv.has_paths) return 2;
+    out[0] = path_cover_hash(dv.pstream.data(), dv.colex_at.data(), dv.pos_of_node.data(), dv.puniq.data(), hx.n,
+                             hx.k, dv.tlen);
+    out[1] = dv.tlen;
+    out[2] = dv.n_paths;
+    return 0;
+}
 
 extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const uint64_t *offs, uint64_t n_reads,
                           uint64_t *rec_out, uint64_t cap, uint64_t *rec_offsets, int64_t *bad, uint32_t *d_out,

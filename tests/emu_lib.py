@@ -25,6 +25,8 @@ def emu_lib():
         P, u64 = ctypes.c_void_p, ctypes.c_uint64
         L.emu_encode.restype = ctypes.c_int
         L.emu_encode.argtypes = [P, P, P, u64, P, u64, P, P, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.emu_path_cover.restype = ctypes.c_int
+        L.emu_path_cover.argtypes = [P, P]
         L.emu_decode.restype = ctypes.c_int
         L.emu_decode.argtypes = [P, P, u64, P, u64, P, u64, P]
         _lib = L
@@ -79,3 +81,13 @@ def emu_decode(n, k, rows, C, lcs, recs):
     if rc:
         raise RuntimeError(f"emu_decode rc={rc}")
     return out[:total], offs[: nr.value + 1]
+
+
+def emu_path_cover(n, k, rows, C, lcs):
+    """(hash, text length, paths) of the host-built path cover (derived.cpp build_paths)."""
+    v, keep = make_view(n, k, rows, C, lcs)
+    out = np.zeros(3, dtype=np.uint64)
+    rc = emu_lib().emu_path_cover(ctypes.byref(v), _p(out))
+    if rc:
+        raise RuntimeError(f"emu_path_cover rc={rc}")
+    return int(out[0]), int(out[1]), int(out[2])

@@ -51,9 +51,94 @@ def test_fastx_batches_split_on_read_count(tmp_path):
     assert sizes == [300, 300, 300, 100]
 
 
+def _norm_table():
+    """needletail normalize(iupac=true) restated as a byte map, 0 = dropped (fastx.cpp header)."""
+    t = np.full(256, ord("N"), dtype=np.uint8)
+    for c in b"ACGTN-BDHVRYSWKM":
+        t[c] = c
+    for c in b"acgbdhvryswkm":
+        t[c] = c - 32
+    for c in b"tuU":
+        t[c] = ord("T")
+    t[ord("n")] = ord("N")
+    for c in b".~":
+        t[c] = ord("-")
+    for c in b" \t\r\n":
+        t[c] = 0
+    return t
+
+
+_NORM = _norm_table()
+
+
+def _normalize(seq):
+    v = _NORM[np.frombuffer(seq, dtype=np.uint8)]
+    return v[v != 0].tobytes()
+
+
+@pytest.mark.parametrize("fmt", ["fasta", "fastq"])
+@pytest.mark.parametrize("gz", [False, True])
+def test_fastx_random_records_across_chunks(tmp_path, fmt, gz):
+    """Records of up to 3 Mbp with mixed case, IUPAC, junk bytes and CRLF endings, spread
+    over several 8 MiB input chunks: every record's bases equal the restated normalize."""
+    rng = np.random.default_rng(7 if fmt == "fasta" else 8)
+    alphabet = np.frombuffer(b"ACGTACGTACGTACGTacgtnNuU.~-RYkmX*\t ", dtype=np.uint8)
+    lens = [3_000_000, 0, 17, 150] + rng.integers(1, 40_000, 600).tolist()
+    expect, parts = [], []
+    for i, L in enumerate(lens):
+        pure = rng.random() < 0.5
+        seq = (np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, L)] if pure
+               else alphabet[rng.integers(0, len(alphabet), L)]).tobytes()
+        expect.append(_normalize(seq))
+        eol = b"\r\n" if i % 5 == 0 else b"\n"
+        if fmt == "fasta":
+            w = int(rng.integers(50, 200)) if i % 3 else max(L, 1)
+            lines = [seq[a:a + w] for a in range(0, L, w)] or [b""]
+            parts.append(b">r%d some description%s%s%s" % (i, eol, eol.join(lines), eol))
+        else:
+            seq = seq.replace(b"\t", b"A").replace(b" ", b"C")  # one line per FASTQ sequence
+            expect[-1] = _normalize(seq)
+            parts.append(b"@r%d%s%s%s+%s%s%s" % (i, eol, seq, eol, eol, b"I" * L, eol))
+    data = b"".join(parts)
+    path = tmp_path / ("x." + fmt + (".gz" if gz else ""))
+    if gz:
+        with gzip.open(path, "wb", compresslevel=1) as f:
+            f.write(data)
+    else:
+        path.write_bytes(data)
+    got = []
+    for b, o in nt.FastxReader(str(path)):
+        got += [b[int(o[r]):int(o[r + 1])].tobytes() for r in range(len(o) - 1)]
+    assert len(got) == len(expect)
+    assert got == expect
+
+
 def test_fasta_format():
     b = np.frombuffer(b"ACGTTT", dtype=np.uint8)
     assert nt.fasta_format(b, np.array([0, 4, 4, 6], dtype=np.uint64), 9) == b">seq.9\nACGT\n>seq.10\n\n>seq.11\nTT\n"
+
+
+def test_block_extents_follow_the_stream_headers():
+    """The decode CLI splits encoded.dat into blocks from the four BlockHeaders alone
+    (lib.rs:37-50) so the blocks can unzip in parallel; a truncated tail ends the list."""
+    from ntcomp_amd.cli import _block_extents
+    rng = np.random.default_rng(3)
+    blocks = []
+    for b in range(3):
+        n = 50 + 20 * b
+        recs = rng.integers(0, 1 << 20, n).astype(np.uint64) | (np.uint64(40) << np.uint64(32))
+        recs[::2] = rng.integers(0, 1 << 10, (n + 1) // 2).astype(np.uint64) | (np.uint64(2 | (5 << 2)) << np.uint64(56))
+        recs[0] |= np.uint64(1) << np.uint64(56)
+        blocks.append(nt.write_block(recs, n))
+    data = nt.file_header() + b"".join(blocks)
+    arr = np.frombuffer(data, dtype=np.uint8)
+    ext = _block_extents(arr, 32)
+    ends = np.cumsum([32] + [len(b) for b in blocks])
+    assert ext == [(int(ends[i]), int(ends[i + 1])) for i in range(3)]
+    for (a, b), blk in zip(ext, blocks):
+        assert nt.read_block(arr[a:b])[1] == len(blk)
+    assert _block_extents(arr[:-5], 32) == ext[:2]
+    assert _block_extents(arr[:32], 32) == []
 
 
 def test_cli_build_writes_a_loadable_index(tmp_path):

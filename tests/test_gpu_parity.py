@@ -290,3 +290,19 @@ def test_gpu_long_reads(ctx):
     assert np.array_equal(goff, eoff) and np.array_equal(got, exp)
     out, o2 = ctx.decode(got)
     assert np.array_equal(out, bases) and np.array_equal(o2, offs)
+
+
+def test_gpu_path_cover_equals_host_cover(ctx):
+    """ntc_index_upload builds the path cover on the device (list ranking, cycle cuts);
+    it must be the host build_paths cover byte for byte (the one the emulation tests run)."""
+    from emu_lib import emu_path_cover
+    g = nt.synth_genome(44, 60_000).tobytes()
+    cases = [([g], 31), ([g], 91), ([g[:20_000]], 7), ([b"ACGGTCATTC" * 20, b"TTGACCAGGATC" * 15, g[:3000]], 31),
+             ([(g[:500] * 30), g[:7000]], 15), ([b"ACGTTGCA" * 100], 2), ([g[:30_000]], 255)]
+    for seqs, k in cases:
+        ix = nt.Index.build(seqs, k)
+        ctx.upload(ix)
+        h, tlen, npaths = emu_path_cover(ix.n, k, ix.rows, ix.C, ix.lcs)
+        assert ctx.get_option("path_text_len") == tlen, k
+        assert ctx.get_option("n_paths") == npaths, k
+        assert ctx.get_option("path_hash") & ((1 << 64) - 1) == h, k

@@ -121,3 +121,23 @@ def test_emulated_absent_character_is_an_invalid_base():
     got, goff = emu_encode(ix.n, 7, ix.rows, ix.C, ix.lcs, b2, o2)
     out, oo = emu_decode(ix.n, 7, ix.rows, ix.C, ix.lcs, got)
     assert np.array_equal(out, b2) and np.array_equal(oo, o2)
+
+
+@pytest.mark.parametrize("k", [13, 31])
+def test_emulated_periodic_genome_cycles(k):
+    """Periodic contigs: with k above the period every k-mer lies on a pure cycle of the
+    de Bruijn graph (no dummy leads in), so the path cover cuts each cycle at its smallest
+    node.  Records stay bit-exact with and without paths."""
+    from emu_lib import emu_path_cover
+    unit_a, unit_b = b"ACGGTCATTC", b"TTGACCAGGATC"
+    seqs = [unit_a * 20, unit_b * 15, nt.synth_genome(9, 3000).tobytes()]
+    ix = nt.Index.build(seqs, k)
+    h, tlen, npaths = emu_path_cover(ix.n, k, ix.rows, ix.C, ix.lcs)
+    assert npaths >= 1 and tlen >= ix.n - 1
+    genome = np.frombuffer(b"".join(seqs), dtype=np.uint8)
+    reads = nt.synth_reads(genome, 4, 0, 400, 60, 20_000)
+    offs = np.arange(0, 400 * 60 + 1, 60, dtype=np.uint64)
+    exp, eoff = OracleIndex(ix.n, k, ix.rows, ix.C, ix.lcs).encode(reads, offs)
+    for paths in (True, False):
+        got, goff = emu_encode(ix.n, k, ix.rows, ix.C, ix.lcs, reads, offs, use_paths=paths)
+        assert np.array_equal(goff, eoff) and np.array_equal(got, exp)
