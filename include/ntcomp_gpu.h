@@ -93,8 +93,13 @@ int ntc_ctx_synchronize(ntc_ctx *ctx);
  * read assignment and path runs, separate parse) or 1 (the first design: one lane per
  * read walking every position, kept for A/B).  "tab_u": suffix-table depth U for the
  * NEXT ntc_index_upload (0 = default ceil(log4 n) + 2 capped at min(k, 14); results
- * never depend on it).  Read-only: "n_paths", "path_text_len" (the path cover built at
- * upload), "tab_u" (after an upload: the depth in use).  Env NTC_ENCODE_VARIANT sets the
+ * never depend on it).  "max_pass_bases" (default 2^30): ntc_encode_batch /
+ * ntc_decode_batch run in device passes of whole reads holding at most this many bases
+ * (device workspace is ~40 B per base of a pass; results never depend on it).
+ * Read-only: "n_paths", "path_text_len" (the path cover built on the device at upload),
+ * "path_hash" (test hook: FNV-1a of the cover arrays, derived.h path_cover_hash),
+ * "tab_u" (after an upload: the depth in use), "upload_host_us" / "upload_total_us"
+ * (last upload: host-side derivation / whole call).  Env NTC_ENCODE_VARIANT sets the
  * default variant at ntc_ctx_create.                                                 */
 int ntc_ctx_set_option(ntc_ctx *ctx, const char *key, int64_t value);
 int ntc_ctx_get_option(const ntc_ctx *ctx, const char *key, int64_t *value);

@@ -59,6 +59,7 @@ struct ntc_ctx {
     uint64_t o2_zeroed_bytes = 0;
     uint64_t n_paths = 0, path_text_len = 0;
     int64_t upload_host_us = 0, upload_total_us = 0;  // last ntc_index_upload: host derive / total
+    uint64_t max_pass_bases = 1ULL << 30;  // host-buffer calls split into device passes of at most this
 };
 
 namespace {
@@ -511,6 +512,11 @@ int ntc_ctx_set_option(ntc_ctx *ctx, const char *key, int64_t value) {
         ctx->tab_u_opt = (uint32_t)value;
         return NTC_OK;
     }
+    if (std::strcmp(key, "max_pass_bases") == 0) {  // device workspace ~40 B per base of a pass
+        if (value < 1) return set_err(ctx, NTC_ERR_INVALID_ARG, "max_pass_bases must be >= 1");
+        ctx->max_pass_bases = (uint64_t)value;
+        return NTC_OK;
+    }
     if (std::strcmp(key, "encode_variant") == 0) {
         if (value != 1 && value != 4)
             return set_err(ctx, NTC_ERR_INVALID_ARG, "encode_variant must be 4 (default) or 1 (A/B baseline)");
@@ -541,6 +547,7 @@ int ntc_ctx_get_option(const ntc_ctx *ctx, const char *key, int64_t *value) {
         *value = (int64_t)path_cover_hash(ps.data(), ca.data(), pn.data(), pu.data(), n, (uint32_t)k, tlen);
     }
     else if (std::strcmp(key, "upload_host_us") == 0) *value = ctx->upload_host_us;
+    else if (std::strcmp(key, "max_pass_bases") == 0) *value = (int64_t)ctx->max_pass_bases;
     else if (std::strcmp(key, "upload_total_us") == 0) *value = ctx->upload_total_us;
     else return NTC_ERR_INVALID_ARG;
     return NTC_OK;
@@ -613,16 +620,11 @@ int ntc_encode_status(ntc_ctx *ctx, int64_t *bad_read, uint64_t *n_records) {
     return NTC_OK;
 }
 
-int ntc_encode_batch(ntc_ctx *ctx, const uint8_t *bases, const uint64_t *read_offsets, uint64_t n_reads,
-                     uint64_t *rec_out, uint64_t rec_capacity, uint64_t *rec_offsets_out, int64_t *bad_read) {
-    if (bad_read) *bad_read = -1;
-    if (!ctx || !read_offsets || !rec_offsets_out || (n_reads && !bases))
-        return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument");
-    HIP_TRY(ctx, hipSetDevice(ctx->device));
+namespace {
+// one device pass of the v1 (A/B baseline) encoder over all reads
+int encode_batch_v1(ntc_ctx *ctx, const uint8_t *bases, const uint64_t *read_offsets, uint64_t n_reads,
+                    uint64_t *rec_out, uint64_t rec_capacity, uint64_t *rec_offsets_out, int64_t *bad_read) {
     const uint64_t o0 = read_offsets[0], total = read_offsets[n_reads] - o0;
-    for (uint64_t r = 0; r < n_reads; r++)
-        if (read_offsets[r + 1] < read_offsets[r])
-            return set_err(ctx, NTC_ERR_INVALID_ARG, "read offsets must be non-decreasing");
     // per-tile scratch rows (host knows every length)
     const uint64_t tiles = (n_reads + 63) / 64;
     std::vector<uint64_t> tb(tiles + 1, 0), offs(n_reads + 1);
@@ -646,26 +648,80 @@ int ntc_encode_batch(ntc_ctx *ctx, const uint8_t *bases, const uint64_t *read_of
     Layout lay;
     lay.d_tile_base = (const uint64_t *)d_tb;
     lay.total_rows = tb[tiles];
-    if (ctx->encode_variant == 4) {
-        if (!ctx->has_index) return set_err(ctx, NTC_ERR_NO_INDEX, "no index uploaded");
-        rc = encode4_impl(ctx, (const uint8_t *)d_bases, (const uint64_t *)d_offs, n_reads, total,
-                          (uint64_t *)d_recs, total + 1, (uint64_t *)d_roffs);
-    } else {
-        rc = encode_impl(ctx, (const uint8_t *)d_bases, (const uint64_t *)d_offs, n_reads, lay,
-                         (uint64_t *)d_recs, total + 1, (uint64_t *)d_roffs, total);
-    }
+    rc = encode_impl(ctx, (const uint8_t *)d_bases, (const uint64_t *)d_offs, n_reads, lay, (uint64_t *)d_recs,
+                     total + 1, (uint64_t *)d_roffs, total);
     if (rc) return rc;
-    int64_t bad = -1;
-    rc = read_status(ctx, &bad);
-    if (rc) {
-        if (bad_read) *bad_read = bad;
-        return rc;
-    }
+    rc = read_status(ctx, bad_read);
+    if (rc) return rc;
     HIP_TRY(ctx, hipMemcpy(rec_offsets_out, d_roffs, (n_reads + 1) * 8, hipMemcpyDeviceToHost));
     const uint64_t nrec = rec_offsets_out[n_reads];
-    if (nrec > rec_capacity)
-        return set_err(ctx, NTC_ERR_CAPACITY, "rec_capacity smaller than the number of records");
+    if (nrec > rec_capacity) return set_err(ctx, NTC_ERR_CAPACITY, "rec_capacity smaller than the number of records");
     if (nrec) HIP_TRY(ctx, hipMemcpy(rec_out, d_recs, nrec * 8, hipMemcpyDeviceToHost));
+    return NTC_OK;
+}
+}  // namespace
+
+int ntc_encode_batch(ntc_ctx *ctx, const uint8_t *bases, const uint64_t *read_offsets, uint64_t n_reads,
+                     uint64_t *rec_out, uint64_t rec_capacity, uint64_t *rec_offsets_out, int64_t *bad_read) {
+    if (bad_read) *bad_read = -1;
+    if (!ctx || !read_offsets || !rec_offsets_out || (n_reads && !bases))
+        return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    for (uint64_t r = 0; r < n_reads; r++)
+        if (read_offsets[r + 1] < read_offsets[r])
+            return set_err(ctx, NTC_ERR_INVALID_ARG, "read offsets must be non-decreasing");
+    if (!ctx->has_index) return set_err(ctx, NTC_ERR_NO_INDEX, "no index uploaded");
+    if (ctx->encode_variant != 4)
+        return encode_batch_v1(ctx, bases, read_offsets, n_reads, rec_out, rec_capacity, rec_offsets_out, bad_read);
+    // passes of whole reads, at most max_pass_bases each (one read may exceed it alone), so
+    // the device workspace stays bounded however large the host batch is
+    std::vector<uint64_t> offs, roffs;
+    uint64_t r0 = 0, produced = 0;
+    rec_offsets_out[0] = 0;
+    do {
+        uint64_t r1 = std::min(n_reads, r0 + 1);
+        if (r1 < n_reads) {  // largest r1 with bases [r0, r1) <= max_pass_bases
+            uint64_t lo = r1, hi = n_reads;
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi + 1) / 2;
+                if (read_offsets[mid] - read_offsets[r0] <= ctx->max_pass_bases) lo = mid;
+                else hi = mid - 1;
+            }
+            r1 = lo;
+        }
+        const uint64_t nr = r1 - r0, o0 = read_offsets[r0], total = read_offsets[r1] - o0;
+        offs.resize(nr + 1);
+        for (uint64_t r = 0; r <= nr; r++) offs[r] = read_offsets[r0 + r] - o0;
+        void *d_bases, *d_offs, *d_recs;
+        int rc;
+        if ((rc = ensure(ctx, WS_STAGE_BASES, total + 64, &d_bases))) return rc;
+        if ((rc = ensure(ctx, WS_STAGE_OFFS, (nr + 1) * 8 * 2, &d_offs))) return rc;
+        if ((rc = ensure(ctx, WS_STAGE_RECS, (total + 1) * 8, &d_recs))) return rc;
+        uint64_t *d_roffs = (uint64_t *)d_offs + (nr + 1);
+        if (total) HIP_TRY(ctx, hipMemcpyAsync(d_bases, bases + o0, total, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(d_offs, offs.data(), (nr + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+        rc = encode4_impl(ctx, (const uint8_t *)d_bases, (const uint64_t *)d_offs, nr, total, (uint64_t *)d_recs,
+                          total + 1, d_roffs);
+        if (rc) return rc;
+        int64_t bad = -1;
+        rc = read_status(ctx, &bad);
+        if (rc) {
+            if (bad_read) *bad_read = bad + (int64_t)r0;
+            char buf[160];
+            std::snprintf(buf, sizeof(buf), "%s at index %lld", status_name(rc), (long long)(bad + (int64_t)r0));
+            ctx->err = buf;
+            return rc;
+        }
+        roffs.resize(nr + 1);
+        HIP_TRY(ctx, hipMemcpy(roffs.data(), d_roffs, (nr + 1) * 8, hipMemcpyDeviceToHost));
+        const uint64_t nrec = roffs[nr];
+        if (produced + nrec > rec_capacity)
+            return set_err(ctx, NTC_ERR_CAPACITY, "rec_capacity smaller than the number of records");
+        for (uint64_t r = 1; r <= nr; r++) rec_offsets_out[r0 + r] = produced + roffs[r];
+        if (nrec) HIP_TRY(ctx, hipMemcpy(rec_out + produced, d_recs, nrec * 8, hipMemcpyDeviceToHost));
+        produced += nrec;
+        r0 = r1;
+    } while (r0 < n_reads);
     return NTC_OK;
 }
 
@@ -759,21 +815,49 @@ int ntc_decode_batch(ntc_ctx *ctx, const uint64_t *recs, uint64_t n_recs, uint8_
     if (n_recs && !((recs[0] >> 56) & 1)) return set_err(ctx, NTC_ERR_FORMAT, "records do not start a read");
     if (nbases > bases_capacity || nreads + 1 > offsets_capacity || !read_offsets_out || (nbases && !bases_out))
         return set_err(ctx, NTC_ERR_CAPACITY, "decode output buffers too small");
-    void *d_recs, *d_out, *d_offs;
-    int rc;
-    if ((rc = ensure(ctx, WS_STAGE_RECS, (n_recs + 1) * 8, &d_recs))) return rc;
-    if ((rc = ensure(ctx, WS_STAGE_BASES, nbases + 64, &d_out))) return rc;
-    if ((rc = ensure(ctx, WS_STAGE_OFFS, (nreads + 1) * 8, &d_offs))) return rc;
-    if (n_recs) HIP_TRY(ctx, hipMemcpyAsync(d_recs, recs, n_recs * 8, hipMemcpyHostToDevice, ctx->stream));
-    rc = ntc_decode_batch_device(ctx, (const uint64_t *)d_recs, n_recs, (uint8_t *)d_out, nbases,
-                                 (uint64_t *)d_offs, nreads + 1);
-    if (rc) return rc;
-    uint64_t nr = 0, nb = 0;
-    rc = ntc_decode_status(ctx, &nr, &nb);
-    if (rc) return rc;
-    if (nr != nreads || nb != nbases) return set_err(ctx, NTC_ERR_FORMAT, "decode size mismatch");
-    HIP_TRY(ctx, hipMemcpy(read_offsets_out, d_offs, (nreads + 1) * 8, hipMemcpyDeviceToHost));
-    if (nbases) HIP_TRY(ctx, hipMemcpy(bases_out, d_out, nbases, hipMemcpyDeviceToHost));
+    // passes of whole reads (a pass ends before a `first` record), at most max_pass_bases
+    // output bases each unless one read alone is larger
+    uint64_t a0 = 0, reads_done = 0, bases_done = 0;
+    read_offsets_out[0] = 0;
+    std::vector<uint64_t> offs;
+    while (a0 < n_recs) {
+        uint64_t a1 = a0, pb = 0, pr = 0;
+        while (a1 < n_recs) {
+            const uint32_t flag = (uint32_t)(recs[a1] >> 56);
+            const uint64_t len = (flag & 2) ? (flag >> 2) : ((uint32_t)(recs[a1] >> 32) & 0xFFFFFFu);
+            if ((flag & 1) && a1 > a0 && pb + len > ctx->max_pass_bases) break;
+            pb += len;
+            pr += flag & 1;
+            a1++;
+        }
+        // a read runs to the next `first` record: extend the pass over the rest of this read
+        while (a1 < n_recs && !((recs[a1] >> 56) & 1)) {
+            const uint32_t flag = (uint32_t)(recs[a1] >> 56);
+            pb += (flag & 2) ? (flag >> 2) : ((uint32_t)(recs[a1] >> 32) & 0xFFFFFFu);
+            a1++;
+        }
+        const uint64_t nrec = a1 - a0;
+        void *d_recs, *d_out, *d_offs;
+        int rc;
+        if ((rc = ensure(ctx, WS_STAGE_RECS, (nrec + 1) * 8, &d_recs))) return rc;
+        if ((rc = ensure(ctx, WS_STAGE_BASES, pb + 64, &d_out))) return rc;
+        if ((rc = ensure(ctx, WS_STAGE_OFFS, (pr + 1) * 8, &d_offs))) return rc;
+        HIP_TRY(ctx, hipMemcpyAsync(d_recs, recs + a0, nrec * 8, hipMemcpyHostToDevice, ctx->stream));
+        rc = ntc_decode_batch_device(ctx, (const uint64_t *)d_recs, nrec, (uint8_t *)d_out, pb, (uint64_t *)d_offs,
+                                     pr + 1);
+        if (rc) return rc;
+        uint64_t nr = 0, nb = 0;
+        rc = ntc_decode_status(ctx, &nr, &nb);
+        if (rc) return rc;
+        if (nr != pr || nb != pb) return set_err(ctx, NTC_ERR_FORMAT, "decode size mismatch");
+        offs.resize(pr + 1);
+        HIP_TRY(ctx, hipMemcpy(offs.data(), d_offs, (pr + 1) * 8, hipMemcpyDeviceToHost));
+        for (uint64_t r = 1; r <= pr; r++) read_offsets_out[reads_done + r] = bases_done + offs[r];
+        if (pb) HIP_TRY(ctx, hipMemcpy(bases_out + bases_done, d_out, pb, hipMemcpyDeviceToHost));
+        reads_done += pr;
+        bases_done += pb;
+        a0 = a1;
+    }
     return NTC_OK;
 }
 

@@ -306,3 +306,35 @@ def test_gpu_path_cover_equals_host_cover(ctx):
         assert ctx.get_option("path_text_len") == tlen, k
         assert ctx.get_option("n_paths") == npaths, k
         assert ctx.get_option("path_hash") & ((1 << 64) - 1) == h, k
+
+
+def test_gpu_host_api_splits_large_batches_into_passes(ctx):
+    """Host-buffer calls run in device passes of at most max_pass_bases (bounded workspace
+    for any batch size): records, offsets, decoded bases and the failing read's index are
+    the same as in one pass."""
+    genome = nt.synth_genome(17, 200_000)
+    ix = nt.Index.build([genome.tobytes()], 31)
+    ctx.upload(ix)
+    rng = np.random.default_rng(4)
+    lens = rng.integers(1, 400, 3000)
+    g = genome.tobytes()
+    reads = [g[s:s + L] for s, L in zip(rng.integers(0, len(g) - 400, 3000), lens)]
+    bases, offs = pack_reads(reads)
+    exp, eoff = OracleIndex(ix.n, 31, ix.rows, ix.C, ix.lcs).encode(bases, offs)
+    default = ctx.get_option("max_pass_bases")
+    try:
+        for mp in (1, 5_000, 77_777, default):
+            ctx.set_option("max_pass_bases", mp)
+            got, goff = ctx.encode(bases, offs)
+            assert np.array_equal(goff, eoff) and np.array_equal(got, exp), mp
+            out, o2 = ctx.decode(got)
+            assert np.array_equal(out, bases) and np.array_equal(o2, offs), mp
+        bad = bytearray(bases.tobytes())
+        bad[int(offs[2500]) + 3] = ord("N")
+        for mp in (5_000, default):
+            ctx.set_option("max_pass_bases", mp)
+            with pytest.raises(nt.NtcError) as e:
+                ctx.encode(np.frombuffer(bytes(bad), dtype=np.uint8), offs)
+            assert e.value.code == 2 and e.value.bad_read == 2500, mp
+    finally:
+        ctx.set_option("max_pass_bases", default)
