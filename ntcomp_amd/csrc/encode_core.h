@@ -23,6 +23,17 @@ typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
                    // 2 exact presence bits, 4 path stream, 8 query words (k_ms4)
 #endif
 
+// Line tracing for the test-only emulator (tests/emu, -DNTC_TRACE): every index load
+// reports (kind, address) so per-read cache-line footprints can be counted on the CPU.
+#if defined(NTC_TRACE) && !defined(__HIP_DEVICE_COMPILE__)
+void ntc_touch(int kind, const void *p);
+#define NTC_TOUCH(kind, p) ntc_touch(kind, (const void *)(p))
+#else
+#define NTC_TOUCH(kind, p) ((void)0)
+#endif
+enum { kTrRank, kTrLcs, kTrUniq, kTrTabU, kTrTabLo, kTrBits, kTrFilt, kTrColex, kTrPon, kTrPst, kTrQ, kTrE,
+       kTrPuniq, kTrEw, kTrKinds };
+
 namespace ntc {
 
 #if defined(NTC_STATS) && !defined(__HIP_DEVICE_COMPILE__)
@@ -144,6 +155,8 @@ NTC_HD uint32_t rank_word(uint2 w, uint32_t x) {  // C[c] + rank_c(x) from x's w
 // extend_right(I, c) = [C[c] + rank_c(l), C[c] + rank_c(r))
 NTC_HD void extend(const DevIndex &ix, int c, uint32_t l, uint32_t r, uint32_t &nl, uint32_t &nr) {
     const uint2 *row = ix.rank + (uint64_t)c * ix.rwords;
+    NTC_TOUCH(kTrRank, row + (l >> 5));
+    NTC_TOUCH(kTrRank, row + (r >> 5));
     const uint2 a = load2(row + (l >> 5)), b = load2(row + (r >> 5));
     nl = rank_word(a, l);
     nr = rank_word(b, r);
@@ -151,8 +164,8 @@ NTC_HD void extend(const DevIndex &ix, int c, uint32_t l, uint32_t r, uint32_t &
 
 // contract_left(I, t) [ext sbwt]: widen I to all nodes sharing the last t characters.
 NTC_HD void widen(const DevIndex &ix, uint32_t &l, uint32_t &r, uint32_t t) {
-    while (l > 0 && ix.lcs[l] >= t) l--;
-    while (r < ix.n && ix.lcs[r] >= t) r++;
+    while (l > 0 && (NTC_TOUCH(kTrLcs, ix.lcs + l), ix.lcs[l]) >= t) l--;
+    while (r < ix.n && (NTC_TOUCH(kTrLcs, ix.lcs + r), ix.lcs[r]) >= t) r++;
 }
 
 // One character of k-bounded matching statistics.  State (d, [l, r)) = length and colex
@@ -463,7 +476,10 @@ NTC_HD uint64_t window1(const uint64_t *w, uint32_t off) {
     return sh ? ((a >> sh) | (w[i + 1] << (64 - sh))) : a;
 }
 NTC_HD uint32_t ctz64(uint64_t x) { return x ? (uint32_t)__builtin_ctzll(x) : 64u; }
-NTC_HD uint32_t uniq_bit(const DevIndex &ix, uint32_t v) { return (ix.uniq[v >> 5] >> (v & 31)) & 1u; }
+NTC_HD uint32_t uniq_bit(const DevIndex &ix, uint32_t v) {
+    NTC_TOUCH(kTrUniq, ix.uniq + (v >> 5));
+    return (ix.uniq[v >> 5] >> (v & 31)) & 1u;
+}
 
 // (d, S) of a position not covered by an entry, from the suffix table: u = min(x+1, U)
 // characters ending at x; long => d = u (x < U-1: the whole prefix; else the predecessor
@@ -471,6 +487,7 @@ NTC_HD uint32_t uniq_bit(const DevIndex &ix, uint32_t v) { return (ix.uniq[v >> 
 NTC_HD void tab_ds(const DevIndex &ix, const uint64_t *Q, uint64_t qo, uint32_t x, uint32_t &d, uint32_t &s) {
     const uint32_t u = x + 1 < ix.tab_u ? x + 1 : ix.tab_u;
     const uint64_t key = window2(Q, qo + x + 1 - u) & ((1ULL << (2 * u)) - 1);
+    NTC_TOUCH(u == ix.tab_u ? kTrTabU : kTrTabLo, ix.tab + tab_base(u) + key);
     const uint2 e = ix.tab[tab_base(u) + key];
     d = tab_long(e) ? u : (e.y & 0xFFu);
     s = e.x;
@@ -482,6 +499,7 @@ NTC_HD uint32_t ones_down(const uint64_t *w, uint32_t a, uint32_t maxn) {
     int64_t pos = a;
     while (cnt < maxn) {
         const uint32_t wi = (uint32_t)(pos >> 6), b = (uint32_t)(pos & 63);
+        NTC_TOUCH(kTrPuniq, w + wi);
         const uint64_t x = ~w[wi] << (63 - b);  // bit b -> bit 63
         const uint32_t z = x ? (uint32_t)__builtin_clzll(x) : 64u;
         if (z <= b) { cnt += z; break; }
@@ -493,6 +511,7 @@ NTC_HD uint32_t ones_down(const uint64_t *w, uint32_t a, uint32_t maxn) {
 }
 
 NTC_HD Entry load_entry(const Entry *E, int32_t i) {
+    NTC_TOUCH(kTrE, E + i);
 #ifdef __HIP_DEVICE_COMPILE__
     const uint4 v = *reinterpret_cast<const uint4 *>(E + i);
     return Entry{v.x, v.y, v.z, v.w};
@@ -539,6 +558,7 @@ struct EntryView {
         return (en.dk & kRunTag) ? (d < k ? d : k) : d0;
     }
     NTC_HD uint32_t sval(const Entry &en, uint32_t x) const {
+        if (en.dk & kRunTag) NTC_TOUCH(kTrColex, ix->colex_at + en.v + (x - en.p));
         return (en.dk & kRunTag) ? (ix->colex_at[en.v + (x - en.p)] & 0x7FFFFFFFu) : en.v;
     }
     NTC_HD uint32_t D(uint32_t x) {
@@ -629,6 +649,7 @@ NTC_HD bool is_acgt(uint32_t b) { return b == 'A' || b == 'C' || b == 'G' || b =
 
 
 NTC_HD void store_entry(Entry *E, uint32_t i, uint32_t p, uint32_t v, uint32_t m, uint32_t dk) {
+    NTC_TOUCH(kTrEw, E + i);
 #if defined(__HIP_DEVICE_COMPILE__) && (NTC_NT & 16)
     u32x4_t x = {p, v, m, dk};
     __builtin_nontemporal_store(x, reinterpret_cast<u32x4_t *>(E + i));
@@ -662,6 +683,8 @@ struct MsLane {
     }
     NTC_HD void window(uint32_t from) {
         qb = from;
+        NTC_TOUCH(kTrQ, Q + ((qo + from) >> 5));
+        NTC_TOUCH(kTrQ, Q + ((qo + from) >> 5) + 1);
         qw = window2(Q, qo + from);
     }
     NTC_HD bool covers(uint32_t x0, uint32_t x1) const { return qb != 0xFFFFFFFFu && x0 >= qb && x1 < qb + 32; }
@@ -672,6 +695,7 @@ struct MsLane {
     NTC_HD void note_single(const DevIndex &ix) {
         j = 0xFFFFFFFFu;
         if (ix.has_paths && r == l + 1 && d >= ix.t_jump) {
+            NTC_TOUCH(kTrPon, ix.pos_of_node + l);
             j = ix.pos_of_node[l];
             try_run = j != 0xFFFFFFFFu;
         }
@@ -718,6 +742,10 @@ struct MsLane {
                 // 64 path characters after node j's k-mer, and whether the k-mer ending at
                 // each of them is a node, from three interleaved 32-char groups
                 const uint64_t T = (uint64_t)j + k + m;
+                NTC_TOUCH(kTrPst, ix.pstream + (T >> 5));
+                NTC_TOUCH(kTrPst, ix.pstream + (T >> 5) + 2);
+                NTC_TOUCH(kTrQ, Q + ((qo + p + m) >> 5));
+                NTC_TOUCH(kTrQ, Q + ((qo + p + m) >> 5) + 2);
                 const uint4 g0 = ld4<4>(ix.pstream + (T >> 5)), g1 = ld4<4>(ix.pstream + (T >> 5) + 1),
                             g2 = ld4<4>(ix.pstream + (T >> 5) + 2);
                 const uint32_t sh = (uint32_t)(T & 31);
@@ -767,6 +795,8 @@ struct MsLane {
             mode = kModeScan;
             if (len >= U + 1) {
                 window(0);
+                NTC_TOUCH(kTrTabU, ix.tab + tab_base(U) + key_at(U - 1, U));
+                NTC_TOUCH(kTrBits, ix.tab_bits + (key_at(U, U) >> 5));
                 const uint2 te = load2_stream(ix.tab + tab_base(U) + key_at(U - 1, U));
                 const uint64_t k2 = key_at(U, U);
                 const uint32_t b2 = (ix.tab_bits[k2 >> 5] >> (k2 & 31)) & 1u;
@@ -802,6 +832,7 @@ struct MsLane {
                 for (uint32_t i = 0; i < kScanW + kFiltGap; i++)
                     if (i < W + kFiltGap) {
                         const uint64_t fk = (qw >> (2 * (p + 1 - U + i - qb))) & ((1ULL << (2 * F)) - 1);
+                        NTC_TOUCH(kTrFilt, ix.filt_bits + (fk >> 5));
                         fm |= ((ix.filt_bits[fk >> 5] >> (fk & 31)) & 1u) << i;
                     }
                 cand &= fm & (fm >> 1) & (fm >> kFiltGap);  // all three F-mers of the U-mer
@@ -822,6 +853,7 @@ struct MsLane {
             for (uint32_t i = 0; i < kScanW; i++)
                 if ((tested >> i) & 1u) {
                     const uint64_t key = key_at(p + i, U);
+                    NTC_TOUCH(kTrBits, ix.tab_bits + (key >> 5));
                     longm |= ((ld_hint<2>(ix.tab_bits + (key >> 5)) >> (key & 31)) & 1u) << i;
                 }
             const uint32_t pairs = longm & (longm >> 1);
@@ -831,10 +863,13 @@ struct MsLane {
                 return 0;
             }
             const uint32_t x = p + (uint32_t)__builtin_ctz(pairs);  // long, short predecessor
+            NTC_TOUCH(kTrTabU, ix.tab + tab_base(U) + key_at(x, U));
             return enter_pair(ix, x, load2_stream(ix.tab + tab_base(U) + key_at(x, U)));
         }
         if (!covers(p + 1 - U, p)) window(p + 1 - U);
         if (mode == kModeBrk) {
+            NTC_TOUCH(kTrTabU, ix.tab + tab_base(U) + key_at(p, U));
+            NTC_TOUCH(kTrColex, ix.colex_at + j);
             const uint2 te = load2_stream(ix.tab + tab_base(U) + key_at(p, U));
             const uint32_t v = ix.colex_at[j] & 0x7FFFFFFFu;  // node before p, for a long p
             if (!tab_long(te)) {
@@ -848,6 +883,7 @@ struct MsLane {
         }
         const int c = (int)((qw >> (2 * (p - qb))) & 3u);
         if (mode == kModeExt) {
+            NTC_TOUCH(kTrTabU, ix.tab + tab_base(U) + key_at(p, U));
             const uint2 te = load2_stream(ix.tab + tab_base(U) + key_at(p, U));  // for a failure
             uint32_t nl, nr;
             extend(ix, c, l, r, nl, nr);
@@ -943,6 +979,7 @@ NTC_HD int parse_read(const DevIndex &ix, const uint64_t *Q, uint64_t qo, const 
         if (seglen > 11) {
             w = (uint64_t)st | ((uint64_t)(seglen & 0xFFFFFFu) << 32) | (first << 56);
         } else {
+            NTC_TOUCH(kTrQ, Q + ((qo + segend - seglen) >> 5));
             const uint64_t bits = window2(Q, qo + segend - seglen);
             w = (bits & ((1ULL << (2 * seglen)) - 1)) | ((uint64_t)((first + 2) | (seglen << 2)) << 56);
         }

@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""Per-read cache-line footprint of the encode lanes (k_ms4 / k_parse4 logic), on the CPU.
+
+Runs the kernels' lane functions through the TEST-ONLY emulator built with -DNTC_TRACE
+(tests/emu libntc_emu_trace.so) and prints, per phase and per structure, the loads and the
+distinct 128-byte lines each read touches.  Distinct lines per read approximate the L2
+misses of a structure far larger than L2 (suffix table, bitmaps, colex_at, ...).
+
+usage: python scripts/trace_lines.py [--genome-bp 5000000] [--k 91] [--reads 20000] [--err-ppm 10000]
+"""
+import argparse
+import ctypes
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+KINDS = ["rank", "lcs", "uniq", "tabU", "tabLo", "bits", "filt", "colex", "pos_of_node", "pstream", "Q", "E",
+         "puniq", "E-store"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--genome-bp", type=int, default=5_000_000)
+    ap.add_argument("--k", type=int, default=91)
+    ap.add_argument("--reads", type=int, default=20_000)
+    ap.add_argument("--read-len", type=int, default=150)
+    ap.add_argument("--err-ppm", type=int, default=10_000)
+    ap.add_argument("--tab-u", type=int, default=0)
+    args = ap.parse_args()
+    so = os.path.join(REPO, "tests", "emu", "libntc_emu_trace.so")
+    subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "tests", "emu"), "libntc_emu_trace.so"])
+    import emu_lib
+    import ntcomp_amd as nt
+
+    emu_lib.EMU_SO = so
+    L = emu_lib.emu_lib()
+    L.emu_trace_report.argtypes = [ctypes.c_void_p]
+    genome = nt.synth_genome(1, args.genome_bp)
+    ix = nt.Index.build([genome.tobytes()], args.k, threads=8)
+    reads = nt.synth_reads(genome, 2, 0, args.reads, args.read_len, args.err_ppm)
+    offs = np.arange(0, args.reads * args.read_len + 1, args.read_len, dtype=np.uint64)
+    recs, _ = emu_lib.emu_encode(ix.n, args.k, ix.rows, ix.C, ix.lcs, reads, offs, tab_u=args.tab_u)
+    K = len(KINDS)
+    out = np.zeros(1 + 4 * K, dtype=np.uint64)
+    L.emu_trace_report(out.ctypes.data)
+    n = int(out[0])
+    req = out[1:1 + 2 * K].reshape(2, K) / n
+    lines = out[1 + 2 * K:].reshape(2, K) / n
+    print(f"reads {n}, records/read {len(recs) / n:.2f}, k={args.k}, err_ppm={args.err_ppm}")
+    for ph, name in enumerate(["ms", "parse"]):
+        print(f"-- {name}: loads/read {req[ph].sum():.2f}, lines/read {lines[ph].sum():.2f}")
+        for i in np.argsort(-lines[ph]):
+            if req[ph][i] > 0:
+                print(f"   {KINDS[i]:12s} loads {req[ph][i]:7.2f}  lines {lines[ph][i]:6.2f}")
+
+
+if __name__ == "__main__":
+    main()

@@ -13,6 +13,48 @@
 
 using namespace ntc;
 
+#ifdef NTC_TRACE
+// Per-read footprint counters (trace build only): requests and distinct 128-byte lines by
+// kind, for the MS phase (0) and the parse phase (1).
+#include <unordered_set>
+namespace {
+int g_phase = -1;
+std::unordered_set<uint64_t> g_lines[2][kTrKinds];
+uint64_t g_req[2][kTrKinds], g_ltot[2][kTrKinds], g_reads;
+void trace_phase(int ph) { g_phase = ph; }
+void trace_read_done() {
+    for (int a = 0; a < 2; a++)
+        for (int b = 0; b < kTrKinds; b++) {
+            g_ltot[a][b] += g_lines[a][b].size();
+            g_lines[a][b].clear();
+        }
+    g_reads++;
+    g_phase = -1;
+}
+}  // namespace
+void ntc_touch(int kind, const void *p) {
+    if (g_phase < 0) return;
+    g_req[g_phase][kind]++;
+    g_lines[g_phase][kind].insert((uint64_t)(uintptr_t)p >> 7);
+}
+extern "C" void emu_trace_report(uint64_t *out) {  // [reads, req[2][K], lines[2][K]]
+    out[0] = g_reads;
+    for (int a = 0; a < 2; a++)
+        for (int b = 0; b < kTrKinds; b++) {
+            out[1 + a * kTrKinds + b] = g_req[a][b];
+            out[1 + 2 * kTrKinds + a * kTrKinds + b] = g_ltot[a][b];
+        }
+    memset(g_req, 0, sizeof g_req);
+    memset(g_ltot, 0, sizeof g_ltot);
+    g_reads = 0;
+}
+#else
+namespace {
+inline void trace_phase(int) {}
+inline void trace_read_done() {}
+}  // namespace
+#endif
+
 namespace {
 bool load(const ntc_index_view *v, HostIndex &hx, Derived &dv, std::vector<WalkEntry> &walk, DevIndex &d,
           std::vector<uint2> &tab, std::vector<uint32_t> &bits, std::vector<uint32_t> &fbits, uint32_t tab_u = 0) {
@@ -92,6 +134,7 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
                 MsLane ms;
                 uint32_t ne = 0;
                 if (rc == 0) {
+                    trace_phase(0);
                     ms.start(d, Q.data(), 0, E4.data(), len);
                     for (;;) {
                         int st = ms.step(d);
@@ -100,7 +143,9 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
                     }
                     ne = ms.ne;
                 }
+                trace_phase(1);
                 if (rc == 0) rc = parse_read(d, Q.data(), 0, E4.data(), ne, len, R4.data(), R4.data());
+                trace_read_done();
                 if (d_out && rc >= 0)
                     read_ms(d, Q.data(), 0, E4.data(), ne, len, d_out + (offs[r] - offs[0]), s_out + (offs[r] - offs[0]));
                 if (rc >= 0) {
