@@ -438,6 +438,9 @@ struct BaseReader {
 
 enum : uint32_t { kModeScan = 0, kModeExt = 1, kModeP1 = 2, kModeBs = 3, kModeBrk = 4, kModeFirst = 5 };
 constexpr uint32_t kScanW = 16;      // presence probes per SCAN unit (U + kScanW - 1 <= 32)
+#ifndef NTC_SCAN_MODE
+#define NTC_SCAN_MODE 0  // 2: SCAN loads the first candidate pair's table entry directly
+#endif
 constexpr uint32_t kScanExact = 4;   // filter candidates tested exactly per SCAN
 
 // ======================================================================================
@@ -837,6 +840,72 @@ struct MsLane {
                     }
                 cand &= fm & (fm >> 1) & (fm >> kFiltGap);  // all three F-mers of the U-mer
             }
+#if NTC_SCAN_MODE == 2
+            if (ix.filt_f) {
+                // first candidate PAIR (x, x + 1 both pass the filter): its table entry is
+                // needed anyway when x is long, so load it in place of x's exact bit
+                const uint32_t cp = cand & (cand >> 1);
+                if (cp == 0) {
+                    if (p + W >= len) { p = len; return 1; }
+                    p += W - ((cand >> (W - 1)) & 1u);  // a passing last position may start a pair
+                    return 0;
+                }
+                const uint32_t x = p + (uint32_t)__builtin_ctz(cp);
+                const uint64_t k1 = key_at(x + 1, U);
+                NTC_TOUCH(kTrTabU, ix.tab + tab_base(U) + key_at(x, U));
+                NTC_TOUCH(kTrBits, ix.tab_bits + (k1 >> 5));
+                const uint2 te = load2_stream(ix.tab + tab_base(U) + key_at(x, U));
+                const uint32_t b1 = (ld_hint<2>(ix.tab_bits + (k1 >> 5)) >> (k1 & 31)) & 1u;
+                if (!tab_long(te)) {  // x short: d_{x+i} <= m + i
+                    p = x;
+                    skip_short(te.y & 0xFFu, U);
+                    return p >= len ? 1 : 0;
+                }
+                if (!b1) {  // x long, x + 1 short
+                    p = x + 2;
+                    return p >= len ? 1 : 0;
+                }
+                return enter_pair(ix, x, te);
+            }
+#endif
+#if NTC_SCAN_MODE == 1
+            if (ix.filt_f) {
+                // exact bits only for the first two candidate PAIRS (x, x + 1 both pass)
+                const uint32_t cp = cand & (cand >> 1);
+                if (cp == 0) {
+                    if (p + W >= len) { p = len; return 1; }
+                    p += W - ((cand >> (W - 1)) & 1u);  // a passing last position may start a pair
+                    return 0;
+                }
+                const uint32_t x0 = (uint32_t)__builtin_ctz(cp);
+                const uint32_t rest = cp & (cp - 1);
+                const uint32_t x1 = rest ? (uint32_t)__builtin_ctz(rest) : x0;
+                const uint32_t starts = (1u << x0) | (1u << x1);
+                const uint32_t tested = (3u << x0) | (3u << x1);
+                uint32_t longm = 0;
+#pragma unroll
+                for (uint32_t i = 0; i < kScanW; i++)
+                    if ((tested >> i) & 1u) {
+                        const uint64_t key = key_at(p + i, U);
+                        NTC_TOUCH(kTrBits, ix.tab_bits + (key >> 5));
+                        longm |= ((ld_hint<2>(ix.tab_bits + (key >> 5)) >> (key & 31)) & 1u) << i;
+                    }
+                const uint32_t pairs = longm & (longm >> 1) & starts;
+                if (pairs == 0) {
+                    const uint32_t more = rest & (rest - 1);  // untested candidate pairs
+                    if (more == 0) {
+                        if (p + W >= len) { p = len; return 1; }
+                        p += W - ((cand >> (W - 1)) & 1u);
+                        return 0;
+                    }
+                    p += x1 + 1;
+                    return p >= len ? 1 : 0;
+                }
+                const uint32_t x = p + (uint32_t)__builtin_ctz(pairs);
+                NTC_TOUCH(kTrTabU, ix.tab + tab_base(U) + key_at(x, U));
+                return enter_pair(ix, x, load2_stream(ix.tab + tab_base(U) + key_at(x, U)));
+            }
+#endif
             // exact test of the first kScanExact candidates only: the pair is almost always
             // among them, and positions past the last one tested are left to the next SCAN
             uint32_t tested = cand, span = W;
@@ -938,9 +1007,11 @@ NTC_HD void read_ms(const DevIndex &ix, const uint64_t *Q, uint64_t qo, const En
 constexpr uint32_t kRecSlot = 8;  // records per read in the dense slot; more spill
 
 // greedy right-to-left parse over the entries, lib.rs:175-218 (+ encode.rs:144-158).
-// Record j goes to slot[j] (j < kRecSlot) or spill[j].
+// Record j goes to slot[j * sstride] (j < kRecSlot) or spill[j].  The kernel interleaves
+// the reads' slots (sstride = reads in the batch): the loop runs in lock step over a
+// wave's lanes, so the lanes' j-th records are one coalesced store.
 NTC_HD int parse_read(const DevIndex &ix, const uint64_t *Q, uint64_t qo, const Entry *E, uint32_t ne,
-                      uint32_t len, uint64_t *slot, uint64_t *spill) {
+                      uint32_t len, uint64_t *slot, uint64_t *spill, uint64_t sstride = 1) {
     const uint32_t k = ix.k;
     EntryView ev(E, &ix, Q, qo, k, (int32_t)ne - 1);
     uint32_t i = len;
@@ -983,7 +1054,7 @@ NTC_HD int parse_read(const DevIndex &ix, const uint64_t *Q, uint64_t qo, const 
             const uint64_t bits = window2(Q, qo + segend - seglen);
             w = (bits & ((1ULL << (2 * seglen)) - 1)) | ((uint64_t)((first + 2) | (seglen << 2)) << 56);
         }
-        if (nrec < (int)kRecSlot) slot[nrec] = w;
+        if (nrec < (int)kRecSlot) slot[(uint64_t)nrec * sstride] = w;
         else spill[nrec] = w;
         nrec++;
         if (i > 0) i -= 1;

@@ -144,7 +144,7 @@ constexpr uint32_t kPoolChunk = 64;
 __device__ __forceinline__ void parse_one(const Enc4Args &a, uint64_t r) {
     const uint64_t o0 = a.offs[0], b = a.offs[r], e = a.offs[r + 1];
     const uint64_t P = b - o0;
-    const int rc = parse_read(a.ix, a.Q, P, a.E + P, a.ne[r], (uint32_t)(e - b), a.R2 + r * kRecSlot, a.R + P);
+    const int rc = parse_read(a.ix, a.Q, P, a.E + P, a.ne[r], (uint32_t)(e - b), a.R2 + r, a.R + P, a.n_reads);
     if (rc < 0) {
         atomicMin(a.status, (unsigned long long)((r << 8) | (uint64_t)(-rc)));
         a.rec_count[r] = 0;
@@ -235,9 +235,9 @@ __global__ __launch_bounds__(256) void k_emit4(Enc4Args a, const uint64_t *rec_o
         atomicMin(a.status, (unsigned long long)((r << 8) | (uint64_t)kErrCapacity));
         return;
     }
-    const uint64_t *slot = a.R2 + r * kRecSlot;
+    const uint64_t *slot = a.R2 + r;  // record j at slot[j * n_reads] (parse_read)
     const uint32_t ns = cnt < kRecSlot ? cnt : kRecSlot;
-    for (uint32_t j = 0; j < ns; j++) out[off + j] = slot[j];
+    for (uint32_t j = 0; j < ns; j++) out[off + j] = slot[(uint64_t)j * a.n_reads];
     if (cnt > kRecSlot) {
         const uint64_t *spill = a.R + (a.offs[r] - a.offs[0]);
         for (uint32_t j = kRecSlot; j < cnt; j++) out[off + j] = spill[j];
