@@ -465,12 +465,26 @@ struct Entry {       // 16 bytes, one uint4 store
 };
 constexpr uint32_t kRunTag = 0x80000000u;
 
-// 32 two-bit characters starting at character offset off of a packed array
+// w[0], w[1] with one 16-byte load (w 8-byte aligned: global loads need dword alignment only)
+typedef uint64_t u64x2_a8 __attribute__((ext_vector_type(2), aligned(8)));
+NTC_HD void load_w2(const uint64_t *w, uint64_t &a, uint64_t &b) {
+#ifdef __HIP_DEVICE_COMPILE__
+    const u64x2_a8 v = *reinterpret_cast<const u64x2_a8 *>(w);
+    a = v.x;
+    b = v.y;
+#else
+    a = w[0];
+    b = w[1];
+#endif
+}
+// 32 two-bit characters starting at character offset off (the packed query arrays carry
+// padding words past their end, so w[i + 1] is always readable)
 NTC_HD uint64_t window2(const uint64_t *w, uint64_t off) {
     const uint64_t i = off >> 5;
     const uint32_t sh = (uint32_t)(off & 31) * 2;
-    const uint64_t a = w[i];
-    return sh ? ((a >> sh) | (w[i + 1] << (64 - sh))) : a;
+    uint64_t a, b;
+    load_w2(w + i, a, b);
+    return sh ? ((a >> sh) | (b << (64 - sh))) : a;
 }
 // 64 bits starting at bit offset off of a bitvector
 NTC_HD uint64_t window1(const uint64_t *w, uint32_t off) {
@@ -663,19 +677,22 @@ NTC_HD void store_entry(Entry *E, uint32_t i, uint32_t p, uint32_t v, uint32_t m
 #endif
 }
 
-struct MsLane {
-    const uint64_t *Q;  // packed query stream; this read starts at character qo
+// The batch's packed query stream and position-space entry array: the same for every lane,
+// so they are passed to each call (scalar registers) rather than held per lane.
+struct MsBufs {
+    const uint64_t *Q;
     Entry *E;
-    uint64_t qo;
+};
+
+struct MsLane {
+    uint64_t qo;        // this read starts at character qo of Q; its entries at E + qo
     uint64_t qw;        // query characters [qb, qb + 32) of this read, cached
     uint32_t qb;
     uint32_t len, p, d, l, r, j, ne, mode, hi, lo, l1, r1, bl, bR;
     bool try_run;
 
-    NTC_HD void start(const DevIndex &ix, const uint64_t *Q_, uint64_t qo_, Entry *E_, uint32_t len_) {
-        Q = Q_;
+    NTC_HD void start(const DevIndex &ix, uint64_t qo_, uint32_t len_) {
         qo = qo_;
-        E = E_;
         len = len_;
         qw = 0;
         qb = 0xFFFFFFFFu;
@@ -684,7 +701,8 @@ struct MsLane {
         hi = kScanW;  // SCAN width cap (hi is free while scanning)
         try_run = false;
     }
-    NTC_HD void window(uint32_t from) {
+    NTC_HD void window(const MsBufs &b, uint32_t from) {
+        const uint64_t *Q = b.Q;
         qb = from;
         NTC_TOUCH(kTrQ, Q + ((qo + from) >> 5));
         NTC_TOUCH(kTrQ, Q + ((qo + from) >> 5) + 1);
@@ -703,9 +721,9 @@ struct MsLane {
             try_run = j != 0xFFFFFFFFu;
         }
     }
-    NTC_HD int commit(const DevIndex &ix, uint32_t nl, uint32_t nr, uint32_t nd) {
+    NTC_HD int commit(const DevIndex &ix, const MsBufs &b, uint32_t nl, uint32_t nr, uint32_t nd) {
         l = nl; r = nr; d = nd;
-        store_entry(E, ne++, p, l, 1u, d);
+        store_entry(b.E + qo, ne++, p, l, 1u, d);
         p++;
         mode = kModeExt;
         note_single(ix);
@@ -735,8 +753,9 @@ struct MsLane {
         return 0;
     }
     // one unit of work: 1 = read finished, 0 = continue, < 0 = error
-    NTC_HD int step(const DevIndex &ix) {
+    NTC_HD int step(const DevIndex &ix, const MsBufs &b) {
         const uint32_t k = ix.k, U = ix.tab_u;
+        const uint64_t *Q = b.Q;
         if (p >= len) return 1;
         if (try_run) {
             try_run = false;
@@ -762,7 +781,9 @@ struct MsLane {
                 const uint64_t q = qo + p + m;
                 const uint64_t qi = q >> 5;
                 const uint32_t qs = (uint32_t)(q & 31) * 2;
-                const uint64_t w0 = ld_hint<8>(Q + qi), w1 = ld_hint<8>(Q + qi + 1), w2 = ld_hint<8>(Q + qi + 2);
+                uint64_t w0, w1;
+                load_w2(Q + qi, w0, w1);
+                const uint64_t w2 = Q[qi + 2];
                 const uint64_t qa = qs ? ((w0 >> qs) | (w1 << (64 - qs))) : w0;
                 const uint64_t qb2 = qs ? ((w1 >> qs) | (w2 << (64 - qs))) : w1;
                 const uint64_t xa = qa ^ pa, xb = qb2 ^ pb;
@@ -781,13 +802,13 @@ struct MsLane {
                 if (lim < 64) break;
             }
             if (m > 0) {
-                store_entry(E, ne++, p, j + 1, m, (d + 1 < k ? d + 1 : k) | kRunTag);
+                store_entry(b.E + qo, ne++, p, j + 1, m, (d + 1 < k ? d + 1 : k) | kRunTag);
                 p += m;
                 j += m;
                 d = d + m < k ? d + m : k;
                 if (p >= len) return 1;
                 // the run broke at p (mostly a sequencing error): table first
-                window(p + 1 - U);
+                window(b, p + 1 - U);
                 mode = kModeBrk;
                 return 0;
             }
@@ -797,7 +818,7 @@ struct MsLane {
             // pair (U - 1, U), so test it directly with U - 1's full entry
             mode = kModeScan;
             if (len >= U + 1) {
-                window(0);
+                window(b, 0);
                 NTC_TOUCH(kTrTabU, ix.tab + tab_base(U) + key_at(U - 1, U));
                 NTC_TOUCH(kTrBits, ix.tab_bits + (key_at(U, U) >> 5));
                 const uint2 te = load2_stream(ix.tab + tab_base(U) + key_at(U - 1, U));
@@ -819,7 +840,7 @@ struct MsLane {
             // p - 1 is short, or p = 0); positions < U - 1 are short by length
             if (p < U - 1) p = U - 1;
             if (p + 1 >= len) { p = len; return 1; }
-            if (!covers(p + 1 - U, p + 1)) window(p + 1 - U);
+            if (!covers(p + 1 - U, p + 1)) window(b, p + 1 - U);
             uint32_t W = qb + 32 - p;
             if (W > hi) W = hi;
             if (W > len - p) W = len - p;
@@ -935,7 +956,7 @@ struct MsLane {
             NTC_TOUCH(kTrTabU, ix.tab + tab_base(U) + key_at(x, U));
             return enter_pair(ix, x, load2_stream(ix.tab + tab_base(U) + key_at(x, U)));
         }
-        if (!covers(p + 1 - U, p)) window(p + 1 - U);
+        if (!covers(p + 1 - U, p)) window(b, p + 1 - U);
         if (mode == kModeBrk) {
             NTC_TOUCH(kTrTabU, ix.tab + tab_base(U) + key_at(p, U));
             NTC_TOUCH(kTrColex, ix.colex_at + j);
@@ -956,14 +977,14 @@ struct MsLane {
             const uint2 te = load2_stream(ix.tab + tab_base(U) + key_at(p, U));  // for a failure
             uint32_t nl, nr;
             extend(ix, c, l, r, nl, nr);
-            if (nl < nr) return commit(ix, nl, nr, d + 1 < k ? d + 1 : k);
+            if (nl < nr) return commit(ix, b, nl, nr, d + 1 < k ? d + 1 : k);
             if (!tab_long(te)) {  // p is short: table-determined, scan on
                 skip_short(te.y & 0xFFu, U);
                 return p >= len ? 1 : 0;
             }
             uint32_t tl, tr, tj;
             tab_interval(ix, te, tl, tr, tj);
-            if (d == U) return commit(ix, tl, tr, U);  // t* = U - 1
+            if (d == U) return commit(ix, b, tl, tr, U);  // t* = U - 1
             lo = U - 1; bl = tl; bR = tr;  // ext(I_{U-1}, c) = the U-mer's interval
             hi = d - 1;
             mode = kModeP1;
@@ -977,12 +998,12 @@ struct MsLane {
         uint32_t el, er;
         extend(ix, c, ql, qr, el, er);
         if (el < er) {
-            if (p1) return commit(ix, el, er, t + 1);
+            if (p1) return commit(ix, b, el, er, t + 1);
             lo = t; bl = el; bR = er;
         } else {
             hi = t; l1 = ql; r1 = qr;
         }
-        if (hi - lo <= 1) return commit(ix, bl, bR, lo + 1);
+        if (hi - lo <= 1) return commit(ix, b, bl, bR, lo + 1);
         mode = kModeBs;
         return 0;
     }

@@ -163,6 +163,7 @@ __global__ __launch_bounds__(256, NTC_MS_WAVES) void k_ms4(Enc4Args a) {
     uint64_t pool_lo = 0, pool_hi = 0;
     bool exhausted = false, idle = true;
     uint64_t rd = 0;
+    const MsBufs bufs{a.Q, a.E};
     MsLane st;
     for (;;) {
         // ---- hand idle lanes the next reads (wave-uniform control flow) ----------------
@@ -186,7 +187,7 @@ __global__ __launch_bounds__(256, NTC_MS_WAVES) void k_ms4(Enc4Args a) {
                 idle = false;
                 const uint64_t b = a.offs[rd], e = a.offs[rd + 1];
                 const uint64_t P = b - o0;
-                st.start(a.ix, a.Q, P, a.E + P, (uint32_t)(e - b));
+                st.start(a.ix, P, (uint32_t)(e - b));
                 if (e <= b) {  // empty read (EncodeError, encode.rs:133-135) or bad offsets
                     atomicMin(a.status, (unsigned long long)((rd << 8) | (uint64_t)(e == b ? kErrEmptyRead : kErrFormat)));
                     a.ne[rd] = 0;
@@ -200,7 +201,7 @@ __global__ __launch_bounds__(256, NTC_MS_WAVES) void k_ms4(Enc4Args a) {
         if (done) break;
         // ---- one unit of work per busy lane --------------------------------------------
         if (!idle) {
-            const int rc = st.step(a.ix);
+            const int rc = st.step(a.ix, bufs);
             if (rc != 0) {
                 if (rc < 0) {
                     atomicMin(a.status, (unsigned long long)((rd << 8) | (uint64_t)(-rc)));

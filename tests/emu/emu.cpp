@@ -135,9 +135,10 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
                 uint32_t ne = 0;
                 if (rc == 0) {
                     trace_phase(0);
-                    ms.start(d, Q.data(), 0, E4.data(), len);
+                    ms.start(d, 0, len);
+                    const MsBufs bufs{Q.data(), E4.data()};
                     for (;;) {
-                        int st = ms.step(d);
+                        int st = ms.step(d, bufs);
                         if (st < 0) { rc = st; break; }
                         if (st == 1) break;
                     }
