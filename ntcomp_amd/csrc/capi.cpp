@@ -55,6 +55,7 @@ struct ntc_ctx {
     int num_cus = 0;
     Enc4Args last4{};
     uint32_t tab_u_opt = 0;  // suffix-table depth for the next upload (0 = default_tab_u)
+    int pair_bytes_opt = 1;  // build the SCAN pair bytes at the next upload (0: bitmap tests, A/B)
     void *o2_zeroed = nullptr;  // WS_O2 buffer known to be all zero (k_dec_expand re-zeroes it)
     uint64_t o2_zeroed_bytes = 0;
     uint64_t n_paths = 0, path_text_len = 0;
@@ -495,6 +496,13 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     d.tab_u = U;
     d.tab_pos = (has_paths && U >= dv.t_jump && n < (1ULL << 31)) ? 1u : 0u;
     launch_tab_build(d, U, (uint2 *)d_tab, (uint32_t *)d_bits, F, (uint32_t *)d_fbits, ctx->stream);
+    d.pair_b = nullptr;
+    if (ctx->pair_bytes_opt) {
+        void *d_pair;
+        if ((rc = dalloc((pair_bytes_count(U) + 3) / 4 * 4, &d_pair))) return rc;
+        launch_pair_bytes((const uint32_t *)d_bits, U, (uint8_t *)d_pair, ctx->stream);
+        d.pair_b = (const uint8_t *)d_pair;
+    }
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     ctx->n_paths = n_paths;
@@ -510,6 +518,11 @@ int ntc_ctx_set_option(ntc_ctx *ctx, const char *key, int64_t value) {
         if (value < 0 || value > (int64_t)kTabMaxU)
             return set_err(ctx, NTC_ERR_INVALID_ARG, "tab_u must be 0 (default) or 1..14");
         ctx->tab_u_opt = (uint32_t)value;
+        return NTC_OK;
+    }
+    if (std::strcmp(key, "pair_bytes") == 0) {  // applies to the next ntc_index_upload
+        if (value != 0 && value != 1) return set_err(ctx, NTC_ERR_INVALID_ARG, "pair_bytes must be 0 or 1");
+        ctx->pair_bytes_opt = (int)value;
         return NTC_OK;
     }
     if (std::strcmp(key, "max_pass_bases") == 0) {  // device workspace ~40 B per base of a pass
@@ -530,6 +543,7 @@ int ntc_ctx_get_option(const ntc_ctx *ctx, const char *key, int64_t *value) {
     if (!ctx || !key || !value) return NTC_ERR_INVALID_ARG;
     if (std::strcmp(key, "encode_variant") == 0) *value = ctx->encode_variant;
     else if (std::strcmp(key, "tab_u") == 0) *value = ctx->has_index ? ctx->dix.tab_u : ctx->tab_u_opt;
+    else if (std::strcmp(key, "pair_bytes") == 0) *value = ctx->has_index ? (ctx->dix.pair_b != nullptr) : ctx->pair_bytes_opt;
     else if (std::strcmp(key, "n_paths") == 0) *value = (int64_t)ctx->n_paths;
     else if (std::strcmp(key, "path_text_len") == 0) *value = (int64_t)ctx->path_text_len;
     else if (std::strcmp(key, "path_hash") == 0) {  // test hook: derived.h path_cover_hash of the device cover

@@ -79,6 +79,7 @@ struct DevIndex {
     const uint32_t *tab_bits;     // bit key of level tab_u: that U-mer is present (long)
     const uint32_t *filt_bits;    // presence bits of level filt_f = U - 2 (L2-resident), or null
     uint32_t filt_f;              // 0: no filter
+    const uint8_t *pair_b;        // pair byte of each (U-1)-mer (see pair_byte), or null
     uint32_t tab_pos;             // 1: top-level singleton entries carry the path position
     uint32_t tab_u;               // U: longest tabulated length (1 <= U <= min(k, 14))
     uint32_t absent;              // bit c: no node ends with character c
@@ -379,6 +380,24 @@ NTC_HD void tab_interval(const DevIndex &ix, uint2 te, uint32_t &l, uint32_t &r,
     }
 }
 
+// Pair byte of the (U-1)-mer M (by key): bit a = the U-mer a.M is present, bit 4 + c = the
+// U-mer M.c is present.  For M = the (U-1)-mer ending at y, a = the character before M and
+// c = the one after it, one byte says whether the U-mers ending at y AND y + 1 are present
+// (one cache line per SCAN pair test instead of two bitmap lines).  4^(U-1) bytes.
+NTC_HD uint64_t pair_bytes_count(uint32_t U) { return 1ULL << (2 * (U - 1)); }
+NTC_HD uint32_t pair_byte(const uint32_t *bits, uint32_t U, uint64_t M) {
+    uint32_t b = 0;
+    for (uint32_t a = 0; a < 4; a++) {
+        const uint64_t key = a | (M << 2);
+        b |= ((bits[key >> 5] >> (key & 31)) & 1u) << a;
+    }
+    for (uint32_t c = 0; c < 4; c++) {
+        const uint64_t key = M | ((uint64_t)c << (2 * (U - 1)));
+        b |= ((bits[key >> 5] >> (key & 31)) & 1u) << (4 + c);
+    }
+    return b;
+}
+
 // presence bits of one level: bit key of word key / 32
 NTC_HD uint32_t tab_bits_word(const uint2 *top, uint64_t w) {
     uint32_t b = 0;
@@ -438,10 +457,19 @@ struct BaseReader {
 
 enum : uint32_t { kModeScan = 0, kModeExt = 1, kModeP1 = 2, kModeBs = 3, kModeBrk = 4, kModeFirst = 5 };
 constexpr uint32_t kScanW = 16;      // presence probes per SCAN unit (U + kScanW - 1 <= 32)
+#ifndef NTC_EXTRA_ENT
+#define NTC_EXTRA_ENT 0  // bit mask: 1 entry for a pair start x, 2 entries for table-short break positions
+#endif
 #ifndef NTC_SCAN_MODE
 #define NTC_SCAN_MODE 0  // 2: SCAN loads the first candidate pair's table entry directly
 #endif
 constexpr uint32_t kScanExact = 4;   // filter candidates tested exactly per SCAN
+#ifndef NTC_RUN_EAGER
+#define NTC_RUN_EAGER 1  // run loop: both 32-char halves' loads issued together
+#endif
+#ifndef NTC_PAIR_TESTS
+#define NTC_PAIR_TESTS 2  // candidate pairs tested per SCAN with pair bytes
+#endif
 
 // ======================================================================================
 // Matching statistics as RUN-LENGTH entries.  Positions whose U-mer is absent ("short")
@@ -732,16 +760,23 @@ struct MsLane {
     // position p is short with table value m: d_{p+i} <= m + i, so p+1 .. p+U-1-m are
     // short too.  A lone error at p leaves the pair (p + U, p + U + 1): the next SCAN
     // needs m + 2 positions to reach it.
-    NTC_HD void skip_short(uint32_t m, uint32_t U) {
+    NTC_HD void skip_short(const MsBufs &b, uint2 te, uint32_t U) {
+        const uint32_t m = te.y & 0xFFu;
+#if NTC_EXTRA_ENT & 2
+        store_entry(b.E + qo, ne++, p, te.x, 1u, m);  // table-determined; saves the parse a lookup
+#endif
         p += U - m;
         mode = kModeScan;
         hi = m + 2 < kScanW ? m + 2 : kScanW;
     }
     // x and x + 1 are long, x's predecessor short: walk from x (d = U, table interval)
-    NTC_HD int enter_pair(const DevIndex &ix, uint32_t x, uint2 te) {
+    NTC_HD int enter_pair(const DevIndex &ix, const MsBufs &b, uint32_t x, uint2 te) {
         uint32_t jj;
         tab_interval(ix, te, l, r, jj);
         d = ix.tab_u;
+#if NTC_EXTRA_ENT & 1
+        store_entry(b.E + qo, ne++, x, l, 1u, d);  // table-determined; saves the parse a lookup
+#endif
         p = x + 1;
         mode = kModeExt;
         if (ix.tab_pos) {  // the table already holds the path position (d = U >= t_jump)
@@ -790,6 +825,13 @@ struct MsLane {
                 uint32_t la = xa ? ctz64(xa) >> 1 : 32u;
                 const uint32_t ia = ~va ? (uint32_t)__builtin_ctz(~va) : 32u;
                 if (ia < la) la = ia;
+#if NTC_RUN_EAGER
+                // second half computed unconditionally: its loads issue with the first half's
+                uint32_t lb = xb ? ctz64(xb) >> 1 : 32u;
+                const uint32_t ib = ~vb ? (uint32_t)__builtin_ctz(~vb) : 32u;
+                if (ib < lb) lb = ib;
+                uint32_t lim = la == 32 ? 32 + lb : la;
+#else
                 uint32_t lim = la;
                 if (la == 32) {
                     uint32_t lb = xb ? ctz64(xb) >> 1 : 32u;
@@ -797,6 +839,7 @@ struct MsLane {
                     if (ib < lb) lb = ib;
                     lim = 32 + lb;
                 }
+#endif
                 if (len - p - m < lim) lim = len - p - m;
                 m += lim;
                 if (lim < 64) break;
@@ -825,6 +868,9 @@ struct MsLane {
                 const uint64_t k2 = key_at(U, U);
                 const uint32_t b2 = (ix.tab_bits[k2 >> 5] >> (k2 & 31)) & 1u;
                 if (!tab_long(te)) {
+#if NTC_EXTRA_ENT & 2
+                    store_entry(b.E + qo, ne++, U - 1, te.x, 1u, te.y & 0xFFu);
+#endif
                     p = U - 1 + U - (te.y & 0xFFu);  // d_{U-1+i} <= m + i
                     return p >= len ? 1 : 0;
                 }
@@ -832,7 +878,7 @@ struct MsLane {
                     p = U + 1;  // U is short
                     return p >= len ? 1 : 0;
                 }
-                return enter_pair(ix, U - 1, te);
+                return enter_pair(ix, b, U - 1, te);
             }
         }
         if (mode == kModeScan) {
@@ -852,14 +898,66 @@ struct MsLane {
             if (ix.filt_f) {
                 const uint32_t F = ix.filt_f;
                 uint32_t fm = 0;  // bit i: F-mer ending at p - 2 + i is present
+                // every load unconditional (slots past W + 2 repeat slot 0), all issued before
+                // the first use: one L2 round trip, not W + 2 dependent ones
+                uint32_t fw[kScanW + kFiltGap];
 #pragma unroll
-                for (uint32_t i = 0; i < kScanW + kFiltGap; i++)
-                    if (i < W + kFiltGap) {
-                        const uint64_t fk = (qw >> (2 * (p + 1 - U + i - qb))) & ((1ULL << (2 * F)) - 1);
-                        NTC_TOUCH(kTrFilt, ix.filt_bits + (fk >> 5));
-                        fm |= ((ix.filt_bits[fk >> 5] >> (fk & 31)) & 1u) << i;
-                    }
+                for (uint32_t i = 0; i < kScanW + kFiltGap; i++) {
+                    const uint32_t ii = i < W + kFiltGap ? i : 0u;
+                    const uint64_t fk = (qw >> (2 * (p + 1 - U + ii - qb))) & ((1ULL << (2 * F)) - 1);
+                    if (i == ii) NTC_TOUCH(kTrFilt, ix.filt_bits + (fk >> 5));
+                    fw[i] = ix.filt_bits[fk >> 5];
+                }
+#pragma unroll
+                for (uint32_t i = 0; i < kScanW + kFiltGap; i++) {
+                    const uint32_t ii = i < W + kFiltGap ? i : 0u;
+                    const uint32_t fk = (uint32_t)(qw >> (2 * (p + 1 - U + ii - qb)));
+                    fm |= ((fw[i] >> (fk & 31)) & 1u) << i;
+                }
+                fm &= (1u << (W + kFiltGap)) - 1u;
                 cand &= fm & (fm >> 1) & (fm >> kFiltGap);  // all three F-mers of the U-mer
+            }
+            if (ix.pair_b) {
+                // exact test of the first candidate PAIRS (y and y + 1 both pass the filter),
+                // one pair byte each; the first pair that is long-long is the SCAN's answer
+                const uint32_t cp = cand & (cand >> 1);
+                uint32_t untested = cp;
+#pragma unroll
+                for (uint32_t t = 0; t < NTC_PAIR_TESTS; t++) untested &= untested - 1;
+                const uint32_t tested = cp ^ untested;
+                // one unconditional load per slot (a missing pair repeats position p), all
+                // issued before the first use
+                uint32_t slot[NTC_PAIR_TESTS], pbv[NTC_PAIR_TESTS];
+                uint32_t rem = tested;
+#pragma unroll
+                for (uint32_t t = 0; t < NTC_PAIR_TESTS; t++) {
+                    slot[t] = rem ? (uint32_t)__builtin_ctz(rem) : 0u;
+                    rem &= rem - 1;
+                    const uint64_t M = key_at(p + slot[t], U - 1);
+                    if ((tested >> slot[t]) & 1u) NTC_TOUCH(kTrBits, ix.pair_b + M);
+                    pbv[t] = ix.pair_b[M];
+                }
+                uint32_t hit = 0;
+#pragma unroll
+                for (uint32_t t = 0; t < NTC_PAIR_TESTS; t++) {
+                    const uint32_t y = p + slot[t];
+                    const uint32_t a = (uint32_t)(qw >> (2 * (y + 1 - U - qb))) & 3u;
+                    const uint32_t c = (uint32_t)(qw >> (2 * (y + 1 - qb))) & 3u;
+                    hit |= ((pbv[t] >> a) & (pbv[t] >> (4 + c)) & 1u) << slot[t];
+                }
+                hit &= tested;
+                if (hit) {
+                    const uint32_t x = p + (uint32_t)__builtin_ctz(hit);  // short predecessor
+                    NTC_TOUCH(kTrTabU, ix.tab + tab_base(U) + key_at(x, U));
+                    return enter_pair(ix, b, x, load2_stream(ix.tab + tab_base(U) + key_at(x, U)));
+                }
+                if (untested) {  // resume at the first untested candidate pair
+                    p += (uint32_t)__builtin_ctz(untested);
+                    return 0;
+                }
+                if (p + W >= len) { p = len; return 1; }
+                p += W - ((cand >> (W - 1)) & 1u);  // a passing last position may start a pair
+                return 0;
             }
 #if NTC_SCAN_MODE == 2
             if (ix.filt_f) {
@@ -879,14 +977,14 @@ struct MsLane {
                 const uint32_t b1 = (ld_hint<2>(ix.tab_bits + (k1 >> 5)) >> (k1 & 31)) & 1u;
                 if (!tab_long(te)) {  // x short: d_{x+i} <= m + i
                     p = x;
-                    skip_short(te.y & 0xFFu, U);
+                    skip_short(b, te, U);
                     return p >= len ? 1 : 0;
                 }
                 if (!b1) {  // x long, x + 1 short
                     p = x + 2;
                     return p >= len ? 1 : 0;
                 }
-                return enter_pair(ix, x, te);
+                return enter_pair(ix, b, x, te);
             }
 #endif
 #if NTC_SCAN_MODE == 1
@@ -924,7 +1022,7 @@ struct MsLane {
                 }
                 const uint32_t x = p + (uint32_t)__builtin_ctz(pairs);
                 NTC_TOUCH(kTrTabU, ix.tab + tab_base(U) + key_at(x, U));
-                return enter_pair(ix, x, load2_stream(ix.tab + tab_base(U) + key_at(x, U)));
+                return enter_pair(ix, b, x, load2_stream(ix.tab + tab_base(U) + key_at(x, U)));
             }
 #endif
             // exact test of the first kScanExact candidates only: the pair is almost always
@@ -954,16 +1052,16 @@ struct MsLane {
             }
             const uint32_t x = p + (uint32_t)__builtin_ctz(pairs);  // long, short predecessor
             NTC_TOUCH(kTrTabU, ix.tab + tab_base(U) + key_at(x, U));
-            return enter_pair(ix, x, load2_stream(ix.tab + tab_base(U) + key_at(x, U)));
+            return enter_pair(ix, b, x, load2_stream(ix.tab + tab_base(U) + key_at(x, U)));
         }
         if (!covers(p + 1 - U, p)) window(b, p + 1 - U);
         if (mode == kModeBrk) {
             NTC_TOUCH(kTrTabU, ix.tab + tab_base(U) + key_at(p, U));
-            NTC_TOUCH(kTrColex, ix.colex_at + j);
             const uint2 te = load2_stream(ix.tab + tab_base(U) + key_at(p, U));
+            NTC_TOUCH(kTrColex, ix.colex_at + j);
             const uint32_t v = ix.colex_at[j] & 0x7FFFFFFFu;  // node before p, for a long p
             if (!tab_long(te)) {
-                skip_short(te.y & 0xFFu, U);
+                skip_short(b, te, U);
                 return p >= len ? 1 : 0;
             }
             l = v;
@@ -979,7 +1077,7 @@ struct MsLane {
             extend(ix, c, l, r, nl, nr);
             if (nl < nr) return commit(ix, b, nl, nr, d + 1 < k ? d + 1 : k);
             if (!tab_long(te)) {  // p is short: table-determined, scan on
-                skip_short(te.y & 0xFFu, U);
+                skip_short(b, te, U);
                 return p >= len ? 1 : 0;
             }
             uint32_t tl, tr, tj;

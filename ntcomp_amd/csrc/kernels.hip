@@ -154,7 +154,7 @@ __device__ __forceinline__ void parse_one(const Enc4Args &a, uint64_t r) {
 }
 
 #ifndef NTC_MS_WAVES
-#define NTC_MS_WAVES 8  // waves per SIMD k_ms4 is compiled for (SGPR <= 80, VGPR <= 64)
+#define NTC_MS_WAVES 6  // waves per SIMD k_ms4 is compiled for (VGPR <= 80: the batched SCAN loads fit unspilled)
 #endif
 __global__ __launch_bounds__(256, NTC_MS_WAVES) void k_ms4(Enc4Args a) {
     const uint32_t lane = threadIdx.x & 63;
@@ -640,6 +640,20 @@ __global__ __launch_bounds__(256) void k_tab_bits(const uint2 *top, uint32_t U, 
         for (uint32_t key = 0; key < (1u << (2 * U)); key++) b |= (uint32_t)tab_long(top[key]) << key;
         bits[0] = b;
     }
+}
+
+__global__ __launch_bounds__(256) void k_pair_bytes(const uint32_t *bits, uint32_t U, uint32_t *out) {
+    const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;  // four pair bytes per thread
+    const uint64_t cnt = pair_bytes_count(U);
+    if (4 * w >= cnt) return;
+    uint32_t v = 0;
+    for (uint32_t i = 0; i < 4 && 4 * w + i < cnt; i++) v |= pair_byte(bits, U, 4 * w + i) << (8 * i);
+    out[w] = v;
+}
+
+void launch_pair_bytes(const uint32_t *bits, uint32_t U, uint8_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_pair_bytes, grid_for((pair_bytes_count(U) + 3) / 4), dim3(256), 0, s, bits, U,
+                       (uint32_t *)out);
 }
 
 void launch_tab_build(const DevIndex &ix, uint32_t U, uint2 *tab, uint32_t *bits, uint32_t F, uint32_t *fbits,

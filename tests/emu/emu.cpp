@@ -4,6 +4,7 @@
 // It lets the -m "not gpu" suite check the kernel ALGORITHM against the oracle on a
 // machine without a GPU.  It is not part of libntcomp_gpu.so and no product path loads it.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -57,7 +58,8 @@ inline void trace_read_done() {}
 
 namespace {
 bool load(const ntc_index_view *v, HostIndex &hx, Derived &dv, std::vector<WalkEntry> &walk, DevIndex &d,
-          std::vector<uint2> &tab, std::vector<uint32_t> &bits, std::vector<uint32_t> &fbits, uint32_t tab_u = 0) {
+          std::vector<uint2> &tab, std::vector<uint32_t> &bits, std::vector<uint32_t> &fbits,
+          std::vector<uint8_t> &pairb, uint32_t tab_u = 0) {
     hx.n = v->n_nodes;
     hx.k = v->k;
     uint64_t nw = (hx.n + 63) / 64;
@@ -80,6 +82,13 @@ bool load(const ntc_index_view *v, HostIndex &hx, Derived &dv, std::vector<WalkE
     d.filt_f = fbits.empty() ? 0u : filter_level(U);
     d.filt_bits = fbits.empty() ? nullptr : fbits.data();
     d.tab_u = U;
+    d.pair_b = nullptr;
+    const char *pe = getenv("NTC_EMU_PAIR_BYTES");
+    if (!pe || atoi(pe) != 0) {
+        pairb.resize(pair_bytes_count(U));
+        for (uint64_t M = 0; M < pairb.size(); M++) pairb[M] = (uint8_t)pair_byte(bits.data(), U, M);
+        d.pair_b = pairb.data();
+    }
     return true;
 }
 }  // namespace
@@ -92,7 +101,8 @@ extern "C" int emu_path_cover(const ntc_index_view *v, uint64_t *out) {
     DevIndex d{};
     std::vector<uint2> tab;
     std::vector<uint32_t> bits, fbits;
-    if (!load(v, hx, dv, walk, d, tab, bits, fbits, 1)) return 1;
+    std::vector<uint8_t> pairb;
+    if (!load(v, hx, dv, walk, d, tab, bits, fbits, pairb, 1)) return 1;
     if (!dv.has_paths) return 2;
     out[0] = path_cover_hash(dv.pstream.data(), dv.colex_at.data(), dv.pos_of_node.data(), dv.puniq.data(), hx.n,
                              hx.k, dv.tlen);
@@ -109,8 +119,9 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
     std::vector<WalkEntry> walk;
     std::vector<uint2> tab;
     std::vector<uint32_t> bits, fbits;
+    std::vector<uint8_t> pairb;
     DevIndex d;
-    if (!load(v, hx, dv, walk, d, tab, bits, fbits, (uint32_t)tab_u)) return NTC_ERR_FORMAT;
+    if (!load(v, hx, dv, walk, d, tab, bits, fbits, pairb, (uint32_t)tab_u)) return NTC_ERR_FORMAT;
     if (!use_paths) d.has_paths = 0;
     *bad = -1;
     uint64_t tiles = (n_reads + 63) / 64, total = 0;
@@ -186,8 +197,9 @@ extern "C" int emu_decode(const ntc_index_view *v, const uint64_t *recs, uint64_
     std::vector<WalkEntry> walk;
     std::vector<uint2> tab;
     std::vector<uint32_t> bits, fbits;
+    std::vector<uint8_t> pairb;
     DevIndex d;
-    if (!load(v, hx, dv, walk, d, tab, bits, fbits, 1)) return NTC_ERR_FORMAT;
+    if (!load(v, hx, dv, walk, d, tab, bits, fbits, pairb, 1)) return NTC_ERR_FORMAT;
     // the kernels' decode: per record, 2-bit codes via CodeWriter, then ASCII (k_dec_rec +
     // k_dec_expand); a read's records are consumed last to first (lib.rs:266)
     std::vector<uint64_t> starts, lens(n), E(n + 1, 0);

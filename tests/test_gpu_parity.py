@@ -338,3 +338,27 @@ def test_gpu_host_api_splits_large_batches_into_passes(ctx):
             assert e.value.code == 2 and e.value.bad_read == 2500, mp
     finally:
         ctx.set_option("max_pass_bases", default)
+
+
+@pytest.mark.parametrize("pair_bytes", [1, 0])
+@pytest.mark.parametrize("k,tab_u", [(91, 0), (31, 12), (21, 5)])
+def test_gpu_scan_exact_test_paths(ctx, k, tab_u, pair_bytes):
+    """SCAN's exact test through the pair bytes (default) and through the level-U bitmap
+    (pair_bytes = 0): identical records, bit-exact vs the oracle, for filtered (U >= 12)
+    and unfiltered table depths."""
+    genome = nt.synth_genome(500 + k, 1_000_000)
+    ix = nt.Index.build([genome.tobytes()], k, threads=8)
+    ctx.set_option("pair_bytes", pair_bytes)
+    ctx.set_option("tab_u", tab_u)
+    try:
+        ctx.upload(ix)
+        assert ctx.get_option("pair_bytes") == pair_bytes
+        n, L = 20_000, 150
+        reads = nt.synth_reads(genome, 9, 0, n, L, 15_000, threads=8)
+        offs = np.arange(0, n * L + 1, L, dtype=np.uint64)
+        exp, eoff = OracleIndex(ix.n, k, ix.rows, ix.C, ix.lcs).encode(reads, offs)
+        got, goff = ctx.encode(reads, offs)
+        assert np.array_equal(goff, eoff) and np.array_equal(got, exp)
+    finally:
+        ctx.set_option("pair_bytes", 1)
+        ctx.set_option("tab_u", 0)
