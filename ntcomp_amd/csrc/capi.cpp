@@ -476,6 +476,7 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     d.t_jump = dv.t_jump;
     for (int c = 0; c < 5; c++) d.C[c] = dv.C[c];
     d.has_paths = has_paths ? 1u : 0u;
+    d.path_len = has_paths ? (uint32_t)tlen : 0u;
     d.pstream = (const uint4 *)d_pstream;
     d.colex_at = (const uint32_t *)d_colex_at;
     d.pos_of_node = (const uint32_t *)d_pos;
@@ -496,12 +497,12 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     d.tab_u = U;
     d.tab_pos = (has_paths && U >= dv.t_jump && n < (1ULL << 31)) ? 1u : 0u;
     launch_tab_build(d, U, (uint2 *)d_tab, (uint32_t *)d_bits, F, (uint32_t *)d_fbits, ctx->stream);
-    d.pair_b = nullptr;
+    d.pair_w = nullptr;
     if (ctx->pair_bytes_opt) {
         void *d_pair;
-        if ((rc = dalloc((pair_bytes_count(U) + 3) / 4 * 4, &d_pair))) return rc;
-        launch_pair_bytes((const uint32_t *)d_bits, U, (uint8_t *)d_pair, ctx->stream);
-        d.pair_b = (const uint8_t *)d_pair;
+        if ((rc = dalloc((pair_words_count(U) + 1) / 2 * 4, &d_pair))) return rc;
+        launch_pair_words((const uint2 *)d_tab + tab_base(U), U, (uint16_t *)d_pair, ctx->stream);
+        d.pair_w = (const uint16_t *)d_pair;
     }
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -543,7 +544,7 @@ int ntc_ctx_get_option(const ntc_ctx *ctx, const char *key, int64_t *value) {
     if (!ctx || !key || !value) return NTC_ERR_INVALID_ARG;
     if (std::strcmp(key, "encode_variant") == 0) *value = ctx->encode_variant;
     else if (std::strcmp(key, "tab_u") == 0) *value = ctx->has_index ? ctx->dix.tab_u : ctx->tab_u_opt;
-    else if (std::strcmp(key, "pair_bytes") == 0) *value = ctx->has_index ? (ctx->dix.pair_b != nullptr) : ctx->pair_bytes_opt;
+    else if (std::strcmp(key, "pair_bytes") == 0) *value = ctx->has_index ? (ctx->dix.pair_w != nullptr) : ctx->pair_bytes_opt;
     else if (std::strcmp(key, "n_paths") == 0) *value = (int64_t)ctx->n_paths;
     else if (std::strcmp(key, "path_text_len") == 0) *value = (int64_t)ctx->path_text_len;
     else if (std::strcmp(key, "path_hash") == 0) {  // test hook: derived.h path_cover_hash of the device cover

@@ -315,6 +315,7 @@ DevIndex host_dev_index(const HostIndex &ix, const Derived &dv, const std::vecto
     d.t_jump = dv.t_jump;
     for (int c = 0; c < 5; c++) d.C[c] = dv.C[c];
     d.has_paths = dv.has_paths ? 1u : 0u;
+    d.path_len = dv.has_paths ? (uint32_t)(dv.colex_at.size() - 8) : 0u;
     d.pstream = dv.pstream.empty() ? nullptr : dv.pstream.data();
     d.colex_at = dv.colex_at.empty() ? nullptr : dv.colex_at.data();
     d.pos_of_node = dv.pos_of_node.empty() ? nullptr : dv.pos_of_node.data();

@@ -79,7 +79,8 @@ struct DevIndex {
     const uint32_t *tab_bits;     // bit key of level tab_u: that U-mer is present (long)
     const uint32_t *filt_bits;    // presence bits of level filt_f = U - 2 (L2-resident), or null
     uint32_t filt_f;              // 0: no filter
-    const uint8_t *pair_b;        // pair byte of each (U-1)-mer (see pair_byte), or null
+    const uint16_t *pair_w;       // pair word of each (U-1)-mer (see pair_word), or null
+    uint32_t path_len;            // path text length (has_paths): path positions are < path_len
     uint32_t tab_pos;             // 1: top-level singleton entries carry the path position
     uint32_t tab_u;               // U: longest tabulated length (1 <= U <= min(k, 14))
     uint32_t absent;              // bit c: no node ends with character c
@@ -380,22 +381,25 @@ NTC_HD void tab_interval(const DevIndex &ix, uint2 te, uint32_t &l, uint32_t &r,
     }
 }
 
-// Pair byte of the (U-1)-mer M (by key): bit a = the U-mer a.M is present, bit 4 + c = the
-// U-mer M.c is present.  For M = the (U-1)-mer ending at y, a = the character before M and
-// c = the one after it, one byte says whether the U-mers ending at y AND y + 1 are present
-// (one cache line per SCAN pair test instead of two bitmap lines).  4^(U-1) bytes.
-NTC_HD uint64_t pair_bytes_count(uint32_t U) { return 1ULL << (2 * (U - 1)); }
-NTC_HD uint32_t pair_byte(const uint32_t *bits, uint32_t U, uint64_t M) {
-    uint32_t b = 0;
+// Pair word of the (U-1)-mer M (by key), from level U of the suffix table:
+//   bit a      the U-mer a.M is present (long),
+//   bit 4 + c  the U-mer M.c is present,
+//   bit 8 + a  the U-mer a.M is present and its interval is a single node.
+// For M = the (U-1)-mer ending at y, a = the character before M and c = the one after it,
+// one word says whether the U-mers ending at y AND y + 1 are present (one cache line per
+// SCAN pair test instead of two bitmap lines).  4^(U-1) x 2 bytes.
+NTC_HD uint64_t pair_words_count(uint32_t U) { return 1ULL << (2 * (U - 1)); }
+NTC_HD bool tab_single(uint2 e) {  // a long entry whose interval is one node
+    return tab_long(e) && ((e.y & kTabPos) ? true : e.y == e.x + 1);
+}
+NTC_HD uint32_t pair_word(const uint2 *top, uint32_t U, uint64_t M) {
+    uint32_t w = 0;
     for (uint32_t a = 0; a < 4; a++) {
-        const uint64_t key = a | (M << 2);
-        b |= ((bits[key >> 5] >> (key & 31)) & 1u) << a;
+        const uint2 e = top[a | (M << 2)];
+        w |= ((uint32_t)tab_long(e) << a) | ((uint32_t)tab_single(e) << (8 + a));
     }
-    for (uint32_t c = 0; c < 4; c++) {
-        const uint64_t key = M | ((uint64_t)c << (2 * (U - 1)));
-        b |= ((bits[key >> 5] >> (key & 31)) & 1u) << (4 + c);
-    }
-    return b;
+    for (uint32_t c = 0; c < 4; c++) w |= (uint32_t)tab_long(top[M | ((uint64_t)c << (2 * (U - 1)))]) << (4 + c);
+    return w;
 }
 
 // presence bits of one level: bit key of word key / 32
@@ -455,17 +459,20 @@ struct BaseReader {
     }
 };
 
-enum : uint32_t { kModeScan = 0, kModeExt = 1, kModeP1 = 2, kModeBs = 3, kModeBrk = 4, kModeFirst = 5 };
+enum : uint32_t { kModeScan = 0, kModeExt = 1, kModeP1 = 2, kModeBs = 3, kModeBrk = 4, kModeFirst = 5, kModeEnter = 6 };
 constexpr uint32_t kScanW = 16;      // presence probes per SCAN unit (U + kScanW - 1 <= 32)
-#ifndef NTC_EXTRA_ENT
-#define NTC_EXTRA_ENT 0  // bit mask: 1 entry for a pair start x, 2 entries for table-short break positions
-#endif
 #ifndef NTC_SCAN_MODE
 #define NTC_SCAN_MODE 0  // 2: SCAN loads the first candidate pair's table entry directly
 #endif
 constexpr uint32_t kScanExact = 4;   // filter candidates tested exactly per SCAN
-#ifndef NTC_RUN_EAGER
-#define NTC_RUN_EAGER 1  // run loop: both 32-char halves' loads issued together
+#ifndef NTC_BRK_PAIR
+#define NTC_BRK_PAIR 1  // run break: long/short from the pair word, not the table entry
+#endif
+#ifndef NTC_GUESS
+#define NTC_GUESS 1  // SCAN after a run break guesses the node along the same path
+#endif
+#ifndef NTC_GUESS_SLACK
+#define NTC_GUESS_SLACK 2  // guess only for x - ge in [U, U + slack] (a lone substitution: x = ge + U)
 #endif
 #ifndef NTC_PAIR_TESTS
 #define NTC_PAIR_TESTS 2  // candidate pairs tested per SCAN with pair bytes
@@ -717,6 +724,8 @@ struct MsLane {
     uint64_t qw;        // query characters [qb, qb + 32) of this read, cached
     uint32_t qb;
     uint32_t len, p, d, l, r, j, ne, mode, hi, lo, l1, r1, bl, bR;
+    uint32_t gj, ge;    // last run break: at position ge, node before it at path position gj (ge = 0: none)
+    uint32_t vfy;       // the next run first verifies the vfy characters ending at node j
     bool try_run;
 
     NTC_HD void start(const DevIndex &ix, uint64_t qo_, uint32_t len_) {
@@ -727,6 +736,7 @@ struct MsLane {
         p = 0; d = 0; l = 0; r = ix.n; j = 0xFFFFFFFFu; ne = 0;
         mode = kModeFirst; lo = l1 = r1 = bl = bR = 0;
         hi = kScanW;  // SCAN width cap (hi is free while scanning)
+        gj = ge = vfy = 0;
         try_run = false;
     }
     NTC_HD void window(const MsBufs &b, uint32_t from) {
@@ -762,9 +772,6 @@ struct MsLane {
     // needs m + 2 positions to reach it.
     NTC_HD void skip_short(const MsBufs &b, uint2 te, uint32_t U) {
         const uint32_t m = te.y & 0xFFu;
-#if NTC_EXTRA_ENT & 2
-        store_entry(b.E + qo, ne++, p, te.x, 1u, m);  // table-determined; saves the parse a lookup
-#endif
         p += U - m;
         mode = kModeScan;
         hi = m + 2 < kScanW ? m + 2 : kScanW;
@@ -774,9 +781,6 @@ struct MsLane {
         uint32_t jj;
         tab_interval(ix, te, l, r, jj);
         d = ix.tab_u;
-#if NTC_EXTRA_ENT & 1
-        store_entry(b.E + qo, ne++, x, l, 1u, d);  // table-determined; saves the parse a lookup
-#endif
         p = x + 1;
         mode = kModeExt;
         if (ix.tab_pos) {  // the table already holds the path position (d = U >= t_jump)
@@ -794,15 +798,17 @@ struct MsLane {
         if (p >= len) return 1;
         if (try_run) {
             try_run = false;
-            uint32_t m = 0;
+            uint32_t m = 0, pre = vfy;
+            vfy = 0;
             for (;;) {
-                // 64 path characters after node j's k-mer, and whether the k-mer ending at
-                // each of them is a node, from three interleaved 32-char groups
-                const uint64_t T = (uint64_t)j + k + m;
+                // 64 path characters after node j's k-mer (from pre characters before its end
+                // when verifying a guessed node), and whether the k-mer ending at each of them
+                // is a node, from three interleaved 32-char groups
+                const uint64_t T = (uint64_t)j + k + m - pre;
                 NTC_TOUCH(kTrPst, ix.pstream + (T >> 5));
                 NTC_TOUCH(kTrPst, ix.pstream + (T >> 5) + 2);
-                NTC_TOUCH(kTrQ, Q + ((qo + p + m) >> 5));
-                NTC_TOUCH(kTrQ, Q + ((qo + p + m) >> 5) + 2);
+                NTC_TOUCH(kTrQ, Q + ((qo + p + m - pre) >> 5));
+                NTC_TOUCH(kTrQ, Q + ((qo + p + m - pre) >> 5) + 2);
                 const uint4 g0 = ld4<4>(ix.pstream + (T >> 5)), g1 = ld4<4>(ix.pstream + (T >> 5) + 1),
                             g2 = ld4<4>(ix.pstream + (T >> 5) + 2);
                 const uint32_t sh = (uint32_t)(T & 31);
@@ -811,9 +817,10 @@ struct MsLane {
                 const uint64_t c2 = (uint64_t)g2.x | ((uint64_t)g2.y << 32);
                 const uint64_t pa = sh ? ((c0 >> (2 * sh)) | (c1 << (64 - 2 * sh))) : c0;
                 const uint64_t pb = sh ? ((c1 >> (2 * sh)) | (c2 << (64 - 2 * sh))) : c1;
-                const uint32_t va = sh ? ((g0.z >> sh) | (g1.z << (32 - sh))) : g0.z;
+                uint32_t va = sh ? ((g0.z >> sh) | (g1.z << (32 - sh))) : g0.z;
+                if (pre) va |= (1u << (pre - 1)) - 1u;  // of the verified k-mers only node j's must exist
                 const uint32_t vb = sh ? ((g1.z >> sh) | (g2.z << (32 - sh))) : g1.z;
-                const uint64_t q = qo + p + m;
+                const uint64_t q = qo + p + m - pre;
                 const uint64_t qi = q >> 5;
                 const uint32_t qs = (uint32_t)(q & 31) * 2;
                 uint64_t w0, w1;
@@ -825,23 +832,18 @@ struct MsLane {
                 uint32_t la = xa ? ctz64(xa) >> 1 : 32u;
                 const uint32_t ia = ~va ? (uint32_t)__builtin_ctz(~va) : 32u;
                 if (ia < la) la = ia;
-#if NTC_RUN_EAGER
                 // second half computed unconditionally: its loads issue with the first half's
                 uint32_t lb = xb ? ctz64(xb) >> 1 : 32u;
                 const uint32_t ib = ~vb ? (uint32_t)__builtin_ctz(~vb) : 32u;
                 if (ib < lb) lb = ib;
                 uint32_t lim = la == 32 ? 32 + lb : la;
-#else
-                uint32_t lim = la;
-                if (la == 32) {
-                    uint32_t lb = xb ? ctz64(xb) >> 1 : 32u;
-                    const uint32_t ib = ~vb ? (uint32_t)__builtin_ctz(~vb) : 32u;
-                    if (ib < lb) lb = ib;
-                    lim = 32 + lb;
+                if (len + pre - p - m < lim) lim = len + pre - p - m;
+                if (lim < pre) {  // the guessed node is not the U-mer's: take it from the table
+                    mode = kModeEnter;
+                    return 0;
                 }
-#endif
-                if (len - p - m < lim) lim = len - p - m;
-                m += lim;
+                m += lim - pre;
+                pre = 0;
                 if (lim < 64) break;
             }
             if (m > 0) {
@@ -850,6 +852,8 @@ struct MsLane {
                 j += m;
                 d = d + m < k ? d + m : k;
                 if (p >= len) return 1;
+                gj = j;
+                ge = p;
                 // the run broke at p (mostly a sequencing error): table first
                 window(b, p + 1 - U);
                 mode = kModeBrk;
@@ -868,9 +872,6 @@ struct MsLane {
                 const uint64_t k2 = key_at(U, U);
                 const uint32_t b2 = (ix.tab_bits[k2 >> 5] >> (k2 & 31)) & 1u;
                 if (!tab_long(te)) {
-#if NTC_EXTRA_ENT & 2
-                    store_entry(b.E + qo, ne++, U - 1, te.x, 1u, te.y & 0xFFu);
-#endif
                     p = U - 1 + U - (te.y & 0xFFu);  // d_{U-1+i} <= m + i
                     return p >= len ? 1 : 0;
                 }
@@ -917,7 +918,7 @@ struct MsLane {
                 fm &= (1u << (W + kFiltGap)) - 1u;
                 cand &= fm & (fm >> 1) & (fm >> kFiltGap);  // all three F-mers of the U-mer
             }
-            if (ix.pair_b) {
+            if (ix.pair_w) {
                 // exact test of the first candidate PAIRS (y and y + 1 both pass the filter),
                 // one pair byte each; the first pair that is long-long is the SCAN's answer
                 const uint32_t cp = cand & (cand >> 1);
@@ -934,20 +935,42 @@ struct MsLane {
                     slot[t] = rem ? (uint32_t)__builtin_ctz(rem) : 0u;
                     rem &= rem - 1;
                     const uint64_t M = key_at(p + slot[t], U - 1);
-                    if ((tested >> slot[t]) & 1u) NTC_TOUCH(kTrBits, ix.pair_b + M);
-                    pbv[t] = ix.pair_b[M];
+                    if ((tested >> slot[t]) & 1u) NTC_TOUCH(kTrBits, ix.pair_w + M);
+                    pbv[t] = ix.pair_w[M];
                 }
-                uint32_t hit = 0;
+                uint32_t hit = 0, single = 0;
 #pragma unroll
                 for (uint32_t t = 0; t < NTC_PAIR_TESTS; t++) {
                     const uint32_t y = p + slot[t];
                     const uint32_t a = (uint32_t)(qw >> (2 * (y + 1 - U - qb))) & 3u;
                     const uint32_t c = (uint32_t)(qw >> (2 * (y + 1 - qb))) & 3u;
                     hit |= ((pbv[t] >> a) & (pbv[t] >> (4 + c)) & 1u) << slot[t];
+                    single |= ((pbv[t] >> (8 + a)) & 1u) << slot[t];
                 }
                 hit &= tested;
                 if (hit) {
-                    const uint32_t x = p + (uint32_t)__builtin_ctz(hit);  // short predecessor
+                    const uint32_t xi = (uint32_t)__builtin_ctz(hit);
+                    const uint32_t x = p + xi;  // x, x + 1 long, x - 1 short
+#if NTC_GUESS
+                    // x's U-mer is one node.  After a run break at ge (mostly a substitution),
+                    // the read most likely goes on along the same path: guess that node at
+                    // path position gj + (x + 1 - ge) and let the run verify it (its U
+                    // characters and that it is a node) instead of fetching x's table entry.
+                    // Exact either way: a single-node interval holding a node whose k-mer
+                    // ends with the U-mer is that node.
+                    const uint32_t jg = gj + (x + 1 - ge);
+                    if (((single >> xi) & 1u) && ix.tab_pos && ge != 0 && x - ge - U <= NTC_GUESS_SLACK &&
+                        x >= ge + U && jg < ix.path_len) {
+                        j = jg;
+                        d = U;
+                        p = x + 1;
+                        vfy = U;
+                        try_run = true;
+                        mode = kModeBrk;  // a run of length 0 leaves p = x + 1, long: its break check
+                        ge = 0;
+                        return 0;
+                    }
+#endif
                     NTC_TOUCH(kTrTabU, ix.tab + tab_base(U) + key_at(x, U));
                     return enter_pair(ix, b, x, load2_stream(ix.tab + tab_base(U) + key_at(x, U)));
                 }
@@ -1055,7 +1078,35 @@ struct MsLane {
             return enter_pair(ix, b, x, load2_stream(ix.tab + tab_base(U) + key_at(x, U)));
         }
         if (!covers(p + 1 - U, p)) window(b, p + 1 - U);
+        if (mode == kModeEnter) {  // guessed node rejected: x = p - 1 from the table
+            if (!covers(p - U, p - 1)) window(b, p - U);
+            NTC_TOUCH(kTrTabU, ix.tab + tab_base(U) + key_at(p - 1, U));
+            return enter_pair(ix, b, p - 1, load2_stream(ix.tab + tab_base(U) + key_at(p - 1, U)));
+        }
         if (mode == kModeBrk) {
+#if NTC_BRK_PAIR
+            if (ix.pair_w) {
+                // is p long?  One pair word (Infinity Cache) instead of p's table entry (HBM):
+                // bit 4 + q[p] of the (U-1)-mer ending at p - 1.  A short p's m is not known
+                // here; m <= U - 1 skips nothing beyond p itself.
+                const uint64_t M = key_at(p - 1, U - 1);
+                const uint32_t c = (uint32_t)(qw >> (2 * (p - qb))) & 3u;
+                NTC_TOUCH(kTrBits, ix.pair_w + M);
+                NTC_TOUCH(kTrColex, ix.colex_at + j);
+                const uint32_t pw = ix.pair_w[M];
+                const uint32_t v = ix.colex_at[j] & 0x7FFFFFFFu;  // node before p, for a long p
+                if (!((pw >> (4 + c)) & 1u)) {
+                    p += 1;
+                    mode = kModeScan;
+                    hi = U + 1 < kScanW ? U + 1 : kScanW;
+                    return p >= len ? 1 : 0;
+                }
+                l = v;
+                r = v + 1;
+                mode = kModeExt;
+                return 0;
+            }
+#endif
             NTC_TOUCH(kTrTabU, ix.tab + tab_base(U) + key_at(p, U));
             const uint2 te = load2_stream(ix.tab + tab_base(U) + key_at(p, U));
             NTC_TOUCH(kTrColex, ix.colex_at + j);

@@ -642,17 +642,17 @@ __global__ __launch_bounds__(256) void k_tab_bits(const uint2 *top, uint32_t U, 
     }
 }
 
-__global__ __launch_bounds__(256) void k_pair_bytes(const uint32_t *bits, uint32_t U, uint32_t *out) {
-    const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;  // four pair bytes per thread
-    const uint64_t cnt = pair_bytes_count(U);
-    if (4 * w >= cnt) return;
-    uint32_t v = 0;
-    for (uint32_t i = 0; i < 4 && 4 * w + i < cnt; i++) v |= pair_byte(bits, U, 4 * w + i) << (8 * i);
+__global__ __launch_bounds__(256) void k_pair_words(const uint2 *top, uint32_t U, uint32_t *out) {
+    const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;  // two pair words per thread
+    const uint64_t cnt = pair_words_count(U);
+    if (2 * w >= cnt) return;
+    uint32_t v = pair_word(top, U, 2 * w);
+    if (2 * w + 1 < cnt) v |= pair_word(top, U, 2 * w + 1) << 16;
     out[w] = v;
 }
 
-void launch_pair_bytes(const uint32_t *bits, uint32_t U, uint8_t *out, hipStream_t s) {
-    hipLaunchKernelGGL(k_pair_bytes, grid_for((pair_bytes_count(U) + 3) / 4), dim3(256), 0, s, bits, U,
+void launch_pair_words(const uint2 *top, uint32_t U, uint16_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_pair_words, grid_for((pair_words_count(U) + 1) / 2), dim3(256), 0, s, top, U,
                        (uint32_t *)out);
 }
 

@@ -59,7 +59,7 @@ inline void trace_read_done() {}
 namespace {
 bool load(const ntc_index_view *v, HostIndex &hx, Derived &dv, std::vector<WalkEntry> &walk, DevIndex &d,
           std::vector<uint2> &tab, std::vector<uint32_t> &bits, std::vector<uint32_t> &fbits,
-          std::vector<uint8_t> &pairb, uint32_t tab_u = 0) {
+          std::vector<uint16_t> &pairb, uint32_t tab_u = 0) {
     hx.n = v->n_nodes;
     hx.k = v->k;
     uint64_t nw = (hx.n + 63) / 64;
@@ -82,12 +82,12 @@ bool load(const ntc_index_view *v, HostIndex &hx, Derived &dv, std::vector<WalkE
     d.filt_f = fbits.empty() ? 0u : filter_level(U);
     d.filt_bits = fbits.empty() ? nullptr : fbits.data();
     d.tab_u = U;
-    d.pair_b = nullptr;
+    d.pair_w = nullptr;
     const char *pe = getenv("NTC_EMU_PAIR_BYTES");
     if (!pe || atoi(pe) != 0) {
-        pairb.resize(pair_bytes_count(U));
-        for (uint64_t M = 0; M < pairb.size(); M++) pairb[M] = (uint8_t)pair_byte(bits.data(), U, M);
-        d.pair_b = pairb.data();
+        pairb.resize(pair_words_count(U));
+        for (uint64_t M = 0; M < pairb.size(); M++) pairb[M] = (uint16_t)pair_word(tab.data() + tab_base(U), U, M);
+        d.pair_w = pairb.data();
     }
     return true;
 }
@@ -101,7 +101,7 @@ extern "C" int emu_path_cover(const ntc_index_view *v, uint64_t *out) {
     DevIndex d{};
     std::vector<uint2> tab;
     std::vector<uint32_t> bits, fbits;
-    std::vector<uint8_t> pairb;
+    std::vector<uint16_t> pairb;
     if (!load(v, hx, dv, walk, d, tab, bits, fbits, pairb, 1)) return 1;
     if (!dv.has_paths) return 2;
     out[0] = path_cover_hash(dv.pstream.data(), dv.colex_at.data(), dv.pos_of_node.data(), dv.puniq.data(), hx.n,
@@ -119,7 +119,7 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
     std::vector<WalkEntry> walk;
     std::vector<uint2> tab;
     std::vector<uint32_t> bits, fbits;
-    std::vector<uint8_t> pairb;
+    std::vector<uint16_t> pairb;
     DevIndex d;
     if (!load(v, hx, dv, walk, d, tab, bits, fbits, pairb, (uint32_t)tab_u)) return NTC_ERR_FORMAT;
     if (!use_paths) d.has_paths = 0;
@@ -197,7 +197,7 @@ extern "C" int emu_decode(const ntc_index_view *v, const uint64_t *recs, uint64_
     std::vector<WalkEntry> walk;
     std::vector<uint2> tab;
     std::vector<uint32_t> bits, fbits;
-    std::vector<uint8_t> pairb;
+    std::vector<uint16_t> pairb;
     DevIndex d;
     if (!load(v, hx, dv, walk, d, tab, bits, fbits, pairb, 1)) return NTC_ERR_FORMAT;
     // the kernels' decode: per record, 2-bit codes via CodeWriter, then ASCII (k_dec_rec +
