@@ -475,7 +475,7 @@ constexpr uint32_t kScanExact = 4;   // filter candidates tested exactly per SCA
 #define NTC_GUESS_SLACK 2  // guess only for x - ge in [U, U + slack] (a lone substitution: x = ge + U)
 #endif
 #ifndef NTC_PAIR_TESTS
-#define NTC_PAIR_TESTS 2  // candidate pairs tested per SCAN with pair bytes
+#define NTC_PAIR_TESTS 4  // candidate pairs tested per SCAN with pair words
 #endif
 
 // ======================================================================================
@@ -899,22 +899,23 @@ struct MsLane {
             if (ix.filt_f) {
                 const uint32_t F = ix.filt_f;
                 uint32_t fm = 0;  // bit i: F-mer ending at p - 2 + i is present
-                // every load unconditional (slots past W + 2 repeat slot 0), all issued before
-                // the first use: one L2 round trip, not W + 2 dependent ones
+                // every load unconditional and issued before the first use: one L2 round
+                // trip, not W + 2 dependent ones
+                // F-mer of slot i = characters p - U + 1 + i ... p - 2 + i: bits 2i.. of v.
+                // Slots past W + 2 repeat slot 0's word (an L1 hit, no extra L2 request).
+                const uint64_t v = qw >> (2 * (p + 1 - U - qb));
+                const uint32_t fmask = (1u << (2 * F)) - 1u;
+                const uint32_t f0 = (uint32_t)v & fmask;
                 uint32_t fw[kScanW + kFiltGap];
 #pragma unroll
                 for (uint32_t i = 0; i < kScanW + kFiltGap; i++) {
-                    const uint32_t ii = i < W + kFiltGap ? i : 0u;
-                    const uint64_t fk = (qw >> (2 * (p + 1 - U + ii - qb))) & ((1ULL << (2 * F)) - 1);
-                    if (i == ii) NTC_TOUCH(kTrFilt, ix.filt_bits + (fk >> 5));
+                    const uint32_t fk = i < W + kFiltGap ? (uint32_t)(v >> (2 * i)) & fmask : f0;
+                    if (i < W + kFiltGap) NTC_TOUCH(kTrFilt, ix.filt_bits + (fk >> 5));
                     fw[i] = ix.filt_bits[fk >> 5];
                 }
 #pragma unroll
-                for (uint32_t i = 0; i < kScanW + kFiltGap; i++) {
-                    const uint32_t ii = i < W + kFiltGap ? i : 0u;
-                    const uint32_t fk = (uint32_t)(qw >> (2 * (p + 1 - U + ii - qb)));
-                    fm |= ((fw[i] >> (fk & 31)) & 1u) << i;
-                }
+                for (uint32_t i = 0; i < kScanW + kFiltGap; i++)
+                    fm |= ((fw[i] >> ((uint32_t)(v >> (2 * i)) & 31u)) & 1u) << i;
                 fm &= (1u << (W + kFiltGap)) - 1u;
                 cand &= fm & (fm >> 1) & (fm >> kFiltGap);  // all three F-mers of the U-mer
             }
