@@ -459,7 +459,8 @@ struct BaseReader {
     }
 };
 
-enum : uint32_t { kModeScan = 0, kModeExt = 1, kModeP1 = 2, kModeBs = 3, kModeBrk = 4, kModeFirst = 5, kModeEnter = 6 };
+enum : uint32_t { kModeScan = 0, kModeExt = 1, kModeP1 = 2, kModeBs = 3, kModeBrk = 4, kModeFirst = 5, kModeEnter = 6,
+                  kModeBrkLong = 7 };
 constexpr uint32_t kScanW = 16;      // presence probes per SCAN unit (U + kScanW - 1 <= 32)
 #ifndef NTC_SCAN_MODE
 #define NTC_SCAN_MODE 0  // 2: SCAN loads the first candidate pair's table entry directly
@@ -467,6 +468,9 @@ constexpr uint32_t kScanW = 16;      // presence probes per SCAN unit (U + kScan
 constexpr uint32_t kScanExact = 4;   // filter candidates tested exactly per SCAN
 #ifndef NTC_BRK_PAIR
 #define NTC_BRK_PAIR 1  // run break: long/short from the pair word, not the table entry
+#endif
+#ifndef NTC_BRK_MERGE
+#define NTC_BRK_MERGE 1  // run break check issued with the SCAN after it
 #endif
 #ifndef NTC_GUESS
 #define NTC_GUESS 1  // SCAN after a run break guesses the node along the same path
@@ -882,6 +886,24 @@ struct MsLane {
                 return enter_pair(ix, b, U - 1, te);
             }
         }
+#if NTC_BRK_MERGE
+        // The run broke at p.  p is short after almost every break, so p's long/short test
+        // (its pair word, and the node before p for a long p) is issued together with the
+        // SCAN of p + 1, ...; a long p abandons that SCAN for EXT at p.  One round trip.
+        uint32_t bpw = 0, bc = 0;
+        bool brk = false;
+        if (mode == kModeBrk && ix.pair_w && p + 2 < len) {
+            if (!covers(p + 1 - U, p + 2)) window(b, p + 1 - U);
+            const uint64_t M = key_at(p - 1, U - 1);
+            bc = (uint32_t)(qw >> (2 * (p - qb))) & 3u;
+            NTC_TOUCH(kTrBits, ix.pair_w + M);
+            bpw = ix.pair_w[M];
+            brk = true;
+            p += 1;  // a short p: m <= U - 1 skips nothing beyond p itself
+            mode = kModeScan;
+            hi = U + 1 < kScanW ? U + 1 : kScanW;
+        }
+#endif
         if (mode == kModeScan) {
             // find the first pair of consecutive long positions at or after p (position
             // p - 1 is short, or p = 0); positions < U - 1 are short by length
@@ -919,6 +941,13 @@ struct MsLane {
                 fm &= (1u << (W + kFiltGap)) - 1u;
                 cand &= fm & (fm >> 1) & (fm >> kFiltGap);  // all three F-mers of the U-mer
             }
+#if NTC_BRK_MERGE
+            if (brk && ((bpw >> (4 + bc)) & 1u)) {  // the break position is long: EXT there
+                p -= 1;
+                mode = kModeBrkLong;
+                return 0;
+            }
+#endif
             if (ix.pair_w) {
                 // exact test of the first candidate PAIRS (y and y + 1 both pass the filter),
                 // one pair byte each; the first pair that is long-long is the SCAN's answer
@@ -1079,6 +1108,13 @@ struct MsLane {
             return enter_pair(ix, b, x, load2_stream(ix.tab + tab_base(U) + key_at(x, U)));
         }
         if (!covers(p + 1 - U, p)) window(b, p + 1 - U);
+        if (mode == kModeBrkLong) {  // the run broke at a long p: extend from the node before p
+            NTC_TOUCH(kTrColex, ix.colex_at + j);
+            l = ix.colex_at[j] & 0x7FFFFFFFu;
+            r = l + 1;
+            mode = kModeExt;
+            return 0;
+        }
         if (mode == kModeEnter) {  // guessed node rejected: x = p - 1 from the table
             if (!covers(p - U, p - 1)) window(b, p - U);
             NTC_TOUCH(kTrTabU, ix.tab + tab_base(U) + key_at(p - 1, U));
