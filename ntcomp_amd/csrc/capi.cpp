@@ -768,8 +768,7 @@ int ntc_decode_batch_device(ntc_ctx *ctx, const uint64_t *d_recs, uint64_t n_rec
     if (n == 0) {
         HIP_TRY(ctx, hipMemsetAsync(fscan, 0, (n + 1) * 16, ctx->stream));
         HIP_TRY(ctx, hipMemsetAsync(d_read_offsets_out, 0, 8, ctx->stream));
-        HIP_TRY(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
-        HIP_TRY(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
+        for (int i = 1; i < 4; i++) HIP_TRY(ctx, hipEventRecord(ctx->ev[i], ctx->stream));
         return NTC_OK;
     }
     DecIndexArgs ia{};
@@ -793,6 +792,7 @@ int ntc_decode_batch_device(ntc_ctx *ctx, const uint64_t *d_recs, uint64_t n_rec
     wa.O2 = (uint64_t *)o2;
     wa.status = ctx->d_status;
     launch_dec_walk(wa, ctx->stream);
+    HIP_TRY(ctx, hipEventRecord(ctx->ev[3], ctx->stream));  // k_dec_rec alone: ev[1] -> ev[3]
     launch_dec_expand((const uint64_t *)E, n, bases_capacity, (uint64_t *)o2, d_bases_out, ctx->d_status,
                       ctx->stream);
     HIP_TRY(ctx, hipGetLastError());
@@ -883,10 +883,12 @@ int ntc_last_timing(ntc_ctx *ctx, ntc_timing *out) {
     HIP_TRY(ctx, hipEventSynchronize(ctx->ev[2]));
     float a = 0, b = 0;
     std::memset(out, 0, sizeof(*out));
-    if (ctx->last == kEncode && ctx->last_variant == 4) {
+    if ((ctx->last == kEncode && ctx->last_variant == 4) || ctx->last == kDecode) {
+        // main = the dominant kernel alone: k_ms4 (ev[3] -> ev[1]) or k_dec_rec (ev[1] -> ev[3])
         float tot = 0, ms = 0;
         HIP_TRY(ctx, hipEventElapsedTime(&tot, ctx->ev[0], ctx->ev[2]));
-        HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->ev[3], ctx->ev[1]));
+        if (ctx->last == kDecode) HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->ev[1], ctx->ev[3]));
+        else HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->ev[3], ctx->ev[1]));
         out->main_ms = ms;
         out->aux_ms = (double)tot - (double)ms;
         out->total_ms = tot;
