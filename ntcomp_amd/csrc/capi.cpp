@@ -68,7 +68,7 @@ namespace {
 enum WsSlot {
     WS_D = 0, WS_S, WS_F, WS_R, WS_RECCOUNT, WS_SCANTMP, WS_TILEBASE, WS_TILEROWS,
     WS_STAGE_BASES, WS_STAGE_OFFS, WS_STAGE_RECS, WS_E, WS_DEC_A, WS_DEC_B, WS_DEC_C,
-    WS_DEC_D, WS_Q, WS_E3, WS_NE, WS_COUNTER, WS_R2, WS_O2
+    WS_DEC_D, WS_Q, WS_E3, WS_NE, WS_COUNTER, WS_R2, WS_O2, WS_ED
 };
 
 #define HIP_TRY(ctx, expr)                                                                   \
@@ -155,6 +155,8 @@ int encode4_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, u
     a.Q = (uint64_t *)p;
     if ((rc = ensure(ctx, WS_E3, (total_bases + 1) * sizeof(Entry), &p))) return rc;
     a.E = (Entry *)p;
+    if ((rc = ensure(ctx, WS_ED, (n_reads + 1) * kEntSlot * sizeof(Entry), &p))) return rc;
+    a.Ed = (Entry *)p;
     if ((rc = ensure(ctx, WS_NE, (n_reads + 1) * 4, &p))) return rc;
     a.ne = (uint32_t *)p;
     if ((rc = ensure(ctx, WS_R, (total_bases + 1) * 8, &p))) return rc;

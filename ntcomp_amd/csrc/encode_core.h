@@ -576,27 +576,40 @@ NTC_HD Entry load_entry(const Entry *E, int32_t i) {
 #endif
 }
 
+// Entry j of a read: j < kEntSlot in the dense slots Ed[j * es] (the kernels interleave the
+// reads' first entries, Ed = base + read id, es = reads in the batch: a wave's lanes write
+// and read neighbouring 16-byte slots, so lines are shared instead of one line per read),
+// later ones at E[j] (position space).  Ed = E, es = 1 is the plain contiguous layout.
+constexpr uint32_t kEntSlot = 4;
+NTC_HD const Entry *ent_ptr(const Entry *E, const Entry *Ed, uint64_t es, uint32_t j) {
+    return j < kEntSlot ? Ed + (uint64_t)j * es : E + j;
+}
+
 // Right-to-left reader of one read's entries (+ suffix table for uncovered positions).
 struct EntryView {
     const Entry *E;
+    const Entry *Ed;  // dense slots (see ent_ptr)
+    uint64_t es;
     const DevIndex *ix;
     const uint64_t *Q;
     uint64_t qo;
     uint32_t k;
     int32_t e;  // cursor (-1: the read has no entries); moves left only
     Entry cur;  // E[e]
-    NTC_HD EntryView(const Entry *E_, const DevIndex *ix_, const uint64_t *Q_, uint64_t qo_, uint32_t k_, int32_t e_)
-        : E(E_), ix(ix_), Q(Q_), qo(qo_), k(k_), e(e_), cur{0, 0, 0, 0} {
-        if (e >= 0) cur = load_entry(E, e);
+    NTC_HD EntryView(const Entry *E_, const DevIndex *ix_, const uint64_t *Q_, uint64_t qo_, uint32_t k_, int32_t e_,
+                     const Entry *Ed_ = nullptr, uint64_t es_ = 1)
+        : E(E_), Ed(Ed_ ? Ed_ : E_), es(Ed_ ? es_ : 1), ix(ix_), Q(Q_), qo(qo_), k(k_), e(e_), cur{0, 0, 0, 0} {
+        if (e >= 0) cur = at(e);
     }
+    NTC_HD Entry at(int32_t i) const { return load_entry(ent_ptr(E, Ed, es, (uint32_t)i), 0); }
     NTC_HD void seek(uint32_t x) {  // last entry with p <= x, or entry 0
         if (e <= 0 || cur.p <= x) return;
         // every entry covers >= 1 position, so entry e - (p - x) starts at or before x
         int32_t g = e - (int32_t)(cur.p - x);
         if (g < 0) g = 0;
-        Entry eg = load_entry(E, g);
+        Entry eg = at(g);
         while (g + 1 < e) {
-            const Entry nx = load_entry(E, g + 1);
+            const Entry nx = at(g + 1);
             if (nx.p > x) break;
             g++;
             eg = nx;
@@ -640,7 +653,7 @@ struct EntryView {
         int64_t pos = x;
         Entry en = cur;
         while (cnt < cap && pos >= 0) {
-            while (c > 0 && en.p > (uint32_t)pos) en = load_entry(E, --c);
+            while (c > 0 && en.p > (uint32_t)pos) en = at(--c);
             if (!(c >= 0 && en.p <= (uint32_t)pos && (uint32_t)pos < en.p + en.m)) {
                 // uncovered: d = min(pos + 1, U), = k only for U = k and a long position
                 if (ix->tab_u != k || (uint32_t)pos + 1 < k) break;
@@ -704,7 +717,7 @@ NTC_HD uint32_t fast_code(uint32_t b) { return ((b >> 1) ^ (b >> 2)) & 3u; }
 NTC_HD bool is_acgt(uint32_t b) { return b == 'A' || b == 'C' || b == 'G' || b == 'T'; }
 
 
-NTC_HD void store_entry(Entry *E, uint32_t i, uint32_t p, uint32_t v, uint32_t m, uint32_t dk) {
+NTC_HD void store_entry(Entry *E, uint64_t i, uint32_t p, uint32_t v, uint32_t m, uint32_t dk) {
     NTC_TOUCH(kTrEw, E + i);
 #if defined(__HIP_DEVICE_COMPILE__) && (NTC_NT & 16)
     u32x4_t x = {p, v, m, dk};
@@ -721,10 +734,13 @@ NTC_HD void store_entry(Entry *E, uint32_t i, uint32_t p, uint32_t v, uint32_t m
 struct MsBufs {
     const uint64_t *Q;
     Entry *E;
+    Entry *Ed;    // dense entry slots (ent_ptr): entry j < kEntSlot of read rid at Ed[rid + j * es]
+    uint64_t es;
 };
 
 struct MsLane {
     uint64_t qo;        // this read starts at character qo of Q; its entries at E + qo
+    uint64_t rid;       // read id (dense entry slots)
     uint64_t qw;        // query characters [qb, qb + 32) of this read, cached
     uint32_t qb;
     uint32_t len, p, d, l, r, j, ne, mode, hi, lo, l1, r1, bl, bR;
@@ -732,8 +748,9 @@ struct MsLane {
     uint32_t vfy;       // the next run first verifies the vfy characters ending at node j
     bool try_run;
 
-    NTC_HD void start(const DevIndex &ix, uint64_t qo_, uint32_t len_) {
+    NTC_HD void start(const DevIndex &ix, uint64_t qo_, uint32_t len_, uint64_t rid_ = 0) {
         qo = qo_;
+        rid = rid_;
         len = len_;
         qw = 0;
         qb = 0xFFFFFFFFu;
@@ -754,6 +771,10 @@ struct MsLane {
     NTC_HD uint64_t key_at(uint32_t x, uint32_t U) const {  // U-mer ending at x (cached window)
         return (qw >> (2 * (x + 1 - U - qb))) & ((1ULL << (2 * U)) - 1);
     }
+    NTC_HD void put_entry(const MsBufs &b, uint32_t p_, uint32_t v, uint32_t m, uint32_t dk) {
+        store_entry(ne < kEntSlot ? b.Ed + rid : b.E + qo, ne < kEntSlot ? (uint64_t)ne * b.es : ne, p_, v, m, dk);
+        ne++;
+    }
     // after a commit: look for the path position of a single-node interval
     NTC_HD void note_single(const DevIndex &ix) {
         j = 0xFFFFFFFFu;
@@ -765,7 +786,7 @@ struct MsLane {
     }
     NTC_HD int commit(const DevIndex &ix, const MsBufs &b, uint32_t nl, uint32_t nr, uint32_t nd) {
         l = nl; r = nr; d = nd;
-        store_entry(b.E + qo, ne++, p, l, 1u, d);
+        put_entry(b, p, l, 1u, d);
         p++;
         mode = kModeExt;
         note_single(ix);
@@ -851,7 +872,7 @@ struct MsLane {
                 if (lim < 64) break;
             }
             if (m > 0) {
-                store_entry(b.E + qo, ne++, p, j + 1, m, (d + 1 < k ? d + 1 : k) | kRunTag);
+                put_entry(b, p, j + 1, m, (d + 1 < k ? d + 1 : k) | kRunTag);
                 p += m;
                 j += m;
                 d = d + m < k ? d + m : k;
@@ -1197,16 +1218,17 @@ struct MsLane {
 
 // (d, S) of every position of one read (diagnostics: ntc_debug_matching_statistics)
 NTC_HD void read_ms(const DevIndex &ix, const uint64_t *Q, uint64_t qo, const Entry *E, uint32_t ne,
-                    uint32_t len, uint32_t *d_out, uint32_t *s_out) {
-    EntryView ev(E, &ix, Q, qo, ix.k, -1);
+                    uint32_t len, uint32_t *d_out, uint32_t *s_out, const Entry *Ed = nullptr, uint64_t es = 1) {
+    EntryView ev(E, &ix, Q, qo, ix.k, -1, Ed, es);
     uint32_t x = 0;
     for (uint32_t i = 0; i <= ne && x < len; i++) {
-        const uint32_t until = i < ne ? E[i].p : len;
+        const Entry en = i < ne ? ev.at((int32_t)i) : Entry{0, 0, 0, 0};
+        const uint32_t until = i < ne ? en.p : len;
         for (; x < until && x < len; x++) tab_ds(ix, Q, qo, x, d_out[x], s_out[x]);
         if (i == ne) break;
-        for (uint32_t t = 0; t < E[i].m && x < len; t++, x++) {
-            d_out[x] = ev.dval(E[i], x);
-            s_out[x] = ev.sval(E[i], x);
+        for (uint32_t t = 0; t < en.m && x < len; t++, x++) {
+            d_out[x] = ev.dval(en, x);
+            s_out[x] = ev.sval(en, x);
         }
     }
 }
@@ -1218,9 +1240,10 @@ constexpr uint32_t kRecSlot = 8;  // records per read in the dense slot; more sp
 // the reads' slots (sstride = reads in the batch): the loop runs in lock step over a
 // wave's lanes, so the lanes' j-th records are one coalesced store.
 NTC_HD int parse_read(const DevIndex &ix, const uint64_t *Q, uint64_t qo, const Entry *E, uint32_t ne,
-                      uint32_t len, uint64_t *slot, uint64_t *spill, uint64_t sstride = 1) {
+                      uint32_t len, uint64_t *slot, uint64_t *spill, uint64_t sstride = 1,
+                      const Entry *Ed = nullptr, uint64_t es = 1) {
     const uint32_t k = ix.k;
-    EntryView ev(E, &ix, Q, qo, k, (int32_t)ne - 1);
+    EntryView ev(E, &ix, Q, qo, k, (int32_t)ne - 1, Ed, es);
     uint32_t i = len;
     int nrec = 0;
     while (i > 0) {

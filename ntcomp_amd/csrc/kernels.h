@@ -29,7 +29,8 @@ struct Enc4Args {
     const uint64_t *offs;        // [n_reads+1], absolute into bases
     uint64_t n_reads;
     uint64_t *Q;                 // packed bases, position space (2 bits, 32 per word)
-    Entry *E;                    // entries, position space
+    Entry *E;                    // entries past kEntSlot, position space
+    Entry *Ed;                   // first kEntSlot entries of each read (dense slots, ent_ptr)
     uint32_t *ne;                // entries per read
     uint64_t *R;                 // records past kRecSlot, position space
     uint64_t *R2;                // first kRecSlot records of each read (dense slots)

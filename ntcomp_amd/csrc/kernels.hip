@@ -144,7 +144,8 @@ constexpr uint32_t kPoolChunk = 64;
 __device__ __forceinline__ void parse_one(const Enc4Args &a, uint64_t r) {
     const uint64_t o0 = a.offs[0], b = a.offs[r], e = a.offs[r + 1];
     const uint64_t P = b - o0;
-    const int rc = parse_read(a.ix, a.Q, P, a.E + P, a.ne[r], (uint32_t)(e - b), a.R2 + r, a.R + P, a.n_reads);
+    const int rc = parse_read(a.ix, a.Q, P, a.E + P, a.ne[r], (uint32_t)(e - b), a.R2 + r, a.R + P, a.n_reads,
+                              a.Ed + r, a.n_reads);
     if (rc < 0) {
         atomicMin(a.status, (unsigned long long)((r << 8) | (uint64_t)(-rc)));
         a.rec_count[r] = 0;
@@ -163,7 +164,7 @@ __global__ __launch_bounds__(256, NTC_MS_WAVES) void k_ms4(Enc4Args a) {
     uint64_t pool_lo = 0, pool_hi = 0;
     bool exhausted = false, idle = true;
     uint64_t rd = 0;
-    const MsBufs bufs{a.Q, a.E};
+    const MsBufs bufs{a.Q, a.E, a.Ed, a.n_reads};
     MsLane st;
     for (;;) {
         // ---- hand idle lanes the next reads (wave-uniform control flow) ----------------
@@ -187,7 +188,7 @@ __global__ __launch_bounds__(256, NTC_MS_WAVES) void k_ms4(Enc4Args a) {
                 idle = false;
                 const uint64_t b = a.offs[rd], e = a.offs[rd + 1];
                 const uint64_t P = b - o0;
-                st.start(a.ix, P, (uint32_t)(e - b));
+                st.start(a.ix, P, (uint32_t)(e - b), rd);
                 if (e <= b) {  // empty read (EncodeError, encode.rs:133-135) or bad offsets
                     atomicMin(a.status, (unsigned long long)((rd << 8) | (uint64_t)(e == b ? kErrEmptyRead : kErrFormat)));
                     a.ne[rd] = 0;
@@ -620,7 +621,7 @@ __global__ __launch_bounds__(256) void k_debug_gather4(Enc4Args a, uint32_t *d_o
     if (r >= a.n_reads) return;
     const uint64_t o0 = a.offs[0], b = a.offs[r], e = a.offs[r + 1];
     const uint64_t P = b - o0;
-    read_ms(a.ix, a.Q, P, a.E + P, a.ne[r], (uint32_t)(e - b), d_out + P, s_out + P);
+    read_ms(a.ix, a.Q, P, a.E + P, a.ne[r], (uint32_t)(e - b), d_out + P, s_out + P, a.Ed + r, a.n_reads);
 }
 
 // suffix table level u (4^u entries) from level u - 1

@@ -147,7 +147,7 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
                 if (rc == 0) {
                     trace_phase(0);
                     ms.start(d, 0, len);
-                    const MsBufs bufs{Q.data(), E4.data()};
+                    const MsBufs bufs{Q.data(), E4.data(), E4.data(), 1};
                     for (;;) {
                         int st = ms.step(d, bufs);
                         if (st < 0) { rc = st; break; }
