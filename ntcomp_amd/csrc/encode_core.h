@@ -892,10 +892,19 @@ struct MsLane {
             if (len >= U + 1) {
                 window(b, 0);
                 NTC_TOUCH(kTrTabU, ix.tab + tab_base(U) + key_at(U - 1, U));
-                NTC_TOUCH(kTrBits, ix.tab_bits + (key_at(U, U) >> 5));
                 const uint2 te = load2_stream(ix.tab + tab_base(U) + key_at(U - 1, U));
-                const uint64_t k2 = key_at(U, U);
-                const uint32_t b2 = (ix.tab_bits[k2 >> 5] >> (k2 & 31)) & 1u;
+                uint32_t b2;
+                if (ix.pair_w) {
+                    // U is long iff bit 4 + q[U] of the pair word of the (U-1)-mer ending at U - 1
+                    // (the 32 MB level-U bitmap then stays out of the Infinity Cache entirely)
+                    const uint64_t M = key_at(U - 1, U - 1);
+                    NTC_TOUCH(kTrBits, ix.pair_w + M);
+                    b2 = (ix.pair_w[M] >> (4 + ((uint32_t)(qw >> (2 * U)) & 3u))) & 1u;
+                } else {
+                    const uint64_t k2 = key_at(U, U);
+                    NTC_TOUCH(kTrBits, ix.tab_bits + (k2 >> 5));
+                    b2 = (ix.tab_bits[k2 >> 5] >> (k2 & 31)) & 1u;
+                }
                 if (!tab_long(te)) {
                     p = U - 1 + U - (te.y & 0xFFu);  // d_{U-1+i} <= m + i
                     return p >= len ? 1 : 0;
