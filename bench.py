@@ -181,6 +181,22 @@ def main():
                         "profiles/pmc_traffic.json); traffic_frac = traffic / kernel time / peak"}
     if traffic:
         roofline["traffic_frac"] = round(traffic / (main_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
+    # The hot kernels are bound by random 64 B line requests, not streaming bytes: L2-miss read
+    # requests per launch (rocprofv3 TCC_EA0_RDREQ) / kernel time, against the random-access
+    # roof measured on the same chip by scripts/randbw (profiles/round1/randbw.jsonl).
+    try:
+        ea = tj.get(kname, {}).get("ea_rdreq_per_launch")
+        roofs = [json.loads(l) for l in open(os.path.join(REPO, "profiles", "round1", "randbw.jsonl"))]
+        roof = max(r["g_lines_per_s"] for r in roofs
+                   if r.get("test") == "random_8B_loads" and r["buffer_bytes"] >= (32 << 20))
+        if ea:
+            rate = ea / (main_ms / 1e3) / 1e9
+            roofline["line_rate"] = {"requests_per_launch": int(ea), "g_requests_per_s": round(rate, 2),
+                                     "roof_g_requests_per_s": roof, "frac": round(rate / roof, 4),
+                                     "note": "random-line roof = best scripts/randbw rate for buffers past L2 "
+                                             "(Infinity-Cache and HBM sizes); one request = one 64 B line"}
+    except (OSError, ValueError, NameError, KeyError):
+        pass
 
     cpu = None
     parity = None

@@ -59,6 +59,8 @@ def main(prof_dir, out_md, out_json):
             traffic[k] = {"fetch_bytes_reported": f, "write_bytes": w,
                           "hbm_bytes_per_launch": 2 * f + w,
                           "note": "2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE half-count correction)"}
+            if "TCC_EA0_RDREQ_sum" in cs:
+                traffic[k]["ea_rdreq_per_launch"] = sum(cs["TCC_EA0_RDREQ_sum"]) / len(cs["TCC_EA0_RDREQ_sum"])
             if "TCC_HIT_sum" in cs:
                 h, m = sum(cs["TCC_HIT_sum"]), sum(cs["TCC_MISS_sum"])
                 traffic[k]["l2_hit_rate"] = h / (h + m) if h + m else None
