@@ -65,6 +65,8 @@ struct ntc_ctx {
 
 namespace {
 
+constexpr uint64_t kCounterBytes = 8 * 64;  // work queue heads (kernels.hip WaveQueue: 8, 64 B apart)
+
 enum WsSlot {
     WS_D = 0, WS_S, WS_F, WS_R, WS_RECCOUNT, WS_SCANTMP, WS_TILEBASE, WS_TILEROWS,
     WS_STAGE_BASES, WS_STAGE_OFFS, WS_STAGE_RECS, WS_E, WS_DEC_A, WS_DEC_B, WS_DEC_C,
@@ -165,12 +167,12 @@ int encode4_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, u
     a.R2 = (uint64_t *)p;
     if ((rc = ensure(ctx, WS_RECCOUNT, (n_reads + 1) * 4, &p))) return rc;
     a.rec_count = (uint32_t *)p;
-    if ((rc = ensure(ctx, WS_COUNTER, 64, &p))) return rc;
+    if ((rc = ensure(ctx, WS_COUNTER, kCounterBytes, &p))) return rc;
     a.counter = (unsigned long long *)p;
     void *tmp;
     if ((rc = ensure(ctx, WS_SCANTMP, scan_tmp_words(n_reads + 1) * 8, &tmp))) return rc;
     HIP_TRY(ctx, hipMemsetAsync(ctx->d_status, 0xFF, 8, ctx->stream));
-    HIP_TRY(ctx, hipMemsetAsync(a.counter, 0, 64, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(a.counter, 0, kCounterBytes, ctx->stream));
     ctx->last = kEncode;
     ctx->last_variant = 4;
     ctx->last_n = n_reads;

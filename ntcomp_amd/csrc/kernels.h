@@ -36,7 +36,7 @@ struct Enc4Args {
     uint64_t *R2;                // first kRecSlot records of each read (dense slots)
     uint32_t *rec_count;
     unsigned long long *status;
-    unsigned long long *counter; // work queue head (zeroed per call)
+    unsigned long long *counter; // work queue heads of k_ms4 (WaveQueue, zeroed per call)
 };
 
 struct EmitArgs {

@@ -140,6 +140,35 @@ __global__ __launch_bounds__(256) void k_pack(Enc4Args a, uint64_t bound) {
 
 constexpr uint32_t kPoolChunk = 64;
 
+// Work queues of the persistent kernels: the items are split into kQueues contiguous ranges,
+// each with its own head (64 B apart, zeroed per call); block b drains queue b % nq.  One
+// head for the whole grid serialises every wave's atomicAdd on one address (device-scope
+// atomics on MI355X run at the memory side), which costs milliseconds at 10^5..10^6 grabs.
+constexpr uint32_t kQueues = 8;       // = XCDs: consecutive blocks land on different XCDs
+constexpr uint32_t kQueueStride = 8;  // u64 words between heads
+struct WaveQueue {
+    unsigned long long *head;
+    uint64_t lo, hi;  // this queue's items
+    __device__ WaveQueue(unsigned long long *heads, uint64_t n) {
+        const uint32_t nq = gridDim.x < kQueues ? gridDim.x : kQueues, q = blockIdx.x % nq;
+        head = heads + (uint64_t)q * kQueueStride;
+        lo = n * q / nq;
+        hi = n * (q + 1) / nq;
+    }
+    // next chunk [b, e) for the wave (lane 0 grabs, all lanes get it); false when drained,
+    // leaving b and e untouched (the pool stays empty: b == e)
+    __device__ bool grab(uint32_t lane, uint32_t chunk, uint64_t &b, uint64_t &e) const {
+        unsigned long long got = 0;
+        if (lane == 0) got = atomicAdd(head, (unsigned long long)chunk);
+        got = __shfl(got, 0, 64);
+        const uint64_t nb = lo + got;
+        if (nb >= hi) return false;
+        b = nb;
+        e = nb + chunk < hi ? nb + chunk : hi;
+        return true;
+    }
+};
+
 // parse of read r (k_parse4's body)
 __device__ __forceinline__ void parse_one(const Enc4Args &a, uint64_t r) {
     const uint64_t o0 = a.offs[0], b = a.offs[r], e = a.offs[r + 1];
@@ -164,23 +193,14 @@ __global__ __launch_bounds__(256, NTC_MS_WAVES) void k_ms4(Enc4Args a) {
     uint64_t pool_lo = 0, pool_hi = 0;
     bool exhausted = false, idle = true;
     uint64_t rd = 0;
+    const WaveQueue wq(a.counter, a.n_reads);
     const MsBufs bufs{a.Q, a.E, a.Ed, a.n_reads};
     MsLane st;
     for (;;) {
         // ---- hand idle lanes the next reads (wave-uniform control flow) ----------------
         const uint64_t want = __ballot(idle);
         if (want) {
-            if (pool_lo >= pool_hi && !exhausted) {
-                unsigned long long got = 0;
-                if (lane == 0) got = atomicAdd(a.counter, (unsigned long long)kPoolChunk);
-                got = __shfl(got, 0, 64);
-                if (got >= a.n_reads) {
-                    exhausted = true;
-                } else {
-                    pool_lo = got;
-                    pool_hi = got + kPoolChunk < a.n_reads ? got + kPoolChunk : a.n_reads;
-                }
-            }
+            if (pool_lo >= pool_hi && !exhausted) exhausted = !wq.grab(lane, kPoolChunk, pool_lo, pool_hi);
             const uint32_t rank = (uint32_t)__popcll(want & ((1ULL << lane) - 1));
             const uint64_t avail = pool_hi - pool_lo;
             if (idle && rank < avail) {
