@@ -56,8 +56,6 @@ struct ntc_ctx {
     Enc4Args last4{};
     uint32_t tab_u_opt = 0;  // suffix-table depth for the next upload (0 = default_tab_u)
     int pair_bytes_opt = 1;  // build the SCAN pair bytes at the next upload (0: bitmap tests, A/B)
-    void *o2_zeroed = nullptr;  // WS_O2 buffer known to be all zero (k_dec_expand re-zeroes it)
-    uint64_t o2_zeroed_bytes = 0;
     uint64_t n_paths = 0, path_text_len = 0;
     int64_t upload_host_us = 0, upload_total_us = 0;  // last ntc_index_upload: host derive / total
     uint64_t max_pass_bases = 1ULL << 30;  // host-buffer calls split into device passes of at most this
@@ -70,7 +68,7 @@ constexpr uint64_t kCounterBytes = 8 * 64;  // work queue heads (kernels.hip Wav
 enum WsSlot {
     WS_D = 0, WS_S, WS_F, WS_R, WS_RECCOUNT, WS_SCANTMP, WS_TILEBASE, WS_TILEROWS,
     WS_STAGE_BASES, WS_STAGE_OFFS, WS_STAGE_RECS, WS_E, WS_DEC_A, WS_DEC_B, WS_DEC_C,
-    WS_DEC_D, WS_Q, WS_E3, WS_NE, WS_COUNTER, WS_R2, WS_O2, WS_ED
+    WS_DEC_D, WS_Q, WS_E3, WS_NE, WS_COUNTER, WS_R2, WS_ED
 };
 
 #define HIP_TRY(ctx, expr)                                                                   \
@@ -756,14 +754,6 @@ int ntc_decode_batch_device(ntc_ctx *ctx, const uint64_t *d_recs, uint64_t n_rec
     E = (uint64_t *)fscan + (n + 1);
     if ((rc = ensure(ctx, WS_SCANTMP, (4 * (n / 2048 + 2) + scan_tmp_words(n / 2048 + 2)) * 8, &tmp)))
         return rc;
-    void *o2;
-    if ((rc = ensure(ctx, WS_O2, (bases_capacity / 32 + 2) * 8, &o2))) return rc;
-    if (o2 != ctx->o2_zeroed || ctx->ws[WS_O2].bytes != ctx->o2_zeroed_bytes) {
-        // fresh buffer: zero once; every call leaves it zeroed
-        HIP_TRY(ctx, hipMemsetAsync(o2, 0, ctx->ws[WS_O2].bytes, ctx->stream));
-        ctx->o2_zeroed = o2;
-        ctx->o2_zeroed_bytes = ctx->ws[WS_O2].bytes;
-    }
     HIP_TRY(ctx, hipMemsetAsync(ctx->d_status, 0xFF, 8, ctx->stream));
     ctx->last = kDecode;
     ctx->last_n = n;
@@ -793,12 +783,9 @@ int ntc_decode_batch_device(ntc_ctx *ctx, const uint64_t *d_recs, uint64_t n_rec
     wa.E = (const uint64_t *)E;
     wa.offs_out = d_read_offsets_out;
     wa.out = d_bases_out;
-    wa.O2 = (uint64_t *)o2;
     wa.status = ctx->d_status;
     launch_dec_walk(wa, ctx->stream);
     HIP_TRY(ctx, hipEventRecord(ctx->ev[3], ctx->stream));  // k_dec_rec alone: ev[1] -> ev[3]
-    launch_dec_expand((const uint64_t *)E, n, bases_capacity, (uint64_t *)o2, d_bases_out, ctx->d_status,
-                      ctx->stream);
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
     return NTC_OK;

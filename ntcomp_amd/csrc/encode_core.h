@@ -1362,9 +1362,68 @@ struct CodeWriter {
     }
 };
 
+// Block-staged decode output (k_dec_rec): the records of one block OR their 2-bit codes into
+// a word buffer (LDS) covering output characters [32 w_lo, 32 (w_lo + words)), with a mask of
+// the characters written; then every staged word goes out as ASCII exactly once (whole words
+// with two 16-byte stores, words shared with other blocks byte by byte: records never share
+// a byte).  No global atomics, no 2-bit round trip through HBM.
+constexpr uint32_t kDecStageWords = 1024;  // 32 K characters per block of 256 records
+struct StageWriter {
+    uint64_t *bits;  // word t: codes of characters 32 (w_lo + t) ... + 31
+    uint32_t *mask;  // bit i of word t: character 32 (w_lo + t) + i is staged
+    uint64_t w_lo;
+    NTC_HD void put_part(uint64_t word, uint64_t b, uint32_t m) {
+        const uint64_t t = word - w_lo;
+#ifdef __HIP_DEVICE_COMPILE__
+        atomicOr(reinterpret_cast<unsigned long long *>(bits + t), (unsigned long long)b);
+        atomicOr(mask + t, m);
+#else
+        bits[t] |= b;
+        mask[t] |= m;
+#endif
+    }
+    // n <= 32 codes (code t at bits 2t) for characters [g, g + n)
+    NTC_HD void put(uint64_t g, uint64_t codes, uint32_t n) {
+        if (n == 0) return;
+        if (n < 32) codes &= (1ULL << (2 * n)) - 1;
+        const uint64_t w0 = g >> 5, w1 = (g + n - 1) >> 5;
+        const uint32_t sh = (uint32_t)(g & 31);
+        const uint32_t cm = n < 32 ? (1u << n) - 1u : 0xFFFFFFFFu;
+        if (w1 != w0) put_part(w1, codes >> (64 - 2 * sh), cm >> (32 - sh));  // crossing: sh > 0
+        put_part(w0, codes << (2 * sh), cm << sh);
+    }
+};
+
+// ASCII of staged word wg (global word index) to out: the masked characters only
+NTC_HD void stage_store_word(uint8_t *out, uint64_t wg, uint64_t bits, uint32_t mask) {
+    if (!mask) return;
+    uint8_t *o = out + 32 * wg;
+    if (mask == 0xFFFFFFFFu) {
+#ifdef __HIP_DEVICE_COMPILE__
+        if ((((uintptr_t)o) & 15) == 0) {
+            uint32_t v[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const uint32_t x = (uint32_t)(bits >> (8 * q)) & 0xFFu;
+                const uint32_t spread = (x & 3u) | ((x & 0xCu) << 6) | ((x & 0x30u) << 12) | ((x & 0xC0u) << 18);
+                v[q] = __builtin_amdgcn_perm(0u, 0x54474341u, spread);
+            }
+            reinterpret_cast<uint4 *>(o)[0] = make_uint4(v[0], v[1], v[2], v[3]);
+            reinterpret_cast<uint4 *>(o)[1] = make_uint4(v[4], v[5], v[6], v[7]);
+            return;
+        }
+#endif
+        store_codes(o, bits, 32);
+        return;
+    }
+    for (uint32_t i = 0; i < 32; i++)
+        if ((mask >> i) & 1u) o[i] = base_char((uint32_t)(bits >> (2 * i)));
+}
+
 // The L characters of the L-step inverse walk from node j, to output characters
-// [g0, g0 + L) of a CodeWriter; false on a malformed record.
-NTC_HD bool walk_record_codes(const DevIndex &ix, uint32_t j, uint32_t L, uint64_t g0, CodeWriter &cw) {
+// [g0, g0 + L) of a code writer (CodeWriter or StageWriter); false on a malformed record.
+template <class Writer>
+NTC_HD bool walk_record_codes(const DevIndex &ix, uint32_t j, uint32_t L, uint64_t g0, Writer &cw) {
     uint32_t end = L, cur = j;
     while (end > 0) {
         if (cur >= ix.n) return false;

@@ -79,7 +79,6 @@ struct DecWalkArgs {
     const uint64_t *E;
     const uint64_t *offs_out;    // each read's output offset [nreads + 1]
     uint8_t *out;
-    uint64_t *O2;                // zeroed 2-bit output (k_dec_rec -> k_dec_expand)
     unsigned long long *status;
 };
 
@@ -99,8 +98,6 @@ void launch_debug_gather(const DebugArgs &a, hipStream_t s);
 // fscan + E + read starts/offsets in one reduce + apply pass (tmp: 4 * tiles + 2 + scan_tmp_words)
 void launch_dec_index_fused(const DecIndexArgs &a, uint64_t *fscan, uint64_t *E, uint64_t *tmp, hipStream_t s);
 void launch_dec_walk(const DecWalkArgs &a, hipStream_t s);
-void launch_dec_expand(const uint64_t *E, uint64_t n, uint64_t max_bases, uint64_t *O2, uint8_t *out,
-                       const unsigned long long *status, hipStream_t s);
 void launch_walk_build(const uint32_t *pred, const uint8_t *code, uint64_t n, WalkEntry *a, WalkEntry *b,
                        WalkEntry **result, hipStream_t s);
 uint64_t scan_tmp_words(uint64_t n);

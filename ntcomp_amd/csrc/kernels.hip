@@ -321,52 +321,69 @@ __global__ __launch_bounds__(256) void k_debug_gather(DebugArgs a) {
 // read's records are consumed last to first (lib.rs:266), so record r of read rid lands at
 // start(rid) + (end(rid) - E[r + 1]), with E the exclusive scan of lengths in record order
 // and start/end(rid) the read's output range (offs_out, written by k_dec_apply).
-// Characters go to the zeroed 2-bit array O2 (CodeWriter); k_dec_expand writes ASCII.
+// Output is staged per block (StageWriter): the block's
+// records cover a contiguous stretch of output words (with at most a few words shared with
+// neighbouring blocks); codes are OR-ed into LDS, then the block writes each word's ASCII once.
+// A block whose stretch exceeds kDecStageWords (very long records) writes ASCII directly.
 __global__ __launch_bounds__(256) void k_dec_rec(DecWalkArgs a) {
+    __shared__ uint64_t s_bits[kDecStageWords];
+    __shared__ uint32_t s_mask[kDecStageWords];
+    __shared__ uint64_t s_lo[4], s_hi[4];
+    if (*a.status != ~0ull) return;  // same value for the whole block
     const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (r >= a.n) return;
-    if (*a.status != ~0ull) return;
-    const uint64_t rid = a.fscan[r];  // read id of record r (k_dec_apply)
-    const uint64_t w = a.recs[r];
-    const uint32_t flag = (uint32_t)(w >> 56);
-    const uint32_t L = (flag & 2) ? (flag >> 2) : ((uint32_t)(w >> 32) & 0xFFFFFFu);
-    const uint64_t g0 = a.offs_out[rid] + (a.offs_out[rid + 1] - (a.E[r] + L));
-    CodeWriter cw{a.O2, g0, g0 + L, ~0ULL, 0};
-    if (flag & 2) {
-        cw.put(g0, w, L);
-    } else if (!walk_record_codes(a.ix, (uint32_t)w, L, g0, cw)) {
-        atomicMin(a.status, (unsigned long long)((rid << 8) | (uint64_t)kErrFormat));
+    uint64_t rid = 0, w = 0, g0 = 0;
+    uint32_t L = 0;
+    if (r < a.n) {
+        rid = a.fscan[r];  // read id of record r (k_dec_apply)
+        w = a.recs[r];
+        const uint32_t flag = (uint32_t)(w >> 56);
+        L = (flag & 2) ? (flag >> 2) : ((uint32_t)(w >> 32) & 0xFFFFFFu);
+        g0 = a.offs_out[rid] + (a.offs_out[rid + 1] - (a.E[r] + L));
+    }
+    // the block's output stretch [lo, hi)
+    uint64_t lo = L ? g0 : ~0ULL, hi = L ? g0 + L : 0;
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t l2 = __shfl_xor(lo, o, 64), h2 = __shfl_xor(hi, o, 64);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        s_lo[threadIdx.x >> 6] = lo;
+        s_hi[threadIdx.x >> 6] = hi;
+    }
+    __syncthreads();
+    for (int q = 0; q < 4; q++) {
+        lo = s_lo[q] < lo ? s_lo[q] : lo;
+        hi = s_hi[q] > hi ? s_hi[q] : hi;
+    }
+    if (lo >= hi) return;  // no characters in this block
+    const bool is_short = ((w >> 56) & 2) != 0;
+    const uint64_t w_lo = lo >> 5, nw = ((hi - 1) >> 5) - w_lo + 1;
+    if (nw > kDecStageWords) {  // whole block: direct ASCII
+        if (L) {
+            if (is_short) store_codes(a.out + g0, w, L);
+            else if (!walk_record(a.ix, (uint32_t)w, L, a.out + g0))
+                atomicMin(a.status, (unsigned long long)((rid << 8) | (uint64_t)kErrFormat));
+        }
         return;
     }
-    cw.flush();
+    for (uint32_t t = threadIdx.x; t < nw; t += 256) {
+        s_bits[t] = 0;
+        s_mask[t] = 0;
+    }
+    __syncthreads();
+    StageWriter sw{s_bits, s_mask, w_lo};
+    if (L) {
+        if (is_short) sw.put(g0, w, L);
+        else if (!walk_record_codes(a.ix, (uint32_t)w, L, g0, sw))
+            atomicMin(a.status, (unsigned long long)((rid << 8) | (uint64_t)kErrFormat));
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < nw; t += 256) stage_store_word(a.out, w_lo + t, s_bits[t], s_mask[t]);
 }
 
 // 2-bit output -> ASCII, 32 characters per thread (two 16-byte stores when the output is
 // 16-byte aligned, the common case), then re-zero the word for the next call
-__global__ __launch_bounds__(256) void k_dec_expand(const uint64_t *E, uint64_t n, uint64_t *O2, uint8_t *out,
-                                                    const unsigned long long *status) {
-    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    const uint64_t total = E[n];
-    if (t * 32 >= total) return;
-    const uint64_t codes = O2[t];
-    O2[t] = 0;
-    if (*status != ~0ull) return;
-    const uint32_t cnt = total - t * 32 < 32 ? (uint32_t)(total - t * 32) : 32u;
-    uint8_t *o = out + t * 32;
-    if (cnt == 32 && (((uintptr_t)out) & 15) == 0) {
-        uint32_t v[8];
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            const uint32_t x = (uint32_t)(codes >> (8 * q)) & 0xFFu;
-            const uint32_t spread = (x & 3u) | ((x & 0xCu) << 6) | ((x & 0x30u) << 12) | ((x & 0xC0u) << 18);
-            v[q] = __builtin_amdgcn_perm(0u, 0x54474341u, spread);
-        }
-        reinterpret_cast<uint4 *>(o)[0] = make_uint4(v[0], v[1], v[2], v[3]);
-        reinterpret_cast<uint4 *>(o)[1] = make_uint4(v[4], v[5], v[6], v[7]);
-        return;
-    }
-    for (uint32_t i = 0; i < cnt; i++) o[i] = base_char((uint32_t)(codes >> (2 * i)));
-}
 
 // ---------------------------------------------------------------------------------
 // walk table: W_{2m}(j) = W_m(pred^m(j)) . W_m(j)
@@ -729,10 +746,6 @@ void launch_debug_gather(const DebugArgs &a, hipStream_t s) {
 }
 void launch_dec_walk(const DecWalkArgs &a, hipStream_t s) {
     hipLaunchKernelGGL(k_dec_rec, grid_for(a.n), dim3(256), 0, s, a);
-}
-void launch_dec_expand(const uint64_t *E, uint64_t n, uint64_t max_bases, uint64_t *O2, uint8_t *out,
-                       const unsigned long long *status, hipStream_t s) {
-    hipLaunchKernelGGL(k_dec_expand, grid_for((max_bases + 31) / 32), dim3(256), 0, s, E, n, O2, out, status);
 }
 void launch_walk_build(const uint32_t *pred, const uint8_t *code, uint64_t n, WalkEntry *a, WalkEntry *b,
                        WalkEntry **result, hipStream_t s) {

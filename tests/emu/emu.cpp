@@ -200,8 +200,9 @@ extern "C" int emu_decode(const ntc_index_view *v, const uint64_t *recs, uint64_
     std::vector<uint16_t> pairb;
     DevIndex d;
     if (!load(v, hx, dv, walk, d, tab, bits, fbits, pairb, 1)) return NTC_ERR_FORMAT;
-    // the kernels' decode: per record, 2-bit codes via CodeWriter, then ASCII (k_dec_rec +
-    // k_dec_expand); a read's records are consumed last to first (lib.rs:266)
+    // the kernel's decode (k_dec_rec): blocks of 256 records (NTC_EMU_STAGE_BLOCK), each
+    // record's 2-bit codes staged per block (StageWriter), then ASCII per staged word; a read's
+    // records are consumed last to first (lib.rs:266)
     std::vector<uint64_t> starts, lens(n), E(n + 1, 0);
     for (uint64_t r = 0; r < n; r++) {
         const uint32_t flag = (uint32_t)(recs[r] >> 56);
@@ -213,21 +214,47 @@ extern "C" int emu_decode(const ntc_index_view *v, const uint64_t *recs, uint64_
     if (total > cap || starts.size() + 1 > offcap) return NTC_ERR_CAPACITY;
     if (n && (starts.empty() || starts[0] != 0)) return NTC_ERR_FORMAT;
     starts.push_back(n);
-    std::vector<uint64_t> O2(total / 32 + 2, 0);
+    std::vector<uint64_t> g0s(n);
     offs[0] = 0;
     for (size_t i = 0; i + 1 < starts.size(); i++) {
         const uint64_t rb = starts[i], re = starts[i + 1];
-        for (uint64_t r = rb; r < re; r++) {
-            const uint64_t g0 = E[rb] + (E[re] - E[r + 1]);
-            CodeWriter cw{O2.data(), g0, g0 + lens[r], ~0ULL, 0};
-            const uint64_t w = recs[r];
-            if ((w >> 56) & 2) cw.put(g0, w, (uint32_t)lens[r]);
-            else if (!walk_record_codes(d, (uint32_t)w, (uint32_t)lens[r], g0, cw)) return NTC_ERR_FORMAT;
-            cw.flush();
-        }
+        for (uint64_t r = rb; r < re; r++) g0s[r] = E[rb] + (E[re] - E[r + 1]);
         offs[i + 1] = E[re];
     }
-    for (uint64_t g = 0; g < total; g++) out[g] = base_char((uint32_t)(O2[g >> 5] >> (2 * (g & 31))));
+    const char *sbe = getenv("NTC_EMU_STAGE_BLOCK");
+    const uint64_t stage_block = sbe && atoi(sbe) > 0 ? (uint64_t)atoi(sbe) : 256;
+    std::vector<uint64_t> sb(kDecStageWords);
+    std::vector<uint32_t> sm(kDecStageWords);
+    for (uint64_t b0 = 0; b0 < n; b0 += stage_block) {
+        const uint64_t b1 = std::min<uint64_t>(n, b0 + stage_block);
+        uint64_t lo = ~0ULL, hi = 0;
+        for (uint64_t r = b0; r < b1; r++)
+            if (lens[r]) {
+                lo = std::min(lo, g0s[r]);
+                hi = std::max(hi, g0s[r] + lens[r]);
+            }
+        if (lo >= hi) continue;
+        const uint64_t w_lo = lo >> 5, nw = ((hi - 1) >> 5) - w_lo + 1;
+        if (nw > kDecStageWords) {  // direct ASCII
+            for (uint64_t r = b0; r < b1; r++) {
+                if (!lens[r]) continue;
+                const uint64_t w = recs[r];
+                if ((w >> 56) & 2) store_codes(out + g0s[r], w, (uint32_t)lens[r]);
+                else if (!walk_record(d, (uint32_t)w, (uint32_t)lens[r], out + g0s[r])) return NTC_ERR_FORMAT;
+            }
+            continue;
+        }
+        std::fill(sb.begin(), sb.begin() + nw, 0);
+        std::fill(sm.begin(), sm.begin() + nw, 0);
+        StageWriter sw{sb.data(), sm.data(), w_lo};
+        for (uint64_t r = b0; r < b1; r++) {
+            if (!lens[r]) continue;
+            const uint64_t w = recs[r];
+            if ((w >> 56) & 2) sw.put(g0s[r], w, (uint32_t)lens[r]);
+            else if (!walk_record_codes(d, (uint32_t)w, (uint32_t)lens[r], g0s[r], sw)) return NTC_ERR_FORMAT;
+        }
+        for (uint64_t t = 0; t < nw; t++) stage_store_word(out, w_lo + t, sb[t], sm[t]);
+    }
     *nreads = starts.size() - 1;
     return NTC_OK;
 }

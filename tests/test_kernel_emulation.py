@@ -141,3 +141,20 @@ def test_emulated_periodic_genome_cycles(k):
     for paths in (True, False):
         got, goff = emu_encode(ix.n, k, ix.rows, ix.C, ix.lcs, reads, offs, use_paths=paths)
         assert np.array_equal(goff, eoff) and np.array_equal(got, exp)
+
+
+@pytest.mark.parametrize("block", [1, 3, 7, 256])
+def test_emulated_staged_decode_block_sizes(block, monkeypatch):
+    # k_dec_rec stages a block's output words in LDS and writes words shared with other
+    # blocks character by character: tiny blocks make almost every word such a shared word
+    monkeypatch.setenv("NTC_EMU_STAGE_BLOCK", str(block))
+    genome = nt.synth_genome(8, 60_000)
+    k = 31
+    ix = nt.Index.build([genome.tobytes()], k)
+    n, L = 300, 150
+    reads = nt.synth_reads(genome, 6, 0, n, L, 20_000)
+    offs = np.arange(0, n * L + 1, L, dtype=np.uint64)
+    got, _ = OracleIndex(ix.n, k, ix.rows, ix.C, ix.lcs).encode(reads, offs)
+    out, oo = emu_decode(ix.n, k, ix.rows, ix.C, ix.lcs, got)
+    assert np.array_equal(out, reads)
+    assert np.array_equal(oo, offs)
