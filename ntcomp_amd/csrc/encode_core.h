@@ -1322,46 +1322,6 @@ NTC_HD void store_codes(uint8_t *out, uint64_t codes, uint32_t n) {
     for (; i < n; i++) out[i] = base_char((uint32_t)(codes >> (2 * i)));
 }
 
-// 2-bit output writer for the decode walk: pieces arrive right to left; one word is
-// accumulated in registers and written when the writer moves left of it -- a plain store
-// when the word lies inside this record's range [lo, hi) (in characters), atomicOr for
-// the (at most two) boundary words shared with neighbouring records.
-struct CodeWriter {
-    uint64_t *O;        // zeroed 2-bit output, character g at bits 2(g%32) of word g/32
-    uint64_t lo, hi;    // this record's characters
-    uint64_t w;         // word being accumulated (~0: none)
-    uint64_t acc;
-    NTC_HD void flush() {
-        if (w == ~0ULL) return;
-        if (w * 32 >= lo && w * 32 + 32 <= hi) {
-            O[w] = acc;
-        } else {
-#ifdef __HIP_DEVICE_COMPILE__
-            atomicOr(reinterpret_cast<unsigned long long *>(O + w), (unsigned long long)acc);
-#else
-            O[w] |= acc;
-#endif
-        }
-    }
-    NTC_HD void put_word_part(uint64_t word, uint64_t bits) {
-        if (word != w) {
-            flush();
-            w = word;
-            acc = 0;
-        }
-        acc |= bits;
-    }
-    // n <= 32 codes (code t at bits 2t) for characters [g, g + n)
-    NTC_HD void put(uint64_t g, uint64_t codes, uint32_t n) {
-        if (n == 0) return;
-        if (n < 32) codes &= (1ULL << (2 * n)) - 1;
-        const uint64_t w0 = g >> 5, w1 = (g + n - 1) >> 5;
-        const uint32_t sh = (uint32_t)(g & 31) * 2;
-        if (w1 != w0) put_word_part(w1, codes >> (64 - sh));  // right part first
-        put_word_part(w0, codes << sh);
-    }
-};
-
 // Block-staged decode output (k_dec_rec): the records of one block OR their 2-bit codes into
 // a word buffer (LDS) covering output characters [32 w_lo, 32 (w_lo + words)), with a mask of
 // the characters written; then every staged word goes out as ASCII exactly once (whole words
@@ -1421,7 +1381,7 @@ NTC_HD void stage_store_word(uint8_t *out, uint64_t wg, uint64_t bits, uint32_t 
 }
 
 // The L characters of the L-step inverse walk from node j, to output characters
-// [g0, g0 + L) of a code writer (CodeWriter or StageWriter); false on a malformed record.
+// [g0, g0 + L) of a code writer (StageWriter); false on a malformed record.
 template <class Writer>
 NTC_HD bool walk_record_codes(const DevIndex &ix, uint32_t j, uint32_t L, uint64_t g0, Writer &cw) {
     uint32_t end = L, cur = j;
