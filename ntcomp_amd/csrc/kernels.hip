@@ -814,11 +814,31 @@ __global__ __launch_bounds__(256) void k_path_cut(PathArgs a, const uint4 *st, u
     }
 }
 
+// path length = max rank + 1 over the path's nodes.  A wave's nodes mostly lie on one path
+// (a few paths cover the whole graph), so the max is taken per distinct path in the wave
+// first: one atomicMax per (wave, path) instead of one per node on the same few addresses.
 __global__ __launch_bounds__(256) void k_path_len(PathArgs a, const uint4 *st, uint32_t *len) {
     const uint32_t z = blockIdx.x * 256u + threadIdx.x;
-    if (z == 0 || z >= a.n || path_dummy(a.dummy, z)) return;
-    const uint4 e = st[z];
-    atomicMax(len + e.x, e.y + 1);
+    const bool valid = !(z == 0 || z >= a.n || path_dummy(a.dummy, z));
+    uint32_t key = 0xFFFFFFFFu, val = 0;
+    if (valid) {
+        const uint4 e = st[z];
+        key = e.x;
+        val = e.y + 1;
+    }
+    uint64_t todo = __ballot(valid);
+    while (todo) {
+        const uint32_t lead = (uint32_t)__builtin_ctzll(todo);
+        const uint32_t k0 = __shfl(key, lead, 64);
+        const bool mine = valid && key == k0;
+        uint32_t v = mine ? val : 0u;
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint32_t t = __shfl_xor(v, o, 64);
+            v = t > v ? t : v;
+        }
+        if ((threadIdx.x & 63) == lead) atomicMax(len + k0, v);
+        todo &= ~__ballot(mine);
+    }
 }
 
 __global__ __launch_bounds__(256) void k_path_vals(PathArgs a, const uint32_t *prv, const uint32_t *len,
