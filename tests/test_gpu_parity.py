@@ -362,3 +362,29 @@ def test_gpu_scan_exact_test_paths(ctx, k, tab_u, pair_bytes):
     finally:
         ctx.set_option("pair_bytes", 1)
         ctx.set_option("tab_u", 0)
+
+
+def test_gpu_decode_direct_path_for_long_records(ctx):
+    """Error-free 30-50 kb reads: one or two records each, so a block of 256 records spans
+    far more than kDecStageWords output words and k_dec_rec writes ASCII directly (its
+    fallback path), next to blocks that stage through LDS (the short-read batch after it)."""
+    genome = nt.synth_genome(17, 300_000)
+    ix = nt.Index.build([genome.tobytes()], 31)
+    ctx.upload(ix)
+    rng = np.random.default_rng(9)
+    g = genome.tobytes()
+    reads = []
+    for _ in range(120):
+        L = int(rng.integers(30_000, 50_000))
+        st = int(rng.integers(0, len(g) - L))
+        reads.append(g[st:st + L])
+    reads += [g[i * 7:i * 7 + 150] for i in range(600)]  # then short reads: staged blocks
+    bases, offs = pack_reads(reads)
+    exp, eoff = OracleIndex(ix.n, 31, ix.rows, ix.C, ix.lcs).encode(bases, offs)
+    got, goff = ctx.encode(bases, offs)
+    assert np.array_equal(goff, eoff) and np.array_equal(got, exp)
+    longm = ((got >> np.uint64(56)) & np.uint64(2)) == 0
+    lens = (got[longm] >> np.uint64(32)) & np.uint64(0xFFFFFF)
+    assert int(lens.max()) > 32 * 1024  # records longer than a whole staging buffer
+    out, o2 = ctx.decode(got)
+    assert np.array_equal(out, bases) and np.array_equal(o2, offs)

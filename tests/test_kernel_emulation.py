@@ -158,3 +158,21 @@ def test_emulated_staged_decode_block_sizes(block, monkeypatch):
     out, oo = emu_decode(ix.n, k, ix.rows, ix.C, ix.lcs, got)
     assert np.array_equal(out, reads)
     assert np.array_equal(oo, offs)
+
+
+@pytest.mark.parametrize("block", [1, 4, 256])
+def test_emulated_decode_direct_path_for_long_records(block, monkeypatch):
+    # error-free 40 kb reads give ~one 40,000-base record each: more than kDecStageWords
+    # (1024 words = 32 K bases) per block, so the decode writes ASCII directly
+    monkeypatch.setenv("NTC_EMU_STAGE_BLOCK", str(block))
+    genome = nt.synth_genome(18, 120_000)
+    k = 31
+    ix = nt.Index.build([genome.tobytes()], k)
+    g = genome.tobytes()
+    reads = [g[s:s + 40_000] for s in (0, 5_000, 31_000, 77_000)]
+    bases = np.frombuffer(b"".join(reads), dtype=np.uint8).copy()
+    offs = np.arange(0, 4 * 40_000 + 1, 40_000, dtype=np.uint64)
+    got, _ = OracleIndex(ix.n, k, ix.rows, ix.C, ix.lcs).encode(bases, offs)
+    out, oo = emu_decode(ix.n, k, ix.rows, ix.C, ix.lcs, got)
+    assert np.array_equal(out, bases)
+    assert np.array_equal(oo, offs)
