@@ -747,41 +747,37 @@ int ntc_decode_batch_device(ntc_ctx *ctx, const uint64_t *d_recs, uint64_t n_rec
     if (!ctx || (!d_recs && n_recs) || !d_read_offsets_out) return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument");
     if (!ctx->has_index) return set_err(ctx, NTC_ERR_NO_INDEX, "no index uploaded");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    void *fscan, *E, *tmp;
+    void *ws, *tmp;
     int rc;
     const uint64_t n = n_recs;
-    if ((rc = ensure(ctx, WS_DEC_C, (n + 1) * 8 * 2, &fscan))) return rc;
-    E = (uint64_t *)fscan + (n + 1);
-    if ((rc = ensure(ctx, WS_SCANTMP, (4 * (n / 2048 + 2) + scan_tmp_words(n / 2048 + 2)) * 8, &tmp)))
-        return rc;
+    // per 256-record tile: pf, pl (sums) then pfs, pls (exclusive scans, totals at [tiles])
+    const uint64_t tiles = (n + 255) / 256;
+    if ((rc = ensure(ctx, WS_DEC_C, (4 * tiles + 2) * 8, &ws))) return rc;
+    uint64_t *pf = (uint64_t *)ws, *pl = pf + tiles, *pfs = pl + tiles, *pls = pfs + tiles + 1;
+    if ((rc = ensure(ctx, WS_SCANTMP, (scan_tmp_words(tiles + 1) + 2) * 8, &tmp))) return rc;
     HIP_TRY(ctx, hipMemsetAsync(ctx->d_status, 0xFF, 8, ctx->stream));
     ctx->last = kDecode;
-    ctx->last_n = n;
-    ctx->last_out_offs = (uint64_t *)fscan;  // fscan[n] = reads, E[n] = bases
+    ctx->last_n = tiles;
+    ctx->last_out_offs = pfs;  // pfs[tiles] = reads, pls[tiles] = bases (ntc_decode_status)
     HIP_TRY(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
     if (n == 0) {
-        HIP_TRY(ctx, hipMemsetAsync(fscan, 0, (n + 1) * 16, ctx->stream));
+        HIP_TRY(ctx, hipMemsetAsync(pfs, 0, 16, ctx->stream));
         HIP_TRY(ctx, hipMemsetAsync(d_read_offsets_out, 0, 8, ctx->stream));
         for (int i = 1; i < 4; i++) HIP_TRY(ctx, hipEventRecord(ctx->ev[i], ctx->stream));
         return NTC_OK;
     }
-    DecIndexArgs ia{};
-    ia.recs = d_recs;
-    ia.n = n;
-    ia.offs_out = d_read_offsets_out;
-    ia.offs_capacity = offsets_capacity;
-    ia.bases_capacity = bases_capacity;
-    ia.status = ctx->d_status;
-    launch_dec_index_fused(ia, (uint64_t *)fscan, (uint64_t *)E, (uint64_t *)tmp, ctx->stream);
+    launch_dec_tiles(d_recs, n, pf, pl, pfs, pls, (uint64_t *)tmp, ctx->stream);
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
     DecWalkArgs wa{};
     wa.ix = ctx->dix;
     wa.recs = d_recs;
     wa.n = n;
-    wa.fscan = (const uint64_t *)fscan;
-    wa.E = (const uint64_t *)E;
+    wa.pfs = pfs;
+    wa.pls = pls;
     wa.offs_out = d_read_offsets_out;
+    wa.offs_capacity = offsets_capacity;
+    wa.bases_capacity = bases_capacity;
     wa.out = d_bases_out;
     wa.status = ctx->d_status;
     launch_dec_walk(wa, ctx->stream);

@@ -62,22 +62,15 @@ struct DebugArgs {
     uint32_t *s_out;
 };
 
-struct DecIndexArgs {
-    const uint64_t *recs;
-    uint64_t n;
-    uint64_t *offs_out;      // caller's read offsets
-    uint64_t offs_capacity;
-    uint64_t bases_capacity;
-    unsigned long long *status;
-};
-
 struct DecWalkArgs {
     DevIndex ix;
     const uint64_t *recs;
     uint64_t n;
-    const uint64_t *fscan;       // read id of each record
-    const uint64_t *E;
-    const uint64_t *offs_out;    // each read's output offset [nreads + 1]
+    const uint64_t *pfs;         // per 256-record tile: first records before it [tiles + 1]
+    const uint64_t *pls;         // per 256-record tile: bases before it [tiles + 1]
+    uint64_t *offs_out;          // each read's output offset [nreads + 1] (written here)
+    uint64_t offs_capacity;
+    uint64_t bases_capacity;
     uint8_t *out;
     unsigned long long *status;
 };
@@ -95,8 +88,11 @@ void launch_tab_build(const DevIndex &ix, uint32_t U, uint2 *tab, uint32_t *bits
 void launch_tile_rows(const uint64_t *offs, uint64_t n_reads, uint32_t *tile_rows, hipStream_t s);
 void launch_emit(const EmitArgs &a, hipStream_t s);
 void launch_debug_gather(const DebugArgs &a, hipStream_t s);
-// fscan + E + read starts/offsets in one reduce + apply pass (tmp: 4 * tiles + 2 + scan_tmp_words)
-void launch_dec_index_fused(const DecIndexArgs &a, uint64_t *fscan, uint64_t *E, uint64_t *tmp, hipStream_t s);
+// decode: per 256-record tile sums (firsts, bases) and their exclusive scans (pfs, pls:
+// tiles + 1 words each; pf, pl: tiles words each; tmp: scan_tmp_words(tiles)), then the
+// walk kernel, which derives every record's read and output offset itself
+void launch_dec_tiles(const uint64_t *recs, uint64_t n, uint64_t *pf, uint64_t *pl, uint64_t *pfs, uint64_t *pls,
+                      uint64_t *tmp, hipStream_t s);
 void launch_dec_walk(const DecWalkArgs &a, hipStream_t s);
 void launch_walk_build(const uint32_t *pred, const uint8_t *code, uint64_t n, WalkEntry *a, WalkEntry *b,
                        WalkEntry **result, hipStream_t s);

@@ -314,13 +314,55 @@ __global__ __launch_bounds__(256) void k_debug_gather(DebugArgs a) {
     }
 }
 
+// ---- decode index: per 256-record tile, the number of first records and of bases --------
+__device__ __forceinline__ void dec_desc(uint64_t w, uint64_t &f, uint64_t &len) {
+    const uint32_t flag = (uint32_t)(w >> 56);
+    f = flag & 1u;
+    len = (flag & 2u) ? (flag >> 2) : ((uint32_t)(w >> 32) & 0xFFFFFFu);
+}
+
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+constexpr uint32_t kDecTileRecs = 256;  // = k_dec_rec's block
+
+// one wave per tile: 4 coalesced loads per lane, wave sums
+__global__ __launch_bounds__(256) void k_dec_tiles(const uint64_t *recs, uint64_t n, uint64_t *pf, uint64_t *pl) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t * kDecTileRecs >= n) return;  // whole wave
+    uint64_t sf = 0, sl = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kDecTileRecs / 64; q++) {
+        const uint64_t r = t * kDecTileRecs + q * 64 + lane;
+        if (r < n) {
+            uint64_t f, l;
+            dec_desc(recs[r], f, l);
+            sf += f;
+            sl += l;
+        }
+    }
+    sf = wave_sum64(sf);
+    sl = wave_sum64(sl);
+    if (lane == 0) {
+        pf[t] = sf;
+        pl[t] = sl;
+    }
+}
+
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t &total);
+
 // ---------------------------------------------------------------------------------
 // decode
 // ---------------------------------------------------------------------------------
 // one lane per RECORD: records are independent once their output offsets are known.  A
 // read's records are consumed last to first (lib.rs:266), so record r of read rid lands at
 // start(rid) + (end(rid) - E[r + 1]), with E the exclusive scan of lengths in record order
-// and start/end(rid) the read's output range (offs_out, written by k_dec_apply).
+// and start/end(rid) the read's output range.  Each block derives E, rid and the ranges of
+// its 256 records from the tile scans (k_dec_tiles) plus a block scan; the read open at the
+// tile start and the read running past its end are found by scanning records outward.
 // Output is staged per block (StageWriter): the block's
 // records cover a contiguous stretch of output words (with at most a few words shared with
 // neighbouring blocks); codes are OR-ed into LDS, then the block writes each word's ASCII once.
@@ -329,16 +371,79 @@ __global__ __launch_bounds__(256) void k_dec_rec(DecWalkArgs a) {
     __shared__ uint64_t s_bits[kDecStageWords];
     __shared__ uint32_t s_mask[kDecStageWords];
     __shared__ uint64_t s_lo[4], s_hi[4];
+    __shared__ uint64_t s_start[kDecTileRecs];  // output offset of each read starting in the tile
+    __shared__ uint64_t s_open[2];              // start of the read open at the tile start, end of the last read
     if (*a.status != ~0ull) return;  // same value for the whole block
-    const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    uint64_t rid = 0, w = 0, g0 = 0;
-    uint32_t L = 0;
-    if (r < a.n) {
-        rid = a.fscan[r];  // read id of record r (k_dec_apply)
+    const uint64_t n = a.n, tiles = (n + kDecTileRecs - 1) / kDecTileRecs, t = blockIdx.x;
+    const uint64_t reads = a.pfs[tiles], bases = a.pls[tiles];
+    if (reads + 1 > a.offs_capacity || bases > a.bases_capacity) {  // every block: nothing is written
+        if (t == 0 && threadIdx.x == 0) atomicMin(a.status, (unsigned long long)kErrCapacity);
+        return;
+    }
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t r0 = t * kDecTileRecs, r = r0 + threadIdx.x;
+    const uint64_t r1 = r0 + kDecTileRecs < n ? r0 + kDecTileRecs : n;
+    uint64_t w = 0, f = 0, len = 0;
+    if (r < n) {
         w = a.recs[r];
-        const uint32_t flag = (uint32_t)(w >> 56);
-        L = (flag & 2) ? (flag >> 2) : ((uint32_t)(w >> 32) & 0xFFFFFFu);
-        g0 = a.offs_out[rid] + (a.offs_out[rid + 1] - (a.E[r] + L));
+        dec_desc(w, f, len);
+    }
+    // E[r] (bases before record r) and the read of r, from the tile scans + a block scan
+    uint64_t tf, tl;
+    const uint64_t ef = block_excl_scan(f, tf);
+    const uint64_t el = block_excl_scan(len, tl);
+    const uint64_t Er = a.pls[t] + el;
+    const uint64_t rid = a.pfs[t] + ef + f - 1;  // a record belongs to the last first record at or before it
+    const int64_t li = (int64_t)(ef + f) - 1;     // read index within the tile (-1: the read open at r0)
+    if (r < n && f) {
+        s_start[li] = Er;
+        if (rid < a.offs_capacity) a.offs_out[rid] = Er;  // the read's output offset
+    }
+    if (wave == 0) {  // start of the read open at r0: back to its first record
+        uint64_t acc = 0, base = r0;
+        bool open = r0 > 0 && __shfl(f, 0, 64) == 0;
+        while (open) {
+            const int64_t rr = (int64_t)base - 64 + lane;
+            uint64_t ff = 0, ll = 0;
+            if (rr >= 0) dec_desc(a.recs[rr], ff, ll);
+            const uint64_t fb = __ballot(ff != 0);
+            if (fb) {
+                const uint32_t hl = 63u - (uint32_t)__builtin_clzll(fb);  // nearest first record
+                acc += wave_sum64(lane >= hl ? ll : 0);
+                break;
+            }
+            acc += wave_sum64(ll);
+            if (base <= 64) break;  // no first record before r0 (reported below as a format error)
+            base -= 64;
+        }
+        if (lane == 0) s_open[0] = a.pls[t] - acc;
+    } else if (wave == 1) {  // end of the tile's last read: on to the next first record
+        uint64_t acc = 0, base = r1;
+        while (base < n) {
+            const uint64_t rr = base + lane;
+            uint64_t ff = 1, ll = 0;
+            if (rr < n) dec_desc(a.recs[rr], ff, ll);
+            const uint64_t fb = __ballot(ff != 0);
+            if (fb) {
+                const uint32_t fl = (uint32_t)__builtin_ctzll(fb);
+                acc += wave_sum64(lane < fl ? ll : 0);
+                break;
+            }
+            acc += wave_sum64(ll);
+            base += 64;
+        }
+        if (lane == 0) s_open[1] = a.pls[t] + tl + acc;
+    }
+    if (t == 0 && threadIdx.x == 0 && n > 0 && !f)
+        atomicMin(a.status, (unsigned long long)kErrFormat);  // records must start a read
+    if (t + 1 == tiles && threadIdx.x == 0) a.offs_out[reads] = bases;
+    __syncthreads();
+    const uint32_t L = (uint32_t)len;
+    uint64_t g0 = 0;
+    if (r < n) {
+        const uint64_t start = li >= 0 ? s_start[li] : s_open[0];
+        const uint64_t end = li + 1 < (int64_t)tf ? s_start[li + 1] : s_open[1];
+        g0 = start + (end - (Er + len));  // a read's records are consumed last to first (lib.rs:266)
     }
     // the block's output stretch [lo, hi)
     uint64_t lo = L ? g0 : ~0ULL, hi = L ? g0 + L : 0;
@@ -502,129 +607,12 @@ void scan_excl_t(const T *in, uint64_t n, uint64_t *out, uint64_t *tmp, hipStrea
                        (const uint64_t *)part_scan, out);
 }
 
-// ---- decode index: one pass over the record words --------------------------------------
-// Per record: fscan (exclusive count of first records = read id of the NEXT read) and E
-// (exclusive sum of segment lengths = output offset in record order).  The apply pass also
-// records each read's first record and its output offset.
-__device__ __forceinline__ void dec_desc(uint64_t w, uint64_t &f, uint64_t &len) {
-    const uint32_t flag = (uint32_t)(w >> 56);
-    f = flag & 1u;
-    len = (flag & 2u) ? (flag >> 2) : ((uint32_t)(w >> 32) & 0xFFFFFFu);
-}
-
-constexpr int kDecItems = 8;  // records per thread in the decode index scan
-constexpr uint64_t kDecTile = (uint64_t)kScanThreads * kDecItems;
-
-__global__ __launch_bounds__(kScanThreads) void k_dec_reduce(const uint64_t *recs, uint64_t n, uint64_t *pf,
-                                                             uint64_t *pl) {
-    const uint64_t base = (uint64_t)blockIdx.x * kDecTile + threadIdx.x;  // coalesced: order-free sums
-    uint64_t sf = 0, sl = 0;
-#pragma unroll
-    for (int j = 0; j < kDecItems; j++) {
-        const uint64_t r = base + (uint64_t)j * kScanThreads;
-        if (r < n) {
-            uint64_t f, l;
-            dec_desc(recs[r], f, l);
-            sf += f;
-            sl += l;
-        }
-    }
-    uint64_t tf, tl;
-    block_excl_scan(sf, tf);
-    block_excl_scan(sl, tl);
-    if (threadIdx.x == 0) {
-        pf[blockIdx.x] = tf;
-        pl[blockIdx.x] = tl;
-    }
-}
-
-// each wave scans its 512 records as 8 coalesced chunks of 64 (shuffle scan + carry),
-// then the 4 wave totals are combined once per block
-__global__ __launch_bounds__(kScanThreads) void k_dec_apply(DecIndexArgs a, const uint64_t *bf, const uint64_t *bl,
-                                                            uint64_t *fscan, uint64_t *E) {
-    __shared__ uint64_t s_wf[kScanThreads / 64], s_wl[kScanThreads / 64];
-    const uint64_t n = a.n;
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t wbase = (uint64_t)blockIdx.x * kDecTile + (uint64_t)wave * 64 * kDecItems;
-    uint32_t exf[kDecItems];
-    uint64_t exl[kDecItems];
-    uint32_t firsts = 0, cf = 0;
-    uint64_t cl = 0;
-#pragma unroll
-    for (int j = 0; j < kDecItems; j++) {
-        const uint64_t r = wbase + (uint64_t)j * 64 + lane;
-        uint64_t f = 0, l = 0;
-        if (r < n) dec_desc(a.recs[r], f, l);
-        uint32_t incf = (uint32_t)f;
-        uint64_t incl = l;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t tf = __shfl_up(incf, o, 64);
-            const uint64_t tl = shfl_up64(incl, o);
-            if (lane >= (uint32_t)o) {
-                incf += tf;
-                incl += tl;
-            }
-        }
-        exf[j] = cf + incf - (uint32_t)f;
-        exl[j] = cl + incl - l;
-        firsts |= (uint32_t)f << j;
-        cf += __shfl(incf, 63, 64);
-        cl += (uint64_t)__shfl((uint32_t)incl, 63, 64) | ((uint64_t)__shfl((uint32_t)(incl >> 32), 63, 64) << 32);
-    }
-    if (lane == 0) {
-        s_wf[wave] = cf;
-        s_wl[wave] = cl;
-    }
-    __syncthreads();
-    uint64_t of = bf ? bf[blockIdx.x] : 0, ol = bl ? bl[blockIdx.x] : 0, tf = of, tl = ol;
-    for (uint32_t w = 0; w < kScanThreads / 64; w++) {
-        if (w < wave) {
-            of += s_wf[w];
-            ol += s_wl[w];
-        }
-        tf += s_wf[w];
-        tl += s_wl[w];
-    }
-#pragma unroll
-    for (int j = 0; j < kDecItems; j++) {
-        const uint64_t r = wbase + (uint64_t)j * 64 + lane;
-        if (r < n) {
-            const uint64_t rf = of + exf[j], rl = ol + exl[j];
-            const bool first = (firsts >> j) & 1u;
-            fscan[r] = first ? rf : rf - 1;  // read id of record r
-            E[r] = rl;
-            if (first) {  // first record of read rf: its output offset
-                if (rf < a.offs_capacity) a.offs_out[rf] = rl;
-            } else if (r == 0) {
-                atomicMin(a.status, (unsigned long long)kErrFormat);  // records must start a read
-            }
-        }
-    }
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {  // totals (n is inside the last tile)
-        fscan[n] = tf;
-        E[n] = tl;
-        if (tf + 1 > a.offs_capacity || tl > a.bases_capacity)
-            atomicMin(a.status, (unsigned long long)kErrCapacity);
-        else
-            a.offs_out[tf] = tl;
-    }
-}
-
-void launch_dec_index_fused(const DecIndexArgs &a, uint64_t *fscan, uint64_t *E, uint64_t *tmp, hipStream_t s) {
-    const uint64_t n = a.n;
-    const uint64_t nb = (n + kDecTile - 1) / kDecTile;
-    if (nb <= 1) {
-        hipLaunchKernelGGL(k_dec_apply, dim3(1), dim3(kScanThreads), 0, s, a, (const uint64_t *)nullptr,
-                           (const uint64_t *)nullptr, fscan, E);
-        return;
-    }
-    uint64_t *pf = tmp, *pl = tmp + nb, *pfs = pl + nb, *pls = pfs + nb + 1, *t2 = pls + nb + 1;
-    hipLaunchKernelGGL(k_dec_reduce, dim3((uint32_t)nb), dim3(kScanThreads), 0, s, a.recs, n, pf, pl);
-    scan_excl_t<uint64_t>(pf, nb, pfs, t2, s);
-    scan_excl_t<uint64_t>(pl, nb, pls, t2, s);
-    hipLaunchKernelGGL(k_dec_apply, dim3((uint32_t)nb), dim3(kScanThreads), 0, s, a, (const uint64_t *)pfs,
-                       (const uint64_t *)pls, fscan, E);
+void launch_dec_tiles(const uint64_t *recs, uint64_t n, uint64_t *pf, uint64_t *pl, uint64_t *pfs, uint64_t *pls,
+                      uint64_t *tmp, hipStream_t s) {
+    const uint64_t tiles = (n + kDecTileRecs - 1) / kDecTileRecs;
+    hipLaunchKernelGGL(k_dec_tiles, dim3((uint32_t)((tiles + 3) / 4)), dim3(256), 0, s, recs, n, pf, pl);
+    scan_excl_t<uint64_t>(pf, tiles, pfs, tmp, s);
+    scan_excl_t<uint64_t>(pl, tiles, pls, tmp, s);
 }
 
 uint64_t scan_tmp_words(uint64_t n) {
@@ -745,7 +733,8 @@ void launch_debug_gather(const DebugArgs &a, hipStream_t s) {
     hipLaunchKernelGGL(k_debug_gather, grid_for(a.n_reads), dim3(256), 0, s, a);
 }
 void launch_dec_walk(const DecWalkArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL(k_dec_rec, grid_for(a.n), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_dec_rec, dim3((uint32_t)((a.n + kDecTileRecs - 1) / kDecTileRecs)), dim3(kDecTileRecs), 0, s,
+                       a);
 }
 void launch_walk_build(const uint32_t *pred, const uint8_t *code, uint64_t n, WalkEntry *a, WalkEntry *b,
                        WalkEntry **result, hipStream_t s) {
