@@ -24,7 +24,7 @@ def rows(path_glob):
 
 def short(name):
     for k in ("k_encode", "k_ms4", "k_parse4", "k_pack", "k_emit4", "k_dec_rec", "k_emit", "k_scan_apply",
-              "k_scan_reduce", "k_dec_reduce", "k_dec_apply", "k_dec_expand", "k_walk_double", "k_walk_init", "k_tile_rows", "k_tab_level",
+              "k_scan_reduce", "k_dec_tiles", "k_dec_reduce", "k_dec_apply", "k_dec_expand", "k_walk_double", "k_walk_init", "k_tile_rows", "k_tab_level",
               "k_tab_bits"):
         if k in name:
             return k
