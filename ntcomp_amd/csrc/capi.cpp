@@ -68,7 +68,7 @@ constexpr uint64_t kCounterBytes = 8 * 64;  // work queue heads (kernels.hip Wav
 enum WsSlot {
     WS_D = 0, WS_S, WS_F, WS_R, WS_RECCOUNT, WS_SCANTMP, WS_TILEBASE, WS_TILEROWS,
     WS_STAGE_BASES, WS_STAGE_OFFS, WS_STAGE_RECS, WS_E, WS_DEC_A, WS_DEC_B, WS_DEC_C,
-    WS_DEC_D, WS_Q, WS_E3, WS_NE, WS_COUNTER, WS_R2, WS_ED
+    WS_DEC_D, WS_Q, WS_E3, WS_NE, WS_COUNTER, WS_R2, WS_ED, WS_WAVECNT
 };
 
 #define HIP_TRY(ctx, expr)                                                                   \
@@ -165,6 +165,10 @@ int encode4_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, u
     a.R2 = (uint64_t *)p;
     if ((rc = ensure(ctx, WS_RECCOUNT, (n_reads + 1) * 4, &p))) return rc;
     a.rec_count = (uint32_t *)p;
+    const uint64_t waves = (n_reads + 63) / 64;
+    if ((rc = ensure(ctx, WS_WAVECNT, (waves + 1) * 4 + (waves + 2) * 8 + 8, &p))) return rc;
+    a.wave_cnt = (uint32_t *)p;
+    uint64_t *wave_off = (uint64_t *)(((uintptr_t)(a.wave_cnt + waves + 1) + 7) & ~(uintptr_t)7);
     if ((rc = ensure(ctx, WS_COUNTER, kCounterBytes, &p))) return rc;
     a.counter = (unsigned long long *)p;
     void *tmp;
@@ -187,8 +191,7 @@ int encode4_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, u
     if (!bpc) bpc = ms4_blocks_per_cu();
     launch_encode4(a, total_bases, (uint32_t)(ctx->num_cus * bpc), ctx->stream, ctx->ev[3], ctx->ev[1]);
     HIP_TRY(ctx, hipGetLastError());
-    scan_excl_u32(a.rec_count, n_reads, d_rec_offs, (uint64_t *)tmp, ctx->stream);
-    launch_emit4(a, d_rec_offs, d_rec_out, cap, ctx->stream);
+    launch_emit4(a, wave_off, (uint64_t *)tmp, d_rec_offs, d_rec_out, cap, ctx->stream);
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
     return NTC_OK;

@@ -35,6 +35,7 @@ struct Enc4Args {
     uint64_t *R;                 // records past kRecSlot, position space
     uint64_t *R2;                // first kRecSlot records of each read (dense slots)
     uint32_t *rec_count;
+    uint32_t *wave_cnt;          // records of each wave's 64 reads (k_parse4 -> scan -> k_emit4)
     unsigned long long *status;
     unsigned long long *counter; // work queue heads of k_ms4 (WaveQueue, zeroed per call)
 };
@@ -78,8 +79,9 @@ struct DecWalkArgs {
 void launch_encode(const EncodeArgs &a, hipStream_t s);
 void launch_encode4(const Enc4Args &a, uint64_t total, uint32_t ms_blocks, hipStream_t s,
                     hipEvent_t ev_ms_begin, hipEvent_t ev_ms_end);
-void launch_emit4(const Enc4Args &a, const uint64_t *rec_offsets, uint64_t *out, uint64_t capacity,
-                  hipStream_t s);
+// record offsets (rec_offsets[0..n], written here) from the per-wave counts, then records
+void launch_emit4(const Enc4Args &a, uint64_t *wave_off, uint64_t *tmp, uint64_t *rec_offsets, uint64_t *out,
+                  uint64_t capacity, hipStream_t s);
 int ms4_blocks_per_cu();
 void launch_debug_gather4(const Enc4Args &a, uint32_t *d_out, uint32_t *s_out, hipStream_t s);
 void launch_pair_words(const uint2 *top, uint32_t U, uint16_t *out, hipStream_t s);

@@ -169,8 +169,8 @@ struct WaveQueue {
     }
 };
 
-// parse of read r (k_parse4's body)
-__device__ __forceinline__ void parse_one(const Enc4Args &a, uint64_t r) {
+// parse of read r (k_parse4's body); returns its record count (0 on error)
+__device__ __forceinline__ uint32_t parse_one(const Enc4Args &a, uint64_t r) {
     const uint64_t o0 = a.offs[0], b = a.offs[r], e = a.offs[r + 1];
     const uint64_t P = b - o0;
     const int rc = parse_read(a.ix, a.Q, P, a.E + P, a.ne[r], (uint32_t)(e - b), a.R2 + r, a.R + P, a.n_reads,
@@ -178,9 +178,10 @@ __device__ __forceinline__ void parse_one(const Enc4Args &a, uint64_t r) {
     if (rc < 0) {
         atomicMin(a.status, (unsigned long long)((r << 8) | (uint64_t)(-rc)));
         a.rec_count[r] = 0;
-    } else {
-        a.rec_count[r] = (uint32_t)rc;
+        return 0;
     }
+    a.rec_count[r] = (uint32_t)rc;
+    return (uint32_t)rc;
 }
 
 #ifndef NTC_MS_WAVES
@@ -238,21 +239,32 @@ __global__ __launch_bounds__(256, NTC_MS_WAVES) void k_ms4(Enc4Args a) {
 
 __global__ __launch_bounds__(256) void k_parse4(Enc4Args a) {
     const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (r >= a.n_reads) return;
-    if (*a.status != ~0ull) {
-        a.rec_count[r] = 0;
-        return;
+    uint32_t cnt = 0;
+    if (r < a.n_reads) {
+        if (*a.status != ~0ull) a.rec_count[r] = 0;
+        else cnt = parse_one(a, r);
     }
-    parse_one(a, r);
+    // the wave's record total: k_emit4 turns the scanned totals into record offsets
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    if ((threadIdx.x & 63) == 0 && r < a.n_reads) a.wave_cnt[r >> 6] = cnt;
 }
 
-__global__ __launch_bounds__(256) void k_emit4(Enc4Args a, const uint64_t *rec_offsets, uint64_t *out,
-                                               uint64_t capacity) {
+// record offsets = scanned wave totals + a wave scan of the reads' counts
+__global__ __launch_bounds__(256) void k_emit4(Enc4Args a, const uint64_t *wave_off, uint64_t *rec_offsets,
+                                               uint64_t *out, uint64_t capacity) {
     const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t cnt = r < a.n_reads ? a.rec_count[r] : 0u;
+    uint32_t inc = cnt;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(inc, o, 64);
+        if (lane >= (uint32_t)o) inc += t;
+    }
     if (r >= a.n_reads) return;
-    if (*a.status != ~0ull) return;  // a read failed: the call reports that, no output
-    const uint32_t cnt = a.rec_count[r];
-    const uint64_t off = rec_offsets[r];
+    const uint64_t off = wave_off[r >> 6] + (inc - cnt);
+    rec_offsets[r] = off;
+    if (r + 1 == a.n_reads) rec_offsets[r + 1] = off + cnt;
+    if (*a.status != ~0ull) return;  // a read failed: the call reports that, no records
     if (off + cnt > capacity) {
         atomicMin(a.status, (unsigned long long)((r << 8) | (uint64_t)kErrCapacity));
         return;
@@ -717,9 +729,11 @@ void launch_encode4(const Enc4Args &a, uint64_t total, uint32_t ms_blocks, hipSt
     hipLaunchKernelGGL(k_parse4, grid_for(a.n_reads), dim3(256), 0, s, a);
 }
 
-void launch_emit4(const Enc4Args &a, const uint64_t *rec_offsets, uint64_t *out, uint64_t capacity,
-                  hipStream_t s) {
-    hipLaunchKernelGGL(k_emit4, grid_for(a.n_reads), dim3(256), 0, s, a, rec_offsets, out, capacity);
+void launch_emit4(const Enc4Args &a, uint64_t *wave_off, uint64_t *tmp, uint64_t *rec_offsets, uint64_t *out,
+                  uint64_t capacity, hipStream_t s) {
+    scan_excl_u32(a.wave_cnt, (a.n_reads + 63) / 64, wave_off, tmp, s);
+    hipLaunchKernelGGL(k_emit4, grid_for(a.n_reads), dim3(256), 0, s, a, (const uint64_t *)wave_off, rec_offsets,
+                       out, capacity);
 }
 
 void launch_tile_rows(const uint64_t *offs, uint64_t n_reads, uint32_t *tile_rows, hipStream_t s) {
