@@ -20,7 +20,7 @@
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 #ifndef NTC_NT
 #define NTC_NT 17  // streaming (nontemporal) hints, bit mask: 1 table entries, 16 entry stores,
-                   // 2 exact presence bits, 4 path stream, 8 query words (k_ms4)
+                   // 2 exact presence bits, 4 path stream, 8 query words, 32 pair words (k_ms4)
 #endif
 
 // Line tracing for the test-only emulator (tests/emu, -DNTC_TRACE): every index load
@@ -899,7 +899,7 @@ struct MsLane {
                     // (the 32 MB level-U bitmap then stays out of the Infinity Cache entirely)
                     const uint64_t M = key_at(U - 1, U - 1);
                     NTC_TOUCH(kTrBits, ix.pair_w + M);
-                    b2 = (ix.pair_w[M] >> (4 + ((uint32_t)(qw >> (2 * U)) & 3u))) & 1u;
+                    b2 = (ld_hint<32>(ix.pair_w + M) >> (4 + ((uint32_t)(qw >> (2 * U)) & 3u))) & 1u;
                 } else {
                     const uint64_t k2 = key_at(U, U);
                     NTC_TOUCH(kTrBits, ix.tab_bits + (k2 >> 5));
@@ -927,7 +927,7 @@ struct MsLane {
             const uint64_t M = key_at(p - 1, U - 1);
             bc = (uint32_t)(qw >> (2 * (p - qb))) & 3u;
             NTC_TOUCH(kTrBits, ix.pair_w + M);
-            bpw = ix.pair_w[M];
+            bpw = ld_hint<32>(ix.pair_w + M);
             brk = true;
             p += 1;  // a short p: m <= U - 1 skips nothing beyond p itself
             mode = kModeScan;
@@ -996,7 +996,7 @@ struct MsLane {
                     rem &= rem - 1;
                     const uint64_t M = key_at(p + slot[t], U - 1);
                     if ((tested >> slot[t]) & 1u) NTC_TOUCH(kTrBits, ix.pair_w + M);
-                    pbv[t] = ix.pair_w[M];
+                    pbv[t] = ld_hint<32>(ix.pair_w + M);
                 }
                 uint32_t hit = 0, single = 0;
 #pragma unroll
@@ -1160,7 +1160,7 @@ struct MsLane {
                 const uint32_t c = (uint32_t)(qw >> (2 * (p - qb))) & 3u;
                 NTC_TOUCH(kTrBits, ix.pair_w + M);
                 NTC_TOUCH(kTrColex, ix.colex_at + j);
-                const uint32_t pw = ix.pair_w[M];
+                const uint32_t pw = ld_hint<32>(ix.pair_w + M);
                 const uint32_t v = ix.colex_at[j] & 0x7FFFFFFFu;  // node before p, for a long p
                 if (!((pw >> (4 + c)) & 1u)) {
                     p += 1;
