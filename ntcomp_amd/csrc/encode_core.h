@@ -1382,26 +1382,34 @@ NTC_HD void stage_store_word(uint8_t *out, uint64_t wg, uint64_t bits, uint32_t 
 
 // The L characters of the L-step inverse walk from node j, to output characters
 // [g0, g0 + L) of a code writer (StageWriter); false on a malformed record.
+// the characters of one walk entry (chars, older) for output characters ending at g0 + end
+template <class Writer>
+NTC_HD void walk_put(uint32_t &end, uint64_t g0, Writer &cw, uint64_t chars, uint32_t older) {
+    const uint32_t take = end < kWalkSpan ? end : kWalkSpan;
+    const uint32_t t32 = take < 32 ? take : 32;
+    cw.put(g0 + end - t32, t32 ? chars >> (2 * (32 - t32)) : 0, t32);
+    const uint32_t t16 = take - t32;
+    if (t16) cw.put(g0 + end - take, (uint64_t)(older >> (2 * (16 - t16))), t16);
+    end -= take;
+}
+
+NTC_HD WalkEntry walk_at(const DevIndex &ix, uint32_t cur) {
+#ifdef __HIP_DEVICE_COMPILE__
+    const uint4 e4 = *reinterpret_cast<const uint4 *>(ix.walk + cur);
+    return WalkEntry{(uint64_t)e4.x | ((uint64_t)e4.y << 32), e4.z, e4.w};
+#else
+    return ix.walk[cur];
+#endif
+}
+
 template <class Writer>
 NTC_HD bool walk_record_codes(const DevIndex &ix, uint32_t j, uint32_t L, uint64_t g0, Writer &cw) {
     uint32_t end = L, cur = j;
     while (end > 0) {
         if (cur >= ix.n) return false;
-#ifdef __HIP_DEVICE_COMPILE__
-        const uint4 e4 = *reinterpret_cast<const uint4 *>(ix.walk + cur);
-        const uint64_t chars = (uint64_t)e4.x | ((uint64_t)e4.y << 32);
-        const uint32_t jump = e4.z, older = e4.w;
-#else
-        const uint64_t chars = ix.walk[cur].chars;
-        const uint32_t jump = ix.walk[cur].jump, older = ix.walk[cur].older;
-#endif
-        const uint32_t take = end < kWalkSpan ? end : kWalkSpan;
-        const uint32_t t32 = take < 32 ? take : 32;
-        cw.put(g0 + end - t32, t32 ? chars >> (2 * (32 - t32)) : 0, t32);
-        const uint32_t t16 = take - t32;
-        if (t16) cw.put(g0 + end - take, (uint64_t)(older >> (2 * (16 - t16))), t16);
-        end -= take;
-        cur = jump;
+        const WalkEntry e = walk_at(ix, cur);
+        walk_put(end, g0, cw, e.chars, e.older);
+        cur = e.jump;
     }
     return true;
 }

@@ -400,6 +400,18 @@ __global__ __launch_bounds__(256) void k_dec_rec(DecWalkArgs a) {
         w = a.recs[r];
         dec_desc(w, f, len);
     }
+    // issued before the index prologue so that they overlap it: the first walk entry of a
+    // long record, and the first 64-record window of the outward scans (waves 0 and 1)
+    const bool is_long = len > 0 && !((w >> 56) & 2) && (uint32_t)w < a.ix.n;
+    WalkEntry e0{0, 0, 0};
+    if (is_long) e0 = walk_at(a.ix, (uint32_t)w);
+    uint64_t wpre = 0;
+    if (wave == 0) {
+        if (r0 >= 64) wpre = a.recs[r0 - 64 + lane];
+        else if (r0 > 0 && lane >= 64 - r0) wpre = a.recs[r0 - 64 + lane];
+    } else if (wave == 1 && r1 + lane < n) {
+        wpre = a.recs[r1 + lane];
+    }
     // E[r] (bases before record r) and the read of r, from the tile scans + a block scan
     uint64_t tf, tl;
     const uint64_t ef = block_excl_scan(f, tf);
@@ -417,7 +429,7 @@ __global__ __launch_bounds__(256) void k_dec_rec(DecWalkArgs a) {
         while (open) {
             const int64_t rr = (int64_t)base - 64 + lane;
             uint64_t ff = 0, ll = 0;
-            if (rr >= 0) dec_desc(a.recs[rr], ff, ll);
+            if (rr >= 0) dec_desc(base == r0 ? wpre : a.recs[rr], ff, ll);
             const uint64_t fb = __ballot(ff != 0);
             if (fb) {
                 const uint32_t hl = 63u - (uint32_t)__builtin_clzll(fb);  // nearest first record
@@ -434,7 +446,7 @@ __global__ __launch_bounds__(256) void k_dec_rec(DecWalkArgs a) {
         while (base < n) {
             const uint64_t rr = base + lane;
             uint64_t ff = 1, ll = 0;
-            if (rr < n) dec_desc(a.recs[rr], ff, ll);
+            if (rr < n) dec_desc(base == r1 ? wpre : a.recs[rr], ff, ll);
             const uint64_t fb = __ballot(ff != 0);
             if (fb) {
                 const uint32_t fl = (uint32_t)__builtin_ctzll(fb);
@@ -491,9 +503,24 @@ __global__ __launch_bounds__(256) void k_dec_rec(DecWalkArgs a) {
     __syncthreads();
     StageWriter sw{s_bits, s_mask, w_lo};
     if (L) {
-        if (is_short) sw.put(g0, w, L);
-        else if (!walk_record_codes(a.ix, (uint32_t)w, L, g0, sw))
+        if (is_short) {
+            sw.put(g0, w, L);
+        } else if (!is_long) {
             atomicMin(a.status, (unsigned long long)((rid << 8) | (uint64_t)kErrFormat));
+        } else {  // walk_record_codes from the prefetched first entry
+            uint32_t end = L;
+            walk_put(end, g0, sw, e0.chars, e0.older);
+            uint32_t cur = e0.jump;
+            while (end > 0) {
+                if (cur >= a.ix.n) {
+                    atomicMin(a.status, (unsigned long long)((rid << 8) | (uint64_t)kErrFormat));
+                    break;
+                }
+                const WalkEntry e = walk_at(a.ix, cur);
+                walk_put(end, g0, sw, e.chars, e.older);
+                cur = e.jump;
+            }
+        }
     }
     __syncthreads();
     for (uint32_t t = threadIdx.x; t < nw; t += 256) stage_store_word(a.out, w_lo + t, s_bits[t], s_mask[t]);
