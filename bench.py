@@ -1,22 +1,41 @@
 #!/usr/bin/env python3
-"""ntcomp encode (or decode) throughput on MI355X -- BASELINE.json's metric:
+"""ntcomp encode/decode throughput on MI355X -- BASELINE.json's metric:
 "encode Mbases/sec at k=91, 150bp reads, 1/2/4/8 MI355X; bit-exact vs CPU".
 
-One process per GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N).
-Workload per GPU: 10M synthetic 150 bp reads (uniform
-starts, 50 % reverse complemented, 1 % i.i.d. substitutions) against the SBWT (k=91,
-with reverse complements) of a 5 Mbp synthetic genome.  Reads shard across GPUs with no
-data-path collective (weak scaling); torch.distributed only provides the barrier and the
-max-over-ranks of the timed region.
+Launch: `python bench.py --gpus N` (N > 1 without RANK in the environment starts a
+torch.distributed.run child with N ranks before anything touches the GPU), or the driver's
+`python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`.  One process
+per GPU; reads shard over ranks with the index replicated and no data-path collective
+(main.rs:152,162-173): torch.distributed (gloo) only carries the barriers,
+the max-over-ranks of the timed region and the per-rank parity verdicts.
 
-A step = one ntc_encode_batch_device call over the GPU's whole 10M-read batch, inputs
-already resident in HBM.  The JSON line also carries the roofline of the dominant kernel
-(k_encode) and the CPU baseline (the faithful C oracle, one pinned core, bounded sample),
-plus a bit-exactness check of the GPU records against that same oracle sample.
+Workload:
+  C91   per GPU 10M (N = 1) or 25M (N > 1: 8 x 25M = C91x8's 200M) synthetic 150 bp reads
+        (uniform starts, 50 % reverse complemented, 1 % i.i.d. substitutions) against the
+        SBWT (k = 91, + reverse complements) of a 5 Mbp synthetic genome.
+  D91   decode of C91's records back to bases (lib.rs:254-318).
+  S91   (N = 1) the same reads drawn from an 11-genome collection: the 5 Mbp genome plus 10
+        strains at 1 % substitutions (reference-based compression of a strain collection,
+        README.md:2): 70 M nodes, a fragmented path cover.
+A step = one pass of the hot path over the rank's whole shard, in device calls of at most
+--batch-reads reads (10M), inputs already resident in HBM.  The top-level line is C91 encode;
+"decode" and "strains" carry D91 and S91 with their own rooflines and parity.
+
+roofline: bytes past L2 per launch of the dominant kernel (k_ms4 / k_dec_rec), from the
+rocprofv3 PMC passes of THIS device build (profiles/pmc_traffic.json, keyed by the device
+source hash; scaled per read or per base to the launch), / the kernel's live HIP-event
+time, against 8 TB/s.  Each read request is counted at its own size (32/64/128 B:
+TCC_EA0_RDREQ_{32B,64B,128B}), writes at theirs (TCC_EA0_WRREQ, _64B), so random 64 B
+lines are not double-counted.  `line_rate` puts the L2-miss request rate against the
+random-line roof measured by scripts/randbw.hip.
+cpu_baseline: the faithful C oracle (oracle/ntcomp_oracle.c, test infrastructure) on one
+pinned host core, rank 0 at N = 1, on a bounded sample; it is also the parity checker.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -25,36 +44,255 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
 METRIC = "encode Mbases/sec at k=91, 150bp reads, 1/2/4/8 MI355X; bit-exact vs CPU"
-HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md "HBM": 8 TB/s spec
+PMC_JSON = os.path.join(REPO, "profiles", "pmc_traffic.json")
+RANDBW_JSONL = os.path.join(REPO, "profiles", "round1", "randbw.jsonl")
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--mode", choices=["encode", "decode"], default="encode")
+    ap.add_argument("--configs", default=None,
+                    help="comma list of encode,decode,strains (default: all three at N=1, encode,decode at N>1)")
+    ap.add_argument("--mode", choices=["encode", "decode"], default=None, help="(legacy) = --configs <mode>")
     ap.add_argument("--k", type=int, default=91)
-    ap.add_argument("--reads-per-gpu", type=int, default=10_000_000)
+    ap.add_argument("--reads-per-gpu", type=int, default=None, help="default 10M at N=1, 25M at N>1 (C91x8)")
+    ap.add_argument("--batch-reads", type=int, default=10_000_000, help="reads per device call")
     ap.add_argument("--read-len", type=int, default=150)
     ap.add_argument("--err-ppm", type=int, default=10_000)
     ap.add_argument("--genome-bp", type=int, default=5_000_000)
+    ap.add_argument("--strains", type=int, default=10)
+    ap.add_argument("--strain-snp-ppm", type=int, default=10_000)
+    ap.add_argument("--strain-reads", type=int, default=10_000_000)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--variant", type=int, default=4, help="encode kernel variant (1, 2 = earlier designs, for A/B)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU only: ranks, shards, oracle samples and the gathers, no GPU calls")
     ap.add_argument("--opt", action="append", default=[], help="ctx option key=value (A/B)")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
-    args = ap.parse_args()
+    ap.add_argument("--pmc-json", default=PMC_JSON)
+    args = ap.parse_args(argv)
+    if args.mode and not args.configs:
+        args.configs = args.mode
+    return args
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args):
+    """`bench.py --gpus N` outside torch.distributed.run: start it as a CHILD process (this
+    process has not touched the GPU or imported torch) and exit with its code."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"[launcher] {args.gpus} ranks: {' '.join(cmd[1:6])} ...")
+    return subprocess.call(cmd, env=env)
+
+
+# ---- counters ----------------------------------------------------------------------
+def load_pmc(path, want_hash):
+    """-> (workloads dict or None, note)"""
+    try:
+        with open(path) as f:
+            pj = json.load(f)
+    except (OSError, ValueError):
+        return None, f"no {os.path.relpath(path, REPO)}"
+    if pj.get("device_source_hash") != want_hash:
+        return None, (f"{os.path.relpath(path, REPO)} is from device build {pj.get('device_source_hash')}, "
+                      f"this build is {want_hash}: counters not applied")
+    return pj.get("workloads", {}), "ok"
+
+
+def random_line_roof():
+    try:
+        roofs = [json.loads(l) for l in open(RANDBW_JSONL)]
+        return max(r["g_lines_per_s"] for r in roofs
+                   if r.get("test") == "random_8B_loads" and r["buffer_bytes"] >= (32 << 20))
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def roofline(kname, kernel_ms, kernel_ms_min, units, unit_name, pmc, pmc_note, wl_key, extra=None):
+    """Roofline of one dominant kernel: PMC bytes past L2 per unit (read or base) x units per
+    launch / live kernel time."""
+    r = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": None, "traffic": None,
+         "kernel": kname, "kernel_ms": round(kernel_ms, 4), "kernel_ms_min": round(kernel_ms_min, 4),
+         "units_per_launch": int(units), "unit_kind": unit_name}
+    kd = ((pmc or {}).get(wl_key) or {}).get("kernels", {}).get(kname) if pmc is not None else None
+    if kd:
+        per = (pmc[wl_key].get("units_per_launch") or 0)
+        scale = units / per if per else 1.0
+        rd, wr = kd["read_bytes"] * scale, kd["write_bytes"] * scale
+        traffic = rd + wr
+        r.update(achieved=round(traffic / (kernel_ms / 1e3) / 1e9, 1), traffic=int(traffic),
+                 read_bytes=int(rd), write_bytes=int(wr))
+        r["frac"] = round(r["achieved"] / HBM_PEAK_GBPS, 4)
+        r["bytes_per_" + unit_name] = round(traffic / units, 2)
+        if kd.get("dram_read_bytes") is not None:
+            r["dram_read_bytes"] = int(kd["dram_read_bytes"] * scale)
+        roof = random_line_roof()
+        req = kd.get("rdreq", 0) * scale
+        if roof and req:
+            rate = req / (kernel_ms / 1e3) / 1e9
+            r["line_rate"] = {"requests_per_launch": int(req), "requests_per_" + unit_name: round(req / units, 3),
+                              "g_requests_per_s": round(rate, 2), "roof_g_requests_per_s": roof,
+                              "frac": round(rate / roof, 4)}
+        r["pmc_profile_kernel_ms"] = round(kd.get("avg_ns", 0) / 1e6 * scale, 4)
+    r["note"] = ("achieved = bytes past L2 per launch (rocprofv3 PMC of this device build, each request at its "
+                 "own 32/64/128 B size, plus writes; " + pmc_note + ") / live HIP-event kernel time")
+    if extra:
+        r.update(extra)
+    return r
+
+
+# ---- workload ----------------------------------------------------------------------
+class Shard:
+    """One rank's reads of one workload, in device batches."""
+
+    def __init__(self, nt, ctx, text, first, n, L, err, batch, threads, dry):
+        import numpy as np
+        self.L, self.n, self.first = L, n, first
+        self.batches = []
+        off = 0
+        while off < n:
+            nb = min(batch, n - off)
+            reads = nt.synth_reads(text, 2, first + off, nb, L, err, threads=threads)
+            b = {"first": first + off, "n": nb, "reads": reads, "bases": nb * L}
+            if not dry:
+                offs = np.arange(0, nb * L + 1, L, dtype=np.uint64)
+                cap = nb * L // 4 + 64
+                b.update(d_bases=ctx.alloc(reads.nbytes), d_offs=ctx.alloc(offs.nbytes), cap=cap,
+                         d_recs=ctx.alloc(cap * 8), d_roffs=ctx.alloc(offs.nbytes))
+                ctx.h2d(b["d_bases"], reads)
+                ctx.h2d(b["d_offs"], offs)
+            self.batches.append(b)
+            off += nb
+        self.bases = n * L
+
+    def free(self, ctx):
+        for b in self.batches:
+            for key in ("d_bases", "d_offs", "d_recs", "d_roffs", "d_out", "d_ooffs"):
+                if b.get(key):
+                    ctx.free(b[key])
+                    b[key] = None
+
+
+def encode_pass(ctx, sh, check=False):
+    ms = []
+    for b in sh.batches:
+        ctx.encode_device(b["d_bases"], b["d_offs"], b["n"], sh.L, b["d_recs"], b["cap"], b["d_roffs"])
+        got = ctx.encode_status()
+        if check:
+            b["n_recs"] = got
+        elif got != b["n_recs"]:
+            raise RuntimeError(f"record count changed between passes: {got} vs {b['n_recs']}")
+        ms.append(ctx.timing()["main_ms"])
+    return ms
+
+
+def decode_pass(ctx, sh):
+    ms = []
+    for b in sh.batches:
+        if not b.get("d_out"):
+            b["d_out"], b["d_ooffs"] = ctx.alloc(b["bases"] + 64), ctx.alloc((b["n"] + 1) * 8)
+        ctx.decode_device(b["d_recs"], b["n_recs"], b["d_out"], b["bases"] + 64, b["d_ooffs"], b["n"] + 1)
+        if ctx.decode_status() != (b["n"], b["bases"]):
+            raise RuntimeError(f"decode status {ctx.decode_status()} != {(b['n'], b['bases'])}")
+        ms.append(ctx.timing()["main_ms"])
+    return ms
+
+
+def timed(fn, steps, warmup, barrier, sync, dist):
+    from ntcomp_amd import shard as shard_mod
+    for _ in range(warmup):
+        fn()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    kms = []
+    for _ in range(steps):
+        kms += fn()
+    sync()
+    el = time.perf_counter() - t0
+    barrier()
+    return shard_mod.max_over_ranks(el, dist), kms
+
+
+def records_of(ctx, b, a_read, b_read):
+    import numpy as np
+    ro = ctx.d2h(np.zeros(b["n"] + 1, dtype=np.uint64), b["d_roffs"])
+    lo, hi = int(ro[a_read]), int(ro[b_read])
+    recs = ctx.d2h(np.zeros(hi - lo, dtype=np.uint64), b["d_recs"] + 8 * lo) if hi > lo else np.zeros(0, np.uint64)
+    return recs, ro
+
+
+def check_shard(ctx, orc, sh, seconds, full_decode, pin, dry):
+    """Bit-exactness of GPU records vs the oracle on a bounded sample of every batch (timed:
+    the CPU baseline), and of the decoded bases vs the reads over the whole shard."""
+    import numpy as np
+    L = sh.L
+    res = {"encode_ok": True, "reads_checked": 0, "cpu_encode_s": 0.0, "decode_ok": None, "cpu_decode_s": 0.0,
+           "cpu_decode_bases": 0}
+    old = os.sched_getaffinity(0)
+    core = sorted(old)[-1]
+    if pin:
+        os.sched_setaffinity(0, {core})
+    try:
+        per_batch = seconds / max(1, len(sh.batches))
+        for b in sh.batches:
+            chunk, done, spent = min(2000, b["n"]), 0, 0.0
+            while spent < per_batch and done + chunk <= b["n"]:
+                sl = b["reads"][done * L:(done + chunk) * L]
+                o = np.arange(0, chunk * L + 1, L, dtype=np.uint64)
+                t1 = time.perf_counter()
+                exp, eoff = orc.encode(sl, o)
+                spent += time.perf_counter() - t1
+                if not dry:
+                    got, ro = records_of(ctx, b, done, done + chunk)
+                    res["encode_ok"] &= bool(np.array_equal(got, exp))
+                    if res["cpu_decode_s"] < seconds / 4:
+                        t1 = time.perf_counter()
+                        out, _ = orc.decode(exp)
+                        res["cpu_decode_s"] += time.perf_counter() - t1
+                        res["cpu_decode_bases"] += len(out)
+                        res["encode_ok"] &= bool(np.array_equal(out, sl))
+                done += chunk
+            res["reads_checked"] += done
+            res["cpu_encode_s"] += spent
+            if full_decode and not dry and b.get("d_out"):
+                out = ctx.d2h(np.zeros(b["bases"], dtype=np.uint8), b["d_out"])
+                oo = ctx.d2h(np.zeros(b["n"] + 1, dtype=np.uint64), b["d_ooffs"])
+                ok = bool(np.array_equal(out, b["reads"])) and bool(
+                    np.array_equal(oo, np.arange(0, b["bases"] + 1, L, dtype=np.uint64)))
+                res["decode_ok"] = ok if res["decode_ok"] is None else (res["decode_ok"] and ok)
+    finally:
+        if pin:
+            os.sched_setaffinity(0, old)
+    res["core"] = core
+    return res
+
+
+def main():
+    args = parse_args()
+    if args.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(spawn_ranks(args))
 
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        world = int(os.environ.get("WORLD_SIZE", "1"))
+    configs = (args.configs or ("encode,decode,strains" if world == 1 else "encode,decode")).split(",")
+    reads_per_gpu = args.reads_per_gpu or (10_000_000 if world == 1 else 25_000_000)
 
     import numpy as np
     import torch  # before ntcomp_amd: one HIP runtime per process
@@ -62,206 +300,207 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("gloo")  # barrier + max of the timed region only
-    # one GPU per rank; on a box with fewer GPUs than ranks (a rehearsal), ranks share them
-    ndev = torch.cuda.device_count()
-    device = local % ndev if ndev else local
-    if torch.cuda.is_available():
+        dist.init_process_group("gloo")  # barriers, max over ranks, parity verdicts
+    device = 0
+    if not args.dry_run:
+        ndev = torch.cuda.device_count()  # a box with fewer GPUs than ranks (rehearsal): ranks share
+        device = local % ndev if ndev else local
         torch.cuda.set_device(device)
 
     import ntcomp_amd as nt
-    from ntcomp_amd import shard
+    from ntcomp_amd import shard as shard_mod
+    from oracle_lib import OracleIndex  # the checker / CPU baseline (test infrastructure)
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
-    def sync(ctx):
-        ctx.synchronize()
-        if torch.cuda.is_available():
+    ctx = None
+
+    def sync():
+        if ctx is not None:
+            ctx.synchronize()
             torch.cuda.synchronize()
 
-    nthreads = max(1, (os.cpu_count() or 8) // max(1, world))
-    nthreads = min(nthreads, 16)
-    t0 = time.time()
+    def gather(obj):
+        if dist is None:
+            return [obj]
+        out = [None] * world
+        dist.all_gather_object(out, obj)
+        return out
+
+    nthreads = max(1, min(16, (os.cpu_count() or 8) // max(1, world)))
+    pmc, pmc_note = load_pmc(args.pmc_json, nt.device_source_hash())
+    L, k = args.read_len, args.k
+    first, n = shard_mod.read_range(rank, world, reads_per_gpu)
+    line = {}
+    t_start = time.time()
+
+    def setup_index(texts, label):
+        nonlocal ctx
+        t0 = time.time()
+        index = nt.Index.build([t.tobytes() for t in texts], k, threads=nthreads)
+        log(f"[rank {rank}] {label} index k={k} n={index.n} built in {time.time() - t0:.1f}s")
+        if not args.dry_run:
+            if ctx is None:
+                ctx = nt.GpuContext(device)
+                for kv in args.opt:
+                    key, val = kv.split("=")
+                    ctx.set_option(key, int(val))
+            t0 = time.time()
+            ctx.upload(index)
+            log(f"[rank {rank}] upload {time.time() - t0:.1f}s, {ctx.get_option('n_paths')} paths")
+        return index
+
     genome = nt.synth_genome(1, args.genome_bp)
-    index = nt.Index.build([genome.tobytes()], args.k, threads=nthreads)
-    log(f"[rank {rank}] index k={args.k} n={index.n} built in {time.time() - t0:.1f}s")
-    ctx = nt.GpuContext(device)
-    ctx.set_option("encode_variant", args.variant)
-    for kv in args.opt:
-        key, val = kv.split("=")
-        ctx.set_option(key, int(val))
-    t0 = time.time()
-    ctx.upload(index)
-    log(f"[rank {rank}] upload (derived structures + path cover) {time.time() - t0:.1f}s, "
-        f"{ctx.get_option('n_paths')} paths, text {ctx.get_option('path_text_len')}")
+    base_cfg = {"k": k, "read_len": L, "genome_bp": args.genome_bp, "err_ppm": args.err_ppm,
+                "reads_per_gpu": n, "batch_reads": min(args.batch_reads, n)}
 
-    n, L = args.reads_per_gpu, args.read_len
-    first, n = shard.read_range(rank, world, n)
-    t0 = time.time()
-    reads = nt.synth_reads(genome, 2, first, n, L, args.err_ppm, threads=nthreads)
-    offs = np.arange(0, n * L + 1, L, dtype=np.uint64)
-    log(f"[rank {rank}] {n} reads generated in {time.time() - t0:.1f}s")
-    total_bases = n * L
-    cap = total_bases // 4 + 64
-    d_bases, d_offs = ctx.alloc(reads.nbytes), ctx.alloc(offs.nbytes)
-    d_recs, d_roffs = ctx.alloc(cap * 8), ctx.alloc(offs.nbytes)
-    ctx.h2d(d_bases, reads)
-    ctx.h2d(d_offs, offs)
+    # ---- C91 encode / D91 decode -------------------------------------------------
+    if "encode" in configs or "decode" in configs:
+        index = setup_index([genome], "C")
+        sh = Shard(nt, ctx, genome, first, n, L, args.err_ppm, args.batch_reads, nthreads, args.dry_run)
+        log(f"[rank {rank}] reads {first}..{first + n} in {len(sh.batches)} batch(es)")
+        orc = OracleIndex(index.n, k, index.rows, index.C, index.lcs)
+        n_recs = None
+        if not args.dry_run:
+            encode_pass(ctx, sh, check=True)
+            n_recs = sum(b["n_recs"] for b in sh.batches)
+        enc = dec = None
+        if "encode" in configs and not args.dry_run:
+            enc = timed(lambda: encode_pass(ctx, sh), args.steps, args.warmup, barrier, sync, dist)
+        if "decode" in configs and not args.dry_run:
+            dec = timed(lambda: decode_pass(ctx, sh), args.steps, args.warmup, barrier, sync, dist)
+        pin = world == 1
+        secs = args.cpu_seconds if (world == 1 and not args.no_cpu) else (0 if args.no_cpu else 2.0)
+        chk = check_shard(ctx, orc, sh, secs, dec is not None, pin, args.dry_run) if secs > 0 else None
+        verdicts = gather({"rank": rank, "first": first, "n": n, "check": chk})
+        units_all = sh.bases * world * args.steps
+        par = {"ranks": world, "encode_bit_exact_all_ranks": all(v["check"]["encode_ok"] for v in verdicts)
+               if chk else None,
+               "reads_checked_per_rank": [v["check"]["reads_checked"] for v in verdicts] if chk else None,
+               "shards": [[v["first"], v["n"]] for v in verdicts]}
+        cpu = None
+        if chk and world == 1 and not args.no_cpu:
+            cv = chk["reads_checked"] * L / chk["cpu_encode_s"] / 1e6
+            cpu = {"value": round(cv, 3), "unit": "Mbases/s", "cores": 1, "kind": "port",
+                   "sample": f"{chk['reads_checked']} reads ({chk['reads_checked'] * L} bases) from the start of "
+                             f"each batch, faithful C oracle (oracle/ntcomp_oracle.c) on one pinned core "
+                             f"({chk['core']}) of {os.cpu_count()}"}
+        wl_c = (f"C{k}: {n} x {L}bp synthetic reads per GPU ({args.err_ppm / 1e4:g}% subst, 50% revcomp) vs SBWT "
+                f"of a {args.genome_bp / 1e6:g} Mbp synthetic genome (+revcomp), k={k}"
+                + (f"; {world} GPUs x {n} = {world * n} reads" if world > 1 else ""))
+        cfg = dict(base_cfg, workload=wl_c, index_nodes=index.n, records_per_gpu=n_recs,
+                   parallelism=f"reads sharded over {world} GPU(s), index replicated, no collective")
+        if enc is not None:
+            el, kms = enc
+            kavg = sum(kms) / len(kms)
+            b0 = sh.batches[0]
+            rl = roofline("k_ms4", kavg, min(kms), b0["n"], "read", pmc, pmc_note, f"C{k}",
+                          {"reference_work_avoided": round(
+                              b0["bases"] * (1 + 2 * 64) / (kavg / 1e3) / 1e9 / HBM_PEAK_GBPS, 3),
+                           "reference_work_note": "SURVEY 8(d) B_enc (1 B + two 64 B rank lines per base) / "
+                                                  "kernel time / peak: the reference algorithm's bytes this "
+                                                  "kernel's suffix table and path runs avoid; not a roofline"})
+            line.update({"metric": METRIC, "value": round(units_all / el / 1e6, 2), "unit": "Mbases/s",
+                         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                         "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+                         "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+                         "data": "synthetic (seeded; reads regenerate per shard)", "config": cfg,
+                         "roofline": rl, "cpu_baseline": cpu, "parity": par,
+                         "kernel_ms_per_step": round(sum(kms) / args.steps, 3)})
+            if cpu:
+                cpu["speedup_gpu_vs_cpu"] = round(line["value"] / cpu["value"], 1)
+        if dec is not None:
+            el, kms = dec
+            kavg = sum(kms) / len(kms)
+            b0 = sh.batches[0]
+            dcpu = None
+            if chk and chk["cpu_decode_s"] > 0 and world == 1:
+                dcpu = {"value": round(chk["cpu_decode_bases"] / chk["cpu_decode_s"] / 1e6, 3), "unit": "Mbases/s",
+                        "cores": 1, "kind": "port",
+                        "sample": f"oracle decode of {chk['cpu_decode_bases']} bases of oracle records, one pinned core"}
+            d = {"metric": f"decode Mbases/sec at k={k}, 150bp reads (output bases), MI355X; bit-exact vs CPU",
+                 "value": round(units_all / el / 1e6, 2), "unit": "Mbases/s",
+                 "ms_per_step": round(el / args.steps * 1e3, 3),
+                 "config": {"workload": f"D{k}: decode of the C{k} records ({n_recs} records, {n} reads per GPU) "
+                                        f"-> bases via the inverse-SBWT walk, k={k}"},
+                 "roofline": roofline("k_dec_rec", kavg, min(kms), b0["bases"], "base", pmc, pmc_note, f"D{k}"),
+                 "cpu_baseline": dcpu,
+                 "parity": {"round_trip_exact_all_ranks": all(v["check"]["decode_ok"] for v in verdicts)
+                            if chk else None, "bases_checked_per_rank": n * L if chk else None},
+                 "kernel_ms_per_step": round(sum(kms) / args.steps, 3)}
+            if dcpu:
+                d["cpu_baseline"]["speedup_gpu_vs_cpu"] = round(d["value"] / dcpu["value"], 1)
+            if line:
+                line["decode"] = d
+            else:
+                line.update({"metric": d["metric"], "value": d["value"], "unit": "Mbases/s", "n_gpus": world,
+                             "steps": args.steps, "warmup": args.warmup, "ms_per_step": d["ms_per_step"],
+                             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+                             "data": "synthetic (seeded; reads regenerate per shard)",
+                             "config": dict(cfg, workload=d["config"]["workload"]), "roofline": d["roofline"],
+                             "cpu_baseline": d["cpu_baseline"], "parity": dict(par, **d["parity"])})
+        if args.dry_run:
+            line.update({"metric": METRIC, "value": None, "unit": "Mbases/s", "n_gpus": world, "dry_run": True,
+                         "config": cfg, "parity": par})
+        if not args.dry_run:
+            sh.free(ctx)
+        del sh
 
-    # one encode pass (also the decode input)
-    ctx.encode_device(d_bases, d_offs, n, L, d_recs, cap, d_roffs)
-    n_recs = ctx.encode_status()
-    d_out = d_ooffs = None
-    if args.mode == "decode":
-        d_out, d_ooffs = ctx.alloc(total_bases + 64), ctx.alloc(offs.nbytes)
-
-    def step():
-        if args.mode == "encode":
-            ctx.encode_device(d_bases, d_offs, n, L, d_recs, cap, d_roffs)
-            got = ctx.encode_status()
-            assert got == n_recs
+    # ---- S91: strain collection ------------------------------------------------------
+    if "strains" in configs:
+        strains = nt.synth_strains(genome, 3, args.strains, args.strain_snp_ppm)
+        texts = [genome] + [strains[i] for i in range(args.strains)]
+        index = setup_index(texts, "S")
+        coll = np.concatenate(texts)
+        ns = args.strain_reads if world == 1 else min(args.strain_reads, n)
+        fs, ns = shard_mod.read_range(rank, world, ns)
+        sh = Shard(nt, ctx, coll, fs, ns, L, args.err_ppm, args.batch_reads, nthreads, args.dry_run)
+        orc = OracleIndex(index.n, k, index.rows, index.C, index.lcs)
+        s = {"config": {"workload": f"S{k}: {ns} x {L}bp reads ({args.err_ppm / 1e4:g}% subst, 50% revcomp) drawn "
+                                    f"from a collection of the {args.genome_bp / 1e6:g} Mbp genome + {args.strains} "
+                                    f"strains at {args.strain_snp_ppm / 1e4:g}% substitutions, SBWT k={k} (+revcomp)",
+                        "index_nodes": index.n}}
+        if not args.dry_run:
+            encode_pass(ctx, sh, check=True)
+            s["config"]["records_per_gpu"] = sum(b["n_recs"] for b in sh.batches)
+            s["config"]["n_paths"] = ctx.get_option("n_paths")
+            el, kms = timed(lambda: encode_pass(ctx, sh), args.steps, args.warmup, barrier, sync, dist)
+            kavg = sum(kms) / len(kms)
+            s.update(value=round(sh.bases * world * args.steps / el / 1e6, 2), unit="Mbases/s",
+                     ms_per_step=round(el / args.steps * 1e3, 3),
+                     roofline=roofline("k_ms4", kavg, min(kms), sh.batches[0]["n"], "read", pmc, pmc_note, f"S{k}"))
+            el, kms = timed(lambda: decode_pass(ctx, sh), args.steps, args.warmup, barrier, sync, dist)
+            kavg = sum(kms) / len(kms)
+            s["decode"] = {"value": round(sh.bases * world * args.steps / el / 1e6, 2), "unit": "Mbases/s",
+                           "ms_per_step": round(el / args.steps * 1e3, 3),
+                           "roofline": roofline("k_dec_rec", kavg, min(kms), sh.batches[0]["bases"], "base", pmc,
+                                                pmc_note, f"SD{k}")}
+        secs = 0 if args.no_cpu else 3.0
+        chk = check_shard(ctx, orc, sh, secs, not args.dry_run, False, args.dry_run) if secs > 0 else None
+        vs = gather(chk)
+        s["parity"] = {"encode_bit_exact_all_ranks": all(v["encode_ok"] for v in vs) if chk else None,
+                       "reads_checked_per_rank": [v["reads_checked"] for v in vs] if chk else None,
+                       "round_trip_exact_all_ranks": all(v["decode_ok"] for v in vs) if chk and not args.dry_run
+                       else None}
+        if not args.dry_run:
+            sh.free(ctx)
+        if line:
+            line["strains"] = s
         else:
-            ctx.decode_device(d_recs, n_recs, d_out, total_bases + 64, d_ooffs, n + 1)
-            assert ctx.decode_status() == (n, total_bases)
-        return ctx.timing()
-
-    for _ in range(args.warmup):
-        step()
-    barrier()
-    sync(ctx)
-    tt = time.perf_counter()
-    mains, totals = [], []
-    for _ in range(args.steps):
-        t = step()
-        mains.append(t["main_ms"])
-        totals.append(t["total_ms"])
-    sync(ctx)
-    elapsed = time.perf_counter() - tt
-    barrier()
-    elapsed = shard.max_over_ranks(elapsed, dist)
-    ms_per_step = elapsed / args.steps * 1e3
-    units_all = total_bases * world * args.steps
-    value = units_all / elapsed / 1e6  # Mbases/s, whole job
-
-    main_ms = sum(mains) / len(mains)
-    main_ms_min = min(mains)
-    if args.mode == "encode":
-        alg_bytes = total_bases * (1 + 2 * 64) + 8 * n_recs  # SURVEY.md 8(d) B_enc
-        kname = "k_ms4" if args.variant == 4 else "k_encode"
-    else:
-        n_long_bases = None
-        alg_bytes = None
-        kname = "k_dec_rec"
-    # decode: B_dec = 64 B per walked base + 1 B/base out + 8 B/record
-    if args.mode == "decode":
-        recs_h = ctx.d2h(np.zeros(n_recs, dtype=np.uint64), d_recs)
-        flags = (recs_h >> np.uint64(56)).astype(np.uint8)
-        longm = (flags & 2) == 0
-        n_long_bases = int(((recs_h[longm] >> np.uint64(32)) & np.uint64(0xFFFFFF)).sum())
-        alg_bytes = 64 * n_long_bases + total_bases + 8 * n_recs
-    achieved = alg_bytes / (main_ms / 1e3) / 1e9
-    traffic = None
-    try:
-        with open(args.traffic_json) as f:
-            tj = json.load(f)
-        traffic = tj.get(kname, {}).get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                "kernel": kname, "kernel_ms": round(main_ms, 3), "kernel_ms_min": round(main_ms_min, 3),
-                "alg_bytes_per_launch": int(alg_bytes),
-                "note": ("achieved = SURVEY 8(d) algorithmic bytes (B_enc: the reference's two 64 B rank-line "
-                         "reads per base) / kernel time; the suffix table and path runs skip most of those "
-                         "reads, so frac can exceed 1" if args.mode == "encode" else
-                         "achieved = SURVEY 8(d) B_dec (one 64 B select line per walked base) / kernel time; "
-                         "the walk table reads 32 bases per 16 B entry, so frac can exceed 1") +
-                        ". traffic = HBM bytes per launch from rocprofv3 PMC (2*FETCH_SIZE + WRITE_SIZE, "
-                        "profiles/pmc_traffic.json); traffic_frac = traffic / kernel time / peak"}
-    if traffic:
-        roofline["traffic_frac"] = round(traffic / (main_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
-    # The hot kernels are bound by random 64 B line requests, not streaming bytes: L2-miss read
-    # requests per launch (rocprofv3 TCC_EA0_RDREQ) / kernel time, against the random-access
-    # roof measured on the same chip by scripts/randbw (profiles/round1/randbw.jsonl).
-    try:
-        ea = tj.get(kname, {}).get("ea_rdreq_per_launch")
-        roofs = [json.loads(l) for l in open(os.path.join(REPO, "profiles", "round1", "randbw.jsonl"))]
-        roof = max(r["g_lines_per_s"] for r in roofs
-                   if r.get("test") == "random_8B_loads" and r["buffer_bytes"] >= (32 << 20))
-        if ea:
-            rate = ea / (main_ms / 1e3) / 1e9
-            roofline["line_rate"] = {"requests_per_launch": int(ea), "g_requests_per_s": round(rate, 2),
-                                     "roof_g_requests_per_s": roof, "frac": round(rate / roof, 4),
-                                     "note": "random-line roof = best scripts/randbw rate for buffers past L2 "
-                                             "(Infinity-Cache and HBM sizes); one request = one 64 B line"}
-    except (OSError, ValueError, NameError, KeyError):
-        pass
-
-    cpu = None
-    parity = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        from oracle_lib import OracleIndex
-        orc = OracleIndex(index.n, args.k, index.rows, index.C, index.lcs)
-        rec_offs_h = ctx.d2h(np.zeros(n + 1, dtype=np.uint64), d_roffs)
-        ctx.synchronize()
-        old_aff = os.sched_getaffinity(0)
-        core = sorted(old_aff)[-1]
-        os.sched_setaffinity(0, {core})
-        try:
-            chunk, done, spent, ok = 2000, 0, 0.0, True
-            while spent < args.cpu_seconds and done + chunk <= n:
-                sl = reads[done * L:(done + chunk) * L]
-                o = np.arange(0, chunk * L + 1, L, dtype=np.uint64)
-                if args.mode == "encode":
-                    t1 = time.perf_counter()
-                    exp, eoff = orc.encode(sl, o)
-                    spent += time.perf_counter() - t1
-                    a, b = int(rec_offs_h[done]), int(rec_offs_h[done + chunk])
-                    got = ctx.d2h(np.zeros(b - a, dtype=np.uint64), d_recs + 8 * a) if b > a else np.zeros(0, np.uint64)
-                    ok &= bool(np.array_equal(got, exp))
-                else:
-                    exp, eoff = orc.encode(sl, o)
-                    t1 = time.perf_counter()
-                    out, _ = orc.decode(exp)
-                    spent += time.perf_counter() - t1
-                    ok &= bool(np.array_equal(out, sl))
-                done += chunk
-        finally:
-            os.sched_setaffinity(0, old_aff)
-        cpu_val = done * L / spent / 1e6
-        cpu = {"value": round(cpu_val, 3), "unit": "Mbases/s", "cores": 1, "kind": "port",
-               "sample": f"first {done} of the {n} reads ({done * L} bases), faithful C oracle "
-                         f"(oracle/ntcomp_oracle.c), one pinned core ({core}) of {os.cpu_count()}",
-               "speedup_gpu_vs_cpu": round(value / cpu_val, 1)}
-        parity = {"bit_exact_vs_oracle": ok, "reads_checked": done}
+            line.update({"metric": METRIC, "value": s.get("value"), "unit": "Mbases/s", "n_gpus": world,
+                         "steps": args.steps, "warmup": args.warmup, "ms_per_step": s.get("ms_per_step"),
+                         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+                         "data": "synthetic (seeded)", "config": dict(base_cfg, **s["config"]),
+                         "roofline": s.get("roofline"), "cpu_baseline": None, "parity": s["parity"],
+                         "decode": s.get("decode")})
 
     if rank == 0:
-        if args.mode == "encode":
-            workload = (f"C{args.k}: {n} x {L}bp synthetic reads per GPU ({args.err_ppm / 1e4:g}% subst, 50% revcomp) "
-                        f"vs SBWT of a {args.genome_bp / 1e6:g} Mbp synthetic genome (+revcomp), k={args.k}")
-            metric = METRIC
-        else:
-            workload = (f"D{args.k}: decode of the C{args.k} records ({n_recs} records, {n} reads) "
-                        f"-> bases via inverse-SBWT walk, k={args.k}")
-            metric = f"decode Mbases/sec at k={args.k}, 150bp reads (output bases), MI355X"
-        line = {
-            "metric": metric, "value": round(value, 2), "unit": "Mbases/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-            "data": "synthetic (seeded; reads regenerate per shard)",
-            "config": {"workload": workload, "k": args.k, "reads_per_gpu": n, "read_len": L,
-                       "genome_bp": args.genome_bp, "index_nodes": index.n, "records_per_gpu": n_recs,
-                       "parallelism": f"reads sharded over {world} GPU(s), index replicated, no collective"},
-            "roofline": roofline, "cpu_baseline": cpu, "parity": parity,
-            "kernel_ms_per_step": round(main_ms, 3), "encode_variant": args.variant, "device_ms_per_step": round(sum(totals) / len(totals), 3),
-        }
+        line["wall_s"] = round(time.time() - t_start, 1)
         print(json.dumps(line), flush=True)
-    for p in (d_bases, d_offs, d_recs, d_roffs, d_out, d_ooffs):
-        if p:
-            ctx.free(p)
-    ctx.close()
+    if ctx is not None:
+        ctx.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -25,6 +25,8 @@
  *   NTC_ERR_EMPTY_READ    encode.rs:133-135 / lib.rs:224 (EncodeError on empty input)
  *   NTC_ERR_INVALID_BASE  non-ACGT byte, or a base the index does not contain
  *   NTC_ERR_LENGTH        a match length >= 2^24 (assert at lib.rs:226)
+ *   NTC_ERR_REFERENCE_PANIC  a short record (len <= 11) longer than k, possible only for
+ *                         k <= 10: encode.rs:151-152 slices kmer[(k - len)..k] and panics
  *
  * Threading: one ntc_ctx per GPU, driven by one host thread at a time.  Contexts on
  * different devices are independent.  The index is read-only once uploaded.
@@ -51,7 +53,8 @@ typedef enum ntc_status {
     NTC_ERR_NO_INDEX = 7,
     NTC_ERR_FORMAT = 8,
     NTC_ERR_IO = 9,
-    NTC_ERR_UNSUPPORTED = 10
+    NTC_ERR_UNSUPPORTED = 10,
+    NTC_ERR_REFERENCE_PANIC = 11
 } ntc_status;
 
 typedef struct ntc_ctx ntc_ctx;

@@ -55,6 +55,11 @@ int ntc_fasta_format(const uint8_t *bases, const uint64_t *offsets, uint64_t n_r
 /* ---- synthetic workload ------------------------------------------- */
 /* i.i.d. uniform ACGT genome from SplitMix64(seed). */
 int ntc_synth_genome(uint64_t seed, uint64_t length, uint8_t *out);
+/* n_strains strains of a collection, each = genome with i.i.d. substitutions at rate
+ * snp_per_million / 1e6 (position i of strain s depends only on (seed, s, i)).
+ * out = n_strains * glen bytes.  Used for the multi-strain index of bench.py.        */
+int ntc_synth_strains(const uint8_t *genome, uint64_t glen, uint64_t seed, uint32_t n_strains,
+                      uint32_t snp_per_million, uint8_t *out);
 /* n_reads reads of read_len bases from genome; read r depends only on (seed, r): start
  * uniform on [0, glen-read_len], reverse-complemented with probability 1/2, i.i.d.
  * substitutions with probability err_per_million / 1e6.  out = n_reads*read_len bytes.

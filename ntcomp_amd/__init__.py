@@ -28,7 +28,7 @@ NTC_OK = 0
 STATUS = {
     0: "NTC_OK", 1: "NTC_ERR_INVALID_ARG", 2: "NTC_ERR_INVALID_BASE", 3: "NTC_ERR_EMPTY_READ",
     4: "NTC_ERR_LENGTH", 5: "NTC_ERR_CAPACITY", 6: "NTC_ERR_HIP", 7: "NTC_ERR_NO_INDEX",
-    8: "NTC_ERR_FORMAT", 9: "NTC_ERR_IO", 10: "NTC_ERR_UNSUPPORTED",
+    8: "NTC_ERR_FORMAT", 9: "NTC_ERR_IO", 10: "NTC_ERR_UNSUPPORTED", 11: "NTC_ERR_REFERENCE_PANIC",
 }
 
 # every symbol include/ntcomp_gpu.h and include/ntcomp_host.h declare
@@ -38,7 +38,7 @@ EXPORTED = [
     "ntc_encode_batch_device", "ntc_encode_status", "ntc_decode_batch", "ntc_decode_batch_device",
     "ntc_decode_status", "ntc_last_timing", "ntc_device_alloc", "ntc_device_free", "ntc_memcpy_h2d",
     "ntc_memcpy_d2h", "ntc_debug_matching_statistics", "ntc_build_index", "ntc_index_free",
-    "ntc_index_view_of", "ntc_index_save", "ntc_index_load", "ntc_synth_genome", "ntc_synth_reads",
+    "ntc_index_view_of", "ntc_index_save", "ntc_index_load", "ntc_synth_genome", "ntc_synth_strains", "ntc_synth_reads",
     "ntc_file_header", "ntc_write_block", "ntc_read_block", "ntc_buffer_free",
     "ntc_fastx_open", "ntc_fastx_next_batch", "ntc_fastx_close", "ntc_fasta_format",
 ]
@@ -61,6 +61,17 @@ class Timing(ctypes.Structure):
 
 
 _lib = None
+
+
+def device_source_hash():
+    """sha256 (16 hex) of the device code (kernels + lane functions): profiles/pmc_traffic.json
+    records it, and bench.py uses counter data only when it matches the build it times."""
+    import hashlib
+    h = hashlib.sha256()
+    for name in ("kernels.hip", "kernels.h", "encode_core.h"):
+        with open(os.path.join(_HERE, "csrc", name), "rb") as f:
+            h.update(name.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
 
 
 def build_library(force=False):
@@ -109,6 +120,7 @@ def lib():
         "ntc_index_save": (I, [P, ctypes.c_char_p]),
         "ntc_index_load": (I, [ctypes.c_char_p, ctypes.POINTER(P)]),
         "ntc_synth_genome": (I, [u64, u64, P]),
+        "ntc_synth_strains": (I, [P, u64, u64, u32, u32, P]),
         "ntc_synth_reads": (I, [P, u64, u64, u64, u64, u32, u32, I, P]),
         "ntc_file_header": (None, [P]),
         "ntc_write_block": (I, [P, u64, u64, ctypes.POINTER(P), ctypes.POINTER(u64)]),
@@ -369,6 +381,16 @@ def synth_genome(seed, length):
     rc = lib().ntc_synth_genome(seed, length, _p(out))
     if rc:
         raise NtcError(rc, "ntc_synth_genome")
+    return out
+
+
+def synth_strains(genome, seed, n_strains, snp_per_million):
+    """n_strains mutated copies of genome (i.i.d. substitutions), as one (n_strains, len) array."""
+    genome = np.ascontiguousarray(genome, dtype=np.uint8)
+    out = np.zeros((n_strains, len(genome)), dtype=np.uint8)
+    rc = lib().ntc_synth_strains(_p(genome), len(genome), seed, n_strains, snp_per_million, _p(out))
+    if rc:
+        raise NtcError(rc, "ntc_synth_strains")
     return out
 
 

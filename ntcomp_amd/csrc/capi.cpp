@@ -110,6 +110,7 @@ const char *status_name(int code) {
     case NTC_ERR_LENGTH: return "match length >= 2^24";
     case NTC_ERR_CAPACITY: return "output capacity exceeded";
     case NTC_ERR_FORMAT: return "malformed input";
+    case NTC_ERR_REFERENCE_PANIC: return "short record longer than k (the reference panics, encode.rs:151-152)";
     default: return "error";
     }
 }

@@ -93,6 +93,7 @@ enum : int {
     kErrLength = 4,
     kErrCapacity = 5,
     kErrFormat = 8,
+    kErrRefPanic = 11,  // an input on which the reference panics (NTC_ERR_REFERENCE_PANIC)
 };
 
 NTC_HD int base_code(uint8_t b) {
@@ -335,6 +336,8 @@ NTC_HD int encode_lane(const DevIndex &ix, const uint8_t *q, uint32_t len, uint3
         if (seglen > 11) {
             w = (uint64_t)st | ((uint64_t)(seglen & 0xFFFFFFu) << 32) | (first << 56);
         } else {
+            // encode.rs:151-152 slices kmer[(k - len)..k]: len > k (only for k <= 10) panics
+            if (seglen > k) return -kErrRefPanic;
             // bitnuc::as_2bit of the segment == the query bases it covers
             uint64_t bits = 0;
             for (uint32_t j = 0; j < seglen; j++)
@@ -1289,6 +1292,7 @@ NTC_HD int parse_read(const DevIndex &ix, const uint64_t *Q, uint64_t qo, const 
         if (seglen > 11) {
             w = (uint64_t)st | ((uint64_t)(seglen & 0xFFFFFFu) << 32) | (first << 56);
         } else {
+            if (seglen > k) return -kErrRefPanic;  // encode.rs:151-152: kmer[(k - len)..k] underflows
             NTC_TOUCH(kTrQ, Q + ((qo + segend - seglen) >> 5));
             const uint64_t bits = window2(Q, qo + segend - seglen);
             w = (bits & ((1ULL << (2 * seglen)) - 1)) | ((uint64_t)((first + 2) | (seglen << 2)) << 56);

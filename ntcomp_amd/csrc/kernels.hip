@@ -385,7 +385,12 @@ __global__ __launch_bounds__(256) void k_dec_rec(DecWalkArgs a) {
     __shared__ uint64_t s_lo[4], s_hi[4];
     __shared__ uint64_t s_start[kDecTileRecs];  // output offset of each read starting in the tile
     __shared__ uint64_t s_open[2];              // start of the read open at the tile start, end of the last read
-    if (*a.status != ~0ull) return;  // same value for the whole block
+    __shared__ uint32_t s_failed;
+    // Another block may set the status at any time (format errors below), so one load
+    // decides for the whole block: waves must not diverge on it before the barriers.
+    if (threadIdx.x == 0) s_failed = *(volatile unsigned long long *)a.status != ~0ull;
+    __syncthreads();
+    if (s_failed) return;
     const uint64_t n = a.n, tiles = (n + kDecTileRecs - 1) / kDecTileRecs, t = blockIdx.x;
     const uint64_t reads = a.pfs[tiles], bases = a.pls[tiles];
     if (reads + 1 > a.offs_capacity || bases > a.bases_capacity) {  // every block: nothing is written

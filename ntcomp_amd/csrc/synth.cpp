@@ -28,6 +28,29 @@ extern "C" int ntc_synth_genome(uint64_t seed, uint64_t length, uint8_t *out) {
     return NTC_OK;
 }
 
+// Strain s (0-based) of a collection: the genome with i.i.d. substitutions at rate
+// snp_per_million / 1e6; whether position i of strain s mutates, and to which base, depends
+// only on (seed, s, i), so strains regenerate identically in any order.
+extern "C" int ntc_synth_strains(const uint8_t *genome, uint64_t glen, uint64_t seed, uint32_t n_strains,
+                                 uint32_t snp_per_million, uint8_t *out) {
+    if ((!genome || !out) && glen && n_strains) return NTC_ERR_INVALID_ARG;
+    for (uint32_t st = 0; st < n_strains; st++) {
+        uint8_t *o = out + (uint64_t)st * glen;
+        for (uint64_t i = 0; i < glen; i++) {
+            uint64_t s = seed ^ (0x9E6C63D0676A9A99ULL * ((uint64_t)st + 1)) ^ (0xD6E8FEB86659FD93ULL * (i + 1));
+            const uint64_t u = splitmix64(s);
+            const uint8_t b0 = genome[i];
+            if ((u % 1000000ULL) < snp_per_million) {
+                const uint32_t c = b0 == 'A' ? 0 : b0 == 'C' ? 1 : b0 == 'G' ? 2 : 3;
+                o[i] = kBase[(c + 1 + (uint32_t)((u >> 32) % 3)) & 3];
+            } else {
+                o[i] = b0;
+            }
+        }
+    }
+    return NTC_OK;
+}
+
 extern "C" int ntc_synth_reads(const uint8_t *genome, uint64_t glen, uint64_t seed, uint64_t first_read,
                                uint64_t n_reads, uint32_t read_len, uint32_t err_per_million, int n_threads,
                                uint8_t *out) {

@@ -83,6 +83,19 @@ class OracleIndex:
             raise RuntimeError(f"oracle encode failed rc={rc} at read {bad.value}")
         return recs[:rc], roff
 
+    def try_encode(self, bases: np.ndarray, offsets: np.ndarray):
+        """-> (rc, bad_read): rc < 0 is the oracle's error (ORC_ERR_PANIC = -5 where the
+        reference panics), bad_read the first failing read."""
+        bases = np.ascontiguousarray(bases, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        cap = int(offsets[-1]) + 1
+        recs = np.zeros(cap, dtype=np.uint64)
+        roff = np.zeros(len(offsets), dtype=np.uint64)
+        bad = ctypes.c_int64(-1)
+        rc = self.lib.orc_encode_batch(self.h, _ptr(bases), _ptr(offsets), len(offsets) - 1, _ptr(recs), cap,
+                                       _ptr(roff), ctypes.byref(bad))
+        return int(rc), int(bad.value)
+
     def decode(self, recs: np.ndarray):
         recs = np.ascontiguousarray(recs, dtype=np.uint64)
         flags = (recs >> np.uint64(56)).astype(np.uint8)

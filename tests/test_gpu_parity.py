@@ -164,16 +164,17 @@ def test_gpu_index_without_a_base():
     ctx = nt.GpuContext(0)
     ctx.upload(ix)
     with pytest.raises(nt.NtcError) as e:
-        ctx.encode(*pack_reads(["ACGACGGAC", "ACGT"]))
+        ctx.encode(*pack_reads(["CGGACCAGACGAGGCAACGA", "ACGT"]))  # not "ACGACGGAC": a reference panic
     assert e.value.code == 2 and e.value.bad_read == 1
     ctx.close()
 
 
-def test_gpu_full_scale_roundtrip_c91():
-    """C91 index (5 Mbp, k=91) with 1M reads: decode(encode(x)) == x for every read, and a
-    20k-read sample bit-exact against the oracle."""
+@pytest.mark.parametrize("k", [91, 31])
+def test_gpu_full_scale_roundtrip(k):
+    """BASELINE configs C91 and C31: the 5 Mbp index at k with 1M reads: decode(encode(x))
+    == x for every read, and a 20k-read sample bit-exact against the oracle."""
     genome = nt.synth_genome(1, 5_000_000)
-    ix = nt.Index.build([genome.tobytes()], 91)
+    ix = nt.Index.build([genome.tobytes()], k)
     ctx = nt.GpuContext(0)
     ctx.upload(ix)
     n, L = 1_000_000, 150
@@ -182,11 +183,87 @@ def test_gpu_full_scale_roundtrip_c91():
     recs, roff = ctx.encode(reads, offs)
     out, o2 = ctx.decode(recs)
     assert np.array_equal(out, reads)
-    orc = OracleIndex(ix.n, 91, ix.rows, ix.C, ix.lcs)
+    orc = OracleIndex(ix.n, k, ix.rows, ix.C, ix.lcs)
     m = 20_000
     exp, eoff = orc.encode(reads[: m * L], offs[: m + 1])
     assert np.array_equal(recs[: int(roff[m])], exp)
     ctx.close()
+
+
+def test_gpu_strain_collection():
+    """An index of a genome + 3 strains at 1 % substitutions (fragmented path cover, many
+    branching nodes): 300k reads from the collection round-trip exactly, 10k bit-exact vs
+    the oracle (bench.py's S91 config at reduced size)."""
+    genome = nt.synth_genome(1, 2_000_000)
+    strains = nt.synth_strains(genome, 3, 3, 10_000)
+    texts = [genome] + [strains[i] for i in range(3)]
+    ix = nt.Index.build([t.tobytes() for t in texts], 91)
+    ctx = nt.GpuContext(0)
+    ctx.upload(ix)
+    assert ctx.get_option("n_paths") > 1000
+    coll = np.concatenate(texts)
+    n, L = 300_000, 150
+    reads = nt.synth_reads(coll, 2, 0, n, L, 10_000)
+    offs = np.arange(0, n * L + 1, L, dtype=np.uint64)
+    recs, roff = ctx.encode(reads, offs)
+    out, o2 = ctx.decode(recs)
+    assert np.array_equal(out, reads) and np.array_equal(o2, offs)
+    orc = OracleIndex(ix.n, 91, ix.rows, ix.C, ix.lcs)
+    m = 10_000
+    exp, eoff = orc.encode(reads[: m * L], offs[: m + 1])
+    assert np.array_equal(recs[: int(roff[m])], exp)
+    ctx.close()
+
+
+@pytest.mark.parametrize("k,glen", [(5, 300), (7, 20_000), (9, 2_000), (9, 20_000)])
+def test_gpu_small_k_reference_panic_status(ctx, k, glen):
+    """k <= 10: a short record with k < len <= 11 panics in the reference (encode.rs:151-152);
+    the GPU reports NTC_ERR_REFERENCE_PANIC at the oracle's first panicking read, and the other
+    reads encode bit-exact."""
+    g = nt.synth_genome(50 + k, glen)
+    ix = nt.Index.build([g.tobytes()], k)
+    ctx.upload(ix)
+    L, n = 150, 200
+    reads = nt.synth_reads(g, 3, 0, n, L, 10_000)
+    offs = np.arange(0, n * L + 1, L, dtype=np.uint64)
+    orc = OracleIndex(ix.n, k, ix.rows, ix.C, ix.lcs)
+    one = np.array([0, L], dtype=np.uint64)
+    panics = [r for r in range(n) if orc.try_encode(reads[r * L:(r + 1) * L], one)[0] == -5]
+    assert panics
+    with pytest.raises(nt.NtcError) as e:
+        ctx.encode(reads, offs)
+    assert e.value.code == 11 and e.value.bad_read == panics[0]
+    keep = [r for r in range(n) if r not in set(panics)]
+    if keep:
+        kr = np.concatenate([reads[r * L:(r + 1) * L] for r in keep])
+        ko = np.arange(0, len(keep) * L + 1, L, dtype=np.uint64)
+        got, goff = ctx.encode(kr, ko)
+        exp, eoff = orc.encode(kr, ko)
+        assert np.array_equal(got, exp) and np.array_equal(goff, eoff)
+
+
+def test_gpu_decode_bad_colex_over_many_tiles(ctx):
+    """Malformed records (colex rank >= n) spread over many 256-record tiles: the decode
+    reports NTC_ERR_FORMAT, writes nothing out of bounds and leaves the context usable."""
+    genome = nt.synth_genome(21, 400_000)
+    ix = nt.Index.build([genome.tobytes()], 31)
+    ctx.upload(ix)
+    n, L = 60_000, 150
+    reads = nt.synth_reads(genome, 5, 0, n, L, 10_000)
+    offs = np.arange(0, n * L + 1, L, dtype=np.uint64)
+    recs, _ = ctx.encode(reads, offs)
+    assert len(recs) > 50 * 256
+    flags = (recs >> np.uint64(56)) & np.uint64(2)
+    longs = np.nonzero(flags == 0)[0]
+    bad = recs.copy()
+    pick = longs[:: max(1, len(longs) // 200)]
+    bad[pick] = (bad[pick] & ~np.uint64(0xFFFFFFFF)) | np.uint64(0xFFFFFFF0)
+    for _ in range(3):
+        with pytest.raises(nt.NtcError) as e:
+            ctx.decode(bad)
+        assert e.value.code == 8
+    out, o2 = ctx.decode(recs)
+    assert np.array_equal(out, reads) and np.array_equal(o2, offs)
 
 
 @pytest.mark.parametrize("lead", [0, 3, 16, 37])

@@ -113,7 +113,8 @@ def test_emulated_absent_character_is_an_invalid_base():
     # genome without 'T': a read holding T has d = 0 there (the reference never
     # terminates, lib.rs:207); the kernels report NTC_ERR_INVALID_BASE for that read
     ix = nt.Index.build(["ACGACGGACCAGACGAGGCAACGAGCACCGA" * 3], 7, add_revcomp=False)
-    reads = [b"ACGACGGAC", b"ACGACGGACCAGACGAGG", b"ACGT"]
+    # (not b"ACGACGGAC": the reference panics on it, encode.rs:151-152 with len 9 > k = 7)
+    reads = [b"CGGACCAGACGAGGCAACGA", b"ACGACGGACCAGACGAGG", b"ACGT"]
     bases, offs = pack_reads(reads)
     with pytest.raises(RuntimeError, match="rc=2 bad=2"):
         emu_encode(ix.n, 7, ix.rows, ix.C, ix.lcs, bases, offs)
@@ -176,3 +177,29 @@ def test_emulated_decode_direct_path_for_long_records(block, monkeypatch):
     out, oo = emu_decode(ix.n, k, ix.rows, ix.C, ix.lcs, got)
     assert np.array_equal(out, bases)
     assert np.array_equal(oo, offs)
+
+
+@pytest.mark.parametrize("k,glen", [(5, 300), (7, 20_000), (9, 2_000), (9, 20_000)])
+def test_emulated_small_k_reference_panic_status(k, glen):
+    """k <= 10: a short record with k < len <= 11 makes the reference panic
+    (encode.rs:151-152, kmer[(k - len)..k]); the kernel returns NTC_ERR_REFERENCE_PANIC (11)
+    for exactly the reads the oracle flags (ORC_ERR_PANIC), at the same first read of a batch,
+    and bit-exact records for the others."""
+    g = nt.synth_genome(50 + k, glen)
+    ix = nt.Index.build([g.tobytes()], k)
+    L, n = 150, 200
+    reads = nt.synth_reads(g, 3, 0, n, L, 10_000)
+    offs = np.arange(0, n * L + 1, L, dtype=np.uint64)
+    orc = OracleIndex(ix.n, k, ix.rows, ix.C, ix.lcs)
+    one = np.array([0, L], dtype=np.uint64)
+    panics = [r for r in range(n) if orc.try_encode(reads[r * L:(r + 1) * L], one)[0] == -5]
+    assert panics, "the case must occur"
+    with pytest.raises(RuntimeError, match=f"rc=11 bad={panics[0]}"):
+        emu_encode(ix.n, k, ix.rows, ix.C, ix.lcs, reads, offs)
+    keep = [r for r in range(n) if r not in set(panics)]
+    if keep:
+        kr = np.concatenate([reads[r * L:(r + 1) * L] for r in keep])
+        ko = np.arange(0, len(keep) * L + 1, L, dtype=np.uint64)
+        got, goff = emu_encode(ix.n, k, ix.rows, ix.C, ix.lcs, kr, ko)
+        exp, eoff = orc.encode(kr, ko)
+        assert np.array_equal(got, exp) and np.array_equal(goff, eoff)
