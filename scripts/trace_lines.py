@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--read-len", type=int, default=150)
     ap.add_argument("--err-ppm", type=int, default=10_000)
     ap.add_argument("--tab-u", type=int, default=0)
+    ap.add_argument("--strains", type=int, default=0, help="index a collection: the genome + N strains")
+    ap.add_argument("--snp-ppm", type=int, default=10_000)
     args = ap.parse_args()
     so = os.path.join(REPO, "tests", "emu", "libntc_emu_trace.so")
     subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "tests", "emu"), "libntc_emu_trace.so"])
@@ -42,8 +44,12 @@ def main():
     L = emu_lib.emu_lib()
     L.emu_trace_report.argtypes = [ctypes.c_void_p]
     genome = nt.synth_genome(1, args.genome_bp)
-    ix = nt.Index.build([genome.tobytes()], args.k, threads=8)
-    reads = nt.synth_reads(genome, 2, 0, args.reads, args.read_len, args.err_ppm)
+    texts = [genome]
+    if args.strains:
+        st = nt.synth_strains(genome, 3, args.strains, args.snp_ppm)
+        texts += [st[i] for i in range(args.strains)]
+    ix = nt.Index.build([t.tobytes() for t in texts], args.k, threads=8)
+    reads = nt.synth_reads(np.concatenate(texts), 2, 0, args.reads, args.read_len, args.err_ppm)
     offs = np.arange(0, args.reads * args.read_len + 1, args.read_len, dtype=np.uint64)
     recs, _ = emu_lib.emu_encode(ix.n, args.k, ix.rows, ix.C, ix.lcs, reads, offs, tab_u=args.tab_u)
     K = len(KINDS)
