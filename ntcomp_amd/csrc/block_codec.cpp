@@ -299,9 +299,14 @@ bool compress_block(const std::vector<uint64_t> &data, uint64_t num_records, boo
     } else if (!minimal_binary_encode(data, words, param)) {
         return false;
     }
+    // Words hold the bitstream MSB-first.  dsi-bitstream's BE BufBitWriter hands each word to
+    // the word writer as to_be(), and encode.rs:107-109 then emits to_ne_bytes (little-endian
+    // on x86): the bytes on disk are the MSB-first bitstream, i.e. each word big-endian
+    // [ext dsi-bitstream 0.5.0, recalled; SURVEY.md A.4].  Parity unpinned vs the reference
+    // (no reference-written encoded.dat exists offline).
     std::vector<uint8_t> bytes(words.size() * 8);
     for (size_t i = 0; i < words.size(); i++)
-        for (int b = 0; b < 8; b++) bytes[i * 8 + b] = (uint8_t)(words[i] >> (8 * b));
+        for (int b = 0; b < 8; b++) bytes[i * 8 + b] = (uint8_t)(words[i] >> (8 * (7 - b)));
     std::vector<uint8_t> gz;
     if (!gzip_bytes(bytes.data(), bytes.size(), gz)) return false;
     BlockHeader h{};
@@ -321,7 +326,11 @@ bool decompress_block(const uint8_t *payload, const BlockHeader &h, bool rice, s
     std::vector<uint8_t> bytes;
     if (!gunzip_bytes(payload, h.block_size, bytes)) return false;
     std::vector<uint64_t> words(bytes.size() / 8);
-    for (size_t i = 0; i < words.size(); i++) words[i] = get_le(bytes.data() + 8 * i, 8);
+    for (size_t i = 0; i < words.size(); i++) {  // big-endian words (see compress_block)
+        uint64_t w = 0;
+        for (int b = 0; b < 8; b++) w = (w << 8) | bytes[8 * i + b];
+        words[i] = w;
+    }
     if (words.size() != h.encoded_size) return false;  // decode.rs:319-321
     return rice ? rice_decode(words, h.num_u64, h.rice_param, out)
                 : minimal_binary_decode(words, h.num_u64, h.rice_param, out);

@@ -96,3 +96,22 @@ def test_multi_block_stream_and_eof():
     out, offs = ix.decode(np.concatenate(allrecs))
     got = [out[offs[i]:offs[i + 1]].tobytes().decode() for i in range(len(offs) - 1)]
     assert len(got) > 0 and all(r in g["reads"] for r in got)
+
+
+def test_stream_bytes_hand_derived_fixture():
+    """Byte order of the stream words, pinned by hand (parity unpinned vs the reference: no
+    reference-written encoded.dat exists offline).  One read of 3 long records with colex
+    0, 1, 2 (lengths 12, 13, 14) and a short one: s1 = [0, 1, 2] -> minimal binary with max = 2 + 2 = 4
+    (encode.rs:77-94): v + 1 = 1, 2, 3 in 2 bits = 01 10 11 -> 0b011011 then zero padding,
+    so the inflated s1 payload is 6C 00 00 00 00 00 00 00 (MSB-first bitstream on disk,
+    SURVEY.md A.4).  s2 = lengths [12, 13, 14] with Rice and s3 = flags follow."""
+    recs = np.array([(1 << 56) | (12 << 32) | 0, (13 << 32) | 1, (14 << 32) | 2, (2 | 1 << 2) << 56],
+                    dtype=np.uint64)  # + one short record "A" (a block without one is dropped, App. B.3)
+    blob = nt.write_block(recs, 1)
+    h = blob[:32]
+    block_size, _, num_u64, encoded_size = np.frombuffer(h[:16], dtype="<u4")
+    assert (num_u64, encoded_size, int(np.frombuffer(h[16:24], dtype="<u8")[0])) == (3, 1, 4)
+    payload = gzip.decompress(blob[32:32 + int(block_size)])
+    assert payload == bytes([0x6C, 0, 0, 0, 0, 0, 0, 0])
+    got, used, _ = nt.read_block(blob)
+    assert np.array_equal(got, recs)
