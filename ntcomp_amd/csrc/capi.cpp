@@ -374,13 +374,14 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
         ctx->index_bytes += bytes;
         return NTC_OK;
     };
-    void *d_lines, *d_lcs, *d_uniq, *d_walk_a, *d_walk_b, *d_pred, *d_code;
+    void *d_lines, *d_lcs, *d_uniq, *d_walk, *d_walk_a, *d_walk_b, *d_pred, *d_code;
     int rc;
     if ((rc = dalloc(dv.rank.size() * sizeof(uint2), &d_lines))) return rc;
     if ((rc = dalloc(n + 256, &d_lcs))) return rc;
     if ((rc = dalloc(dv.uniq.size() * 4, &d_uniq))) return rc;
-    if ((rc = dalloc(n * sizeof(WalkEntry), &d_walk_a))) return rc;
-    HIP_TRY(ctx, hipMalloc(&d_walk_b, n * sizeof(WalkEntry)));
+    if ((rc = dalloc(n * sizeof(WalkEntry), &d_walk))) return rc;
+    HIP_TRY(ctx, hipMalloc(&d_walk_a, n * sizeof(WalkStep)));
+    HIP_TRY(ctx, hipMalloc(&d_walk_b, n * sizeof(WalkStep)));
     HIP_TRY(ctx, hipMalloc(&d_pred, n * 4));
     HIP_TRY(ctx, hipMalloc(&d_code, n + 64));
     HIP_TRY(ctx, hipMemcpy(d_lines, dv.rank.data(), dv.rank.size() * sizeof(uint2), hipMemcpyHostToDevice));
@@ -389,13 +390,9 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     HIP_TRY(ctx, hipMemcpy(d_uniq, dv.uniq.data(), dv.uniq.size() * 4, hipMemcpyHostToDevice));
     HIP_TRY(ctx, hipMemcpy(d_pred, dv.pred.data(), n * 4, hipMemcpyHostToDevice));
     HIP_TRY(ctx, hipMemcpy(d_code, dv.code.data(), n, hipMemcpyHostToDevice));
-    WalkEntry *result = nullptr;
-    launch_walk_build((const uint32_t *)d_pred, (const uint8_t *)d_code, n, (WalkEntry *)d_walk_a,
-                      (WalkEntry *)d_walk_b, &result, ctx->stream);
+    launch_walk_build((const uint32_t *)d_pred, (const uint8_t *)d_code, n, (WalkStep *)d_walk_a,
+                      (WalkStep *)d_walk_b, (WalkEntry *)d_walk, ctx->stream);
     HIP_TRY(ctx, hipGetLastError());
-    if (result != (WalkEntry *)d_walk_a)
-        HIP_TRY(ctx, hipMemcpyAsync(d_walk_a, result, n * sizeof(WalkEntry), hipMemcpyDeviceToDevice,
-                                    ctx->stream));
     // path cover, built on the device (kernels.hip "path cover"; derived.cpp build_paths is
     // the same cover on the host, for emulation)
     void *d_pstream = nullptr, *d_colex_at = nullptr, *d_pos = nullptr, *d_puniq = nullptr;
@@ -468,6 +465,7 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
         free_tmp();
     }
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipFree(d_walk_a));
     HIP_TRY(ctx, hipFree(d_walk_b));
     HIP_TRY(ctx, hipFree(d_pred));
     HIP_TRY(ctx, hipFree(d_code));
@@ -475,7 +473,7 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     d.rank = (const uint2 *)d_lines;
     d.lcs = (const uint8_t *)d_lcs;
     d.uniq = (const uint32_t *)d_uniq;
-    d.walk = (const WalkEntry *)d_walk_a;
+    d.walk = (const WalkEntry *)d_walk;
     d.rwords = dv.rwords;
     d.n = (uint32_t)n;
     d.k = hx.k;
@@ -754,8 +752,8 @@ int ntc_decode_batch_device(ntc_ctx *ctx, const uint64_t *d_recs, uint64_t n_rec
     void *ws, *tmp;
     int rc;
     const uint64_t n = n_recs;
-    // per 256-record tile: pf, pl (sums) then pfs, pls (exclusive scans, totals at [tiles])
-    const uint64_t tiles = (n + 255) / 256;
+    // per kDecTileRecs-record tile: pf, pl (sums) then pfs, pls (exclusive scans, totals at [tiles])
+    const uint64_t tiles = (n + kDecTileRecs - 1) / kDecTileRecs;
     if ((rc = ensure(ctx, WS_DEC_C, (4 * tiles + 2) * 8, &ws))) return rc;
     uint64_t *pf = (uint64_t *)ws, *pl = pf + tiles, *pfs = pl + tiles, *pls = pfs + tiles + 1;
     if ((rc = ensure(ctx, WS_SCANTMP, (scan_tmp_words(tiles + 1) + 2) * 8, &tmp))) return rc;

@@ -278,7 +278,7 @@ void build_paths(const HostIndex &ix, Derived &dv) {
 }
 
 void build_walk_host(const Derived &dv, uint64_t n, std::vector<WalkEntry> &walk) {
-    std::vector<WalkEntry> a(n), b(n);
+    std::vector<WalkStep> a(n), b(n);
     for (uint64_t j = 0; j < n; j++) {
         a[j].chars = dv.code[j];
         a[j].jump = dv.pred[j];
@@ -286,21 +286,25 @@ void build_walk_host(const Derived &dv, uint64_t n, std::vector<WalkEntry> &walk
     }
     for (uint32_t m = 1; m < 32; m *= 2) {
         for (uint64_t j = 0; j < n; j++) {
-            const WalkEntry &x = a[j];
-            const WalkEntry &y = a[x.jump];
+            const WalkStep &x = a[j];
+            const WalkStep &y = a[x.jump];
             b[j].chars = y.chars | (x.chars << (2 * m));
             b[j].jump = y.jump;
             b[j].older = 0;
         }
         a.swap(b);
     }
-    // a = 32-step entries, b = 16-step: extend to kWalkSpan = 48 steps
+    // a = 32-step entries, b = 16-step: extend a to 48 steps, then compose 48 + 48 + 16
     for (uint64_t j = 0; j < n; j++) {
-        const WalkEntry &y = b[a[j].jump];
+        const WalkStep &y = b[a[j].jump];
         a[j].older = (uint32_t)y.chars;
         a[j].jump = y.jump;
     }
-    walk.swap(a);
+    walk.resize(n);
+    for (uint64_t j = 0; j < n; j++) {
+        const WalkStep &x = a[j], &y = a[x.jump];
+        walk[j] = walk_compose(x, y, b[y.jump]);
+    }
 }
 
 DevIndex host_dev_index(const HostIndex &ix, const Derived &dv, const std::vector<WalkEntry> &walk) {

@@ -49,15 +49,37 @@ NTC_HD void ntc_stat_add(int, uint64_t) {}
 // (ones of row c before the word), y = the 32 row bits.  extend = two 8-byte loads + two
 // popcounts (DESIGN.md "Data layout in HBM").  Rows live in 4 separate arrays of rwords.
 
-// Inverse-walk jump table: the 32 characters met by walking 32 steps backwards from node
-// j (text order, character t in bits 2t..2t+1) and the node reached.  Replaces 32
-// dependent select()s of access_kmer by one 16-byte load.
-struct alignas(16) WalkEntry {
-    uint64_t chars;  // the last 32 of the 48 characters (text order, oldest in the low bits)
+// Inverse-walk jump table: the kWalkSpan = 112 characters met by walking 112 steps
+// backwards from node j, in text order t0..t111 (t111 = node j's own last character), and
+// the node reached.  One 32-byte entry (one 128 B line) replaces 112 dependent select()s of
+// access_kmer: a long record of up to 112 bases (every long record of a 150 bp read at
+// k = 91 with errors) is ONE random line, where 48-character entries took 1.1 per record.
+struct alignas(32) WalkEntry {
+    uint64_t w0;     // t80..t111 (character t80 + i in bits 2i..2i+1)
+    uint64_t w1;     // t48..t79
+    uint64_t w2;     // t16..t47
+    uint32_t older;  // t0..t15
     uint32_t jump;   // the node kWalkSpan steps back
-    uint32_t older;  // the 16 characters before those
 };
-constexpr uint32_t kWalkSpan = 48;
+constexpr uint32_t kWalkSpan = 112;
+// 16-byte doubling steps the table is built from at upload (k_walk_*, build_walk_host):
+// chars = the last 32 characters of the step (text order), older = the 16 before them
+struct alignas(16) WalkStep {
+    uint64_t chars;
+    uint32_t jump;
+    uint32_t older;
+};
+// 112-step entry of node j from its 48-step entry x, the 48-step entry y at x's jump and the
+// 16-step entry z at y's jump
+NTC_HD WalkEntry walk_compose(const WalkStep &x, const WalkStep &y, const WalkStep &z) {
+    WalkEntry e;
+    e.w0 = x.chars;                                            // t80..t111
+    e.w1 = (y.chars >> 32) | ((uint64_t)x.older << 32);        // t48..t63 | t64..t79
+    e.w2 = (uint64_t)y.older | ((y.chars & 0xFFFFFFFFull) << 32);  // t16..t31 | t32..t47
+    e.older = (uint32_t)z.chars;                               // t0..t15
+    e.jump = z.jump;
+    return e;
+}
 
 struct DevIndex {
     const uint2 *rank;      // [4][rwords] rank words
@@ -463,7 +485,10 @@ struct BaseReader {
 };
 
 enum : uint32_t { kModeScan = 0, kModeExt = 1, kModeP1 = 2, kModeBs = 3, kModeBrk = 4, kModeFirst = 5, kModeEnter = 6,
-                  kModeBrkLong = 7 };
+                  kModeBrkLong = 7, kModeExtFail = 8 };
+#ifndef NTC_EXT_EAGER
+#define NTC_EXT_EAGER 0  // 1: every EXT also loads p's table entry (HBM line) in case the extension fails
+#endif
 constexpr uint32_t kScanW = 16;      // presence probes per SCAN unit (U + kScanW - 1 <= 32)
 #ifndef NTC_SCAN_MODE
 #define NTC_SCAN_MODE 0  // 2: SCAN loads the first candidate pair's table entry directly
@@ -1191,12 +1216,22 @@ struct MsLane {
             return 0;
         }
         const int c = (int)((qw >> (2 * (p - qb))) & 3u);
-        if (mode == kModeExt) {
-            NTC_TOUCH(kTrTabU, ix.tab + tab_base(U) + key_at(p, U));
-            const uint2 te = load2_stream(ix.tab + tab_base(U) + key_at(p, U));  // for a failure
-            uint32_t nl, nr;
-            extend(ix, c, l, r, nl, nr);
-            if (nl < nr) return commit(ix, b, nl, nr, d + 1 < k ? d + 1 : k);
+        if (mode == kModeExt || mode == kModeExtFail) {
+            uint2 te;
+            if (NTC_EXT_EAGER || mode == kModeExtFail) {
+                // p's table entry, wanted only when the extension fails
+                NTC_TOUCH(kTrTabU, ix.tab + tab_base(U) + key_at(p, U));
+                te = load2_stream(ix.tab + tab_base(U) + key_at(p, U));
+            }
+            if (mode == kModeExt) {
+                uint32_t nl, nr;
+                extend(ix, c, l, r, nl, nr);
+                if (nl < nr) return commit(ix, b, nl, nr, d + 1 < k ? d + 1 : k);
+                if (!NTC_EXT_EAGER) {  // one more round trip for the entry, only on a failure
+                    mode = kModeExtFail;
+                    return 0;
+                }
+            }
             if (!tab_long(te)) {  // p is short: table-determined, scan on
                 skip_short(b, te, U);
                 return p >= len ? 1 : 0;
@@ -1386,60 +1421,59 @@ NTC_HD void stage_store_word(uint8_t *out, uint64_t wg, uint64_t bits, uint32_t 
 
 // The L characters of the L-step inverse walk from node j, to output characters
 // [g0, g0 + L) of a code writer (StageWriter); false on a malformed record.
-// the characters of one walk entry (chars, older) for output characters ending at g0 + end
+// the characters of one walk entry for output characters ending at g0 + end (newest first)
 template <class Writer>
-NTC_HD void walk_put(uint32_t &end, uint64_t g0, Writer &cw, uint64_t chars, uint32_t older) {
-    const uint32_t take = end < kWalkSpan ? end : kWalkSpan;
-    const uint32_t t32 = take < 32 ? take : 32;
-    cw.put(g0 + end - t32, t32 ? chars >> (2 * (32 - t32)) : 0, t32);
-    const uint32_t t16 = take - t32;
-    if (t16) cw.put(g0 + end - take, (uint64_t)(older >> (2 * (16 - t16))), t16);
-    end -= take;
+NTC_HD void walk_put(uint32_t &end, uint64_t g0, Writer &cw, const WalkEntry &e) {
+    const uint64_t piece[4] = {e.w0, e.w1, e.w2, (uint64_t)e.older};
+    const uint32_t width[4] = {32, 32, 32, 16};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t t = end < width[i] ? end : width[i];
+        if (t) cw.put(g0 + end - t, piece[i] >> (2 * (width[i] - t)), t);
+        end -= t;
+    }
 }
 
 NTC_HD WalkEntry walk_at(const DevIndex &ix, uint32_t cur) {
 #ifdef __HIP_DEVICE_COMPILE__
-    const uint4 e4 = *reinterpret_cast<const uint4 *>(ix.walk + cur);
-    return WalkEntry{(uint64_t)e4.x | ((uint64_t)e4.y << 32), e4.z, e4.w};
+    const uint4 a = reinterpret_cast<const uint4 *>(ix.walk + cur)[0];
+    const uint4 b = reinterpret_cast<const uint4 *>(ix.walk + cur)[1];
+    WalkEntry e;
+    e.w0 = (uint64_t)a.x | ((uint64_t)a.y << 32);
+    e.w1 = (uint64_t)a.z | ((uint64_t)a.w << 32);
+    e.w2 = (uint64_t)b.x | ((uint64_t)b.y << 32);
+    e.older = b.z;
+    e.jump = b.w;
+    return e;
 #else
     return ix.walk[cur];
 #endif
 }
 
+// The L characters of the L-step inverse walk from node j, to output characters
+// [g0, g0 + L) of a code writer (StageWriter); false on a malformed record.
 template <class Writer>
 NTC_HD bool walk_record_codes(const DevIndex &ix, uint32_t j, uint32_t L, uint64_t g0, Writer &cw) {
     uint32_t end = L, cur = j;
     while (end > 0) {
         if (cur >= ix.n) return false;
         const WalkEntry e = walk_at(ix, cur);
-        walk_put(end, g0, cw, e.chars, e.older);
+        walk_put(end, g0, cw, e);
         cur = e.jump;
     }
     return true;
 }
 
+// ASCII straight to memory (a Writer for walk_put)
+struct DirectWriter {
+    uint8_t *out;  // output character 0
+    NTC_HD void put(uint64_t g, uint64_t codes, uint32_t n) { store_codes(out + g, codes, n); }
+};
+
 // Writes the L characters of the L-step inverse walk from node j into out[0..L).
 NTC_HD bool walk_record(const DevIndex &ix, uint32_t j, uint32_t L, uint8_t *out) {
-    uint32_t end = L, cur = j;
-    while (end > 0) {
-        if (cur >= ix.n) return false;
-#ifdef __HIP_DEVICE_COMPILE__
-        const uint4 e4 = *reinterpret_cast<const uint4 *>(ix.walk + cur);
-        const uint64_t chars = (uint64_t)e4.x | ((uint64_t)e4.y << 32);
-        const uint32_t jump = e4.z, older = e4.w;
-#else
-        const uint64_t chars = ix.walk[cur].chars;
-        const uint32_t jump = ix.walk[cur].jump, older = ix.walk[cur].older;
-#endif
-        const uint32_t take = end < kWalkSpan ? end : kWalkSpan;
-        const uint32_t t32 = take < 32 ? take : 32;  // from `chars`
-        store_codes(out + end - t32, t32 ? chars >> (2 * (32 - t32)) : 0, t32);
-        const uint32_t t16 = take - t32;  // from `older`
-        if (t16) store_codes(out + end - take, (uint64_t)(older >> (2 * (16 - t16))), t16);
-        end -= take;
-        cur = jump;
-    }
-    return true;
+    DirectWriter dw{out};
+    return walk_record_codes(ix, j, L, 0, dw);
 }
 
 // decode_sequence for one read: its records [rb, re) were emitted rightmost first, so

@@ -63,12 +63,20 @@ struct DebugArgs {
     uint32_t *s_out;
 };
 
+// decode tiles: k_dec_rec's block of 256 threads owns kDecTileRecs consecutive records, kDecR
+// per thread (two independent walk chains per lane: twice the loads in flight per wave)
+#ifndef NTC_DEC_R
+#define NTC_DEC_R 2
+#endif
+constexpr uint32_t kDecR = NTC_DEC_R;
+constexpr uint32_t kDecTileRecs = 256 * kDecR;
+
 struct DecWalkArgs {
     DevIndex ix;
     const uint64_t *recs;
     uint64_t n;
-    const uint64_t *pfs;         // per 256-record tile: first records before it [tiles + 1]
-    const uint64_t *pls;         // per 256-record tile: bases before it [tiles + 1]
+    const uint64_t *pfs;         // per kDecTileRecs-record tile: first records before it [tiles + 1]
+    const uint64_t *pls;         // per tile: bases before it [tiles + 1]
     uint64_t *offs_out;          // each read's output offset [nreads + 1] (written here)
     uint64_t offs_capacity;
     uint64_t bases_capacity;
@@ -96,8 +104,8 @@ void launch_debug_gather(const DebugArgs &a, hipStream_t s);
 void launch_dec_tiles(const uint64_t *recs, uint64_t n, uint64_t *pf, uint64_t *pl, uint64_t *pfs, uint64_t *pls,
                       uint64_t *tmp, hipStream_t s);
 void launch_dec_walk(const DecWalkArgs &a, hipStream_t s);
-void launch_walk_build(const uint32_t *pred, const uint8_t *code, uint64_t n, WalkEntry *a, WalkEntry *b,
-                       WalkEntry **result, hipStream_t s);
+void launch_walk_build(const uint32_t *pred, const uint8_t *code, uint64_t n, WalkStep *a, WalkStep *b,
+                       WalkEntry *out, hipStream_t s);
 uint64_t scan_tmp_words(uint64_t n);
 
 // Path cover on the device (derived.cpp build_paths, same cover): unitigs of the real

@@ -338,7 +338,6 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
     return v;
 }
 
-constexpr uint32_t kDecTileRecs = 256;  // = k_dec_rec's block
 
 // one wave per tile: 4 coalesced loads per lane, wave sums
 __global__ __launch_bounds__(256) void k_dec_tiles(const uint64_t *recs, uint64_t n, uint64_t *pf, uint64_t *pl) {
@@ -369,17 +368,20 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t &total)
 // ---------------------------------------------------------------------------------
 // decode
 // ---------------------------------------------------------------------------------
-// one lane per RECORD: records are independent once their output offsets are known.  A
-// read's records are consumed last to first (lib.rs:266), so record r of read rid lands at
-// start(rid) + (end(rid) - E[r + 1]), with E the exclusive scan of lengths in record order
-// and start/end(rid) the read's output range.  Each block derives E, rid and the ranges of
-// its 256 records from the tile scans (k_dec_tiles) plus a block scan; the read open at the
-// tile start and the read running past its end are found by scanning records outward.
-// Output is staged per block (StageWriter): the block's
+// Records are independent once their output offsets are known.  A read's records are
+// consumed last to first (lib.rs:266), so record r of read rid lands at start(rid) +
+// (end(rid) - E[r + 1]), with E the exclusive scan of lengths in record order and
+// start/end(rid) the read's output range.  A block owns one tile of kDecTileRecs records,
+// kDecR consecutive ones per thread (coalesced loads, and kDecR independent walk chains per
+// lane), and derives E, rid and the reads' ranges from the tile scans (k_dec_tiles) plus a
+// block scan; the read open at the tile start and the read running past its end are found
+// by scanning records outward.  Output is staged per block (StageWriter): the block's
 // records cover a contiguous stretch of output words (with at most a few words shared with
-// neighbouring blocks); codes are OR-ed into LDS, then the block writes each word's ASCII once.
-// A block whose stretch exceeds kDecStageWords (very long records) writes ASCII directly.
+// neighbouring blocks); codes are OR-ed into LDS, then the block writes each word's ASCII
+// once.  A block whose stretch exceeds kDecStageWords (very long records) writes ASCII
+// directly.
 __global__ __launch_bounds__(256) void k_dec_rec(DecWalkArgs a) {
+    constexpr uint32_t R = kDecR;
     __shared__ uint64_t s_bits[kDecStageWords];
     __shared__ uint32_t s_mask[kDecStageWords];
     __shared__ uint64_t s_lo[4], s_hi[4];
@@ -397,40 +399,62 @@ __global__ __launch_bounds__(256) void k_dec_rec(DecWalkArgs a) {
         if (t == 0 && threadIdx.x == 0) atomicMin(a.status, (unsigned long long)kErrCapacity);
         return;
     }
+    // the tile's prefixes, loaded before the walk entries below: the wait for them (in-order
+    // vmcnt) then leaves the walk loads in flight
+    const uint64_t pf_t = a.pfs[t], pl_t = a.pls[t];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t r0 = t * kDecTileRecs, r = r0 + threadIdx.x;
+    const uint64_t r0 = t * kDecTileRecs, rb = r0 + (uint64_t)threadIdx.x * R;  // this thread's records
     const uint64_t r1 = r0 + kDecTileRecs < n ? r0 + kDecTileRecs : n;
-    uint64_t w = 0, f = 0, len = 0;
-    if (r < n) {
-        w = a.recs[r];
-        dec_desc(w, f, len);
+    // Every load below is unconditional (indices clamped into range, results masked after):
+    // a load under a branch makes hipcc wait for it inside the branch, which would serialise
+    // the records, the walk entries and the scan window into separate round trips.
+    uint64_t w[R], f[R], len[R];
+#pragma unroll
+    for (uint32_t i = 0; i < R; i++) w[i] = a.recs[rb + i < n ? rb + i : n - 1];
+    // the first 64-record window of the outward scans (waves 0 and 1)
+    const int64_t wi = wave == 0 ? (int64_t)r0 - 64 + lane : (int64_t)(r1 + lane);
+    const uint64_t wraw = a.recs[wi < 0 ? 0 : ((uint64_t)wi < n ? (uint64_t)wi : n - 1)];
+    // the first walk entry of each long record, issued before the index prologue so that its
+    // latency overlaps the scans
+    bool is_long[R];
+    WalkEntry e0[R];
+#pragma unroll
+    for (uint32_t i = 0; i < R; i++) {
+        if (rb + i >= n) w[i] = 0;
+        dec_desc(w[i], f[i], len[i]);
+        if (rb + i >= n) f[i] = len[i] = 0;
+        is_long[i] = len[i] > 0 && !((w[i] >> 56) & 2) && (uint32_t)w[i] < a.ix.n;
+        e0[i] = walk_at(a.ix, is_long[i] ? (uint32_t)w[i] : 0u);
     }
-    // issued before the index prologue so that they overlap it: the first walk entry of a
-    // long record, and the first 64-record window of the outward scans (waves 0 and 1)
-    const bool is_long = len > 0 && !((w >> 56) & 2) && (uint32_t)w < a.ix.n;
-    WalkEntry e0{0, 0, 0};
-    if (is_long) e0 = walk_at(a.ix, (uint32_t)w);
-    uint64_t wpre = 0;
-    if (wave == 0) {
-        if (r0 >= 64) wpre = a.recs[r0 - 64 + lane];
-        else if (r0 > 0 && lane >= 64 - r0) wpre = a.recs[r0 - 64 + lane];
-    } else if (wave == 1 && r1 + lane < n) {
-        wpre = a.recs[r1 + lane];
-    }
+    const uint64_t wpre = (wave == 0 && wi >= 0) || (wave == 1 && (uint64_t)wi < n) ? wraw : 0;
     // E[r] (bases before record r) and the read of r, from the tile scans + a block scan
+    uint64_t sf = 0, sl = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < R; i++) {
+        sf += f[i];
+        sl += len[i];
+    }
     uint64_t tf, tl;
-    const uint64_t ef = block_excl_scan(f, tf);
-    const uint64_t el = block_excl_scan(len, tl);
-    const uint64_t Er = a.pls[t] + el;
-    const uint64_t rid = a.pfs[t] + ef + f - 1;  // a record belongs to the last first record at or before it
-    const int64_t li = (int64_t)(ef + f) - 1;     // read index within the tile (-1: the read open at r0)
-    if (r < n && f) {
-        s_start[li] = Er;
-        if (rid < a.offs_capacity) a.offs_out[rid] = Er;  // the read's output offset
+    uint64_t cf = block_excl_scan(sf, tf);
+    uint64_t cl = block_excl_scan(sl, tl);
+    uint64_t Er[R];
+    int64_t li[R];  // read index within the tile (-1: the read open at r0)
+    uint64_t rid[R];
+#pragma unroll
+    for (uint32_t i = 0; i < R; i++) {
+        Er[i] = pl_t + cl;
+        rid[i] = pf_t + cf + f[i] - 1;  // a record belongs to the last first record at or before it
+        li[i] = (int64_t)(cf + f[i]) - 1;
+        if (rb + i < n && f[i]) {
+            s_start[li[i]] = Er[i];
+            if (rid[i] < a.offs_capacity) a.offs_out[rid[i]] = Er[i];  // the read's output offset
+        }
+        cf += f[i];
+        cl += len[i];
     }
     if (wave == 0) {  // start of the read open at r0: back to its first record
         uint64_t acc = 0, base = r0;
-        bool open = r0 > 0 && __shfl(f, 0, 64) == 0;
+        bool open = r0 > 0 && __shfl(f[0], 0, 64) == 0;  // thread 0 holds record r0
         while (open) {
             const int64_t rr = (int64_t)base - 64 + lane;
             uint64_t ff = 0, ll = 0;
@@ -445,7 +469,7 @@ __global__ __launch_bounds__(256) void k_dec_rec(DecWalkArgs a) {
             if (base <= 64) break;  // no first record before r0 (reported below as a format error)
             base -= 64;
         }
-        if (lane == 0) s_open[0] = a.pls[t] - acc;
+        if (lane == 0) s_open[0] = pl_t - acc;
     } else if (wave == 1) {  // end of the tile's last read: on to the next first record
         uint64_t acc = 0, base = r1;
         while (base < n) {
@@ -461,29 +485,36 @@ __global__ __launch_bounds__(256) void k_dec_rec(DecWalkArgs a) {
             acc += wave_sum64(ll);
             base += 64;
         }
-        if (lane == 0) s_open[1] = a.pls[t] + tl + acc;
+        if (lane == 0) s_open[1] = pl_t + tl + acc;
     }
-    if (t == 0 && threadIdx.x == 0 && n > 0 && !f)
+    if (t == 0 && threadIdx.x == 0 && n > 0 && !f[0])
         atomicMin(a.status, (unsigned long long)kErrFormat);  // records must start a read
     if (t + 1 == tiles && threadIdx.x == 0) a.offs_out[reads] = bases;
     __syncthreads();
-    const uint32_t L = (uint32_t)len;
-    uint64_t g0 = 0;
-    if (r < n) {
-        const uint64_t start = li >= 0 ? s_start[li] : s_open[0];
-        const uint64_t end = li + 1 < (int64_t)tf ? s_start[li + 1] : s_open[1];
-        g0 = start + (end - (Er + len));  // a read's records are consumed last to first (lib.rs:266)
+    uint64_t g0[R];
+    uint64_t lo = ~0ULL, hi = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < R; i++) {
+        g0[i] = 0;
+        if (rb + i < n) {
+            const uint64_t start = li[i] >= 0 ? s_start[li[i]] : s_open[0];
+            const uint64_t end = li[i] + 1 < (int64_t)tf ? s_start[li[i] + 1] : s_open[1];
+            g0[i] = start + (end - (Er[i] + len[i]));  // a read's records are consumed last to first (lib.rs:266)
+        }
+        if (len[i]) {
+            lo = g0[i] < lo ? g0[i] : lo;
+            hi = g0[i] + len[i] > hi ? g0[i] + len[i] : hi;
+        }
     }
     // the block's output stretch [lo, hi)
-    uint64_t lo = L ? g0 : ~0ULL, hi = L ? g0 + L : 0;
     for (int o = 32; o > 0; o >>= 1) {
         const uint64_t l2 = __shfl_xor(lo, o, 64), h2 = __shfl_xor(hi, o, 64);
         lo = l2 < lo ? l2 : lo;
         hi = h2 > hi ? h2 : hi;
     }
-    if ((threadIdx.x & 63) == 0) {
-        s_lo[threadIdx.x >> 6] = lo;
-        s_hi[threadIdx.x >> 6] = hi;
+    if (lane == 0) {
+        s_lo[wave] = lo;
+        s_hi[wave] = hi;
     }
     __syncthreads();
     for (int q = 0; q < 4; q++) {
@@ -491,44 +522,49 @@ __global__ __launch_bounds__(256) void k_dec_rec(DecWalkArgs a) {
         hi = s_hi[q] > hi ? s_hi[q] : hi;
     }
     if (lo >= hi) return;  // no characters in this block
-    const bool is_short = ((w >> 56) & 2) != 0;
     const uint64_t w_lo = lo >> 5, nw = ((hi - 1) >> 5) - w_lo + 1;
     if (nw > kDecStageWords) {  // whole block: direct ASCII
-        if (L) {
-            if (is_short) store_codes(a.out + g0, w, L);
-            else if (!walk_record(a.ix, (uint32_t)w, L, a.out + g0))
-                atomicMin(a.status, (unsigned long long)((rid << 8) | (uint64_t)kErrFormat));
+#pragma unroll
+        for (uint32_t i = 0; i < R; i++) {
+            const uint32_t L = (uint32_t)len[i];
+            if (!L) continue;
+            if ((w[i] >> 56) & 2) store_codes(a.out + g0[i], w[i], L);
+            else if (!walk_record(a.ix, (uint32_t)w[i], L, a.out + g0[i]))
+                atomicMin(a.status, (unsigned long long)((rid[i] << 8) | (uint64_t)kErrFormat));
         }
         return;
     }
-    for (uint32_t t = threadIdx.x; t < nw; t += 256) {
-        s_bits[t] = 0;
-        s_mask[t] = 0;
+    for (uint32_t q = threadIdx.x; q < nw; q += 256) {
+        s_bits[q] = 0;
+        s_mask[q] = 0;
     }
     __syncthreads();
     StageWriter sw{s_bits, s_mask, w_lo};
-    if (L) {
-        if (is_short) {
-            sw.put(g0, w, L);
-        } else if (!is_long) {
-            atomicMin(a.status, (unsigned long long)((rid << 8) | (uint64_t)kErrFormat));
+#pragma unroll
+    for (uint32_t i = 0; i < R; i++) {
+        const uint32_t L = (uint32_t)len[i];
+        if (!L) continue;
+        if ((w[i] >> 56) & 2) {
+            sw.put(g0[i], w[i], L);
+        } else if (!is_long[i]) {
+            atomicMin(a.status, (unsigned long long)((rid[i] << 8) | (uint64_t)kErrFormat));
         } else {  // walk_record_codes from the prefetched first entry
             uint32_t end = L;
-            walk_put(end, g0, sw, e0.chars, e0.older);
-            uint32_t cur = e0.jump;
+            walk_put(end, g0[i], sw, e0[i]);
+            uint32_t cur = e0[i].jump;
             while (end > 0) {
                 if (cur >= a.ix.n) {
-                    atomicMin(a.status, (unsigned long long)((rid << 8) | (uint64_t)kErrFormat));
+                    atomicMin(a.status, (unsigned long long)((rid[i] << 8) | (uint64_t)kErrFormat));
                     break;
                 }
                 const WalkEntry e = walk_at(a.ix, cur);
-                walk_put(end, g0, sw, e.chars, e.older);
+                walk_put(end, g0[i], sw, e);
                 cur = e.jump;
             }
         }
     }
     __syncthreads();
-    for (uint32_t t = threadIdx.x; t < nw; t += 256) stage_store_word(a.out, w_lo + t, s_bits[t], s_mask[t]);
+    for (uint32_t q = threadIdx.x; q < nw; q += 256) stage_store_word(a.out, w_lo + q, s_bits[q], s_mask[q]);
 }
 
 // 2-bit output -> ASCII, 32 characters per thread (two 16-byte stores when the output is
@@ -538,23 +574,22 @@ __global__ __launch_bounds__(256) void k_dec_rec(DecWalkArgs a) {
 // walk table: W_{2m}(j) = W_m(pred^m(j)) . W_m(j)
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_walk_init(const uint32_t *pred, const uint8_t *code, uint64_t n,
-                                                   WalkEntry *w) {
+                                                   WalkStep *w) {
     const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (j >= n) return;
-    WalkEntry e;
+    WalkStep e;
     e.chars = code[j];
     e.jump = pred[j];
     e.older = 0;
     w[j] = e;
 }
 
-__global__ __launch_bounds__(256) void k_walk_double(const WalkEntry *a, WalkEntry *b, uint64_t n,
-                                                     uint32_t m) {
+__global__ __launch_bounds__(256) void k_walk_double(const WalkStep *a, WalkStep *b, uint64_t n, uint32_t m) {
     const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (j >= n) return;
-    const WalkEntry x = a[j];
-    const WalkEntry y = a[x.jump];
-    WalkEntry o;
+    const WalkStep x = a[j];
+    const WalkStep y = a[x.jump];
+    WalkStep o;
     o.chars = y.chars | (x.chars << (2 * m));
     o.jump = y.jump;
     o.older = 0;
@@ -562,14 +597,24 @@ __global__ __launch_bounds__(256) void k_walk_double(const WalkEntry *a, WalkEnt
 }
 
 // 48-step entries: the 16 characters before the 32 of w32[j], from w16 at its jump
-__global__ __launch_bounds__(256) void k_walk_ext(WalkEntry *w32, const WalkEntry *w16, uint64_t n) {
+__global__ __launch_bounds__(256) void k_walk_ext(WalkStep *w32, const WalkStep *w16, uint64_t n) {
     const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (j >= n) return;
-    WalkEntry x = w32[j];
-    const WalkEntry y = w16[x.jump];
+    WalkStep x = w32[j];
+    const WalkStep y = w16[x.jump];
     x.older = (uint32_t)y.chars;
     x.jump = y.jump;
     w32[j] = x;
+}
+
+// 112-step entries: 48 + 48 + 16 steps (walk_compose)
+__global__ __launch_bounds__(256) void k_walk_final(const WalkStep *w48, const WalkStep *w16, uint64_t n,
+                                                    WalkEntry *out) {
+    const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    const WalkStep x = w48[j];
+    const WalkStep y = w48[x.jump];
+    out[j] = walk_compose(x, y, w16[y.jump]);
 }
 
 // ---------------------------------------------------------------------------------
@@ -779,21 +824,21 @@ void launch_debug_gather(const DebugArgs &a, hipStream_t s) {
     hipLaunchKernelGGL(k_debug_gather, grid_for(a.n_reads), dim3(256), 0, s, a);
 }
 void launch_dec_walk(const DecWalkArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL(k_dec_rec, dim3((uint32_t)((a.n + kDecTileRecs - 1) / kDecTileRecs)), dim3(kDecTileRecs), 0, s,
+    hipLaunchKernelGGL(k_dec_rec, dim3((uint32_t)((a.n + kDecTileRecs - 1) / kDecTileRecs)), dim3(256), 0, s,
                        a);
 }
-void launch_walk_build(const uint32_t *pred, const uint8_t *code, uint64_t n, WalkEntry *a, WalkEntry *b,
-                       WalkEntry **result, hipStream_t s) {
+void launch_walk_build(const uint32_t *pred, const uint8_t *code, uint64_t n, WalkStep *a, WalkStep *b,
+                       WalkEntry *out, hipStream_t s) {
     hipLaunchKernelGGL(k_walk_init, grid_for(n), dim3(256), 0, s, pred, code, n, a);
     for (uint32_t m = 1; m < 32; m *= 2) {
-        hipLaunchKernelGGL(k_walk_double, grid_for(n), dim3(256), 0, s, (const WalkEntry *)a, b, n, m);
-        WalkEntry *t = a;
+        hipLaunchKernelGGL(k_walk_double, grid_for(n), dim3(256), 0, s, (const WalkStep *)a, b, n, m);
+        WalkStep *t = a;
         a = b;
         b = t;
     }
     // a = 32-step entries, b = 16-step entries
-    hipLaunchKernelGGL(k_walk_ext, grid_for(n), dim3(256), 0, s, a, (const WalkEntry *)b, n);
-    *result = a;
+    hipLaunchKernelGGL(k_walk_ext, grid_for(n), dim3(256), 0, s, a, (const WalkStep *)b, n);
+    hipLaunchKernelGGL(k_walk_final, grid_for(n), dim3(256), 0, s, (const WalkStep *)a, (const WalkStep *)b, n, out);
 }
 
 
