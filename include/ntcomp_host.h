@@ -34,7 +34,14 @@ void ntc_index_free(ntc_index_host *ix);
 /* Borrowed view (valid until ntc_index_free) for ntc_index_upload or inspection. */
 int ntc_index_view_of(const ntc_index_host *ix, ntc_index_view *view);
 int ntc_index_save(const ntc_index_host *ix, const char *prefix);
-int ntc_index_load(const char *prefix, ntc_index_host **out);
+int ntc_index_load(const char *prefix, ntc_index_host **out);  /* detects the layout */
+/* Save in a chosen layout: NTC_INDEX_OWN (= ntc_index_save) or NTC_INDEX_SBWT_RS, a
+ * restatement of sbwt 0.3.11 / kbo 0.5.1 serialisation (write_sbwt_index_variant +
+ * LcsArray, main.rs:138) [ext, recalled -- parity unpinned: no reference-written index
+ * exists offline]. */
+#define NTC_INDEX_OWN 0
+#define NTC_INDEX_SBWT_RS 1
+int ntc_index_save_as(const ntc_index_host *ix, const char *prefix, int layout);
 
 /* ---- FASTX ingest (CLI) -------------------------------------------------------------- */
 /* needletail::parse_fastx_file + SequenceRecord::normalize(true) as src/main.rs:51-62 and

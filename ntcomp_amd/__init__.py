@@ -38,7 +38,7 @@ EXPORTED = [
     "ntc_encode_batch_device", "ntc_encode_status", "ntc_decode_batch", "ntc_decode_batch_device",
     "ntc_decode_status", "ntc_last_timing", "ntc_device_alloc", "ntc_device_free", "ntc_memcpy_h2d",
     "ntc_memcpy_d2h", "ntc_debug_matching_statistics", "ntc_build_index", "ntc_index_free",
-    "ntc_index_view_of", "ntc_index_save", "ntc_index_load", "ntc_synth_genome", "ntc_synth_strains", "ntc_synth_reads",
+    "ntc_index_view_of", "ntc_index_save", "ntc_index_save_as", "ntc_index_load", "ntc_synth_genome", "ntc_synth_strains", "ntc_synth_reads",
     "ntc_file_header", "ntc_write_block", "ntc_read_block", "ntc_buffer_free",
     "ntc_fastx_open", "ntc_fastx_next_batch", "ntc_fastx_close", "ntc_fasta_format",
 ]
@@ -118,6 +118,7 @@ def lib():
         "ntc_index_free": (None, [P]),
         "ntc_index_view_of": (I, [P, ctypes.POINTER(IndexView)]),
         "ntc_index_save": (I, [P, ctypes.c_char_p]),
+        "ntc_index_save_as": (I, [P, ctypes.c_char_p, I]),
         "ntc_index_load": (I, [ctypes.c_char_p, ctypes.POINTER(P)]),
         "ntc_synth_genome": (I, [u64, u64, P]),
         "ntc_synth_strains": (I, [P, u64, u64, u32, u32, P]),
@@ -181,10 +182,13 @@ class Index:
             raise NtcError(rc, f"ntc_index_load({prefix})")
         return cls(h)
 
-    def save(self, prefix):
-        rc = lib().ntc_index_save(self.h, str(prefix).encode())
+    def save(self, prefix, layout="own"):
+        """layout "own" (default) or "sbwt-rs" (a recalled restatement of sbwt 0.3.11 / kbo
+        0.5.1 files, parity unpinned); Index.load detects either."""
+        code = {"own": 0, "sbwt-rs": 1}[layout]
+        rc = lib().ntc_index_save_as(self.h, str(prefix).encode(), code)
         if rc:
-            raise NtcError(rc, f"ntc_index_save({prefix})")
+            raise NtcError(rc, f"ntc_index_save_as({prefix}, {layout})")
 
     def __del__(self):
         if getattr(self, "h", None) and _lib is not None:

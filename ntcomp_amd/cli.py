@@ -92,7 +92,7 @@ def cmd_build(args):
     ix = nt.Index.build(seqs, args.kmer_size, add_revcomp=True, threads=args.num_threads)
     log(f"Serializing SBWT index to {args.output_prefix}.sbwt ...")
     log(f"Serializing LCS array to {args.output_prefix}.lcs ...")
-    ix.save(args.output_prefix)
+    ix.save(args.output_prefix, layout=args.index_format)
 
 
 def _open_gpus(index, n, st=None):
@@ -299,6 +299,9 @@ def main(argv=None):
     b.add_argument("-m", "--mem-gb", type=int, default=4, help="Accepted for compatibility (unused).")
     b.add_argument("--temp-dir", help="Accepted for compatibility (unused; builds in memory).")
     b.add_argument("--verbose", action="store_true")
+    b.add_argument("--index-format", choices=["own", "sbwt-rs"], default="own",
+                   help="own layout (default) or a restatement of sbwt 0.3.11/kbo 0.5.1 files (parity unpinned); "
+                        "encode/decode read either")
     e = sub.add_parser("encode", help="Encode fastX data using an SBWT index")
     e.add_argument("query_file", help="Query file with sequence data.")
     e.add_argument("-i", "--index", dest="index_prefix", required=True, help="Prefix for prebuilt <prefix>.sbwt and <prefix>.lcs")

@@ -1006,6 +1006,16 @@ int ntc_index_save(const ntc_index_host *ix, const char *prefix) {
     return NTC_OK;
 }
 
+int ntc_index_save_as(const ntc_index_host *ix, const char *prefix, int layout) {
+    if (!ix || !prefix || (layout != kIndexOwn && layout != kIndexSbwtRs)) return NTC_ERR_INVALID_ARG;
+    std::string err;
+    if (!save_index_as(ix->ix, prefix, layout, err)) {
+        std::fprintf(stderr, "ntc_index_save_as: %s\n", err.c_str());
+        return NTC_ERR_IO;
+    }
+    return NTC_OK;
+}
+
 int ntc_index_load(const char *prefix, ntc_index_host **out) {
     if (!prefix || !out) return NTC_ERR_INVALID_ARG;
     *out = nullptr;

@@ -1,10 +1,25 @@
-// <prefix>.sbwt / <prefix>.lcs -- this library's native index files, the counterpart of
-// kbo::index::serialize_sbwt (src/main.rs:138) and kbo::index::load_sbwt (src/main.rs:149,
-// :190).  Like the reference, encode and decode both want the two files side by side
-// (README.md:44).  The byte layout is this library's own (sbwt 0.3.11's serialisation is
-// not available offline: DESIGN.md "Index files"); all integers little-endian:
+// <prefix>.sbwt / <prefix>.lcs -- the counterpart of kbo::index::serialize_sbwt
+// (src/main.rs:138) and kbo::index::load_sbwt (src/main.rs:149, :190).  Like the reference,
+// encode and decode both want the two files side by side (README.md:44).  Two layouts:
+//
+// kIndexOwn (default): this library's own, all integers little-endian:
 //   .sbwt: "NTCSBWT1" u64 version=1, u64 n, u64 k, u64 C[4], u64 nwords, 4 x nwords u64
 //   .lcs : "NTCLCS01" u64 n, n bytes
+//
+// kIndexSbwtRs: a RESTATEMENT of sbwt 0.3.11 / kbo 0.5.1 serialisation [ext, recalled --
+// PARITY UNPINNED: neither crate nor any reference-written index exists offline, so this
+// layout is written from memory of the published crates and may differ from theirs].
+// Built on simple-sds conventions (every integer a little-endian u64 word):
+//   Vec<u64>   = u64 len, len words           RawVector = u64 len_bits, Vec<u64>
+//   IntVector  = u64 len, u64 width, RawVector  (width-bit fields packed LSB-first)
+//   Option<T>  = u64 size in words (0 = None), then the words
+//   BitVector  = u64 ones, RawVector, Option<rank>, Option<select>, Option<select_zero>
+//   .sbwt = u64 L, "plain-matrix" (the variant id, L bytes), then SbwtIndex<SubsetMatrix>:
+//           4 BitVectors (rows A, C, G, T; n bits each), Vec<u64> C (4 entries),
+//           u64 n_sets (= n), u64 k, prefix lookup table (u64 prefix_len = 0, Vec<u64> empty)
+//   .lcs  = IntVector of n entries, width = bits of k
+// Written with every Option None; read tolerantly (Options are skipped by their size).
+// load_index detects the layout from the first 8 bytes.
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -47,7 +62,135 @@ bool save_index(const HostIndex &ix, const std::string &prefix, std::string &err
     return true;
 }
 
+namespace {
+// ---- sbwt-rs / simple-sds layout (kIndexSbwtRs, see the header) -----------------------
+const char kVariantId[] = "plain-matrix";
+
+bool wr64(FILE *f, uint64_t v) { return wr(f, &v, 8); }
+bool rd64(FILE *f, uint64_t &v) { return rd(f, &v, 8); }
+bool wr_raw(FILE *f, const uint64_t *w, uint64_t bits) {  // RawVector
+    const uint64_t nw = (bits + 63) / 64;
+    return wr64(f, bits) && wr64(f, nw) && (nw == 0 || wr(f, w, nw * 8));
+}
+bool rd_raw(FILE *f, std::vector<uint64_t> &w, uint64_t &bits) {
+    uint64_t nw = 0;
+    if (!rd64(f, bits) || !rd64(f, nw) || nw != (bits + 63) / 64 || nw > (1ULL << 40)) return false;
+    w.assign(nw, 0);
+    return nw == 0 || rd(f, w.data(), nw * 8);
+}
+bool skip_option(FILE *f) {
+    uint64_t sz = 0;
+    return rd64(f, sz) && (sz == 0 || std::fseek(f, (long)(sz * 8), SEEK_CUR) == 0);
+}
+
+bool save_sbwt_rs(const HostIndex &ix, const std::string &prefix, std::string &err) {
+    {
+        File f(prefix + ".sbwt", "wb");
+        if (!f.f) { err = "cannot open " + prefix + ".sbwt for writing"; return false; }
+        const uint64_t L = sizeof(kVariantId) - 1;
+        bool ok = wr64(f.f, L) && wr(f.f, kVariantId, L);
+        for (int c = 0; c < 4 && ok; c++) {
+            uint64_t ones = 0;
+            for (uint64_t x : ix.rows[c]) ones += (uint64_t)__builtin_popcountll(x);
+            ok = wr64(f.f, ones) && wr_raw(f.f, ix.rows[c].data(), ix.n) && wr64(f.f, 0) && wr64(f.f, 0) &&
+                 wr64(f.f, 0);
+        }
+        ok = ok && wr64(f.f, 4);
+        for (int c = 0; c < 4 && ok; c++) ok = wr64(f.f, ix.C[c]);
+        ok = ok && wr64(f.f, ix.n) && wr64(f.f, ix.k) && wr64(f.f, 0) && wr64(f.f, 0);
+        if (!ok) { err = "write failed: " + prefix + ".sbwt"; return false; }
+    }
+    {
+        File f(prefix + ".lcs", "wb");
+        if (!f.f) { err = "cannot open " + prefix + ".lcs for writing"; return false; }
+        uint64_t width = 1;
+        while ((1ULL << width) <= ix.k) width++;
+        std::vector<uint64_t> packed((ix.n * width + 63) / 64, 0);
+        for (uint64_t i = 0; i < ix.n; i++) {
+            const uint64_t bit = i * width, v = ix.lcs[i];
+            packed[bit >> 6] |= v << (bit & 63);
+            if ((bit & 63) + width > 64) packed[(bit >> 6) + 1] |= v >> (64 - (bit & 63));
+        }
+        if (!(wr64(f.f, ix.n) && wr64(f.f, width) && wr_raw(f.f, packed.data(), ix.n * width))) {
+            err = "write failed: " + prefix + ".lcs";
+            return false;
+        }
+    }
+    return true;
+}
+
+bool load_sbwt_rs(const std::string &prefix, HostIndex &ix, std::string &err) {
+    {
+        File f(prefix + ".sbwt", "rb");
+        if (!f.f) { err = "cannot open " + prefix + ".sbwt"; return false; }
+        uint64_t L = 0;
+        char id[64] = {0};
+        if (!rd64(f.f, L) || L >= sizeof(id) || !rd(f.f, id, L) || std::strcmp(id, kVariantId) != 0) {
+            err = prefix + ".sbwt: not a plain-matrix SBWT";
+            return false;
+        }
+        uint64_t n = ~0ULL;
+        for (int c = 0; c < 4; c++) {
+            uint64_t ones = 0, bits = 0;
+            if (!rd64(f.f, ones) || !rd_raw(f.f, ix.rows[c], bits) || !skip_option(f.f) || !skip_option(f.f) ||
+                !skip_option(f.f)) {
+                err = prefix + ".sbwt: truncated subset matrix";
+                return false;
+            }
+            if (n != ~0ULL && bits != n) { err = prefix + ".sbwt: rows of different lengths"; return false; }
+            n = bits;
+        }
+        uint64_t nc = 0, n_sets = 0, k = 0;
+        if (!rd64(f.f, nc) || nc < 4 || nc > 8) { err = prefix + ".sbwt: bad C array"; return false; }
+        for (uint64_t c = 0; c < nc; c++) {
+            uint64_t v = 0;
+            if (!rd64(f.f, v)) { err = prefix + ".sbwt: truncated C array"; return false; }
+            if (c < 4) ix.C[c] = v;
+        }
+        if (!rd64(f.f, n_sets) || !rd64(f.f, k) || n_sets != n || k < 1 || k > 255) {
+            err = prefix + ".sbwt: inconsistent header";
+            return false;
+        }
+        ix.n = n;
+        ix.k = (uint32_t)k;
+    }
+    {
+        File f(prefix + ".lcs", "rb");
+        if (!f.f) { err = "cannot open " + prefix + ".lcs"; return false; }
+        uint64_t len = 0, width = 0, bits = 0;
+        std::vector<uint64_t> packed;
+        if (!rd64(f.f, len) || !rd64(f.f, width) || len != ix.n || width < 1 || width > 8 ||
+            !rd_raw(f.f, packed, bits) || bits != len * width) {
+            err = prefix + ".lcs: missing, foreign or not matching " + prefix + ".sbwt";
+            return false;
+        }
+        ix.lcs.assign(len, 0);
+        const uint64_t mask = (1ULL << width) - 1;
+        for (uint64_t i = 0; i < len; i++) {
+            const uint64_t bit = i * width;
+            uint64_t v = packed[bit >> 6] >> (bit & 63);
+            if ((bit & 63) + width > 64) v |= packed[(bit >> 6) + 1] << (64 - (bit & 63));
+            ix.lcs[i] = (uint8_t)(v & mask);
+        }
+    }
+    return true;
+}
+}  // namespace
+
+bool save_index_as(const HostIndex &ix, const std::string &prefix, int layout, std::string &err) {
+    if (layout == kIndexSbwtRs) return save_sbwt_rs(ix, prefix, err);
+    return save_index(ix, prefix, err);
+}
+
 bool load_index(const std::string &prefix, HostIndex &ix, std::string &err) {
+    bool own = true;
+    {  // layout detection: the own magic, else the sbwt-rs variant id
+        File f(prefix + ".sbwt", "rb");
+        if (!f.f) { err = "cannot open " + prefix + ".sbwt"; return false; }
+        char magic[8];
+        own = !(rd(f.f, magic, 8) && std::memcmp(magic, "NTCSBWT1", 8) != 0);
+    }
+    if (!own) return load_sbwt_rs(prefix, ix, err);
     {
         File f(prefix + ".sbwt", "rb");
         if (!f.f) { err = "cannot open " + prefix + ".sbwt"; return false; }

@@ -18,7 +18,9 @@ struct HostIndex {
 void build_index(const uint8_t *seqs, const uint64_t *offs, uint64_t nseqs, uint32_t k,
                  bool revcomp, int threads, HostIndex &out);
 bool save_index(const HostIndex &ix, const std::string &prefix, std::string &err);
-bool load_index(const std::string &prefix, HostIndex &ix, std::string &err);
+bool load_index(const std::string &prefix, HostIndex &ix, std::string &err);  // either layout
+enum { kIndexOwn = 0, kIndexSbwtRs = 1 };  // ntc_index_save_as layouts (index_io.cpp)
+bool save_index_as(const HostIndex &ix, const std::string &prefix, int layout, std::string &err);
 
 }  // namespace ntc
 

@@ -52,3 +52,22 @@ def test_index_files_roundtrip(tmp_path):
     (tmp_path / "idx.lcs").unlink()
     with pytest.raises(nt.NtcError):
         nt.Index.load(tmp_path / "idx")
+
+
+@pytest.mark.parametrize("k", [15, 31, 91])
+def test_index_sbwt_rs_layout_round_trip(tmp_path, k):
+    """own layout -> sbwt-rs layout (restated sbwt 0.3.11 / kbo 0.5.1 serialisation,
+    main.rs:138; [ext, recalled], parity unpinned) -> own layout: rows, C, k and LCS survive
+    bit for bit, and Index.load detects each layout."""
+    g = nt.synth_genome(5 + k, 30_000)
+    ix = nt.Index.build([g.tobytes()], k)
+    ix.save(tmp_path / "a", layout="sbwt-rs")
+    assert (tmp_path / "a.sbwt").read_bytes()[:20] == (12).to_bytes(8, "little") + b"plain-matrix"
+    b = nt.Index.load(tmp_path / "a")
+    b.save(tmp_path / "b")
+    assert (tmp_path / "b.sbwt").read_bytes()[:8] == b"NTCSBWT1"
+    c = nt.Index.load(tmp_path / "b")
+    for x in (b, c):
+        assert (x.n, x.k, x.C) == (ix.n, ix.k, ix.C)
+        assert all(np.array_equal(p, q) for p, q in zip(x.rows, ix.rows))
+        assert np.array_equal(x.lcs, ix.lcs)
