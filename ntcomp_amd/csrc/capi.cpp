@@ -56,6 +56,8 @@ struct ntc_ctx {
     Enc4Args last4{};
     uint32_t tab_u_opt = 0;  // suffix-table depth for the next upload (0 = default_tab_u)
     int pair_bytes_opt = 1;  // build the SCAN pair bytes at the next upload (0: bitmap tests, A/B)
+    int ext2_opt = 0;        // build the two-character rank chunks at the next upload (A/B option: 1 measured
+                             // slower -- 8 B/node from HBM against 1 B/node of Infinity-Cache-resident rank words)
     uint64_t n_paths = 0, path_text_len = 0;
     int64_t upload_host_us = 0, upload_total_us = 0;  // last ntc_index_upload: host derive / total
     uint64_t max_pass_bases = 1ULL << 30;  // host-buffer calls split into device passes of at most this
@@ -486,6 +488,13 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     d.pos_of_node = (const uint32_t *)d_pos;
     d.puniq = (const uint64_t *)d_puniq;
     d.absent = dv.absent;
+    d.rank2 = nullptr;
+    if (ctx->ext2_opt) {  // two-character rank lines (8 B per node)
+        void *d_r2;
+        if ((rc = dalloc(rank2_blocks(n) * 4 * sizeof(Rank2Chunk), &d_r2))) return rc;
+        launch_rank2(d, (Rank2Chunk *)d_r2, ctx->stream);
+        d.rank2 = (const Rank2Chunk *)d_r2;
+    }
     // suffix table, levels 1..U, built on the device from the rank lines
     uint32_t U = ctx->tab_u_opt ? std::min<uint32_t>(ctx->tab_u_opt, std::min<uint32_t>(hx.k, kTabMaxU))
                                 : default_tab_u(n, hx.k);
@@ -530,6 +539,11 @@ int ntc_ctx_set_option(ntc_ctx *ctx, const char *key, int64_t value) {
         ctx->pair_bytes_opt = (int)value;
         return NTC_OK;
     }
+    if (std::strcmp(key, "ext2") == 0) {  // applies to the next ntc_index_upload
+        if (value != 0 && value != 1) return set_err(ctx, NTC_ERR_INVALID_ARG, "ext2 must be 0 or 1");
+        ctx->ext2_opt = (int)value;
+        return NTC_OK;
+    }
     if (std::strcmp(key, "max_pass_bases") == 0) {  // device workspace ~40 B per base of a pass
         if (value < 1) return set_err(ctx, NTC_ERR_INVALID_ARG, "max_pass_bases must be >= 1");
         ctx->max_pass_bases = (uint64_t)value;
@@ -549,6 +563,7 @@ int ntc_ctx_get_option(const ntc_ctx *ctx, const char *key, int64_t *value) {
     if (std::strcmp(key, "encode_variant") == 0) *value = ctx->encode_variant;
     else if (std::strcmp(key, "tab_u") == 0) *value = ctx->has_index ? ctx->dix.tab_u : ctx->tab_u_opt;
     else if (std::strcmp(key, "pair_bytes") == 0) *value = ctx->has_index ? (ctx->dix.pair_w != nullptr) : ctx->pair_bytes_opt;
+    else if (std::strcmp(key, "ext2") == 0) *value = ctx->has_index ? (ctx->dix.rank2 != nullptr) : ctx->ext2_opt;
     else if (std::strcmp(key, "n_paths") == 0) *value = (int64_t)ctx->n_paths;
     else if (std::strcmp(key, "path_text_len") == 0) *value = (int64_t)ctx->path_text_len;
     else if (std::strcmp(key, "path_hash") == 0) {  // test hook: derived.h path_cover_hash of the device cover

@@ -307,6 +307,12 @@ void build_walk_host(const Derived &dv, uint64_t n, std::vector<WalkEntry> &walk
     }
 }
 
+void build_rank2_host(const DevIndex &d, std::vector<Rank2Chunk> &out) {
+    const uint64_t lines = rank2_blocks(d.n);
+    out.resize(lines * 4);
+    for (uint64_t i = 0; i < lines * 4; i++) out[i] = rank2_make(d, i % lines, (int)(i / lines));  // c1-major
+}
+
 DevIndex host_dev_index(const HostIndex &ix, const Derived &dv, const std::vector<WalkEntry> &walk) {
     DevIndex d{};
     d.rank = dv.rank.data();

@@ -64,6 +64,8 @@ uint32_t filter_level(uint32_t U);
 bool build_derived(const HostIndex &ix, Derived &out, std::string &err, bool host_paths);
 // Host doubling of the walk table (the GPU builds the same table on device).
 void build_walk_host(const Derived &dv, uint64_t n, std::vector<WalkEntry> &walk);
+// two-character rank lines of d (Rank2Chunk, encode_core.h): host build for the emulation
+void build_rank2_host(const DevIndex &d, std::vector<Rank2Chunk> &out);
 // DevIndex over host arrays (test emulation only).
 DevIndex host_dev_index(const HostIndex &ix, const Derived &dv, const std::vector<WalkEntry> &walk);
 

@@ -81,6 +81,24 @@ NTC_HD WalkEntry walk_compose(const WalkStep &x, const WalkStep &y, const WalkSt
     return e;
 }
 
+// Two-character rank chunks: per 32 SBWT positions (block b, positions 32b ... 32b + 31)
+// and first character c1, one 64-byte chunk (two per 128-byte line):
+//   base      = C[c1] + rank_c1(32b)           (where the block's c1-successors start, L0)
+//   bits      = row c1's 32 bits of the block
+//   pbase[c2] = C[c2] + rank_c2(L0), pbits[c2] = row c2's 32 bits at L0 ... L0 + 31
+// so ext(ext([l, r), c1), c2) -- two MS steps -- costs the chunks of l's and r's blocks
+// (one line when they share a block) instead of two dependent rank-word lines.  At most 32
+// positions of a block carry c1, so l1 - L0 <= 32 stays inside pbits.
+struct alignas(64) Rank2Chunk {
+    uint32_t base;
+    uint32_t bits;
+    uint32_t pbase[4];
+    uint32_t pbits[4];
+    uint32_t pad[6];
+};
+static_assert(sizeof(Rank2Chunk) == 64, "rank2 chunk");
+NTC_HD uint64_t rank2_blocks(uint64_t n) { return (n >> 5) + 2; }  // every block of 32 positions up to n
+
 struct DevIndex {
     const uint2 *rank;      // [4][rwords] rank words
     const uint8_t *lcs;     // [n]
@@ -106,6 +124,7 @@ struct DevIndex {
     uint32_t tab_pos;             // 1: top-level singleton entries carry the path position
     uint32_t tab_u;               // U: longest tabulated length (1 <= U <= min(k, 14))
     uint32_t absent;              // bit c: no node ends with character c
+    const Rank2Chunk *rank2;      // [4][rank2_blocks(n)] two-character rank chunks, or null
 };
 
 // per-read status codes (values of ntc_status)
@@ -185,6 +204,45 @@ NTC_HD void extend(const DevIndex &ix, int c, uint32_t l, uint32_t r, uint32_t &
     const uint2 a = load2(row + (l >> 5)), b = load2(row + (r >> 5));
     nl = rank_word(a, l);
     nr = rank_word(b, r);
+}
+
+// 32 bits of row c starting at position x, from the rank words
+NTC_HD uint32_t row_bits32(const DevIndex &ix, int c, uint64_t x) {
+    const uint2 *row = ix.rank + (uint64_t)c * ix.rwords;
+    const uint32_t sh = (uint32_t)(x & 31);
+    const uint32_t a = row[x >> 5].y;
+    return sh ? (a >> sh) | (row[(x >> 5) + 1].y << (32 - sh)) : a;
+}
+// chunk (block b, c1) of the two-character rank table (built at upload: k_rank2 / build_rank2_host)
+NTC_HD Rank2Chunk rank2_make(const DevIndex &ix, uint64_t b, int c1) {
+    Rank2Chunk e{};
+    const uint64_t x0 = 32 * b;
+    const uint64_t x = x0 <= ix.n ? x0 : ix.n;  // blocks past the end: empty
+    e.base = rank_word(ix.rank[(uint64_t)c1 * ix.rwords + (x >> 5)], (uint32_t)x);
+    e.bits = x0 <= ix.n ? ix.rank[(uint64_t)c1 * ix.rwords + (x0 >> 5)].y : 0u;
+    const uint64_t L0 = e.base <= ix.n ? e.base : ix.n;
+    for (int c2 = 0; c2 < 4; c2++) {
+        e.pbase[c2] = rank_word(ix.rank[(uint64_t)c2 * ix.rwords + (L0 >> 5)], (uint32_t)L0);
+        e.pbits[c2] = row_bits32(ix, c2, L0);
+    }
+    return e;
+}
+// ext by c1 then c2 from [l, r): (l1, r1) after c1 and (l2, r2) after c2 (empty = failure)
+NTC_HD void extend2(const DevIndex &ix, int c1, int c2, uint32_t l, uint32_t r, uint32_t &l1, uint32_t &r1,
+                    uint32_t &l2, uint32_t &r2) {
+    // c1-major: chunks of neighbouring blocks share 128-byte lines
+    const Rank2Chunk *T = ix.rank2 + (uint64_t)c1 * rank2_blocks(ix.n);
+    const Rank2Chunk *A = T + (l >> 5), *B = T + (r >> 5);
+    NTC_TOUCH(kTrRank, A);
+    NTC_TOUCH(kTrRank, B);
+    const uint32_t abase = A->base, abits = A->bits, apb = A->pbase[c2], apbits = A->pbits[c2];
+    const uint32_t bbase = B->base, bbits = B->bits, bpb = B->pbase[c2], bpbits = B->pbits[c2];
+    const uint32_t ol = (uint32_t)__builtin_popcount(abits & ((1u << (l & 31)) - 1u));
+    const uint32_t orr = (uint32_t)__builtin_popcount(bbits & ((1u << (r & 31)) - 1u));
+    l1 = abase + ol;
+    r1 = bbase + orr;
+    l2 = apb + (uint32_t)__builtin_popcountll((uint64_t)apbits & ((1ull << ol) - 1ull));
+    r2 = bpb + (uint32_t)__builtin_popcountll((uint64_t)bpbits & ((1ull << orr) - 1ull));
 }
 
 // contract_left(I, t) [ext sbwt]: widen I to all nodes sharing the last t characters.
@@ -1216,6 +1274,24 @@ struct MsLane {
             return 0;
         }
         const int c = (int)((qw >> (2 * (p - qb))) & 3u);
+        if (mode == kModeExt && ix.rank2 && p + 1 < len && p + 1 < qb + 32) {
+            // two positions from one line (Rank2Chunk): the usual case inside a climb from
+            // d = U to k over a multi-node interval (strain collections)
+            const int c2 = (int)((qw >> (2 * (p + 1 - qb))) & 3u);
+            uint32_t l1, r1, l2, r2;
+            extend2(ix, c, c2, l, r, l1, r1, l2, r2);
+            if (l1 < r1) {
+                const uint32_t d1 = d + 1 < k ? d + 1 : k;
+                put_entry(b, p, l1, 1u, d1);
+                p++;
+                if (l2 < r2) return commit(ix, b, l2, r2, d1 + 1 < k ? d1 + 1 : k);
+                l = l1; r = r1; d = d1;
+                mode = kModeExtFail;  // the second extension failed: position p (was p + 1)
+                return 0;
+            }
+            mode = kModeExtFail;  // the first failed: failure handling at p
+            return 0;
+        }
         if (mode == kModeExt || mode == kModeExtFail) {
             uint2 te;
             if (NTC_EXT_EAGER || mode == kModeExtFail) {

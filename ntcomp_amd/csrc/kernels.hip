@@ -738,6 +738,17 @@ __global__ __launch_bounds__(256) void k_debug_gather4(Enc4Args a, uint32_t *d_o
     read_ms(a.ix, a.Q, P, a.E + P, a.ne[r], (uint32_t)(e - b), d_out + P, s_out + P, a.Ed + r, a.n_reads);
 }
 
+// two-character rank lines (encode_core.h Rank2Chunk): one thread per (block, c1) chunk
+__global__ __launch_bounds__(256) void k_rank2(DevIndex ix, Rank2Chunk *out, uint64_t lines) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= lines * 4) return;
+    out[i] = rank2_make(ix, i % lines, (int)(i / lines));  // c1-major
+}
+void launch_rank2(const DevIndex &ix, Rank2Chunk *out, hipStream_t s) {
+    const uint64_t lines = rank2_blocks(ix.n);
+    hipLaunchKernelGGL(k_rank2, grid_for(lines * 4), dim3(256), 0, s, ix, out, lines);
+}
+
 // suffix table level u (4^u entries) from level u - 1
 __global__ __launch_bounds__(256) void k_tab_level(DevIndex ix, uint32_t u, const uint2 *prev, uint2 *cur) {
     const uint64_t key = (uint64_t)blockIdx.x * 256 + threadIdx.x;

@@ -73,6 +73,15 @@ bool load(const ntc_index_view *v, HostIndex &hx, Derived &dv, std::vector<WalkE
     if (!build_derived(hx, dv, err, true)) return false;
     build_walk_host(dv, hx.n, walk);
     d = host_dev_index(hx, dv, walk);
+    {  // two-character rank chunks, as the upload's ext2 option builds them (NTC_EMU_EXT2=1)
+        static std::vector<Rank2Chunk> r2;
+        const char *e2 = getenv("NTC_EMU_EXT2");
+        d.rank2 = nullptr;
+        if (e2 && atoi(e2) != 0) {
+            build_rank2_host(d, r2);
+            d.rank2 = r2.data();
+        }
+    }
     const uint32_t U = tab_u ? std::min<uint32_t>(tab_u, std::min<uint32_t>(hx.k, kTabMaxU)) : default_tab_u(hx.n, hx.k);
     d.tab_u = U;
     d.tab_pos = (dv.has_paths && U >= dv.t_jump && hx.n < (1ULL << 31)) ? 1u : 0u;

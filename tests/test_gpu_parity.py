@@ -190,16 +190,20 @@ def test_gpu_full_scale_roundtrip(k):
     ctx.close()
 
 
-def test_gpu_strain_collection():
+@pytest.mark.parametrize("ext2", [0, 1])
+def test_gpu_strain_collection(ext2):
     """An index of a genome + 3 strains at 1 % substitutions (fragmented path cover, many
     branching nodes): 300k reads from the collection round-trip exactly, 10k bit-exact vs
-    the oracle (bench.py's S91 config at reduced size)."""
+    the oracle (bench.py's S91 config at reduced size); also with the two-character rank
+    chunks (ctx option ext2)."""
     genome = nt.synth_genome(1, 2_000_000)
     strains = nt.synth_strains(genome, 3, 3, 10_000)
     texts = [genome] + [strains[i] for i in range(3)]
     ix = nt.Index.build([t.tobytes() for t in texts], 91)
     ctx = nt.GpuContext(0)
+    ctx.set_option("ext2", ext2)
     ctx.upload(ix)
+    assert ctx.get_option("ext2") == ext2
     assert ctx.get_option("n_paths") > 1000
     coll = np.concatenate(texts)
     n, L = 300_000, 150

@@ -203,3 +203,24 @@ def test_emulated_small_k_reference_panic_status(k, glen):
         got, goff = emu_encode(ix.n, k, ix.rows, ix.C, ix.lcs, kr, ko)
         exp, eoff = orc.encode(kr, ko)
         assert np.array_equal(got, exp) and np.array_equal(goff, eoff)
+
+
+@pytest.mark.parametrize("ext2", ["1", "0"])
+@pytest.mark.parametrize("k", [31, 91])
+def test_emulated_strain_collection(k, ext2, monkeypatch):
+    """A genome + 5 strains at 1 % substitutions (multi-node MS intervals over long climbs,
+    short unitigs): records equal the oracle's with and without the two-character rank
+    lines (NTC_EMU_EXT2), and decode back exactly."""
+    monkeypatch.setenv("NTC_EMU_EXT2", ext2)
+    g = nt.synth_genome(17, 150_000)
+    st = nt.synth_strains(g, 3, 5, 10_000)
+    texts = [g] + [st[i] for i in range(5)]
+    ix = nt.Index.build([t.tobytes() for t in texts], k)
+    n, L = 1500, 150
+    reads = nt.synth_reads(np.concatenate(texts), 2, 0, n, L, 10_000)
+    offs = np.arange(0, n * L + 1, L, dtype=np.uint64)
+    got, goff = emu_encode(ix.n, k, ix.rows, ix.C, ix.lcs, reads, offs)
+    exp, eoff = OracleIndex(ix.n, k, ix.rows, ix.C, ix.lcs).encode(reads, offs)
+    assert np.array_equal(goff, eoff) and np.array_equal(got, exp)
+    out, oo = emu_decode(ix.n, k, ix.rows, ix.C, ix.lcs, got)
+    assert np.array_equal(out, reads)
