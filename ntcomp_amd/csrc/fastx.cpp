@@ -1,8 +1,11 @@
 // FASTA / FASTQ ingest for the CLI (include/ntcomp_host.h "FASTX").
 //
 // Replaces needletail::parse_fastx_file + SequenceRecord::normalize(true) as the reference
-// uses them (src/main.rs:51-62 build input, :158-163 encode input): plain or gzip input
-// (zlib's gz* reads both), FASTA records (">" header, sequence over any number of lines)
+// uses them (src/main.rs:51-62 build input, :158-163 encode input): plain, gzip, bzip2 or
+// xz input, detected from the magic bytes like needletail's niffler (zlib's gz* reads plain
+// and gzip; bzip2 and xz go through libbz2.so.1 / liblzma.so.5, loaded at run time -- the
+// image has their runtime libraries but no headers, so the few stable entry points and
+// stream structs used are declared below), FASTA records (">" header, sequence over any number of lines)
 // and FASTQ records ("@" header, sequence, "+", quality).  normalize(iupac = true) is
 // restated from needletail [ext, recalled, needletail 0.6]: A C G T N - kept; a c g ->
 // upper case; t u U -> T; n -> N; . ~ -> -; IUPAC B D H V R Y S W K M kept (lower case
@@ -12,6 +15,7 @@
 // Feed rate: a producer thread inflates (or reads) 8 MiB chunks into a small ring while
 // the caller's thread scans records in place (memchr per line, branch-free table
 // normalisation into one growing buffer), so a gzip input is bound by inflate alone.
+#include <dlfcn.h>
 #include <emmintrin.h>
 #include <zlib.h>
 
@@ -57,9 +61,202 @@ void init_norm() {
 constexpr size_t kChunk = 8u << 20;
 constexpr size_t kRing = 4;
 
-// Producer: gzread into chunks, bounded queue of kRing chunks.
-struct ChunkSource {
+// ---- byte sources ---------------------------------------------------------------------
+struct ByteReader {  // read up to n decoded bytes: > 0 bytes, 0 at the end, < 0 on error
+    virtual ~ByteReader() {}
+    virtual int read(char *dst, unsigned n) = 0;
+};
+
+struct GzReader : ByteReader {  // plain or gzip (zlib's transparent gz* reader)
     gzFile f;
+    explicit GzReader(gzFile file) : f(file) {}
+    ~GzReader() override { gzclose(f); }
+    int read(char *dst, unsigned n) override { return gzread(f, dst, n); }
+};
+
+// Stream decoders over a FILE*: feed kIn-byte blocks of the compressed file to a decoder
+template <class Codec>
+struct StreamReader : ByteReader {
+    static constexpr size_t kIn = 1u << 20;
+    FILE *f;
+    Codec codec;
+    std::vector<char> in = std::vector<char>(kIn);
+    bool ok = false;
+    explicit StreamReader(FILE *file) : f(file) { ok = codec.init(); }
+    ~StreamReader() override {
+        codec.end();
+        std::fclose(f);
+    }
+    bool eof_in = false, ended = false;  // input exhausted; the last decoded stream is complete
+    int read(char *dst, unsigned n) override {
+        if (!ok) return -1;
+        codec.set_out(dst, n);
+        while (codec.out_left() > 0) {
+            if (codec.in_left() == 0) {
+                if (eof_in) break;
+                const size_t got = std::fread(in.data(), 1, kIn, f);
+                if (got == 0) {
+                    if (std::ferror(f)) return -1;
+                    eof_in = true;
+                }
+                codec.set_in(in.data(), got);
+                if (got == 0 && ended) break;  // clean end after a complete stream
+            }
+            const unsigned before = codec.out_left();
+            const size_t in_before = codec.in_left();
+            const int rc = codec.step(eof_in);
+            if (rc < 0) return -1;
+            ended = rc == 1 || (ended && codec.out_left() == before && codec.in_left() == in_before);
+            if (rc == 0 && codec.out_left() == before && codec.in_left() == in_before && eof_in) {
+                if (!ended) return -1;  // truncated input
+                break;
+            }
+        }
+        return (int)(n - codec.out_left());
+    }
+};
+
+// libbz2 (bzlib.h ABI): concatenated streams are decoded one after another
+struct BzStream {
+    char *next_in;
+    unsigned avail_in, total_in_lo32, total_in_hi32;
+    char *next_out;
+    unsigned avail_out, total_out_lo32, total_out_hi32;
+    void *state;
+    void *(*bzalloc)(void *, int, int);
+    void (*bzfree)(void *, void *);
+    void *opaque;
+};
+struct Bz2Codec {
+    int (*init_fn)(BzStream *, int, int) = nullptr;
+    int (*dec_fn)(BzStream *) = nullptr;
+    int (*end_fn)(BzStream *) = nullptr;
+    BzStream z{};
+    bool live = false;
+    bool init() {
+        void *h = dlopen("libbz2.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("libbz2.so.1.0", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return false;
+        init_fn = (int (*)(BzStream *, int, int))dlsym(h, "BZ2_bzDecompressInit");
+        dec_fn = (int (*)(BzStream *))dlsym(h, "BZ2_bzDecompress");
+        end_fn = (int (*)(BzStream *))dlsym(h, "BZ2_bzDecompressEnd");
+        if (!init_fn || !dec_fn || !end_fn) return false;
+        std::memset(&z, 0, sizeof(z));
+        live = init_fn(&z, 0, 0) == 0;
+        return live;
+    }
+    void end() {
+        if (live) end_fn(&z);
+        live = false;
+    }
+    void set_in(char *p, size_t n) { z.next_in = p; z.avail_in = (unsigned)n; }
+    void set_out(char *p, unsigned n) { z.next_out = p; z.avail_out = n; }
+    size_t in_left() const { return z.avail_in; }
+    unsigned out_left() const { return z.avail_out; }
+    int step(bool) {  // 0 progress, 1 a stream ended, -1 error
+        const int rc = dec_fn(&z);
+        if (rc == 4) {  // BZ_STREAM_END: a following stream (pbzip2) starts a new decoder
+            char *ni = z.next_in, *no = z.next_out;
+            const unsigned ai = z.avail_in, ao = z.avail_out;
+            end_fn(&z);
+            std::memset(&z, 0, sizeof(z));
+            live = init_fn(&z, 0, 0) == 0;
+            z.next_in = ni;
+            z.avail_in = ai;
+            z.next_out = no;
+            z.avail_out = ao;
+            return live ? 1 : -1;
+        }
+        return rc == 0 ? 0 : -1;  // BZ_OK
+    }
+};
+
+// liblzma (lzma/base.h ABI, stable since 5.0): xz with concatenated streams
+struct LzmaStream {
+    const uint8_t *next_in;
+    size_t avail_in;
+    uint64_t total_in;
+    uint8_t *next_out;
+    size_t avail_out;
+    uint64_t total_out;
+    const void *allocator;
+    void *internal;
+    void *reserved_ptr1, *reserved_ptr2, *reserved_ptr3, *reserved_ptr4;
+    uint64_t reserved_int1, reserved_int2;
+    size_t reserved_int3, reserved_int4;
+    int reserved_enum1, reserved_enum2;
+};
+struct XzCodec {
+    int (*dec_init)(LzmaStream *, uint64_t, uint32_t) = nullptr;
+    int (*code_fn)(LzmaStream *, int) = nullptr;
+    void (*end_fn)(LzmaStream *) = nullptr;
+    LzmaStream z{};
+    bool live = false;
+    bool init() {
+        void *h = dlopen("liblzma.so.5", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return false;
+        dec_init = (int (*)(LzmaStream *, uint64_t, uint32_t))dlsym(h, "lzma_stream_decoder");
+        code_fn = (int (*)(LzmaStream *, int))dlsym(h, "lzma_code");
+        end_fn = (void (*)(LzmaStream *))dlsym(h, "lzma_end");
+        if (!dec_init || !code_fn || !end_fn) return false;
+        std::memset(&z, 0, sizeof(z));                       // LZMA_STREAM_INIT
+        live = dec_init(&z, ~0ULL, 0x08u /* LZMA_CONCATENATED */) == 0;
+        return live;
+    }
+    void end() {
+        if (live) end_fn(&z);
+        live = false;
+    }
+    void set_in(char *p, size_t n) { z.next_in = (const uint8_t *)p; z.avail_in = n; }
+    void set_out(char *p, unsigned n) { z.next_out = (uint8_t *)p; z.avail_out = n; }
+    size_t in_left() const { return z.avail_in; }
+    unsigned out_left() const { return (unsigned)z.avail_out; }
+    int step(bool finished) {
+        const int rc = code_fn(&z, finished ? 3 /* LZMA_FINISH */ : 0 /* LZMA_RUN */);
+        if (rc == 1) return 1;  // LZMA_STREAM_END
+        return rc == 0 ? 0 : -1;
+    }
+};
+
+// the reader for a path, by its first bytes; *rc = NTC_ERR_IO / NTC_ERR_UNSUPPORTED on failure
+ByteReader *open_reader(const char *path, int *rc) {
+    unsigned char m[6] = {0};
+    FILE *f = std::fopen(path, "rb");
+    if (!f) {
+        *rc = NTC_ERR_IO;
+        return nullptr;
+    }
+    const size_t got = std::fread(m, 1, 6, f);
+    std::rewind(f);
+    ByteReader *r = nullptr;
+    if (got >= 3 && m[0] == 'B' && m[1] == 'Z' && m[2] == 'h') {
+        auto *b = new StreamReader<Bz2Codec>(f);
+        if (!b->ok) { delete b; *rc = NTC_ERR_UNSUPPORTED; return nullptr; }
+        r = b;
+    } else if (got >= 6 && std::memcmp(m, "\xFD" "7zXZ\0", 6) == 0) {
+        auto *x = new StreamReader<XzCodec>(f);
+        if (!x->ok) { delete x; *rc = NTC_ERR_UNSUPPORTED; return nullptr; }
+        r = x;
+    } else if (got >= 4 && m[0] == 0x28 && m[1] == 0xB5 && m[2] == 0x2F && m[3] == 0xFD) {
+        std::fclose(f);  // zstd: no library in the image
+        *rc = NTC_ERR_UNSUPPORTED;
+        return nullptr;
+    } else {
+        std::fclose(f);
+        gzFile g = gzopen(path, "rb");
+        if (!g) {
+            *rc = NTC_ERR_IO;
+            return nullptr;
+        }
+        gzbuffer(g, 1u << 20);
+        r = new GzReader(g);
+    }
+    return r;
+}
+
+// Producer: decoded chunks from a ByteReader, bounded queue of kRing chunks.
+struct ChunkSource {
+    ByteReader *f;
     std::thread th;
     std::mutex mu;
     std::condition_variable cv;
@@ -67,7 +264,7 @@ struct ChunkSource {
     std::vector<std::vector<char>> spare;
     bool done = false, stop = false, error = false;
 
-    explicit ChunkSource(gzFile file) : f(file) { th = std::thread([this] { run(); }); }
+    explicit ChunkSource(ByteReader *reader) : f(reader) { th = std::thread([this] { run(); }); }
     ~ChunkSource() {
         {
             std::lock_guard<std::mutex> g(mu);
@@ -89,7 +286,7 @@ struct ChunkSource {
                 }
             }
             c.resize(kChunk);
-            const int got = gzread(f, c.data(), (unsigned)kChunk);
+            const int got = f->read(c.data(), (unsigned)kChunk);
             std::lock_guard<std::mutex> g(mu);
             if (got < 0) error = true;
             if (got <= 0) {
@@ -122,7 +319,7 @@ struct ChunkSource {
 }  // namespace
 
 struct ntc_fastx {
-    gzFile f = nullptr;
+    ByteReader *f = nullptr;
     ChunkSource *src = nullptr;
     std::vector<char> buf;  // unparsed bytes live in [pos, end)
     std::vector<char> chunk;
@@ -265,9 +462,9 @@ int ntc_fastx_open(const char *path, ntc_fastx **out) {
     if (!path || !out) return NTC_ERR_INVALID_ARG;
     *out = nullptr;
     init_norm();
-    gzFile f = gzopen(path, "rb");
-    if (!f) return NTC_ERR_IO;
-    gzbuffer(f, 1u << 20);
+    int orc = NTC_OK;
+    ByteReader *f = open_reader(path, &orc);
+    if (!f) return orc;
     auto *fx = new ntc_fastx();
     fx->f = f;
     fx->src = new ChunkSource(f);
@@ -301,7 +498,7 @@ int ntc_fastx_next_batch(ntc_fastx *fx, uint64_t max_reads, uint64_t max_bases, 
     while (fx->offsets.size() - 1 < max_reads && fx->nb < max_bases) {
         const int rc = fx->format == '@' ? fx->next_fastq() : fx->next_fasta();
         if (rc == 1) break;
-        if (rc < 0) return NTC_ERR_FORMAT;
+        if (rc < 0) return fx->io_error ? NTC_ERR_IO : NTC_ERR_FORMAT;  // a truncated stream is an I/O error
         fx->offsets.push_back(fx->nb);
     }
     if (fx->io_error) return NTC_ERR_IO;
@@ -338,7 +535,7 @@ int ntc_fasta_format(const uint8_t *bases, const uint64_t *offsets, uint64_t n_r
 void ntc_fastx_close(ntc_fastx *fx) {
     if (!fx) return;
     delete fx->src;  // joins the producer before the file goes away
-    if (fx->f) gzclose(fx->f);
+    delete fx->f;
     delete fx;
 }
 

@@ -77,7 +77,7 @@ def _normalize(seq):
 
 
 @pytest.mark.parametrize("fmt", ["fasta", "fastq"])
-@pytest.mark.parametrize("gz", [False, True])
+@pytest.mark.parametrize("gz", [False, True, "bz2", "xz"])
 def test_fastx_random_records_across_chunks(tmp_path, fmt, gz):
     """Records of up to 3 Mbp with mixed case, IUPAC, junk bytes and CRLF endings, spread
     over several 8 MiB input chunks: every record's bases equal the restated normalize."""
@@ -100,10 +100,17 @@ def test_fastx_random_records_across_chunks(tmp_path, fmt, gz):
             expect[-1] = _normalize(seq)
             parts.append(b"@r%d%s%s%s+%s%s%s" % (i, eol, seq, eol, eol, b"I" * L, eol))
     data = b"".join(parts)
-    path = tmp_path / ("x." + fmt + (".gz" if gz else ""))
-    if gz:
+    path = tmp_path / ("x." + fmt + {False: "", True: ".gz", "bz2": ".bz2", "xz": ".xz"}[gz])
+    if gz is True:
         with gzip.open(path, "wb", compresslevel=1) as f:
             f.write(data)
+    elif gz == "bz2":  # two concatenated streams (pbzip2-style), decoded back to back
+        import bz2
+        h = len(data) // 2
+        path.write_bytes(bz2.compress(data[:h], 1) + bz2.compress(data[h:], 1))
+    elif gz == "xz":
+        import lzma
+        path.write_bytes(lzma.compress(data, preset=0))
     else:
         path.write_bytes(data)
     got = []
@@ -111,6 +118,22 @@ def test_fastx_random_records_across_chunks(tmp_path, fmt, gz):
         got += [b[int(o[r]):int(o[r + 1])].tobytes() for r in range(len(o) - 1)]
     assert len(got) == len(expect)
     assert got == expect
+
+
+def test_fastx_truncated_and_unsupported_compression(tmp_path):
+    """needletail/niffler-style detection by magic bytes: a truncated bzip2 stream is an I/O
+    error, a zstd file (no libzstd in the image) is NTC_ERR_UNSUPPORTED, never garbage."""
+    import bz2
+    data = b"".join(b"@r%d\nACGTACGTAC\n+\nIIIIIIIIII\n" % i for i in range(20000))
+    (tmp_path / "t.fq.bz2").write_bytes(bz2.compress(data)[:-200])
+    with pytest.raises(nt.NtcError) as e:
+        for _ in nt.FastxReader(str(tmp_path / "t.fq.bz2")):
+            pass
+    assert e.value.code == 9
+    (tmp_path / "z.fq.zst").write_bytes(bytes([0x28, 0xB5, 0x2F, 0xFD]) + b"\0" * 64)
+    with pytest.raises(nt.NtcError) as e:
+        nt.FastxReader(str(tmp_path / "z.fq.zst"))
+    assert e.value.code == 10
 
 
 def test_fasta_format():
