@@ -75,6 +75,8 @@ def parse_args(argv=None):
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU only: ranks, shards, oracle samples and the gathers, no GPU calls")
     ap.add_argument("--opt", action="append", default=[], help="ctx option key=value (A/B)")
+    ap.add_argument("--presort", action="store_true",
+                    help="experiment: reorder each batch's reads by minimizer on the host before upload")
     ap.add_argument("--pmc-json", default=PMC_JSON)
     args = ap.parse_args(argv)
     if args.mode and not args.configs:
@@ -157,10 +159,16 @@ def roofline(kname, kernel_ms, kernel_ms_min, units, unit_name, pmc, pmc_note, w
 
 
 # ---- workload ----------------------------------------------------------------------
+def minimizer_order(nt, reads, n, L, threads):
+    """(experiment) read order grouped by minimizer: smallest hashed 20-mer, strand as read"""
+    import numpy as np
+    return np.argsort(nt.minimizer_keys(reads, n, L, 20, threads), kind="stable")
+
+
 class Shard:
     """One rank's reads of one workload, in device batches."""
 
-    def __init__(self, nt, ctx, text, first, n, L, err, batch, threads, dry):
+    def __init__(self, nt, ctx, text, first, n, L, err, batch, threads, dry, presort=False):
         import numpy as np
         self.L, self.n, self.first = L, n, first
         self.batches = []
@@ -168,6 +176,8 @@ class Shard:
         while off < n:
             nb = min(batch, n - off)
             reads = nt.synth_reads(text, 2, first + off, nb, L, err, threads=threads)
+            if presort:
+                reads = reads.reshape(nb, L)[minimizer_order(nt, reads, nb, L, threads)].ravel()
             b = {"first": first + off, "n": nb, "reads": reads, "bases": nb * L}
             if not dry:
                 offs = np.arange(0, nb * L + 1, L, dtype=np.uint64)
@@ -359,7 +369,8 @@ def main():
     # ---- C91 encode / D91 decode -------------------------------------------------
     if "encode" in configs or "decode" in configs:
         index = setup_index([genome], "C")
-        sh = Shard(nt, ctx, genome, first, n, L, args.err_ppm, args.batch_reads, nthreads, args.dry_run)
+        sh = Shard(nt, ctx, genome, first, n, L, args.err_ppm, args.batch_reads, nthreads, args.dry_run,
+                   args.presort)
         log(f"[rank {rank}] reads {first}..{first + n} in {len(sh.batches)} batch(es)")
         orc = OracleIndex(index.n, k, index.rows, index.C, index.lcs)
         n_recs = None
@@ -456,7 +467,8 @@ def main():
         coll = np.concatenate(texts)
         ns = args.strain_reads if world == 1 else min(args.strain_reads, n)
         fs, ns = shard_mod.read_range(rank, world, ns)
-        sh = Shard(nt, ctx, coll, fs, ns, L, args.err_ppm, args.batch_reads, nthreads, args.dry_run)
+        sh = Shard(nt, ctx, coll, fs, ns, L, args.err_ppm, args.batch_reads, nthreads, args.dry_run,
+                   args.presort)
         orc = OracleIndex(index.n, k, index.rows, index.C, index.lcs)
         s = {"config": {"workload": f"S{k}: {ns} x {L}bp reads ({args.err_ppm / 1e4:g}% subst, 50% revcomp) drawn "
                                     f"from a collection of the {args.genome_bp / 1e6:g} Mbp genome + {args.strains} "

@@ -67,6 +67,10 @@ int ntc_synth_genome(uint64_t seed, uint64_t length, uint8_t *out);
  * out = n_strains * glen bytes.  Used for the multi-strain index of bench.py.        */
 int ntc_synth_strains(const uint8_t *genome, uint64_t glen, uint64_t seed, uint32_t n_strains,
                       uint32_t snp_per_million, uint8_t *out);
+/* Minimizer key of each of n_reads reads of read_len bases (smallest 64-bit hash of its
+ * 2-bit w-mers, w <= 32), for read-ordering experiments (bench.py --presort).          */
+int ntc_minimizer_keys(const uint8_t *reads, uint64_t n_reads, uint32_t read_len, uint32_t w,
+                       int n_threads, uint64_t *keys);
 /* n_reads reads of read_len bases from genome; read r depends only on (seed, r): start
  * uniform on [0, glen-read_len], reverse-complemented with probability 1/2, i.i.d.
  * substitutions with probability err_per_million / 1e6.  out = n_reads*read_len bytes.

@@ -38,7 +38,7 @@ EXPORTED = [
     "ntc_encode_batch_device", "ntc_encode_status", "ntc_decode_batch", "ntc_decode_batch_device",
     "ntc_decode_status", "ntc_last_timing", "ntc_device_alloc", "ntc_device_free", "ntc_memcpy_h2d",
     "ntc_memcpy_d2h", "ntc_debug_matching_statistics", "ntc_build_index", "ntc_index_free",
-    "ntc_index_view_of", "ntc_index_save", "ntc_index_save_as", "ntc_index_load", "ntc_synth_genome", "ntc_synth_strains", "ntc_synth_reads",
+    "ntc_index_view_of", "ntc_index_save", "ntc_index_save_as", "ntc_index_load", "ntc_synth_genome", "ntc_synth_strains", "ntc_synth_reads", "ntc_minimizer_keys",
     "ntc_file_header", "ntc_write_block", "ntc_read_block", "ntc_buffer_free",
     "ntc_fastx_open", "ntc_fastx_next_batch", "ntc_fastx_close", "ntc_fasta_format",
 ]
@@ -122,6 +122,7 @@ def lib():
         "ntc_index_load": (I, [ctypes.c_char_p, ctypes.POINTER(P)]),
         "ntc_synth_genome": (I, [u64, u64, P]),
         "ntc_synth_strains": (I, [P, u64, u64, u32, u32, P]),
+        "ntc_minimizer_keys": (I, [P, u64, u32, u32, I, P]),
         "ntc_synth_reads": (I, [P, u64, u64, u64, u64, u32, u32, I, P]),
         "ntc_file_header": (None, [P]),
         "ntc_write_block": (I, [P, u64, u64, ctypes.POINTER(P), ctypes.POINTER(u64)]),
@@ -396,6 +397,16 @@ def synth_strains(genome, seed, n_strains, snp_per_million):
     if rc:
         raise NtcError(rc, "ntc_synth_strains")
     return out
+
+
+def minimizer_keys(reads, n_reads, read_len, w=20, threads=0):
+    """smallest hashed w-mer of each read (bench.py --presort locality experiment)"""
+    reads = np.ascontiguousarray(reads, dtype=np.uint8)
+    keys = np.zeros(n_reads, dtype=np.uint64)
+    rc = lib().ntc_minimizer_keys(_p(reads), n_reads, read_len, w, threads, _p(keys))
+    if rc:
+        raise NtcError(rc, "ntc_minimizer_keys")
+    return keys
 
 
 def synth_reads(genome, seed, first_read, n_reads, read_len, err_per_million, threads=0):

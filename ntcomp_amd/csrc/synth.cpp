@@ -87,3 +87,36 @@ extern "C" int ntc_synth_reads(const uint8_t *genome, uint64_t glen, uint64_t se
     }
     return NTC_OK;
 }
+
+// Minimizer of each read (bench.py --presort locality experiment): the smallest
+// 64-bit-hashed w-mer (2-bit codes, strand as read) of read r = reads[r*L, (r+1)*L).
+extern "C" int ntc_minimizer_keys(const uint8_t *reads, uint64_t n_reads, uint32_t read_len, uint32_t w,
+                                  int n_threads, uint64_t *keys) {
+    if ((!reads || !keys) && n_reads) return NTC_ERR_INVALID_ARG;
+    if (w == 0 || w > 32 || read_len < w) return NTC_ERR_INVALID_ARG;
+    if (n_threads <= 0) n_threads = (int)std::max(1u, std::thread::hardware_concurrency());
+    const uint64_t mask = w == 32 ? ~0ULL : ((1ULL << (2 * w)) - 1);
+    auto work = [&](uint64_t a, uint64_t b) {
+        for (uint64_t r = a; r < b; r++) {
+            const uint8_t *q = reads + r * read_len;
+            uint64_t v = 0, best = ~0ULL;
+            for (uint32_t j = 0; j < read_len; j++) {
+                v = ((v << 2) | (((uint64_t)q[j] >> 1 ^ (uint64_t)q[j] >> 2) & 3)) & mask;
+                if (j + 1 >= w) {
+                    const uint64_t h = (v * 0x9E3779B97F4A7C15ULL) >> 20;
+                    best = h < best ? h : best;
+                }
+            }
+            keys[r] = best;
+        }
+    };
+    std::vector<std::thread> ts;
+    const uint64_t chunk = (n_reads + n_threads - 1) / n_threads;
+    for (int t = 0; t < n_threads; t++) {
+        const uint64_t a = t * chunk, b = std::min(n_reads, a + chunk);
+        if (a >= b) break;
+        ts.emplace_back(work, a, b);
+    }
+    for (auto &t : ts) t.join();
+    return NTC_OK;
+}

@@ -24,6 +24,16 @@ KINDS = ["rank", "lcs", "uniq", "tabU", "tabLo", "bits", "filt", "colex", "pos_o
          "puniq", "E-store"]
 
 
+def minimizer_order(reads, n, L, w=20):
+    """read order grouped by each read's minimizer (smallest hashed w-mer, strand as read)"""
+    codes = ((reads.reshape(n, L).astype(np.uint64) >> np.uint64(1)) ^ (reads.reshape(n, L).astype(np.uint64) >> np.uint64(2))) & np.uint64(3)
+    v = np.zeros((n, L - w + 1), dtype=np.uint64)
+    for i in range(w):
+        v = (v << np.uint64(2)) | codes[:, i:i + L - w + 1]
+    h = (v * np.uint64(0x9E3779B97F4A7C15)) >> np.uint64(20)
+    return np.argsort(h.min(axis=1), kind="stable")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--genome-bp", type=int, default=5_000_000)
@@ -34,6 +44,9 @@ def main():
     ap.add_argument("--tab-u", type=int, default=0)
     ap.add_argument("--strains", type=int, default=0, help="index a collection: the genome + N strains")
     ap.add_argument("--snp-ppm", type=int, default=10_000)
+    ap.add_argument("--group", type=int, default=1, help="count distinct lines per this many consecutive reads")
+    ap.add_argument("--order", choices=["input", "minimizer"], default="input",
+                    help="process reads as generated, or grouped by their minimizer (locality experiment)")
     args = ap.parse_args()
     so = os.path.join(REPO, "tests", "emu", "libntc_emu_trace.so")
     subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "tests", "emu"), "libntc_emu_trace.so"])
@@ -50,6 +63,9 @@ def main():
         texts += [st[i] for i in range(args.strains)]
     ix = nt.Index.build([t.tobytes() for t in texts], args.k, threads=8)
     reads = nt.synth_reads(np.concatenate(texts), 2, 0, args.reads, args.read_len, args.err_ppm)
+    if args.order == "minimizer":
+        reads = reads.reshape(args.reads, args.read_len)[minimizer_order(reads, args.reads, args.read_len)].ravel()
+    os.environ["NTC_TRACE_GROUP"] = str(args.group)
     offs = np.arange(0, args.reads * args.read_len + 1, args.read_len, dtype=np.uint64)
     recs, _ = emu_lib.emu_encode(ix.n, args.k, ix.rows, ix.C, ix.lcs, reads, offs, tab_u=args.tab_u)
     K = len(KINDS)
@@ -58,7 +74,8 @@ def main():
     n = int(out[0])
     req = out[1:1 + 2 * K].reshape(2, K) / n
     lines = out[1 + 2 * K:].reshape(2, K) / n
-    print(f"reads {n}, records/read {len(recs) / n:.2f}, k={args.k}, err_ppm={args.err_ppm}")
+    print(f"reads {n}, records/read {len(recs) / n:.2f}, k={args.k}, err_ppm={args.err_ppm}, "
+          f"order {args.order}, lines counted per {args.group} reads")
     for ph, name in enumerate(["ms", "parse"]):
         print(f"-- {name}: loads/read {req[ph].sum():.2f}, lines/read {lines[ph].sum():.2f}")
         for i in np.argsort(-lines[ph]):

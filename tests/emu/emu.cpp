@@ -23,14 +23,21 @@ int g_phase = -1;
 std::unordered_set<uint64_t> g_lines[2][kTrKinds];
 uint64_t g_req[2][kTrKinds], g_ltot[2][kTrKinds], g_reads;
 void trace_phase(int ph) { g_phase = ph; }
+uint64_t g_group = 0, g_in_group = 0;  // NTC_TRACE_GROUP=G: distinct lines per G consecutive reads
 void trace_read_done() {
+    if (g_group == 0) {
+        const char *e = getenv("NTC_TRACE_GROUP");
+        g_group = e && atoi(e) > 0 ? (uint64_t)atoi(e) : 1;
+    }
+    g_reads++;
+    g_phase = -1;
+    if (++g_in_group < g_group) return;
+    g_in_group = 0;
     for (int a = 0; a < 2; a++)
         for (int b = 0; b < kTrKinds; b++) {
             g_ltot[a][b] += g_lines[a][b].size();
             g_lines[a][b].clear();
         }
-    g_reads++;
-    g_phase = -1;
 }
 }  // namespace
 void ntc_touch(int kind, const void *p) {
