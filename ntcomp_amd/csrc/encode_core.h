@@ -1442,7 +1442,8 @@ NTC_HD void store_codes(uint8_t *out, uint64_t codes, uint32_t n) {
 // the characters written; then every staged word goes out as ASCII exactly once (whole words
 // with two 16-byte stores, words shared with other blocks byte by byte: records never share
 // a byte).  No global atomics, no 2-bit round trip through HBM.
-constexpr uint32_t kDecStageWords = 1024;  // 32 K characters per block of 256 records
+constexpr uint32_t kDecStageWords = 2048;  // 64 K characters per block of 512 records (error-free
+                                           // 150 bp reads: 2 records per read, 38 K characters)
 struct StageWriter {
     uint64_t *bits;  // word t: codes of characters 32 (w_lo + t) ... + 31
     uint32_t *mask;  // bit i of word t: character 32 (w_lo + t) + i is staged
