@@ -469,3 +469,29 @@ def test_gpu_decode_direct_path_for_long_records(ctx):
     assert int(lens.max()) > 32 * 1024  # records longer than a whole staging buffer
     out, o2 = ctx.decode(got)
     assert np.array_equal(out, bases) and np.array_equal(o2, offs)
+
+
+def test_gpu_random_cases_equal_oracle(ctx):
+    """The property test's random cases (tests/test_property.py: random k 11..127, genome,
+    repeats, read lengths 1..400, error rates, reverse complements) through the GPU: records
+    bit-exact vs the oracle, decode(encode(x)) == x, failures at the oracle's first read."""
+    from test_property import _case
+    rng = np.random.default_rng(2024)
+    for i in range(60):
+        k = int(rng.integers(11, 128))
+        ix, bases, offs = _case(int(rng.integers(0, 2**32)), k, int(rng.integers(300, 6000)),
+                                int(rng.integers(1, 60)), int(rng.integers(1, 400)),
+                                float(rng.choice([0.0, 0.005, 0.02, 0.08])), bool(rng.integers(0, 2)))
+        ctx.upload(ix)
+        orc = OracleIndex(ix.n, k, ix.rows, ix.C, ix.lcs)
+        rc, bad = orc.try_encode(bases, offs)
+        if rc < 0:
+            with pytest.raises(nt.NtcError) as e:
+                ctx.encode(bases, offs)
+            assert e.value.bad_read == bad, (i, k)
+            continue
+        exp, eoff = orc.encode(bases, offs)
+        got, goff = ctx.encode(bases, offs)
+        assert np.array_equal(goff, eoff) and np.array_equal(got, exp), (i, k)
+        out, o2 = ctx.decode(got)
+        assert np.array_equal(out, bases) and np.array_equal(o2, offs), (i, k)
