@@ -364,7 +364,8 @@ def main():
                     ctx.set_option(key, int(val))
             t0 = time.time()
             ctx.upload(index)
-            log(f"[rank {rank}] upload {time.time() - t0:.1f}s, {ctx.get_option('n_paths')} paths")
+            log(f"[rank {rank}] upload {time.time() - t0:.1f}s, {ctx.get_option('n_paths')} paths, SCAN filter "
+                f"{'on' if ctx.get_option('filter') else 'off'} (density {ctx.get_option('filter_density_ppm') / 1e4:.1f} %)")
         return index
 
     genome = nt.synth_genome(1, args.genome_bp)
@@ -484,6 +485,7 @@ def main():
             encode_pass(ctx, sh, check=True)
             s["config"]["records_per_gpu"] = sum(b["n_recs"] for b in sh.batches)
             s["config"]["n_paths"] = ctx.get_option("n_paths")
+            s["config"]["scan_filter"] = bool(ctx.get_option("filter"))
             el, kms = timed(lambda: encode_pass(ctx, sh), args.steps, args.warmup, barrier, sync, dist)
             kavg = sum(kms) / len(kms)
             s.update(value=round(sh.bases * world * args.steps / el / 1e6, 2), unit="Mbases/s",

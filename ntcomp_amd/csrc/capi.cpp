@@ -56,6 +56,8 @@ struct ntc_ctx {
     Enc4Args last4{};
     uint32_t tab_u_opt = 0;  // suffix-table depth for the next upload (0 = default_tab_u)
     int pair_bytes_opt = 1;  // build the SCAN pair bytes at the next upload (0: bitmap tests, A/B)
+    int filter_opt = -1;     // SCAN pre-filter at the next upload: -1 auto (off when saturated), 0 off, 1 on
+    int64_t filter_density_ppm = -1;  // presence density of the filter level at the last upload
     int ext2_opt = 0;        // build the two-character rank chunks at the next upload (A/B option: 1 measured
                              // slower -- 8 B/node from HBM against 1 B/node of Infinity-Cache-resident rank words)
     uint64_t n_paths = 0, path_text_len = 0;
@@ -510,6 +512,20 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     d.tab_u = U;
     d.tab_pos = (has_paths && U >= dv.t_jump && n < (1ULL << 31)) ? 1u : 0u;
     launch_tab_build(d, U, (uint2 *)d_tab, (uint32_t *)d_bits, F, (uint32_t *)d_fbits, ctx->stream);
+    ctx->filter_density_ppm = -1;
+    if (F) {
+        // A filter over a large index is mostly ones (S91's 70 M nodes: 72 % of all 12-mers)
+        // and passes most positions, so it costs more lines than it saves: auto mode drops it
+        // above kFiltMaxDensityPpm (every SCAN then goes straight to the exact pair words).
+        std::vector<uint32_t> fb(tab_bits_words(F));
+        HIP_TRY(ctx, hipMemcpyAsync(fb.data(), d_fbits, fb.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        uint64_t ones = 0;
+        for (uint32_t x : fb) ones += (uint64_t)__builtin_popcount(x);
+        ctx->filter_density_ppm = (int64_t)(ones * 1000000 / ((uint64_t)fb.size() * 32));
+        const bool on = ctx->filter_opt == 1 || (ctx->filter_opt < 0 && ctx->filter_density_ppm <= kFiltMaxDensityPpm);
+        if (!on) d.filt_f = 0;
+    }
     d.pair_w = nullptr;
     if (ctx->pair_bytes_opt) {
         void *d_pair;
@@ -539,6 +555,11 @@ int ntc_ctx_set_option(ntc_ctx *ctx, const char *key, int64_t value) {
         ctx->pair_bytes_opt = (int)value;
         return NTC_OK;
     }
+    if (std::strcmp(key, "filter") == 0) {  // applies to the next ntc_index_upload
+        if (value < -1 || value > 1) return set_err(ctx, NTC_ERR_INVALID_ARG, "filter must be -1 (auto), 0 or 1");
+        ctx->filter_opt = (int)value;
+        return NTC_OK;
+    }
     if (std::strcmp(key, "ext2") == 0) {  // applies to the next ntc_index_upload
         if (value != 0 && value != 1) return set_err(ctx, NTC_ERR_INVALID_ARG, "ext2 must be 0 or 1");
         ctx->ext2_opt = (int)value;
@@ -564,6 +585,8 @@ int ntc_ctx_get_option(const ntc_ctx *ctx, const char *key, int64_t *value) {
     else if (std::strcmp(key, "tab_u") == 0) *value = ctx->has_index ? ctx->dix.tab_u : ctx->tab_u_opt;
     else if (std::strcmp(key, "pair_bytes") == 0) *value = ctx->has_index ? (ctx->dix.pair_w != nullptr) : ctx->pair_bytes_opt;
     else if (std::strcmp(key, "ext2") == 0) *value = ctx->has_index ? (ctx->dix.rank2 != nullptr) : ctx->ext2_opt;
+    else if (std::strcmp(key, "filter") == 0) *value = ctx->has_index ? (ctx->dix.filt_f != 0) : ctx->filter_opt;
+    else if (std::strcmp(key, "filter_density_ppm") == 0) *value = ctx->filter_density_ppm;
     else if (std::strcmp(key, "n_paths") == 0) *value = (int64_t)ctx->n_paths;
     else if (std::strcmp(key, "path_text_len") == 0) *value = (int64_t)ctx->path_text_len;
     else if (std::strcmp(key, "path_hash") == 0) {  // test hook: derived.h path_cover_hash of the device cover
