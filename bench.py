@@ -125,6 +125,13 @@ def random_line_roof():
         return None
 
 
+def launch_ms(kms, units, ref):
+    """kernel ms of a launch of `ref` units from launches of different sizes (a shard's last
+    batch is smaller): (mean, min) of time per unit x ref, launches in timed() order"""
+    per = [t / u for t, u in zip(kms, units * (len(kms) // len(units)))]
+    return sum(kms) / sum(units * (len(kms) // len(units))) * ref, min(per) * ref
+
+
 def roofline(kname, kernel_ms, kernel_ms_min, units, unit_name, pmc, pmc_note, wl_key, extra=None):
     """Roofline of one dominant kernel: PMC bytes past L2 per unit (read or base) x units per
     launch / live kernel time."""
@@ -411,9 +418,9 @@ def main():
                    parallelism=f"reads sharded over {world} GPU(s), index replicated, no collective")
         if enc is not None:
             el, kms = enc
-            kavg = sum(kms) / len(kms)
             b0 = sh.batches[0]
-            rl = roofline("k_ms4", kavg, min(kms), b0["n"], "read", pmc, pmc_note, f"C{k}",
+            kavg, kmin = launch_ms(kms, [b["n"] for b in sh.batches], b0["n"])
+            rl = roofline("k_ms4", kavg, kmin, b0["n"], "read", pmc, pmc_note, f"C{k}",
                           {"reference_work_avoided": round(
                               b0["bases"] * (1 + 2 * 64) / (kavg / 1e3) / 1e9 / HBM_PEAK_GBPS, 3),
                            "reference_work_note": "SURVEY 8(d) B_enc (1 B + two 64 B rank lines per base) / "
@@ -431,8 +438,8 @@ def main():
                 cpu["speedup_gpu_vs_cpu"] = round(line["value"] / cpu["value"], 1)
         if dec is not None:
             el, kms = dec
-            kavg = sum(kms) / len(kms)
             b0 = sh.batches[0]
+            kavg, kmin = launch_ms(kms, [b["bases"] for b in sh.batches], b0["bases"])
             dcpu = None
             if chk and chk["cpu_decode_s"] > 0 and world == 1:
                 dcpu = {"value": round(chk["cpu_decode_bases"] / chk["cpu_decode_s"] / 1e6, 3), "unit": "Mbases/s",
@@ -443,7 +450,7 @@ def main():
                  "ms_per_step": round(el / args.steps * 1e3, 3),
                  "config": {"workload": f"D{k}: decode of the C{k} records ({n_recs} records, {n} reads per GPU) "
                                         f"-> bases via the inverse-SBWT walk, k={k}"},
-                 "roofline": roofline("k_dec_rec", kavg, min(kms), b0["bases"], "base", pmc, pmc_note, f"D{k}"),
+                 "roofline": roofline("k_dec_rec", kavg, kmin, b0["bases"], "base", pmc, pmc_note, f"D{k}"),
                  "cpu_baseline": dcpu,
                  "parity": {"round_trip_exact_all_ranks": all(v["check"]["decode_ok"] for v in verdicts)
                             if chk else None, "bases_checked_per_rank": n * L if chk else None},
@@ -487,16 +494,17 @@ def main():
             s["config"]["n_paths"] = ctx.get_option("n_paths")
             s["config"]["scan_filter"] = bool(ctx.get_option("filter"))
             el, kms = timed(lambda: encode_pass(ctx, sh), args.steps, args.warmup, barrier, sync, dist)
-            kavg = sum(kms) / len(kms)
+            b0 = sh.batches[0]
+            kavg, kmin = launch_ms(kms, [b["n"] for b in sh.batches], b0["n"])
             s.update(value=round(sh.bases * world * args.steps / el / 1e6, 2), unit="Mbases/s",
                      ms_per_step=round(el / args.steps * 1e3, 3),
-                     roofline=roofline("k_ms4", kavg, min(kms), sh.batches[0]["n"], "read", pmc, pmc_note, f"S{k}"))
+                     roofline=roofline("k_ms4", kavg, kmin, b0["n"], "read", pmc, pmc_note, f"S{k}"))
             el, kms = timed(lambda: decode_pass(ctx, sh), args.steps, args.warmup, barrier, sync, dist)
-            kavg = sum(kms) / len(kms)
+            kavg, kmin = launch_ms(kms, [b["bases"] for b in sh.batches], b0["bases"])
             s["decode"] = {"value": round(sh.bases * world * args.steps / el / 1e6, 2), "unit": "Mbases/s",
                            "ms_per_step": round(el / args.steps * 1e3, 3),
-                           "roofline": roofline("k_dec_rec", kavg, min(kms), sh.batches[0]["bases"], "base", pmc,
-                                                pmc_note, f"SD{k}")}
+                           "roofline": roofline("k_dec_rec", kavg, kmin, b0["bases"], "base", pmc, pmc_note,
+                                                f"SD{k}")}
         secs = 0 if args.no_cpu else 3.0
         chk = check_shard(ctx, orc, sh, secs, not args.dry_run, False, args.dry_run) if secs > 0 else None
         vs = gather(chk)
