@@ -44,6 +44,10 @@ struct ntc_ctx {
     // workspace buffers (grown, never shrunk)
     DevBuf ws[28];
     unsigned long long *d_status = nullptr;
+    // status mailbox in pinned host memory: {status, count a, count b}, written by k_status_box
+    // at the end of a device call, so *_status() is one stream sync instead of D2H copies
+    uint64_t *h_box = nullptr;
+    bool box_valid = false;
     // last call
     CallKind last = kNone;
     uint64_t last_n = 0;           // reads (encode) / records (decode)
@@ -180,6 +184,7 @@ int encode4_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, u
     if ((rc = ensure(ctx, WS_SCANTMP, scan_tmp_words(n_reads + 1) * 8, &tmp))) return rc;
     HIP_TRY(ctx, hipMemsetAsync(ctx->d_status, 0xFF, 8, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(a.counter, 0, kCounterBytes, ctx->stream));
+    ctx->box_valid = false;
     ctx->last = kEncode;
     ctx->last_variant = 4;
     ctx->last_n = n_reads;
@@ -199,6 +204,9 @@ int encode4_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, u
     launch_emit4(a, wave_off, (uint64_t *)tmp, d_rec_offs, d_rec_out, cap, ctx->stream);
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
+    launch_status_box(ctx->d_status, d_rec_offs + n_reads, nullptr, ctx->h_box, ctx->stream);
+    HIP_TRY(ctx, hipGetLastError());
+    ctx->box_valid = true;
     return NTC_OK;
 }
 
@@ -221,6 +229,7 @@ int encode_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, ui
     void *tmp;
     if ((rc = ensure(ctx, WS_SCANTMP, scan_tmp_words(n_reads + 1) * 8, &tmp))) return rc;
     HIP_TRY(ctx, hipMemsetAsync(ctx->d_status, 0xFF, 8, ctx->stream));
+    ctx->box_valid = false;
     ctx->last = kEncode;
     ctx->last_n = n_reads;
     ctx->last_out_offs = d_rec_offs;
@@ -253,8 +262,13 @@ int encode_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, ui
 
 int read_status(ntc_ctx *ctx, int64_t *bad_index) {
     unsigned long long st = 0;
-    HIP_TRY(ctx, hipMemcpyAsync(&st, ctx->d_status, 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->box_valid) {  // the call's mailbox (k_status_box): one stream sync
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        st = ((volatile uint64_t *)ctx->h_box)[0];
+    } else {
+        HIP_TRY(ctx, hipMemcpyAsync(&st, ctx->d_status, 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    }
     if (st == ~0ULL) {
         if (bad_index) *bad_index = -1;
         return NTC_OK;
@@ -284,7 +298,8 @@ int ntc_ctx_create(int device, ntc_ctx **out) {
     ctx->device = device;
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc((void **)&ctx->d_status, 64) != hipSuccess) {
+        hipMalloc((void **)&ctx->d_status, 64) != hipSuccess ||
+        hipHostMalloc((void **)&ctx->h_box, 64, hipHostMallocDefault) != hipSuccess) {
         delete ctx;
         return NTC_ERR_HIP;
     }
@@ -312,6 +327,7 @@ void ntc_ctx_destroy(ntc_ctx *ctx) {
         if (b.p) (void)hipFree(b.p);
     for (void *p : ctx->index_mem) (void)hipFree(p);
     if (ctx->d_status) (void)hipFree(ctx->d_status);
+    if (ctx->h_box) (void)hipHostFree(ctx->h_box);
     for (auto &e : ctx->ev)
         if (e) (void)hipEventDestroy(e);
     if (ctx->stream && ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
@@ -672,7 +688,8 @@ int ntc_encode_status(ntc_ctx *ctx, int64_t *bad_read, uint64_t *n_records) {
     if (rc) return rc;
     if (n_records) {
         if (ctx->last != kEncode || !ctx->last_out_offs) return set_err(ctx, NTC_ERR_INVALID_ARG, "no encode call");
-        HIP_TRY(ctx, hipMemcpy(n_records, ctx->last_out_offs + ctx->last_n, 8, hipMemcpyDeviceToHost));
+        if (ctx->box_valid) *n_records = ((volatile uint64_t *)ctx->h_box)[1];
+        else HIP_TRY(ctx, hipMemcpy(n_records, ctx->last_out_offs + ctx->last_n, 8, hipMemcpyDeviceToHost));
     }
     return NTC_OK;
 }
@@ -796,6 +813,7 @@ int ntc_decode_batch_device(ntc_ctx *ctx, const uint64_t *d_recs, uint64_t n_rec
     uint64_t *pf = (uint64_t *)ws, *pl = pf + tiles, *pfs = pl + tiles, *pls = pfs + tiles + 1;
     if ((rc = ensure(ctx, WS_SCANTMP, (scan_tmp_words(tiles + 1) + 2) * 8, &tmp))) return rc;
     HIP_TRY(ctx, hipMemsetAsync(ctx->d_status, 0xFF, 8, ctx->stream));
+    ctx->box_valid = false;
     ctx->last = kDecode;
     ctx->last_n = tiles;
     ctx->last_out_offs = pfs;  // pfs[tiles] = reads, pls[tiles] = bases (ntc_decode_status)
@@ -824,6 +842,9 @@ int ntc_decode_batch_device(ntc_ctx *ctx, const uint64_t *d_recs, uint64_t n_rec
     HIP_TRY(ctx, hipEventRecord(ctx->ev[3], ctx->stream));  // k_dec_rec alone: ev[1] -> ev[3]
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
+    launch_status_box(ctx->d_status, pfs + tiles, pls + tiles, ctx->h_box, ctx->stream);
+    HIP_TRY(ctx, hipGetLastError());
+    ctx->box_valid = true;
     return NTC_OK;
 }
 
@@ -833,8 +854,13 @@ int ntc_decode_status(ntc_ctx *ctx, uint64_t *n_reads, uint64_t *n_bases) {
     int rc = read_status(ctx, nullptr);
     if (ctx->last != kDecode) return set_err(ctx, NTC_ERR_INVALID_ARG, "no decode call");
     uint64_t nr = 0, nb = 0;
-    HIP_TRY(ctx, hipMemcpy(&nr, ctx->last_out_offs + ctx->last_n, 8, hipMemcpyDeviceToHost));
-    HIP_TRY(ctx, hipMemcpy(&nb, ctx->last_out_offs + (ctx->last_n + 1) + ctx->last_n, 8, hipMemcpyDeviceToHost));
+    if (ctx->box_valid) {
+        nr = ((volatile uint64_t *)ctx->h_box)[1];
+        nb = ((volatile uint64_t *)ctx->h_box)[2];
+    } else {
+        HIP_TRY(ctx, hipMemcpy(&nr, ctx->last_out_offs + ctx->last_n, 8, hipMemcpyDeviceToHost));
+        HIP_TRY(ctx, hipMemcpy(&nb, ctx->last_out_offs + (ctx->last_n + 1) + ctx->last_n, 8, hipMemcpyDeviceToHost));
+    }
     if (n_reads) *n_reads = nr;
     if (n_bases) *n_bases = nb;
     ctx->last_units = nb;

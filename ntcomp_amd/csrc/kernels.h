@@ -105,6 +105,8 @@ void launch_dec_tiles(const uint64_t *recs, uint64_t n, uint64_t *pf, uint64_t *
                       uint64_t *tmp, hipStream_t s);
 void launch_dec_walk(const DecWalkArgs &a, hipStream_t s);
 void launch_rank2(const DevIndex &ix, Rank2Chunk *out, hipStream_t s);
+void launch_status_box(const unsigned long long *status, const uint64_t *a, const uint64_t *b, uint64_t *box,
+                       hipStream_t s);
 void launch_walk_build(const uint32_t *pred, const uint8_t *code, uint64_t n, WalkStep *a, WalkStep *b,
                        WalkEntry *out, hipStream_t s);
 uint64_t scan_tmp_words(uint64_t n);

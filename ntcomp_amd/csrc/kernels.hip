@@ -254,28 +254,57 @@ __global__ __launch_bounds__(256) void k_emit4(Enc4Args a, const uint64_t *wave_
                                                uint64_t *out, uint64_t capacity) {
     const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t cnt = r < a.n_reads ? a.rec_count[r] : 0u;
+    // every load first and unconditional (clamped index): the count, the wave's offset, the
+    // status and the first kEmitEarly record slots (record j of read r at R2[j * n_reads + r],
+    // coalesced over the wave); a load under a branch or between dependent stores would be
+    // its own round trip
+    constexpr uint32_t kEmitEarly = 4;
+    const uint64_t rc = r < a.n_reads ? r : a.n_reads - 1;
+    const uint32_t cnt0 = a.rec_count[rc];
+    const uint64_t woff = wave_off[rc >> 6];
+    const unsigned long long st = *a.status;
+    const uint64_t *slot = a.R2 + rc;
+    uint64_t early[kEmitEarly];
+#pragma unroll
+    for (uint32_t j = 0; j < kEmitEarly; j++) early[j] = slot[(uint64_t)j * a.n_reads];
+    const uint32_t cnt = r < a.n_reads ? cnt0 : 0u;
     uint32_t inc = cnt;
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t t = __shfl_up(inc, o, 64);
         if (lane >= (uint32_t)o) inc += t;
     }
     if (r >= a.n_reads) return;
-    const uint64_t off = wave_off[r >> 6] + (inc - cnt);
+    const uint64_t off = woff + (inc - cnt);
     rec_offsets[r] = off;
     if (r + 1 == a.n_reads) rec_offsets[r + 1] = off + cnt;
-    if (*a.status != ~0ull) return;  // a read failed: the call reports that, no records
+    if (st != ~0ull) return;  // a read failed: the call reports that, no records
     if (off + cnt > capacity) {
         atomicMin(a.status, (unsigned long long)((r << 8) | (uint64_t)kErrCapacity));
         return;
     }
-    const uint64_t *slot = a.R2 + r;  // record j at slot[j * n_reads] (parse_read)
     const uint32_t ns = cnt < kRecSlot ? cnt : kRecSlot;
-    for (uint32_t j = 0; j < ns; j++) out[off + j] = slot[(uint64_t)j * a.n_reads];
+#pragma unroll
+    for (uint32_t j = 0; j < kEmitEarly; j++)
+        if (j < ns) out[off + j] = early[j];
+    for (uint32_t j = kEmitEarly; j < ns; j++) out[off + j] = slot[(uint64_t)j * a.n_reads];
     if (cnt > kRecSlot) {
         const uint64_t *spill = a.R + (a.offs[r] - a.offs[0]);
         for (uint32_t j = kRecSlot; j < cnt; j++) out[off + j] = spill[j];
     }
+}
+
+// the call's status and up to two counts into the host mailbox (pinned memory): thread t
+// writes word t with a vector store; the host reads it after one stream sync
+__global__ __launch_bounds__(64) void k_status_box(const unsigned long long *status, const uint64_t *a,
+                                                   const uint64_t *b, uint64_t *box) {
+    const uint32_t t = threadIdx.x;
+    if (t >= 3) return;
+    const uint64_t v = t == 0 ? (uint64_t)*status : t == 1 ? (a ? *a : 0) : (b ? *b : 0);
+    box[t] = v;  // per-lane address: a vector store
+}
+void launch_status_box(const unsigned long long *status, const uint64_t *a, const uint64_t *b, uint64_t *box,
+                       hipStream_t s) {
+    hipLaunchKernelGGL(k_status_box, dim3(1), dim3(64), 0, s, status, a, b, box);
 }
 
 // rows of scratch a tile of 64 reads needs = longest read, rounded up to 32
@@ -344,16 +373,22 @@ __global__ __launch_bounds__(256) void k_dec_tiles(const uint64_t *recs, uint64_
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (t * kDecTileRecs >= n) return;  // whole wave
-    uint64_t sf = 0, sl = 0;
+    // all loads unconditional (clamped, masked after): a load under `if (r < n)` is waited for
+    // inside its branch, which serialised the tile's eight loads into eight round trips
+    uint64_t w[kDecTileRecs / 64];
 #pragma unroll
     for (uint32_t q = 0; q < kDecTileRecs / 64; q++) {
         const uint64_t r = t * kDecTileRecs + q * 64 + lane;
-        if (r < n) {
-            uint64_t f, l;
-            dec_desc(recs[r], f, l);
-            sf += f;
-            sl += l;
-        }
+        w[q] = recs[r < n ? r : n - 1];
+    }
+    uint64_t sf = 0, sl = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kDecTileRecs / 64; q++) {
+        uint64_t f, l;
+        dec_desc(w[q], f, l);
+        const bool in = t * kDecTileRecs + q * 64 + lane < n;
+        sf += in ? f : 0;
+        sl += in ? l : 0;
     }
     sf = wave_sum64(sf);
     sl = wave_sum64(sl);
