@@ -562,7 +562,7 @@ int ntc_ctx_set_option(ntc_ctx *ctx, const char *key, int64_t value) {
     if (!ctx || !key) return NTC_ERR_INVALID_ARG;
     if (std::strcmp(key, "tab_u") == 0) {  // applies to the next ntc_index_upload
         if (value < 0 || value > (int64_t)kTabMaxU)
-            return set_err(ctx, NTC_ERR_INVALID_ARG, "tab_u must be 0 (default) or 1..14");
+            return set_err(ctx, NTC_ERR_INVALID_ARG, "tab_u must be 0 (default) or 1..15");
         ctx->tab_u_opt = (uint32_t)value;
         return NTC_OK;
     }

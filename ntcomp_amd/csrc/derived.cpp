@@ -112,7 +112,7 @@ uint32_t default_tab_u(uint64_t n, uint32_t k) {
     // U-mers are present by chance, so few table-long positions need the SBWT
     const double l4 = std::log((double)std::max<uint64_t>(n, 2)) / std::log(4.0);
     uint32_t u = (uint32_t)std::ceil(l4) + 2;
-    u = std::min<uint32_t>(u, kTabMaxU);
+    u = std::min<uint32_t>(u, kTabDefaultMaxU);
     return std::max<uint32_t>(1u, std::min<uint32_t>(u, k));
 }
 

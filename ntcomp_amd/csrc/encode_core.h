@@ -122,7 +122,7 @@ struct DevIndex {
     const uint16_t *pair_w;       // pair word of each (U-1)-mer (see pair_word), or null
     uint32_t path_len;            // path text length (has_paths): path positions are < path_len
     uint32_t tab_pos;             // 1: top-level singleton entries carry the path position
-    uint32_t tab_u;               // U: longest tabulated length (1 <= U <= min(k, 14))
+    uint32_t tab_u;               // U: longest tabulated length (1 <= U <= min(k, kTabMaxU))
     uint32_t absent;              // bit c: no node ends with character c
     const Rank2Chunk *rank2;      // [4][rank2_blocks(n)] two-character rank chunks, or null
 };
@@ -445,7 +445,8 @@ NTC_HD int encode_lane(const DevIndex &ix, const uint8_t *q, uint32_t len, uint3
 constexpr uint32_t kTabShort = 0xFFFFFF00u;  // y >= kTabShort: absent, m = y & 0xFF
 constexpr uint32_t kTabPos = 0x80000000u;    // top level, tab_pos: y = kTabPos | path position
                                              // of the single node x (interval [x, x + 1))
-constexpr uint32_t kTabMaxU = 14;            // 4^14 entries x 8 B at the top level
+constexpr uint32_t kTabMaxU = 15;            // 4^15 entries x 8 B (8.6 GB) at the top level (tab_u option)
+constexpr uint32_t kTabDefaultMaxU = 14;     // default cap: U = 15 measured +1 % on S91 for 4x the table
 
 NTC_HD uint64_t tab_base(uint32_t u) { return ((1ULL << (2 * u)) - 4) / 3; }
 NTC_HD bool tab_long(uint2 e) { return e.y < kTabShort; }

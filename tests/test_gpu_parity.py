@@ -495,3 +495,24 @@ def test_gpu_random_cases_equal_oracle(ctx):
         assert np.array_equal(goff, eoff) and np.array_equal(got, exp), (i, k)
         out, o2 = ctx.decode(got)
         assert np.array_equal(out, bases) and np.array_equal(o2, offs), (i, k)
+
+
+def test_gpu_suffix_table_depth_15():
+    """The deepest suffix table (U = 15, 8.6 GB top level; the default for indexes of more than
+    ~17 M nodes) gives the same records as the oracle on the C91 index."""
+    genome = nt.synth_genome(1, 5_000_000)
+    ix = nt.Index.build([genome.tobytes()], 91)
+    ctx = nt.GpuContext(0)
+    ctx.set_option("tab_u", 15)
+    ctx.upload(ix)
+    assert ctx.get_option("tab_u") == 15
+    n, L = 200_000, 150
+    reads = nt.synth_reads(genome, 9, 0, n, L, 10_000)
+    offs = np.arange(0, n * L + 1, L, dtype=np.uint64)
+    recs, roff = ctx.encode(reads, offs)
+    out, o2 = ctx.decode(recs)
+    assert np.array_equal(out, reads)
+    m = 20_000
+    exp, eoff = OracleIndex(ix.n, 91, ix.rows, ix.C, ix.lcs).encode(reads[: m * L], offs[: m + 1])
+    assert np.array_equal(recs[: int(roff[m])], exp)
+    ctx.close()
