@@ -3,9 +3,9 @@
 
 Per workload and kernel, the mean per launch of:
   read_bytes   = 32 * TCC_EA0_RDREQ_32B + 64 * TCC_EA0_RDREQ_64B + 128 * TCC_EA0_RDREQ_128B
-                 (every L2->fabric read request at its own size: random 64 B lines count once,
-                 128 B streaming requests twice -- the gfx950 FETCH_SIZE half-count the guide
-                 describes is the 128 B requests tallied at 64 B)
+                 (every L2->fabric read request at its own size; on gfx950 random 4..16 B loads
+                 and streaming loads alike go out as 128 B requests -- the FETCH_SIZE half-count
+                 the guide describes is those 128 B requests tallied at 64 B through TCC_BUBBLE = 0)
   write_bytes  = 32 * (TCC_EA0_WRREQ - TCC_EA0_WRREQ_64B) + 64 * TCC_EA0_WRREQ_64B (= WRITE_SIZE)
   dram_read_bytes = 32 * TCC_EA0_RDREQ_DRAM_32B
   fetch_size_bytes = the rocprofv3 FETCH_SIZE expression for gfx950 from the same counters
@@ -78,6 +78,8 @@ def main():
 
     # ---- kernel durations per workload from the kernel trace of the default command ----
     kt = rows(os.path.join(a.prof_dir, "kt", "**", "*kernel_trace.csv"))
+    if not kt:  # an incomplete profile must not replace the committed counters
+        sys.exit(f"no kernel trace under {a.prof_dir}/kt: nothing written")
     kt.sort(key=lambda r: int(r["Start_Timestamp"]))
     seq = defaultdict(list)
     for r in kt:
@@ -158,6 +160,8 @@ def main():
                   f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['MinNs']) / 1e3:.1f} | {float(r['MaxNs']) / 1e3:.1f} | "
                   f"{float(r['Percentage']):.1f} |")
     md += ["", "Per-workload trace averages (dispatch order split):", "", "```json", json.dumps(dur, indent=1), "```"]
+    if not all(out["workloads"].get(w, {}).get("kernels") for w in ("C91", "D91")):
+        sys.exit("counter passes missing for C91/D91: nothing written")
     json.dump(out, open(a.out_json, "w"), indent=1)
     open(a.out_md, "w").write("\n".join(md) + "\n")
     print("\n".join(md))
