@@ -1,9 +1,10 @@
 // FASTA / FASTQ ingest for the CLI (include/ntcomp_host.h "FASTX").
 //
 // Replaces needletail::parse_fastx_file + SequenceRecord::normalize(true) as the reference
-// uses them (src/main.rs:51-62 build input, :158-163 encode input): plain, gzip, bzip2 or
-// xz input, detected from the magic bytes like needletail's niffler (zlib's gz* reads plain
-// and gzip; bzip2 and xz go through libbz2.so.1 / liblzma.so.5, loaded at run time -- the
+// uses them (src/main.rs:51-62 build input, :158-163 encode input): plain, gzip, bzip2,
+// xz or zstd input, detected from the magic bytes like needletail's niffler (zlib's gz* reads
+// plain and gzip; bzip2, xz and zstd go through libbz2.so.1 / liblzma.so.5 / libzstd.so.1,
+// loaded at run time -- the
 // image has their runtime libraries but no headers, so the few stable entry points and
 // stream structs used are declared below), FASTA records (">" header, sequence over any number of lines)
 // and FASTQ records ("@" header, sequence, "+", quality).  normalize(iupac = true) is
@@ -218,6 +219,50 @@ struct XzCodec {
     }
 };
 
+// libzstd (zstd.h streaming ABI, stable since 1.0): concatenated frames decode one after
+// another through the same stream
+struct ZstdIn {
+    const void *src;
+    size_t size, pos;
+};
+struct ZstdOut {
+    void *dst;
+    size_t size, pos;
+};
+struct ZstdCodec {
+    void *(*create_fn)() = nullptr;
+    size_t (*free_fn)(void *) = nullptr;
+    size_t (*dec_fn)(void *, ZstdOut *, ZstdIn *) = nullptr;
+    unsigned (*is_error)(size_t) = nullptr;
+    void *ds = nullptr;
+    ZstdIn zi{nullptr, 0, 0};
+    ZstdOut zo{nullptr, 0, 0};
+    bool init() {
+        void *h = dlopen("libzstd.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return false;
+        create_fn = (void *(*)())dlsym(h, "ZSTD_createDStream");
+        free_fn = (size_t(*)(void *))dlsym(h, "ZSTD_freeDStream");
+        dec_fn = (size_t(*)(void *, ZstdOut *, ZstdIn *))dlsym(h, "ZSTD_decompressStream");
+        is_error = (unsigned (*)(size_t))dlsym(h, "ZSTD_isError");
+        if (!create_fn || !free_fn || !dec_fn || !is_error) return false;
+        ds = create_fn();  // a new DStream starts a frame without ZSTD_initDStream
+        return ds != nullptr;
+    }
+    void end() {
+        if (ds) free_fn(ds);
+        ds = nullptr;
+    }
+    void set_in(char *p, size_t n) { zi = ZstdIn{p, n, 0}; }
+    void set_out(char *p, unsigned n) { zo = ZstdOut{p, n, 0}; }
+    size_t in_left() const { return zi.size - zi.pos; }
+    unsigned out_left() const { return (unsigned)(zo.size - zo.pos); }
+    int step(bool) {  // 0 progress, 1 a frame ended, -1 error
+        const size_t rc = dec_fn(ds, &zo, &zi);
+        if (is_error(rc)) return -1;
+        return rc == 0 ? 1 : 0;
+    }
+};
+
 // the reader for a path, by its first bytes; *rc = NTC_ERR_IO / NTC_ERR_UNSUPPORTED on failure
 ByteReader *open_reader(const char *path, int *rc) {
     unsigned char m[6] = {0};
@@ -238,9 +283,9 @@ ByteReader *open_reader(const char *path, int *rc) {
         if (!x->ok) { delete x; *rc = NTC_ERR_UNSUPPORTED; return nullptr; }
         r = x;
     } else if (got >= 4 && m[0] == 0x28 && m[1] == 0xB5 && m[2] == 0x2F && m[3] == 0xFD) {
-        std::fclose(f);  // zstd: no library in the image
-        *rc = NTC_ERR_UNSUPPORTED;
-        return nullptr;
+        auto *z = new StreamReader<ZstdCodec>(f);
+        if (!z->ok) { delete z; *rc = NTC_ERR_UNSUPPORTED; return nullptr; }
+        r = z;
     } else {
         std::fclose(f);
         gzFile g = gzopen(path, "rb");

@@ -77,7 +77,7 @@ def _normalize(seq):
 
 
 @pytest.mark.parametrize("fmt", ["fasta", "fastq"])
-@pytest.mark.parametrize("gz", [False, True, "bz2", "xz"])
+@pytest.mark.parametrize("gz", [False, True, "bz2", "xz", "zst"])
 def test_fastx_random_records_across_chunks(tmp_path, fmt, gz):
     """Records of up to 3 Mbp with mixed case, IUPAC, junk bytes and CRLF endings, spread
     over several 8 MiB input chunks: every record's bases equal the restated normalize."""
@@ -100,7 +100,7 @@ def test_fastx_random_records_across_chunks(tmp_path, fmt, gz):
             expect[-1] = _normalize(seq)
             parts.append(b"@r%d%s%s%s+%s%s%s" % (i, eol, seq, eol, eol, b"I" * L, eol))
     data = b"".join(parts)
-    path = tmp_path / ("x." + fmt + {False: "", True: ".gz", "bz2": ".bz2", "xz": ".xz"}[gz])
+    path = tmp_path / ("x." + fmt + {False: "", True: ".gz", "bz2": ".bz2", "xz": ".xz", "zst": ".zst"}[gz])
     if gz is True:
         with gzip.open(path, "wb", compresslevel=1) as f:
             f.write(data)
@@ -111,6 +111,9 @@ def test_fastx_random_records_across_chunks(tmp_path, fmt, gz):
     elif gz == "xz":
         import lzma
         path.write_bytes(lzma.compress(data, preset=0))
+    elif gz == "zst":  # two concatenated frames, decoded back to back
+        h = len(data) // 2
+        path.write_bytes(_zstd_compress(data[:h]) + _zstd_compress(data[h:]))
     else:
         path.write_bytes(data)
     got = []
@@ -120,9 +123,25 @@ def test_fastx_random_records_across_chunks(tmp_path, fmt, gz):
     assert got == expect
 
 
-def test_fastx_truncated_and_unsupported_compression(tmp_path):
-    """needletail/niffler-style detection by magic bytes: a truncated bzip2 stream is an I/O
-    error, a zstd file (no libzstd in the image) is NTC_ERR_UNSUPPORTED, never garbage."""
+def _zstd_compress(data, level=1):
+    """one zstd frame through the image's libzstd.so.1 (test helper; no zstd module or CLI here)"""
+    import ctypes
+    z = ctypes.CDLL("libzstd.so.1")
+    z.ZSTD_compressBound.restype = ctypes.c_size_t
+    z.ZSTD_compressBound.argtypes = [ctypes.c_size_t]
+    z.ZSTD_compress.restype = ctypes.c_size_t
+    z.ZSTD_compress.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int]
+    z.ZSTD_isError.argtypes = [ctypes.c_size_t]
+    cap = z.ZSTD_compressBound(len(data))
+    buf = ctypes.create_string_buffer(cap)
+    n = z.ZSTD_compress(buf, cap, data, len(data), level)
+    assert not z.ZSTD_isError(n)
+    return buf.raw[:n]
+
+
+def test_fastx_truncated_and_corrupt_compression(tmp_path):
+    """needletail/niffler-style detection by magic bytes: a truncated bzip2 or zstd stream and
+    a corrupt zstd frame are I/O errors, never garbage."""
     import bz2
     data = b"".join(b"@r%d\nACGTACGTAC\n+\nIIIIIIIIII\n" % i for i in range(20000))
     (tmp_path / "t.fq.bz2").write_bytes(bz2.compress(data)[:-200])
@@ -130,10 +149,13 @@ def test_fastx_truncated_and_unsupported_compression(tmp_path):
         for _ in nt.FastxReader(str(tmp_path / "t.fq.bz2")):
             pass
     assert e.value.code == 9
+    (tmp_path / "t.fq.zst").write_bytes(_zstd_compress(data)[:-50])
     (tmp_path / "z.fq.zst").write_bytes(bytes([0x28, 0xB5, 0x2F, 0xFD]) + b"\0" * 64)
-    with pytest.raises(nt.NtcError) as e:
-        nt.FastxReader(str(tmp_path / "z.fq.zst"))
-    assert e.value.code == 10
+    for name in ("t.fq.zst", "z.fq.zst"):
+        with pytest.raises(nt.NtcError) as e:
+            for _ in nt.FastxReader(str(tmp_path / name)):
+                pass
+        assert e.value.code == 9
 
 
 def test_fasta_format():
