@@ -263,6 +263,95 @@ struct ZstdCodec {
     }
 };
 
+// gzip through libdeflate (libdeflate.so.0, ~4x zlib's inflate rate on this image): whole
+// members at once, so the compressed file is read into memory and each member inflates into
+// one buffer (a BGZF member's size is in its header; otherwise the output size is guessed
+// from the last ISIZE, mod 2^32, and grown on LIBDEFLATE_INSUFFICIENT_SPACE).  Used for
+// files up to kDeflateMaxFile compressed bytes; larger ones stream through zlib.
+constexpr uint64_t kDeflateMaxFile = 2ull << 30;
+struct DeflateReader : ByteReader {
+    void *(*alloc_fn)() = nullptr;
+    void (*free_fn)(void *) = nullptr;
+    int (*gz_fn)(void *, const void *, size_t, void *, size_t, size_t *, size_t *) = nullptr;
+    void *dec = nullptr;
+    std::vector<unsigned char> comp;
+    size_t ci = 0;  // next member
+    char *out = nullptr;
+    size_t out_n = 0, out_pos = 0, cap = 0;
+    bool ok = false;
+    DeflateReader(FILE *f, uint64_t size) {
+        void *h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+        if (h) {
+            alloc_fn = (void *(*)())dlsym(h, "libdeflate_alloc_decompressor");
+            free_fn = (void (*)(void *))dlsym(h, "libdeflate_free_decompressor");
+            gz_fn = (int (*)(void *, const void *, size_t, void *, size_t, size_t *, size_t *))dlsym(
+                h, "libdeflate_gzip_decompress_ex");
+        }
+        if (alloc_fn && free_fn && gz_fn && (dec = alloc_fn())) {
+            comp.resize(size);
+            ok = std::fread(comp.data(), 1, size, f) == size;
+        }
+        std::fclose(f);
+    }
+    ~DeflateReader() override {
+        if (dec) free_fn(dec);
+        std::free(out);
+    }
+    static uint32_t le32(const unsigned char *p) { return p[0] | p[1] << 8 | p[2] << 16 | (uint32_t)p[3] << 24; }
+    // the member at ci into out: 1 done, 0 no member left, -1 error
+    int next_member() {
+        const size_t left = comp.size() - ci;
+        if (left == 0) return 0;
+        const unsigned char *m = comp.data() + ci;
+        if (left < 18 || m[0] != 0x1F || m[1] != 0x8B) return -1;
+        uint64_t want;
+        if ((m[3] & 4) && left >= 18 && m[12] == 'B' && m[13] == 'C' && le32(m + 10) >= 6) {
+            const size_t bsize = (size_t)(m[16] | m[17] << 8) + 1;  // BGZF: the member's size
+            if (bsize > left || bsize < 26) return -1;
+            want = le32(m + bsize - 4);
+        } else {
+            // the last member's ISIZE + j 2^32 >= what is left (inflated >= its input - headers)
+            want = le32(comp.data() + comp.size() - 4);
+            while (want + 64 < left) want += 1ull << 32;
+        }
+        for (;;) {
+            if (want + 1 > cap) {
+                std::free(out);
+                cap = want + 1;
+                out = (char *)std::malloc(cap);
+                if (!out) return -1;
+            }
+            size_t in_used = 0, got = 0;
+            const int rc = gz_fn(dec, m, left, out, cap, &in_used, &got);
+            if (rc == 0) {
+                ci += in_used;
+                out_n = got;
+                out_pos = 0;
+                return 1;
+            }
+            // 3 = INSUFFICIENT_SPACE (a multi-member file's earlier, larger member): grow
+            if (rc != 3 || want > (uint64_t)left * 1100 + (1u << 20)) return -1;
+            want = want * 2 + (1u << 20);
+        }
+    }
+    int read(char *dst, unsigned n) override {  // fills dst across (BGZF's 64 KB) members
+        unsigned done = 0;
+        while (done < n) {
+            if (out_pos == out_n) {
+                const int rc = next_member();
+                if (rc < 0) return -1;
+                if (rc == 0) break;
+                continue;
+            }
+            const size_t t = std::min<size_t>(n - done, out_n - out_pos);
+            std::memcpy(dst + done, out + out_pos, t);
+            out_pos += t;
+            done += (unsigned)t;
+        }
+        return (int)done;
+    }
+};
+
 // the reader for a path, by its first bytes; *rc = NTC_ERR_IO / NTC_ERR_UNSUPPORTED on failure
 ByteReader *open_reader(const char *path, int *rc) {
     unsigned char m[6] = {0};
@@ -287,7 +376,18 @@ ByteReader *open_reader(const char *path, int *rc) {
         if (!z->ok) { delete z; *rc = NTC_ERR_UNSUPPORTED; return nullptr; }
         r = z;
     } else {
-        std::fclose(f);
+        if (got >= 3 && m[0] == 0x1F && m[1] == 0x8B && m[2] == 8) {
+            std::fseek(f, 0, SEEK_END);
+            const long size = std::ftell(f);
+            std::rewind(f);
+            if (size > 0 && (uint64_t)size <= kDeflateMaxFile && !std::getenv("NTC_FASTX_ZLIB")) {
+                auto *d = new DeflateReader(f, (uint64_t)size);  // closes f
+                if (d->ok) return d;
+                delete d;
+                f = nullptr;
+            }
+        }
+        if (f) std::fclose(f);
         gzFile g = gzopen(path, "rb");
         if (!g) {
             *rc = NTC_ERR_IO;

@@ -77,8 +77,8 @@ def _normalize(seq):
 
 
 @pytest.mark.parametrize("fmt", ["fasta", "fastq"])
-@pytest.mark.parametrize("gz", [False, True, "bz2", "xz", "zst"])
-def test_fastx_random_records_across_chunks(tmp_path, fmt, gz):
+@pytest.mark.parametrize("gz", [False, True, "bz2", "xz", "zst", "bgzf", "gzmulti", "gzlib"])
+def test_fastx_random_records_across_chunks(tmp_path, monkeypatch, fmt, gz):
     """Records of up to 3 Mbp with mixed case, IUPAC, junk bytes and CRLF endings, spread
     over several 8 MiB input chunks: every record's bases equal the restated normalize."""
     rng = np.random.default_rng(7 if fmt == "fasta" else 8)
@@ -100,10 +100,18 @@ def test_fastx_random_records_across_chunks(tmp_path, fmt, gz):
             expect[-1] = _normalize(seq)
             parts.append(b"@r%d%s%s%s+%s%s%s" % (i, eol, seq, eol, eol, b"I" * L, eol))
     data = b"".join(parts)
-    path = tmp_path / ("x." + fmt + {False: "", True: ".gz", "bz2": ".bz2", "xz": ".xz", "zst": ".zst"}[gz])
-    if gz is True:
+    path = tmp_path / ("x." + fmt + {False: "", True: ".gz", "bz2": ".bz2", "xz": ".xz", "zst": ".zst", "bgzf": ".gz",
+                                         "gzmulti": ".gz", "gzlib": ".gz"}[gz])
+    if gz is True or gz == "gzlib":  # libdeflate whole-member path; gzlib: zlib's streaming path
         with gzip.open(path, "wb", compresslevel=1) as f:
             f.write(data)
+        if gz == "gzlib":
+            monkeypatch.setenv("NTC_FASTX_ZLIB", "1")
+    elif gz == "bgzf":  # BGZF (bgzip): members of <= 64 KB with the BC extra field
+        path.write_bytes(b"".join(_bgzf_member(data[i:i + 65280]) for i in range(0, len(data), 65280)))
+    elif gz == "gzmulti":  # concatenated members, the first larger than the last (output size grows)
+        h = len(data) * 9 // 10
+        path.write_bytes(gzip.compress(data[:h], 1) + gzip.compress(data[h:], 1))
     elif gz == "bz2":  # two concatenated streams (pbzip2-style), decoded back to back
         import bz2
         h = len(data) // 2
@@ -121,6 +129,16 @@ def test_fastx_random_records_across_chunks(tmp_path, fmt, gz):
         got += [b[int(o[r]):int(o[r + 1])].tobytes() for r in range(len(o) - 1)]
     assert len(got) == len(expect)
     assert got == expect
+
+
+def _bgzf_member(chunk):
+    import struct
+    import zlib
+    c = zlib.compressobj(1, zlib.DEFLATED, -15)
+    body = c.compress(chunk) + c.flush()
+    bsize = 18 + len(body) + 8
+    hdr = b"\x1f\x8b\x08\x04" + b"\0" * 4 + b"\x00\xff" + struct.pack("<H", 6) + b"BC" + struct.pack("<HH", 2, bsize - 1)
+    return hdr + body + struct.pack("<II", zlib.crc32(chunk), len(chunk))
 
 
 def _zstd_compress(data, level=1):
@@ -151,7 +169,9 @@ def test_fastx_truncated_and_corrupt_compression(tmp_path):
     assert e.value.code == 9
     (tmp_path / "t.fq.zst").write_bytes(_zstd_compress(data)[:-50])
     (tmp_path / "z.fq.zst").write_bytes(bytes([0x28, 0xB5, 0x2F, 0xFD]) + b"\0" * 64)
-    for name in ("t.fq.zst", "z.fq.zst"):
+    (tmp_path / "t.fq.gz").write_bytes(gzip.compress(data)[:-100])
+    (tmp_path / "c.fq.gz").write_bytes(gzip.compress(data)[:-8] + b"\0" * 8)  # bad CRC / ISIZE
+    for name in ("t.fq.zst", "z.fq.zst", "t.fq.gz", "c.fq.gz"):
         with pytest.raises(nt.NtcError) as e:
             for _ in nt.FastxReader(str(tmp_path / name)):
                 pass
