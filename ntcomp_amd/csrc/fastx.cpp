@@ -295,19 +295,79 @@ struct DeflateReader : ByteReader {
     }
     ~DeflateReader() override {
         if (dec) free_fn(dec);
+        for (void *d : pool) free_fn(d);
         std::free(out);
     }
     static uint32_t le32(const unsigned char *p) { return p[0] | p[1] << 8 | p[2] << 16 | (uint32_t)p[3] << 24; }
+    // BGZF member at m (left bytes on): its size, or 0 when it is not one
+    static size_t bgzf_size(const unsigned char *m, size_t left) {
+        if (left < 26 || m[0] != 0x1F || m[1] != 0x8B || !(m[3] & 4) || (m[10] | m[11] << 8) < 6 || m[12] != 'B' ||
+            m[13] != 'C')
+            return 0;
+        const size_t bsize = (size_t)(m[16] | m[17] << 8) + 1;
+        return bsize >= 26 && bsize <= left ? bsize : 0;
+    }
+    // BGZF: the next run of up to kBatch members, inflated in parallel into out at the offsets
+    // their ISIZE trailers give (bgzip's 64 KB members are independent).  1 done, 0 not BGZF here
+    // (or a single member), -1 error
+    static constexpr size_t kBatch = 256;
+    std::vector<void *> pool;
+    int next_bgzf_batch() {
+        std::vector<size_t> at, sz, off(1, 0);
+        size_t c = ci;
+        while (at.size() < kBatch && c < comp.size()) {
+            const size_t b = bgzf_size(comp.data() + c, comp.size() - c);
+            if (!b) break;
+            at.push_back(c);
+            sz.push_back(b);
+            off.push_back(off.back() + le32(comp.data() + c + b - 4));
+            c += b;
+        }
+        if (at.size() < 2) return 0;
+        if (off.back() + 1 > cap) {
+            std::free(out);
+            cap = std::max<size_t>(off.back() + 1, kBatch << 16);
+            out = (char *)std::malloc(cap);
+            if (!out) return -1;
+        }
+        const unsigned T = std::max(1u, std::min<unsigned>(8, std::thread::hardware_concurrency()));
+        while (pool.size() < T) {
+            void *d = alloc_fn();
+            if (!d) return -1;
+            pool.push_back(d);
+        }
+        bool bad = false;
+        std::mutex mu;
+        auto work = [&](unsigned t) {
+            for (size_t i = t; i < at.size(); i += T) {
+                size_t used = 0, got = 0;
+                const int rc = gz_fn(pool[t], comp.data() + at[i], sz[i], out + off[i], off[i + 1] - off[i], &used, &got);
+                if (rc != 0 || used != sz[i] || got != off[i + 1] - off[i]) {
+                    std::lock_guard<std::mutex> g(mu);
+                    bad = true;
+                }
+            }
+        };
+        std::vector<std::thread> th;
+        for (unsigned t = 1; t < T; t++) th.emplace_back(work, t);
+        work(0);
+        for (auto &x : th) x.join();
+        if (bad) return -1;
+        ci = c;
+        out_n = off.back();
+        out_pos = 0;
+        return 1;
+    }
     // the member at ci into out: 1 done, 0 no member left, -1 error
     int next_member() {
         const size_t left = comp.size() - ci;
         if (left == 0) return 0;
+        const int rb = next_bgzf_batch();
+        if (rb != 0) return rb;
         const unsigned char *m = comp.data() + ci;
         if (left < 18 || m[0] != 0x1F || m[1] != 0x8B) return -1;
         uint64_t want;
-        if ((m[3] & 4) && left >= 18 && m[12] == 'B' && m[13] == 'C' && le32(m + 10) >= 6) {
-            const size_t bsize = (size_t)(m[16] | m[17] << 8) + 1;  // BGZF: the member's size
-            if (bsize > left || bsize < 26) return -1;
+        if (const size_t bsize = bgzf_size(m, left)) {  // BGZF: the member's size, its ISIZE exact
             want = le32(m + bsize - 4);
         } else {
             // the last member's ISIZE + j 2^32 >= what is left (inflated >= its input - headers)
