@@ -1,22 +1,23 @@
 #!/usr/bin/env python3
-"""Per-arm kernel durations and counters from scripts/ab_sq.sh output."""
-import collections, csv, glob, os, sys
+"""summary of scripts/ab_run.sh results: step and dominant-kernel ms per build and run"""
+import glob
+import json
+import os
+import sys
+
 d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/ab"
-for i in range(1, 20):
-    if not os.path.exists(f"{d}/arm{i}.json"):
-        break
-    agg = collections.defaultdict(lambda: collections.defaultdict(list))
-    dur = collections.defaultdict(list)
-    for f in glob.glob(f"{d}/pmc{i}/*counter_collection.csv") + glob.glob(f"{d}/tcc{i}/*counter_collection.csv"):
-        for r in csv.DictReader(open(f)):
-            kn = r["Kernel_Name"].split("(")[0].replace("ntc::", "")
-            agg[kn][r["Counter_Name"]].append(float(r["Counter_Value"]))
-            if "pmc" in f:
-                dur[kn].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
-    print(f"arm{i}: {open(f'{d}/arm{i}.json').read()[:0]}")
-    for kn, cs in agg.items():
-        row = {c: sum(v) / len(v) for c, v in cs.items()}
-        hit = row.get("TCC_HIT_sum"), row.get("TCC_MISS_sum")
-        hr = hit[0] / (hit[0] + hit[1]) if None not in hit and sum(hit) else None
-        print(f"  {kn:10s} {sum(dur[kn])/max(1,len(dur[kn])):7.3f} ms  VALU {row.get('SQ_INSTS_VALU',0):.3g}  "
-              f"RDREQ {row.get('TCC_EA0_RDREQ_sum',0):.3g}  L2hit {hr if hr is None else round(hr,3)}")
+for f in sorted(glob.glob(os.path.join(d, "*.json"))):
+    try:
+        j = json.loads(open(f).read().strip().splitlines()[-1])
+    except Exception as e:  # noqa: BLE001
+        print(os.path.basename(f), "unreadable", e)
+        continue
+    out = [os.path.basename(f)]
+    if "ms_per_step" in j and j.get("config", {}).get("workload", "").startswith("C"):
+        out.append(f"C step {j['ms_per_step']:.3f} k {j['roofline'].get('kernel_ms')}")
+    if "decode" in j:
+        out.append(f"D step {j['decode']['ms_per_step']:.3f} k {j['decode']['roofline'].get('kernel_ms')}")
+    s = j.get("strains")
+    if s:
+        out.append(f"S step {s['ms_per_step']:.3f} k {s['roofline'].get('kernel_ms')}")
+    print(" | ".join(out))

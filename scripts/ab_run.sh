@@ -1,8 +1,16 @@
+# alternating A/B of device builds: bash scripts/ab_run.sh "<configs>" lib1 lib2 ...  (lib "cur" = the in-tree build)
 set -e
 mkdir -p gpurun_out/ab
-B="python -u bench.py --configs encode,strains --no-cpu --steps 10 --warmup 3"
+CFG=${1:-encode,strains}
+shift
+B="python -u bench.py --configs $CFG --no-cpu --steps 10 --warmup 3"
 for i in 1 2; do
-  timeout -k 10 200 $B > gpurun_out/ab/new$i.json 2> gpurun_out/ab/new$i.err
-  NTC_GPU_LIB=ntcomp_amd/ab/libprev.so timeout -k 10 200 $B > gpurun_out/ab/old$i.json 2> gpurun_out/ab/old$i.err
+  for L in "$@"; do
+    n=$(basename $L .so)
+    if [ "$L" = cur ]; then
+      timeout -k 10 300 $B > gpurun_out/ab/$n.$i.json 2> gpurun_out/ab/$n.$i.err
+    else
+      NTC_GPU_LIB=$L timeout -k 10 300 $B > gpurun_out/ab/$n.$i.json 2> gpurun_out/ab/$n.$i.err
+    fi
+  done
 done
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/ab/gpu_tests.log 2>&1
