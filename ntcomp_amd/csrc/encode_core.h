@@ -826,7 +826,12 @@ struct MsBufs {
     Entry *E;
     Entry *Ed;    // dense entry slots (ent_ptr): entry j < kEntSlot of read rid at Ed[rid + j * es]
     uint64_t es;
+    uint4 *stage = nullptr;  // k_ms4: the block's LDS write-combining slots (MsLane::put_entry)
 };
+#ifndef NTC_ECOMB
+#define NTC_ECOMB 1  // combine a read's spilled entries into 64-byte groups in LDS before storing
+#endif
+constexpr uint32_t kStageSlots = 4;  // 64 B: one write request instead of four 16 B partial ones
 
 struct MsLane {
     uint64_t qo;        // this read starts at character qo of Q; its entries at E + qo
@@ -862,8 +867,41 @@ struct MsLane {
         return (qw >> (2 * (x + 1 - U - qb))) & ((1ULL << (2 * U)) - 1);
     }
     NTC_HD void put_entry(const MsBufs &b, uint32_t p_, uint32_t v, uint32_t m, uint32_t dk) {
+#if defined(__HIP_DEVICE_COMPILE__) && NTC_ECOMB
+        // Spilled entries of one read are consecutive 16 B slots E[qo + ne], written one per
+        // lane iteration; stored one by one, each became its own 32 B partial write request
+        // past L2 (S91: 60 per read, 38 % of k_ms4's requests).  They are collected per
+        // aligned 64-byte group in LDS and stored together, so L2 sends one 64 B request.
+        if (ne >= kEntSlot) {
+            const uint64_t at = qo + ne;
+            const uint32_t t = threadIdx.x;
+            b.stage[(uint32_t)(at & (kStageSlots - 1)) * 256 + t] = make_uint4(p_, v, m, dk);
+            ne++;
+            if ((at & (kStageSlots - 1)) == kStageSlots - 1) flush_stage(b);
+            return;
+        }
+#endif
         store_entry(ne < kEntSlot ? b.Ed + rid : b.E + qo, ne < kEntSlot ? (uint64_t)ne * b.es : ne, p_, v, m, dk);
         ne++;
+    }
+    // the staged entries of the group holding entry ne - 1 (at the end of a group or of the read)
+    NTC_HD void flush_stage(const MsBufs &b) {
+#if defined(__HIP_DEVICE_COMPILE__) && NTC_ECOMB
+        if (ne <= kEntSlot) return;
+        const uint64_t last = qo + ne - 1, first = qo + kEntSlot;
+        const uint64_t g = last & ~(uint64_t)(kStageSlots - 1);
+        const uint32_t t = threadIdx.x;
+#pragma unroll
+        for (uint32_t i = 0; i < kStageSlots; i++) {
+            const uint64_t at = g + i;
+            if (at >= first && at <= last) {
+                const uint4 x = b.stage[i * 256 + t];
+                store_entry(b.E, at, x.x, x.y, x.z, x.w);
+            }
+        }
+#else
+        (void)b;
+#endif
     }
     // after a commit: look for the path position of a single-node interval
     NTC_HD void note_single(const DevIndex &ix) {

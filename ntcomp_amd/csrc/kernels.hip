@@ -195,7 +195,8 @@ __global__ __launch_bounds__(256, NTC_MS_WAVES) void k_ms4(Enc4Args a) {
     bool exhausted = false, idle = true;
     uint64_t rd = 0;
     const WaveQueue wq(a.counter, a.n_reads);
-    const MsBufs bufs{a.Q, a.E, a.Ed, a.n_reads};
+    __shared__ uint4 s_stage[kStageSlots * 256];  // MsLane::put_entry write combining
+    const MsBufs bufs{a.Q, a.E, a.Ed, a.n_reads, s_stage};
     MsLane st;
     for (;;) {
         // ---- hand idle lanes the next reads (wave-uniform control flow) ----------------
@@ -229,6 +230,7 @@ __global__ __launch_bounds__(256, NTC_MS_WAVES) void k_ms4(Enc4Args a) {
                     atomicMin(a.status, (unsigned long long)((rd << 8) | (uint64_t)(-rc)));
                     a.ne[rd] = 0;
                 } else {
+                    st.flush_stage(bufs);
                     a.ne[rd] = st.ne;
                 }
                 idle = true;
