@@ -832,6 +832,12 @@ struct MsBufs {
 #define NTC_ECOMB 1  // combine a read's spilled entries into 64-byte groups in LDS before storing
 #endif
 constexpr uint32_t kStageSlots = 4;  // 64 B: one write request instead of four 16 B partial ones
+// k_ms4 keeps a read's entry 0 in LDS too and stores it when the read is done, with the read's
+// entry count in bits 8..30 of its dk (d is 8 bits, bit 31 the run tag): the separate 4-byte
+// count store per read (a partial write request of its own) is needed only for counts
+// >= kNeInE0 (read_entry_count)
+constexpr uint32_t kNeInE0 = 0x7FFFFFu;
+NTC_HD uint32_t entry0_count(const Entry &e0) { return (e0.dk >> 8) & kNeInE0; }
 
 struct MsLane {
     uint64_t qo;        // this read starts at character qo of Q; its entries at E + qo
@@ -872,12 +878,17 @@ struct MsLane {
         // lane iteration; stored one by one, each became its own 32 B partial write request
         // past L2 (S91: 60 per read, 38 % of k_ms4's requests).  They are collected per
         // aligned 64-byte group in LDS and stored together, so L2 sends one 64 B request.
+        const uint32_t t = threadIdx.x;
         if (ne >= kEntSlot) {
             const uint64_t at = qo + ne;
-            const uint32_t t = threadIdx.x;
             b.stage[(uint32_t)(at & (kStageSlots - 1)) * 256 + t] = make_uint4(p_, v, m, dk);
             ne++;
             if ((at & (kStageSlots - 1)) == kStageSlots - 1) flush_stage(b);
+            return;
+        }
+        if (ne == 0) {  // entry 0 waits for the count (finish)
+            b.stage[kStageSlots * 256 + t] = make_uint4(p_, v, m, dk);
+            ne++;
             return;
         }
 #endif
@@ -901,6 +912,20 @@ struct MsLane {
         }
 #else
         (void)b;
+#endif
+    }
+    // the read is done: staged entries out, entry 0 with the count; true when the count does
+    // not fit entry 0 and goes to the count array instead
+    NTC_HD bool finish(const MsBufs &b) {
+#if defined(__HIP_DEVICE_COMPILE__) && NTC_ECOMB
+        flush_stage(b);
+        const uint4 x = ne ? b.stage[kStageSlots * 256 + threadIdx.x] : make_uint4(0, 0, 0, 0);
+        const uint32_t c = ne < kNeInE0 ? ne : kNeInE0;
+        store_entry(b.Ed + rid, 0, x.x, x.y, x.z, (x.w & ~(kNeInE0 << 8)) | (c << 8));
+        return c == kNeInE0;
+#else
+        (void)b;
+        return true;
 #endif
     }
     // after a commit: look for the path position of a single-node interval
