@@ -666,10 +666,11 @@ NTC_HD Entry load_entry(const Entry *E, int32_t i) {
 #endif
 }
 
-// Entry j of a read: j < kEntSlot in the dense slots Ed[j * es] (the kernels interleave the
-// reads' first entries, Ed = base + read id, es = reads in the batch: a wave's lanes write
-// and read neighbouring 16-byte slots, so lines are shared instead of one line per read),
-// later ones at E[j] (position space).  Ed = E, es = 1 is the plain contiguous layout.
+// Entry j of a read: j < kEntSlot in the dense slots Ed[j * es] (the kernels keep each read's
+// first entries together, Ed = base + read id * kEntSlot, es = 1: k_ms4 writes them as one
+// 64-byte group when the read ends, MsLane::finish, and the parse finds a read's first
+// entries in one line), later ones at E[j] (position space).  Ed = E is the plain
+// contiguous layout.
 constexpr uint32_t kEntSlot = 4;
 NTC_HD const Entry *ent_ptr(const Entry *E, const Entry *Ed, uint64_t es, uint32_t j) {
     return j < kEntSlot ? Ed + (uint64_t)j * es : E + j;
@@ -824,9 +825,10 @@ NTC_HD void store_entry(Entry *E, uint64_t i, uint32_t p, uint32_t v, uint32_t m
 struct MsBufs {
     const uint64_t *Q;
     Entry *E;
-    Entry *Ed;    // dense entry slots (ent_ptr): entry j < kEntSlot of read rid at Ed[rid + j * es]
+    Entry *Ed;    // dense entry slots (ent_ptr): entry j < kEntSlot of read rid at Ed[rid * ds + j * es]
     uint64_t es;
     uint4 *stage = nullptr;  // k_ms4: the block's LDS write-combining slots (MsLane::put_entry)
+    uint64_t ds = 1;
 };
 #ifndef NTC_ECOMB
 #define NTC_ECOMB 1  // combine a read's spilled entries into 64-byte groups in LDS before storing
@@ -878,21 +880,33 @@ struct MsLane {
         // lane iteration; stored one by one, each became its own 32 B partial write request
         // past L2 (S91: 60 per read, 38 % of k_ms4's requests).  They are collected per
         // aligned 64-byte group in LDS and stored together, so L2 sends one 64 B request.
+        // The dense slots of a read are one 64-byte group too (k_ms4 lays them out read-major,
+        // Ed[rid * kEntSlot + j]): staged until the read ends, or until its first spilled
+        // entry, when entries 1..3 go out and entry 0 moves to slot kStageSlots to wait for
+        // the count (finish).
+        static_assert(kEntSlot == kStageSlots, "dense slots and staging groups share the LDS slots");
         const uint32_t t = threadIdx.x;
-        if (ne >= kEntSlot) {
-            const uint64_t at = qo + ne;
-            b.stage[(uint32_t)(at & (kStageSlots - 1)) * 256 + t] = make_uint4(p_, v, m, dk);
-            ne++;
-            if ((at & (kStageSlots - 1)) == kStageSlots - 1) flush_stage(b);
-            return;
-        }
-        if (ne == 0) {  // entry 0 waits for the count (finish)
-            b.stage[kStageSlots * 256 + t] = make_uint4(p_, v, m, dk);
+        if (ne < kEntSlot) {
+            b.stage[ne * 256 + t] = make_uint4(p_, v, m, dk);
             ne++;
             return;
         }
+        if (ne == kEntSlot) {
+            Entry *dst = b.Ed + rid * b.ds;
+#pragma unroll
+            for (uint32_t i = 1; i < kEntSlot; i++) {
+                const uint4 x = b.stage[i * 256 + t];
+                store_entry(dst, (uint64_t)i * b.es, x.x, x.y, x.z, x.w);
+            }
+            b.stage[kStageSlots * 256 + t] = b.stage[t];
+        }
+        const uint64_t at = qo + ne;
+        b.stage[(uint32_t)(at & (kStageSlots - 1)) * 256 + t] = make_uint4(p_, v, m, dk);
+        ne++;
+        if ((at & (kStageSlots - 1)) == kStageSlots - 1) flush_stage(b);
+        return;
 #endif
-        store_entry(ne < kEntSlot ? b.Ed + rid : b.E + qo, ne < kEntSlot ? (uint64_t)ne * b.es : ne, p_, v, m, dk);
+        store_entry(ne < kEntSlot ? b.Ed + rid * b.ds : b.E + qo, ne < kEntSlot ? (uint64_t)ne * b.es : ne, p_, v, m, dk);
         ne++;
     }
     // the staged entries of the group holding entry ne - 1 (at the end of a group or of the read)
@@ -918,10 +932,23 @@ struct MsLane {
     // not fit entry 0 and goes to the count array instead
     NTC_HD bool finish(const MsBufs &b) {
 #if defined(__HIP_DEVICE_COMPILE__) && NTC_ECOMB
-        flush_stage(b);
-        const uint4 x = ne ? b.stage[kStageSlots * 256 + threadIdx.x] : make_uint4(0, 0, 0, 0);
+        const uint32_t t = threadIdx.x;
         const uint32_t c = ne < kNeInE0 ? ne : kNeInE0;
-        store_entry(b.Ed + rid, 0, x.x, x.y, x.z, (x.w & ~(kNeInE0 << 8)) | (c << 8));
+        Entry *dst = b.Ed + rid * b.ds;
+        if (ne > kEntSlot) {
+            flush_stage(b);
+            const uint4 x = b.stage[kStageSlots * 256 + t];
+            store_entry(dst, 0, x.x, x.y, x.z, (x.w & ~(kNeInE0 << 8)) | (c << 8));
+        } else {  // the dense group: entry 0 (with the count, also for ne = 0) .. ne - 1
+            const uint4 x = ne ? b.stage[t] : make_uint4(0, 0, 0, 0);
+            store_entry(dst, 0, x.x, x.y, x.z, (x.w & ~(kNeInE0 << 8)) | (c << 8));
+#pragma unroll
+            for (uint32_t i = 1; i < kEntSlot; i++)
+                if (i < ne) {
+                    const uint4 y = b.stage[i * 256 + t];
+                    store_entry(dst, (uint64_t)i * b.es, y.x, y.y, y.z, y.w);
+                }
+        }
         return c == kNeInE0;
 #else
         (void)b;

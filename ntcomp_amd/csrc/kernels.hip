@@ -172,7 +172,7 @@ struct WaveQueue {
 // entries of read r (k_ms4: in entry 0's dk, MsLane::finish; the count array past kNeInE0)
 __device__ __forceinline__ uint32_t read_entry_count(const Enc4Args &a, uint64_t r) {
 #if NTC_ECOMB
-    const uint32_t c = entry0_count(load_entry(a.Ed + r, 0));
+    const uint32_t c = entry0_count(load_entry(a.Ed + r * kEntSlot, 0));
     return c == kNeInE0 ? a.ne[r] : c;
 #else
     return a.ne[r];
@@ -184,7 +184,7 @@ __device__ __forceinline__ uint32_t parse_one(const Enc4Args &a, uint64_t r) {
     const uint64_t o0 = a.offs[0], b = a.offs[r], e = a.offs[r + 1];
     const uint64_t P = b - o0;
     const int rc = parse_read(a.ix, a.Q, P, a.E + P, read_entry_count(a, r), (uint32_t)(e - b), a.R2 + r, a.R + P, a.n_reads,
-                              a.Ed + r, a.n_reads);
+                              a.Ed + r * kEntSlot, 1);
     if (rc < 0) {
         atomicMin(a.status, (unsigned long long)((r << 8) | (uint64_t)(-rc)));
         a.rec_count[r] = 0;
@@ -206,7 +206,7 @@ __global__ __launch_bounds__(256, NTC_MS_WAVES) void k_ms4(Enc4Args a) {
     uint64_t rd = 0;
     const WaveQueue wq(a.counter, a.n_reads);
     __shared__ uint4 s_stage[(kStageSlots + 1) * 256];  // MsLane::put_entry write combining, entry 0
-    const MsBufs bufs{a.Q, a.E, a.Ed, a.n_reads, s_stage};
+    const MsBufs bufs{a.Q, a.E, a.Ed, 1, s_stage, kEntSlot};  // dense slots read-major
     MsLane st;
     for (;;) {
         // ---- hand idle lanes the next reads (wave-uniform control flow) ----------------
@@ -781,7 +781,7 @@ __global__ __launch_bounds__(256) void k_debug_gather4(Enc4Args a, uint32_t *d_o
     if (r >= a.n_reads) return;
     const uint64_t o0 = a.offs[0], b = a.offs[r], e = a.offs[r + 1];
     const uint64_t P = b - o0;
-    read_ms(a.ix, a.Q, P, a.E + P, read_entry_count(a, r), (uint32_t)(e - b), d_out + P, s_out + P, a.Ed + r, a.n_reads);
+    read_ms(a.ix, a.Q, P, a.E + P, read_entry_count(a, r), (uint32_t)(e - b), d_out + P, s_out + P, a.Ed + r * kEntSlot, 1);
 }
 
 // two-character rank lines (encode_core.h Rank2Chunk): one thread per (block, c1) chunk
