@@ -45,7 +45,8 @@ int ntc_index_save_as(const ntc_index_host *ix, const char *prefix, int layout);
 
 /* ---- FASTX ingest (CLI) -------------------------------------------------------------- */
 /* needletail::parse_fastx_file + SequenceRecord::normalize(true) as src/main.rs:51-62 and
- * :158-163 use them: plain or gzip FASTA/FASTQ, sequences normalized (ACGTN- kept, lower
+ * :158-163 use them: plain, gzip (BGZF too), bzip2, xz or zstd FASTA/FASTQ
+ * (detected from the magic bytes), sequences normalized (ACGTN- kept, lower
  * case upper-cased, U -> T, IUPAC kept, whitespace dropped, anything else -> N), names
  * dropped.  Batches hold up to max_reads reads / about max_bases bases; the buffers are
  * owned by the reader and valid until the next call.  n_reads = 0 at end of input.    */
