@@ -1168,13 +1168,18 @@ struct MsLane {
                 const uint32_t tested = cp ^ untested;
                 // one unconditional load per slot (a missing pair repeats position p), all
                 // issued before the first use
+                // A slot without a candidate repeats the first candidate's word (the same line,
+                // no further request past L2); with no candidate at all every slot reads word 0,
+                // one line all lanes share, instead of a pair word nobody needs
                 uint32_t slot[NTC_PAIR_TESTS], pbv[NTC_PAIR_TESTS];
                 uint32_t rem = tested;
+                const uint32_t first = tested ? (uint32_t)__builtin_ctz(tested) : 0u;
+                const uint64_t M0 = tested ? key_at(p + first, U - 1) : 0u;
 #pragma unroll
                 for (uint32_t t = 0; t < NTC_PAIR_TESTS; t++) {
-                    slot[t] = rem ? (uint32_t)__builtin_ctz(rem) : 0u;
+                    slot[t] = rem ? (uint32_t)__builtin_ctz(rem) : first;
+                    const uint64_t M = rem ? key_at(p + slot[t], U - 1) : M0;
                     rem &= rem - 1;
-                    const uint64_t M = key_at(p + slot[t], U - 1);
                     if ((tested >> slot[t]) & 1u) NTC_TOUCH(kTrBits, ix.pair_w + M);
                     pbv[t] = ld_hint<32>(ix.pair_w + M);
                 }
