@@ -26,8 +26,8 @@ rocprofv3 PMC passes of THIS device build (profiles/pmc_traffic.json, keyed by t
 source hash; scaled per read or per base to the launch), / the kernel's live HIP-event
 time, against 8 TB/s.  Each read request is counted at its own size (32/64/128 B:
 TCC_EA0_RDREQ_{32B,64B,128B}), writes at theirs (TCC_EA0_WRREQ, _64B), so random 64 B
-lines are not double-counted.  `line_rate` puts the L2-miss request rate against the
-random-line roof measured by scripts/randbw.hip.
+lines are not double-counted.  `line_rate` puts the request rate past L2 (reads and
+writes) against the random-line roof measured by scripts/randbw.hip.
 cpu_baseline: the faithful C oracle (oracle/ntcomp_oracle.c, test infrastructure) on one
 pinned host core, rank 0 at N = 1, on a bounded sample; it is also the parity checker.
 """
@@ -151,10 +151,12 @@ def roofline(kname, kernel_ms, kernel_ms_min, units, unit_name, pmc, pmc_note, w
         if kd.get("dram_read_bytes") is not None:
             r["dram_read_bytes"] = int(kd["dram_read_bytes"] * scale)
         roof = random_line_roof()
-        req = kd.get("rdreq", 0) * scale
+        rq, wq = kd.get("rdreq", 0) * scale, (kd.get("wrreq") or 0) * scale
+        req = rq + wq  # every request past L2 occupies the fabric, reads and writes alike
         if roof and req:
             rate = req / (kernel_ms / 1e3) / 1e9
-            r["line_rate"] = {"requests_per_launch": int(req), "requests_per_" + unit_name: round(req / units, 3),
+            r["line_rate"] = {"requests_per_launch": int(req), "read_requests_per_launch": int(rq),
+                              "write_requests_per_launch": int(wq), "requests_per_" + unit_name: round(req / units, 3),
                               "g_requests_per_s": round(rate, 2), "roof_g_requests_per_s": roof,
                               "frac": round(rate / roof, 4)}
         r["pmc_profile_kernel_ms"] = round(kd.get("avg_ns", 0) / 1e6 * scale, 4)
