@@ -13,8 +13,9 @@ for f in sorted(glob.glob(os.path.join(d, "*.json"))):
         print(os.path.basename(f), "unreadable", e)
         continue
     out = [os.path.basename(f)]
-    if "ms_per_step" in j and j.get("config", {}).get("workload", "").startswith("C"):
-        out.append(f"C step {j['ms_per_step']:.3f} k {j['roofline'].get('kernel_ms')}")
+    if "ms_per_step" in j:
+        w = j.get("config", {}).get("workload", "?")[:1]
+        out.append(f"{w} step {j['ms_per_step']:.3f} k {j['roofline'].get('kernel_ms')}")
     if "decode" in j:
         out.append(f"D step {j['decode']['ms_per_step']:.3f} k {j['decode']['roofline'].get('kernel_ms')}")
     s = j.get("strains")
