@@ -687,12 +687,32 @@ struct EntryView {
     uint32_t k;
     int32_t e;  // cursor (-1: the read has no entries); moves left only
     Entry cur;  // E[e]
+    // the dense group in registers (k_parse4 loads it in one round trip; dc = held): entries
+    // 0..3 then cost no dependent load in the seeks and run scans
+    Entry c0{0, 0, 0, 0}, c1{0, 0, 0, 0}, c2{0, 0, 0, 0}, c3{0, 0, 0, 0};
+    bool dc = false;
     NTC_HD EntryView(const Entry *E_, const DevIndex *ix_, const uint64_t *Q_, uint64_t qo_, uint32_t k_, int32_t e_,
-                     const Entry *Ed_ = nullptr, uint64_t es_ = 1)
+                     const Entry *Ed_ = nullptr, uint64_t es_ = 1, const Entry *pre = nullptr)
         : E(E_), Ed(Ed_ ? Ed_ : E_), es(Ed_ ? es_ : 1), ix(ix_), Q(Q_), qo(qo_), k(k_), e(e_), cur{0, 0, 0, 0} {
+        if (pre) {
+            c0 = pre[0];
+            c1 = pre[1];
+            c2 = pre[2];
+            c3 = pre[3];
+            dc = true;
+        }
         if (e >= 0) cur = at(e);
     }
-    NTC_HD Entry at(int32_t i) const { return load_entry(ent_ptr(E, Ed, es, (uint32_t)i), 0); }
+    NTC_HD Entry at(int32_t i) const {
+        if (dc && i < (int32_t)kEntSlot) {  // field by field: a select of whole structs goes through scratch
+            uint32_t p = c0.p, v = c0.v, m = c0.m, dk = c0.dk;
+            p = i == 1 ? c1.p : p; v = i == 1 ? c1.v : v; m = i == 1 ? c1.m : m; dk = i == 1 ? c1.dk : dk;
+            p = i == 2 ? c2.p : p; v = i == 2 ? c2.v : v; m = i == 2 ? c2.m : m; dk = i == 2 ? c2.dk : dk;
+            p = i == 3 ? c3.p : p; v = i == 3 ? c3.v : v; m = i == 3 ? c3.m : m; dk = i == 3 ? c3.dk : dk;
+            return Entry{p, v, m, dk};
+        }
+        return load_entry(ent_ptr(E, Ed, es, (uint32_t)i), 0);
+    }
     NTC_HD void seek(uint32_t x) {  // last entry with p <= x, or entry 0
         if (e <= 0 || cur.p <= x) return;
         // every entry covers >= 1 position, so entry e - (p - x) starts at or before x
@@ -1463,9 +1483,9 @@ constexpr uint32_t kRecSlot = 8;  // records per read in the dense slot; more sp
 // wave's lanes, so the lanes' j-th records are one coalesced store.
 NTC_HD int parse_read(const DevIndex &ix, const uint64_t *Q, uint64_t qo, const Entry *E, uint32_t ne,
                       uint32_t len, uint64_t *slot, uint64_t *spill, uint64_t sstride = 1,
-                      const Entry *Ed = nullptr, uint64_t es = 1) {
+                      const Entry *Ed = nullptr, uint64_t es = 1, const Entry *pre = nullptr) {
     const uint32_t k = ix.k;
-    EntryView ev(E, &ix, Q, qo, k, (int32_t)ne - 1, Ed, es);
+    EntryView ev(E, &ix, Q, qo, k, (int32_t)ne - 1, Ed, es, pre);
     uint32_t i = len;
     int nrec = 0;
     while (i > 0) {

@@ -179,12 +179,26 @@ __device__ __forceinline__ uint32_t read_entry_count(const Enc4Args &a, uint64_t
 #endif
 }
 
+#ifndef NTC_PARSE_DC
+#define NTC_PARSE_DC 1  // k_parse4 holds each read's dense entry group in registers
+#endif
 // parse of read r (k_parse4's body); returns its record count (0 on error)
 __device__ __forceinline__ uint32_t parse_one(const Enc4Args &a, uint64_t r) {
     const uint64_t o0 = a.offs[0], b = a.offs[r], e = a.offs[r + 1];
     const uint64_t P = b - o0;
+#if NTC_PARSE_DC && NTC_ECOMB
+    // the read's dense group (its first 4 entries, entry 0 with the count) in one round trip
+    Entry pre[kEntSlot];
+#pragma unroll
+    for (uint32_t j = 0; j < kEntSlot; j++) pre[j] = load_entry(a.Ed + r * kEntSlot, (int32_t)j);
+    const uint32_t c0 = entry0_count(pre[0]);
+    const uint32_t ne = c0 == kNeInE0 ? a.ne[r] : c0;
+    const int rc = parse_read(a.ix, a.Q, P, a.E + P, ne, (uint32_t)(e - b), a.R2 + r, a.R + P, a.n_reads,
+                              a.Ed + r * kEntSlot, 1, pre);
+#else
     const int rc = parse_read(a.ix, a.Q, P, a.E + P, read_entry_count(a, r), (uint32_t)(e - b), a.R2 + r, a.R + P, a.n_reads,
                               a.Ed + r * kEntSlot, 1);
+#endif
     if (rc < 0) {
         atomicMin(a.status, (unsigned long long)((r << 8) | (uint64_t)(-rc)));
         a.rec_count[r] = 0;
