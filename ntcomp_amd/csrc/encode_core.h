@@ -568,6 +568,13 @@ constexpr uint32_t kScanExact = 4;   // filter candidates tested exactly per SCA
 #ifndef NTC_GUESS_SLACK
 #define NTC_GUESS_SLACK 2  // guess only for x - ge in [U, U + slack] (a lone substitution: x = ge + U)
 #endif
+#ifndef NTC_CHAIN
+// A wave runs the blocks of MsLane::step in program order for all its lanes (a wave
+// iteration holds ~7.6 distinct modes on C91, so nearly every block runs anyway): a lane
+// whose run breaks goes on into the break / SCAN blocks below within the same call instead
+// of waiting for the next iteration
+#define NTC_CHAIN 1
+#endif
 #ifndef NTC_PAIR_TESTS
 #define NTC_PAIR_TESTS 4  // candidate pairs tested per SCAN with pair words
 #endif
@@ -1065,7 +1072,11 @@ struct MsLane {
                 if (len + pre - p - m < lim) lim = len + pre - p - m;
                 if (lim < pre) {  // the guessed node is not the U-mer's: take it from the table
                     mode = kModeEnter;
+#if NTC_CHAIN
+                    break;  // m = 0: on to the Enter block below, in this same call
+#else
                     return 0;
+#endif
                 }
                 m += lim - pre;
                 pre = 0;
@@ -1082,7 +1093,9 @@ struct MsLane {
                 // the run broke at p (mostly a sequencing error): table first
                 window(b, p + 1 - U);
                 mode = kModeBrk;
+#if !NTC_CHAIN
                 return 0;
+#endif
             }
         }
         if (mode == kModeFirst) {

@@ -274,3 +274,61 @@ extern "C" int emu_decode(const ntc_index_view *v, const uint64_t *recs, uint64_
     *nreads = starts.size() - 1;
     return NTC_OK;
 }
+
+// Wave divergence of k_ms4 (diagnostic): one wave of 64 lanes runs MsLane::step in lock step
+// over the reads, idle lanes taking the next read as the kernel's pool hands them out.  out:
+// [0] wave iterations, [1] sum over iterations of the distinct entry modes among busy lanes
+// (a "run" pending counts as its own mode), [2] lane steps, [3..12] steps per entry mode
+// (Scan, Ext, P1, Bs, Brk, First, Enter, BrkLong, ExtFail, run), [13..22] iterations by
+// number of distinct modes (1..10).
+extern "C" int emu_wave_modes(const ntc_index_view *v, const uint8_t *bases, const uint64_t *offs, uint64_t n_reads,
+                              uint64_t *out) {
+    HostIndex hx;
+    Derived dv;
+    std::vector<WalkEntry> walk;
+    std::vector<uint2> tab;
+    std::vector<uint32_t> bits, fbits;
+    std::vector<uint16_t> pairb;
+    DevIndex d;
+    if (!load(v, hx, dv, walk, d, tab, bits, fbits, pairb, 0)) return NTC_ERR_FORMAT;
+    memset(out, 0, 23 * sizeof(uint64_t));
+    struct Lane {
+        MsLane ms;
+        std::vector<uint64_t> Q;
+        std::vector<Entry> E;
+        bool busy = false;
+    };
+    std::vector<Lane> L(64);
+    uint64_t next = 0;
+    for (;;) {
+        for (auto &l : L) {
+            if (l.busy || next >= n_reads) continue;
+            const uint64_t r = next++;
+            const uint32_t len = (uint32_t)(offs[r + 1] - offs[r]);
+            l.Q.assign(len / 32 + 3, 0);
+            l.E.assign(len + 1, Entry{0, 0, 0, 0});
+            if (len == 0 || pack_read(bases + offs[r], len, l.Q.data(), d.absent) != 0) continue;
+            l.ms.start(d, 0, len);
+            l.busy = true;
+        }
+        uint32_t modes = 0;
+        bool any = false;
+        for (auto &l : L) {
+            if (!l.busy) continue;
+            any = true;
+            const uint32_t m = l.ms.try_run ? 9u : l.ms.mode;
+            modes |= 1u << m;
+            out[3 + m]++;
+            out[2]++;
+            const MsBufs bufs{l.Q.data(), l.E.data(), l.E.data(), 1};
+            const int st = l.ms.step(d, bufs);
+            if (st != 0) l.busy = false;
+        }
+        if (!any) break;
+        out[0]++;
+        const uint32_t dm = (uint32_t)__builtin_popcount(modes);
+        out[1] += dm;
+        out[12 + dm]++;
+    }
+    return 0;
+}

@@ -91,3 +91,15 @@ def emu_path_cover(n, k, rows, C, lcs):
     if rc:
         raise RuntimeError(f"emu_path_cover rc={rc}")
     return int(out[0]), int(out[1]), int(out[2])
+
+
+def emu_wave_modes(n, k, rows, C, lcs, bases, offs):
+    """k_ms4 wave divergence statistics (tests/emu/emu.cpp emu_wave_modes)"""
+    v, keep = make_view(n, k, rows, C, lcs)
+    bases = np.ascontiguousarray(bases, dtype=np.uint8)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    out = np.zeros(23, dtype=np.uint64)
+    rc = emu_lib().emu_wave_modes(ctypes.byref(v), _p(bases), _p(offs), len(offs) - 1, _p(out))
+    if rc:
+        raise RuntimeError(f"emu_wave_modes rc={rc}")
+    return out
