@@ -1120,13 +1120,14 @@ struct MsLane {
                 }
                 if (!tab_long(te)) {
                     p = U - 1 + U - (te.y & 0xFFu);  // d_{U-1+i} <= m + i
-                    return p >= len ? 1 : 0;
-                }
-                if (!b2) {
+                    if (p >= len || !NTC_CHAIN) return p >= len ? 1 : 0;
+                } else if (!b2) {
                     p = U + 1;  // U is short
-                    return p >= len ? 1 : 0;
+                    if (p >= len || !NTC_CHAIN) return p >= len ? 1 : 0;
+                } else {
+                    return enter_pair(ix, b, U - 1, te);
                 }
-                return enter_pair(ix, b, U - 1, te);
+                // (NTC_CHAIN) on into the SCAN block below, in this same call
             }
         }
 #if NTC_BRK_MERGE
@@ -1361,7 +1362,9 @@ struct MsLane {
             l = ix.colex_at[j] & 0x7FFFFFFFu;
             r = l + 1;
             mode = kModeExt;
+#if !NTC_CHAIN
             return 0;
+#endif
         }
         if (mode == kModeEnter) {  // guessed node rejected: x = p - 1 from the table
             if (!covers(p - U, p - 1)) window(b, p - U);
