@@ -179,6 +179,9 @@ __device__ __forceinline__ uint32_t read_entry_count(const Enc4Args &a, uint64_t
 #endif
 }
 
+#ifndef NTC_PARSE_WAVES
+#define NTC_PARSE_WAVES 8  // waves per SIMD k_parse4 is compiled for (62 VGPRs, no scratch)
+#endif
 #ifndef NTC_PARSE_DC
 #define NTC_PARSE_DC 1  // k_parse4 holds each read's dense entry group in registers
 #endif
@@ -262,7 +265,7 @@ __global__ __launch_bounds__(256, NTC_MS_WAVES) void k_ms4(Enc4Args a) {
     }
 }
 
-__global__ __launch_bounds__(256) void k_parse4(Enc4Args a) {
+__global__ __launch_bounds__(256, NTC_PARSE_WAVES) void k_parse4(Enc4Args a) {
     const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     uint32_t cnt = 0;
     if (r < a.n_reads) {
