@@ -1,9 +1,10 @@
 # alternating A/B of device builds: bash scripts/ab_run.sh "<configs>" lib1 lib2 ...  (lib "cur" = the in-tree build)
+# extra bench arguments: AB_ARGS="--err-ppm 0"
 set -e
 mkdir -p gpurun_out/ab
 CFG=${1:-encode,strains}
 shift
-B="python -u bench.py --configs $CFG --no-cpu --steps 10 --warmup 3"
+B="python -u bench.py --configs $CFG --no-cpu --steps 10 --warmup 3 ${AB_ARGS:-}"
 for i in 1 2; do
   for L in "$@"; do
     n=$(basename $L .so)
