@@ -578,6 +578,10 @@ constexpr uint32_t kScanExact = 4;   // filter candidates tested exactly per SCA
 #ifndef NTC_PAIR_TESTS
 #define NTC_PAIR_TESTS 4  // candidate pairs tested per SCAN with pair words
 #endif
+#ifndef NTC_JOINT
+#define NTC_JOINT 1  // joint path runs over multi-node intervals (MsLane::note_single)
+#endif
+constexpr uint32_t kJointPending = 0xFFFFFFFEu;  // joint run wanted, path positions not loaded yet
 
 // ======================================================================================
 // Matching statistics as RUN-LENGTH entries.  Positions whose U-mer is absent ("short")
@@ -593,6 +597,30 @@ constexpr uint32_t kScanExact = 4;   // filter candidates tested exactly per SCA
 // (t = d-1, then binary search between U-1 and d-1, each a widen + extend).
 // Entries cover exactly the walked positions; the parse reads the rest from the table.
 // ======================================================================================
+// Characters (<= 64) from path text position T (its three 32-char groups g0..g2) that equal
+// the query words qa, qb and end a node's k-mer; with pre > 0 (verifying a guessed node) only
+// the k-mer after the first pre characters must be a node
+NTC_HD uint32_t path_lim(const uint4 &g0, const uint4 &g1, const uint4 &g2, uint32_t sh, uint64_t qa, uint64_t qb,
+                         uint32_t pre) {
+    const uint64_t c0 = (uint64_t)g0.x | ((uint64_t)g0.y << 32);
+    const uint64_t c1 = (uint64_t)g1.x | ((uint64_t)g1.y << 32);
+    const uint64_t c2 = (uint64_t)g2.x | ((uint64_t)g2.y << 32);
+    const uint64_t pa = sh ? ((c0 >> (2 * sh)) | (c1 << (64 - 2 * sh))) : c0;
+    const uint64_t pb = sh ? ((c1 >> (2 * sh)) | (c2 << (64 - 2 * sh))) : c1;
+    uint32_t va = sh ? ((g0.z >> sh) | (g1.z << (32 - sh))) : g0.z;
+    if (pre) va |= (1u << (pre - 1)) - 1u;  // of the verified k-mers only node j's must exist
+    const uint32_t vb = sh ? ((g1.z >> sh) | (g2.z << (32 - sh))) : g1.z;
+    const uint64_t xa = qa ^ pa, xb = qb ^ pb;
+    uint32_t la = xa ? (uint32_t)(__builtin_ctzll(xa) >> 1) : 32u;
+    const uint32_t ia = ~va ? (uint32_t)__builtin_ctz(~va) : 32u;
+    if (ia < la) la = ia;
+    // second half computed unconditionally: its loads issue with the first half's
+    uint32_t lb = xb ? (uint32_t)(__builtin_ctzll(xb) >> 1) : 32u;
+    const uint32_t ib = ~vb ? (uint32_t)__builtin_ctz(~vb) : 32u;
+    if (ib < lb) lb = ib;
+    return la == 32 ? 32 + lb : la;
+}
+
 struct Entry {       // 16 bytes, one uint4 store
     uint32_t p;      // first position
     uint32_t v;      // SBWT entry: colex start S; run entry: path position of node at p
@@ -876,6 +904,10 @@ struct MsLane {
     uint32_t len, p, d, l, r, j, ne, mode, hi, lo, l1, r1, bl, bR;
     uint32_t gj, ge;    // last run break: at position ge, node before it at path position gj (ge = 0: none)
     uint32_t vfy;       // the next run first verifies the vfy characters ending at node j
+    // Joint run (note_single): path position of the interval's last node, else kNoJoint.  It
+    // lives in l1, which only the binary-search probes use (written before read in kModeBs);
+    // a separate field costs k_ms4 a wave of occupancy (72 VGPRs is the 7-wave limit).
+#define jy l1
     bool try_run;
 
     NTC_HD void start(const DevIndex &ix, uint64_t qo_, uint32_t len_, uint64_t rid_ = 0) {
@@ -885,9 +917,10 @@ struct MsLane {
         qw = 0;
         qb = 0xFFFFFFFFu;
         p = 0; d = 0; l = 0; r = ix.n; j = 0xFFFFFFFFu; ne = 0;
-        mode = kModeFirst; lo = l1 = r1 = bl = bR = 0;
+        mode = kModeFirst; lo = r1 = bl = bR = 0;
         hi = kScanW;  // SCAN width cap (hi is free while scanning)
         gj = ge = vfy = 0;
+        jy = 0xFFFFFFFFu;
         try_run = false;
     }
     NTC_HD void window(const MsBufs &b, uint32_t from) {
@@ -982,14 +1015,27 @@ struct MsLane {
         return true;
 #endif
     }
-    // after a commit: look for the path position of a single-node interval
+    // after a commit: look for the path position of a single-node interval.  A multi-node
+    // interval [l, r) (d < k: strains sharing the read's suffix) starts a JOINT run when both
+    // its first and its last node lie on paths: while both paths go on with the query's next
+    // character c, both nodes have edge c and ext([l, r), c) = [succ(l), succ(r - 1) + 1)
+    // (successors keep colex order; the first and last nodes with edge c bound the
+    // extension), so the interval start follows l's path and d climbs by one per position --
+    // the entries are ordinary run entries on l's path
     NTC_HD void note_single(const DevIndex &ix) {
         j = 0xFFFFFFFFu;
+        jy = 0xFFFFFFFFu;
         if (ix.has_paths && r == l + 1 && d >= ix.t_jump) {
             NTC_TOUCH(kTrPon, ix.pos_of_node + l);
             j = ix.pos_of_node[l];
             try_run = j != 0xFFFFFFFFu;
         }
+#if NTC_JOINT
+        else if (ix.has_paths && r > l + 1 && d >= ix.t_jump && d + 1 < ix.k) {
+            jy = kJointPending;  // both path positions are looked up by the run block (step)
+            try_run = true;
+        }
+#endif
     }
     NTC_HD int commit(const DevIndex &ix, const MsBufs &b, uint32_t nl, uint32_t nr, uint32_t nd) {
         l = nl; r = nr; d = nd;
@@ -1016,6 +1062,7 @@ struct MsLane {
         p = x + 1;
         mode = kModeExt;
         if (ix.tab_pos) {  // the table already holds the path position (d = U >= t_jump)
+            jy = 0xFFFFFFFFu;
             j = jj;
             try_run = jj != 0xFFFFFFFFu;
         } else {
@@ -1028,6 +1075,18 @@ struct MsLane {
         const uint32_t k = ix.k, U = ix.tab_u;
         const uint64_t *Q = b.Q;
         if (p >= len) return 1;
+#if NTC_JOINT
+        if (try_run && jy == kJointPending) {
+            NTC_TOUCH(kTrPon, ix.pos_of_node + l);
+            NTC_TOUCH(kTrPon, ix.pos_of_node + r - 1);
+            j = ix.pos_of_node[l];
+            jy = ix.pos_of_node[r - 1];
+            if (j == 0xFFFFFFFFu || jy == 0xFFFFFFFFu) {
+                jy = 0xFFFFFFFFu;
+                try_run = false;  // on with the extension at p
+            }
+        }
+#endif
         if (try_run) {
             try_run = false;
             uint32_t m = 0, pre = vfy;
@@ -1069,6 +1128,20 @@ struct MsLane {
                 const uint32_t ib = ~vb ? (uint32_t)__builtin_ctz(~vb) : 32u;
                 if (ib < lb) lb = ib;
                 uint32_t lim = la == 32 ? 32 + lb : la;
+#if NTC_JOINT
+                if (jy != 0xFFFFFFFFu) {  // joint run: the interval's last node follows its path too
+#if defined(__HIP_DEVICE_COMPILE__)
+                    __asm__ volatile("" ::: "memory");  // after lim: the loads below must not overlap the x path's
+#endif
+                    const uint64_t Ty = (uint64_t)jy + k + m;
+                    NTC_TOUCH(kTrPst, ix.pstream + (Ty >> 5));
+                    NTC_TOUCH(kTrPst, ix.pstream + (Ty >> 5) + 2);
+                    const uint4 h0 = ld4<4>(ix.pstream + (Ty >> 5)), h1 = ld4<4>(ix.pstream + (Ty >> 5) + 1),
+                                h2 = ld4<4>(ix.pstream + (Ty >> 5) + 2);
+                    const uint32_t ly = path_lim(h0, h1, h2, (uint32_t)(Ty & 31), qa, qb2, 0);
+                    if (ly < lim) lim = ly;
+                }
+#endif
                 if (len + pre - p - m < lim) lim = len + pre - p - m;
                 if (lim < pre) {  // the guessed node is not the U-mer's: take it from the table
                     mode = kModeEnter;
@@ -1082,6 +1155,25 @@ struct MsLane {
                 pre = 0;
                 if (lim < 64) break;
             }
+#if NTC_JOINT
+            if (jy != 0xFFFFFFFFu) {
+                // joint run over a multi-node interval [l, r) (its first and last nodes followed
+                // along their paths): the interval at p + m - 1 is [node at j + m, node at jy + m
+                // + 1) and the extension at p + m goes on from it (see note_path)
+                if (m > 0) {
+                    put_entry(b, p, j + 1, m, (d + 1 < k ? d + 1 : k) | kRunTag);
+                    p += m;
+                    d = d + m < k ? d + m : k;
+                    if (p >= len) { jy = 0xFFFFFFFFu; return 1; }
+                    NTC_TOUCH(kTrColex, ix.colex_at + j + m);
+                    NTC_TOUCH(kTrColex, ix.colex_at + jy + m);
+                    l = ix.colex_at[j + m] & 0x7FFFFFFFu;
+                    r = (ix.colex_at[jy + m] & 0x7FFFFFFFu) + 1;
+                }
+                jy = 0xFFFFFFFFu;
+                m = 0;  // on into the EXT block below, in this same call
+            }
+#endif
             if (m > 0) {
                 put_entry(b, p, j + 1, m, (d + 1 < k ? d + 1 : k) | kRunTag);
                 p += m;
@@ -1241,6 +1333,7 @@ struct MsLane {
                     if (((single >> xi) & 1u) && ix.tab_pos && ge != 0 && x - ge - U <= NTC_GUESS_SLACK &&
                         x >= ge + U && jg < ix.path_len) {
                         j = jg;
+                        jy = 0xFFFFFFFFu;
                         d = U;
                         p = x + 1;
                         vfy = U;
@@ -1473,6 +1566,7 @@ struct MsLane {
         return 0;
     }
 };
+#undef jy
 
 // (d, S) of every position of one read (diagnostics: ntc_debug_matching_statistics)
 NTC_HD void read_ms(const DevIndex &ix, const uint64_t *Q, uint64_t qo, const Entry *E, uint32_t ne,

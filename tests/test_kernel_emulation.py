@@ -210,7 +210,9 @@ def test_emulated_small_k_reference_panic_status(k, glen):
 def test_emulated_strain_collection(k, ext2, monkeypatch):
     """A genome + 5 strains at 1 % substitutions (multi-node MS intervals over long climbs,
     short unitigs): records equal the oracle's with and without the two-character rank
-    lines (NTC_EMU_EXT2), and decode back exactly."""
+    lines (NTC_EMU_EXT2), and decode back exactly.  The climbs run as joint path runs over
+    the interval's first and last nodes (MsLane::note_single): (d, S) of every position of a
+    read sample equals the oracle's matching statistics."""
     monkeypatch.setenv("NTC_EMU_EXT2", ext2)
     g = nt.synth_genome(17, 150_000)
     st = nt.synth_strains(g, 3, 5, 10_000)
@@ -219,8 +221,13 @@ def test_emulated_strain_collection(k, ext2, monkeypatch):
     n, L = 1500, 150
     reads = nt.synth_reads(np.concatenate(texts), 2, 0, n, L, 10_000)
     offs = np.arange(0, n * L + 1, L, dtype=np.uint64)
-    got, goff = emu_encode(ix.n, k, ix.rows, ix.C, ix.lcs, reads, offs)
-    exp, eoff = OracleIndex(ix.n, k, ix.rows, ix.C, ix.lcs).encode(reads, offs)
+    got, goff, d, s = emu_encode(ix.n, k, ix.rows, ix.C, ix.lcs, reads, offs, want_ms=True)
+    orc = OracleIndex(ix.n, k, ix.rows, ix.C, ix.lcs)
+    exp, eoff = orc.encode(reads, offs)
     assert np.array_equal(goff, eoff) and np.array_equal(got, exp)
+    for r in range(0, n, 11):
+        od, olo = orc.ms(reads[r * L:(r + 1) * L].tobytes())
+        assert np.array_equal(d[r * L:(r + 1) * L], od), r
+        assert np.array_equal(s[r * L:(r + 1) * L].astype(np.uint64), olo), r
     out, oo = emu_decode(ix.n, k, ix.rows, ix.C, ix.lcs, got)
     assert np.array_equal(out, reads)
