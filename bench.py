@@ -495,6 +495,7 @@ def main():
             s["config"]["records_per_gpu"] = sum(b["n_recs"] for b in sh.batches)
             s["config"]["n_paths"] = ctx.get_option("n_paths")
             s["config"]["scan_filter"] = bool(ctx.get_option("filter"))
+            s["config"]["joint_runs"] = bool(ctx.get_option("joint"))
             el, kms = timed(lambda: encode_pass(ctx, sh), args.steps, args.warmup, barrier, sync, dist)
             b0 = sh.batches[0]
             kavg, kmin = launch_ms(kms, [b["n"] for b in sh.batches], b0["n"])

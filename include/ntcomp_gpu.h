@@ -99,6 +99,11 @@ int ntc_ctx_synchronize(ntc_ctx *ctx);
  * never depend on it).  "max_pass_bases" (default 2^30): ntc_encode_batch /
  * ntc_decode_batch run in device passes of whole reads holding at most this many bases
  * (device workspace is ~40 B per base of a pass; results never depend on it).
+ * "joint" for the NEXT upload: -1 (default, auto: on when the path cover averages fewer
+ * than 4096 nodes per path, i.e. a genome collection), 0 or 1: joint path runs over
+ * multi-node matching-statistics intervals (results never depend on it; after an upload
+ * get_option returns the setting in use).  Also "filter" (-1 auto / 0 / 1: SCAN
+ * pre-filter), "ext2" (0 / 1: two-character rank chunks), "pair_bytes" (0 / 1), same rules.
  * Read-only: "n_paths", "path_text_len" (the path cover built on the device at upload),
  * "path_hash" (test hook: FNV-1a of the cover arrays, derived.h path_cover_hash),
  * "tab_u" (after an upload: the depth in use), "upload_host_us" / "upload_total_us"

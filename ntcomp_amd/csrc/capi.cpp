@@ -62,6 +62,7 @@ struct ntc_ctx {
     int pair_bytes_opt = 1;  // build the SCAN pair bytes at the next upload (0: bitmap tests, A/B)
     int filter_opt = -1;     // SCAN pre-filter at the next upload: -1 auto (off when saturated), 0 off, 1 on
     int64_t filter_density_ppm = -1;  // presence density of the filter level at the last upload
+    int joint_opt = -1;      // joint path runs at the next upload: -1 auto (fragmented path cover), 0 off, 1 on
     int ext2_opt = 0;        // build the two-character rank chunks at the next upload (A/B option: 1 measured
                              // slower -- 8 B/node from HBM against 1 B/node of Infinity-Cache-resident rank words)
     uint64_t n_paths = 0, path_text_len = 0;
@@ -506,6 +507,12 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     d.pos_of_node = (const uint32_t *)d_pos;
     d.puniq = (const uint64_t *)d_puniq;
     d.absent = dv.absent;
+    // Joint path runs pay off when MS intervals above U hold several nodes for long stretches:
+    // genome collections, whose shared regions split the path cover into short unitigs (S91:
+    // 1.19 M paths over 70 M nodes).  A cover of long paths (one genome, C91: 2 paths) keeps
+    // the lighter k_ms4 build.
+    d.joint = has_paths && (ctx->joint_opt == 1 || (ctx->joint_opt < 0 && (uint64_t)n_paths * kJointAutoNodesPerPath > n))
+                  ? 1u : 0u;
     d.rank2 = nullptr;
     if (ctx->ext2_opt) {  // two-character rank lines (8 B per node)
         void *d_r2;
@@ -576,6 +583,11 @@ int ntc_ctx_set_option(ntc_ctx *ctx, const char *key, int64_t value) {
         ctx->filter_opt = (int)value;
         return NTC_OK;
     }
+    if (std::strcmp(key, "joint") == 0) {  // applies to the next ntc_index_upload
+        if (value < -1 || value > 1) return set_err(ctx, NTC_ERR_INVALID_ARG, "joint must be -1 (auto), 0 or 1");
+        ctx->joint_opt = (int)value;
+        return NTC_OK;
+    }
     if (std::strcmp(key, "ext2") == 0) {  // applies to the next ntc_index_upload
         if (value != 0 && value != 1) return set_err(ctx, NTC_ERR_INVALID_ARG, "ext2 must be 0 or 1");
         ctx->ext2_opt = (int)value;
@@ -602,6 +614,7 @@ int ntc_ctx_get_option(const ntc_ctx *ctx, const char *key, int64_t *value) {
     else if (std::strcmp(key, "pair_bytes") == 0) *value = ctx->has_index ? (ctx->dix.pair_w != nullptr) : ctx->pair_bytes_opt;
     else if (std::strcmp(key, "ext2") == 0) *value = ctx->has_index ? (ctx->dix.rank2 != nullptr) : ctx->ext2_opt;
     else if (std::strcmp(key, "filter") == 0) *value = ctx->has_index ? (ctx->dix.filt_f != 0) : ctx->filter_opt;
+    else if (std::strcmp(key, "joint") == 0) *value = ctx->has_index ? (int64_t)ctx->dix.joint : ctx->joint_opt;
     else if (std::strcmp(key, "filter_density_ppm") == 0) *value = ctx->filter_density_ppm;
     else if (std::strcmp(key, "n_paths") == 0) *value = (int64_t)ctx->n_paths;
     else if (std::strcmp(key, "path_text_len") == 0) *value = (int64_t)ctx->path_text_len;

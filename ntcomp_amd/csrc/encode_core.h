@@ -125,6 +125,7 @@ struct DevIndex {
     uint32_t tab_u;               // U: longest tabulated length (1 <= U <= min(k, kTabMaxU))
     uint32_t absent;              // bit c: no node ends with character c
     const Rank2Chunk *rank2;      // [4][rank2_blocks(n)] two-character rank chunks, or null
+    uint32_t joint;               // 1: encode with joint path runs (k_ms4<true>, MsLaneT)
 };
 
 // per-read status codes (values of ntc_status)
@@ -456,6 +457,8 @@ constexpr uint32_t kFiltMinU = 12; // below this the level-U bitmap is small eno
 // auto mode: no filter above 60 % presence (measured: C91's filter at 45 % saves 28 % of
 // k_ms4; S91's at 72 % passes ~ 0.72^3 of the positions and costs 5 %)
 constexpr int64_t kFiltMaxDensityPpm = 600000;
+// joint path runs (MsLaneT<true>) by default when the path cover averages fewer nodes per path
+constexpr uint64_t kJointAutoNodesPerPath = 4096;
 // interval of a present top-level entry (+ path position of a single node, or ~0)
 NTC_HD void tab_interval(const DevIndex &ix, uint2 te, uint32_t &l, uint32_t &r, uint32_t &j) {
     l = te.x;
@@ -577,9 +580,6 @@ constexpr uint32_t kScanExact = 4;   // filter candidates tested exactly per SCA
 #endif
 #ifndef NTC_PAIR_TESTS
 #define NTC_PAIR_TESTS 4  // candidate pairs tested per SCAN with pair words
-#endif
-#ifndef NTC_JOINT
-#define NTC_JOINT 1  // joint path runs over multi-node intervals (MsLane::note_single)
 #endif
 constexpr uint32_t kJointPending = 0xFFFFFFFEu;  // joint run wanted, path positions not loaded yet
 
@@ -896,7 +896,10 @@ constexpr uint32_t kStageSlots = 4;  // 64 B: one write request instead of four 
 constexpr uint32_t kNeInE0 = 0x7FFFFFu;
 NTC_HD uint32_t entry0_count(const Entry &e0) { return (e0.dk >> 8) & kNeInE0; }
 
-struct MsLane {
+// kJoint: joint path runs over multi-node intervals (note_single); k_ms4 is built both ways
+// and the upload picks one (ctx option "joint"), since the code costs C91 ~1 % of k_ms4
+template <bool kJoint>
+struct MsLaneT {
     uint64_t qo;        // this read starts at character qo of Q; its entries at E + qo
     uint64_t rid;       // read id (dense entry slots)
     uint64_t qw;        // query characters [qb, qb + 32) of this read, cached
@@ -1030,12 +1033,10 @@ struct MsLane {
             j = ix.pos_of_node[l];
             try_run = j != 0xFFFFFFFFu;
         }
-#if NTC_JOINT
-        else if (ix.has_paths && r > l + 1 && d >= ix.t_jump && d + 1 < ix.k) {
+        else if (kJoint && ix.has_paths && r > l + 1 && d >= ix.t_jump && d + 1 < ix.k) {
             jy = kJointPending;  // both path positions are looked up by the run block (step)
             try_run = true;
         }
-#endif
     }
     NTC_HD int commit(const DevIndex &ix, const MsBufs &b, uint32_t nl, uint32_t nr, uint32_t nd) {
         l = nl; r = nr; d = nd;
@@ -1075,8 +1076,7 @@ struct MsLane {
         const uint32_t k = ix.k, U = ix.tab_u;
         const uint64_t *Q = b.Q;
         if (p >= len) return 1;
-#if NTC_JOINT
-        if (try_run && jy == kJointPending) {
+        if (kJoint && try_run && jy == kJointPending) {
             NTC_TOUCH(kTrPon, ix.pos_of_node + l);
             NTC_TOUCH(kTrPon, ix.pos_of_node + r - 1);
             j = ix.pos_of_node[l];
@@ -1086,7 +1086,6 @@ struct MsLane {
                 try_run = false;  // on with the extension at p
             }
         }
-#endif
         if (try_run) {
             try_run = false;
             uint32_t m = 0, pre = vfy;
@@ -1128,8 +1127,7 @@ struct MsLane {
                 const uint32_t ib = ~vb ? (uint32_t)__builtin_ctz(~vb) : 32u;
                 if (ib < lb) lb = ib;
                 uint32_t lim = la == 32 ? 32 + lb : la;
-#if NTC_JOINT
-                if (jy != 0xFFFFFFFFu) {  // joint run: the interval's last node follows its path too
+                if (kJoint && jy != 0xFFFFFFFFu) {  // joint run: the interval's last node follows its path too
 #if defined(__HIP_DEVICE_COMPILE__)
                     __asm__ volatile("" ::: "memory");  // after lim: the loads below must not overlap the x path's
 #endif
@@ -1141,7 +1139,6 @@ struct MsLane {
                     const uint32_t ly = path_lim(h0, h1, h2, (uint32_t)(Ty & 31), qa, qb2, 0);
                     if (ly < lim) lim = ly;
                 }
-#endif
                 if (len + pre - p - m < lim) lim = len + pre - p - m;
                 if (lim < pre) {  // the guessed node is not the U-mer's: take it from the table
                     mode = kModeEnter;
@@ -1155,8 +1152,7 @@ struct MsLane {
                 pre = 0;
                 if (lim < 64) break;
             }
-#if NTC_JOINT
-            if (jy != 0xFFFFFFFFu) {
+            if (kJoint && jy != 0xFFFFFFFFu) {
                 // joint run over a multi-node interval [l, r) (its first and last nodes followed
                 // along their paths): the interval at p + m - 1 is [node at j + m, node at jy + m
                 // + 1) and the extension at p + m goes on from it (see note_path)
@@ -1173,7 +1169,6 @@ struct MsLane {
                 jy = 0xFFFFFFFFu;
                 m = 0;  // on into the EXT block below, in this same call
             }
-#endif
             if (m > 0) {
                 put_entry(b, p, j + 1, m, (d + 1 < k ? d + 1 : k) | kRunTag);
                 p += m;
@@ -1567,6 +1562,7 @@ struct MsLane {
     }
 };
 #undef jy
+using MsLane = MsLaneT<true>;
 
 // (d, S) of every position of one read (diagnostics: ntc_debug_matching_statistics)
 NTC_HD void read_ms(const DevIndex &ix, const uint64_t *Q, uint64_t qo, const Entry *E, uint32_t ne,

@@ -214,6 +214,7 @@ __device__ __forceinline__ uint32_t parse_one(const Enc4Args &a, uint64_t r) {
 #ifndef NTC_MS_WAVES
 #define NTC_MS_WAVES 6  // waves per SIMD k_ms4 is compiled for (VGPR <= 80: the batched SCAN loads fit unspilled)
 #endif
+template <bool kJoint>
 __global__ __launch_bounds__(256, NTC_MS_WAVES) void k_ms4(Enc4Args a) {
     const uint32_t lane = threadIdx.x & 63;
     if (*a.status != ~0ull) return;  // a read failed to pack: nothing to do
@@ -224,7 +225,7 @@ __global__ __launch_bounds__(256, NTC_MS_WAVES) void k_ms4(Enc4Args a) {
     const WaveQueue wq(a.counter, a.n_reads);
     __shared__ uint4 s_stage[(kStageSlots + 1) * 256];  // MsLane::put_entry write combining, entry 0
     const MsBufs bufs{a.Q, a.E, a.Ed, 1, s_stage, kEntSlot};  // dense slots read-major
-    MsLane st;
+    MsLaneT<kJoint> st;
     for (;;) {
         // ---- hand idle lanes the next reads (wave-uniform control flow) ----------------
         const uint64_t want = __ballot(idle);
@@ -865,9 +866,11 @@ void launch_debug_gather4(const Enc4Args &a, uint32_t *d_out, uint32_t *s_out, h
 
 int ms4_blocks_per_cu() {
     int blocks = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_ms4, 256, 0) != hipSuccess || blocks <= 0)
+    int bj = 0;  // both builds: the grid must fit either
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_ms4<false>, 256, 0) != hipSuccess || blocks <= 0 ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&bj, k_ms4<true>, 256, 0) != hipSuccess || bj <= 0)
         blocks = 4;
-    return blocks;
+    return bj < blocks ? bj : blocks;
 }
 
 void launch_encode4(const Enc4Args &a, uint64_t total, uint32_t ms_blocks, hipStream_t s, hipEvent_t ev_ms_begin,
@@ -875,7 +878,10 @@ void launch_encode4(const Enc4Args &a, uint64_t total, uint32_t ms_blocks, hipSt
     hipLaunchKernelGGL(k_pack, grid_for((total + 31) / 32), dim3(256), 0, s, a, total);
     (void)hipEventRecord(ev_ms_begin, s);
     const uint64_t need = (a.n_reads + 255) / 256;
-    hipLaunchKernelGGL(k_ms4, dim3(need < ms_blocks ? (uint32_t)need : ms_blocks), dim3(256), 0, s, a);
+    if (a.ix.joint)
+        hipLaunchKernelGGL(k_ms4<true>, dim3(need < ms_blocks ? (uint32_t)need : ms_blocks), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_ms4<false>, dim3(need < ms_blocks ? (uint32_t)need : ms_blocks), dim3(256), 0, s, a);
     (void)hipEventRecord(ev_ms_end, s);
     hipLaunchKernelGGL(k_parse4, grid_for(a.n_reads), dim3(256), 0, s, a);
 }

@@ -89,6 +89,11 @@ bool load(const ntc_index_view *v, HostIndex &hx, Derived &dv, std::vector<WalkE
             d.rank2 = r2.data();
         }
     }
+    {  // joint path runs (MsLaneT<true>) unless NTC_EMU_JOINT=0: the upload turns them on only for
+       // fragmented path covers, the emulation checks them on every index
+        const char *ej = getenv("NTC_EMU_JOINT");
+        d.joint = (ej && atoi(ej) == 0) ? 0u : 1u;
+    }
     const uint32_t U = tab_u ? std::min<uint32_t>(tab_u, std::min<uint32_t>(hx.k, kTabMaxU)) : default_tab_u(hx.n, hx.k);
     d.tab_u = U;
     d.tab_pos = (dv.has_paths && U >= dv.t_jump && hx.n < (1ULL << 31)) ? 1u : 0u;
@@ -158,9 +163,8 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
                 std::vector<Entry> E4(len + 1);
                 std::vector<uint64_t> R4(len + 1);
                 rc = pack_read(bases + offs[r], len, Q.data(), d.absent);
-                MsLane ms;
                 uint32_t ne = 0;
-                if (rc == 0) {
+                auto run = [&](auto &ms) {
                     trace_phase(0);
                     ms.start(d, 0, len);
                     const MsBufs bufs{Q.data(), E4.data(), E4.data(), 1};
@@ -170,6 +174,15 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
                         if (st == 1) break;
                     }
                     ne = ms.ne;
+                };
+                if (rc == 0) {
+                    if (d.joint) {
+                        MsLaneT<true> ms;
+                        run(ms);
+                    } else {
+                        MsLaneT<false> ms;
+                        run(ms);
+                    }
                 }
                 trace_phase(1);
                 if (rc == 0) rc = parse_read(d, Q.data(), 0, E4.data(), ne, len, R4.data(), R4.data());

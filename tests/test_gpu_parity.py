@@ -66,8 +66,9 @@ def test_gpu_v2_repetitive_genome_and_ms(ctx):
             u[int(rng.integers(0, len(u)))] = b"ACGT"[int(rng.integers(0, 4))]
         parts.append(bytes(u) + nt.synth_genome(int(rng.integers(1, 1 << 30)), 97).tobytes())
     genome = np.frombuffer(b"".join(parts), dtype=np.uint8)
-    for k, variant in ((31, 4), (91, 4), (91, 1)):
+    for k, variant, joint in ((31, 4, 1), (91, 4, 1), (91, 4, 0), (91, 1, -1)):
         ix = nt.Index.build([genome.tobytes()], k)
+        ctx.set_option("joint", joint)  # repeats: multi-node intervals, joint path runs on and off
         ctx.upload(ix)
         ctx.set_option("encode_variant", variant)
         assert ctx.get_option("n_paths") > 0
@@ -83,6 +84,7 @@ def test_gpu_v2_repetitive_genome_and_ms(ctx):
             assert np.array_equal(d[r * 150:(r + 1) * 150], od)
             assert np.array_equal(s[r * 150:(r + 1) * 150].astype(np.uint64), olo)
     ctx.set_option("encode_variant", 4)
+    ctx.set_option("joint", -1)
 
 
 def test_gpu_ragged_and_edge_lengths(ctx):
@@ -190,20 +192,24 @@ def test_gpu_full_scale_roundtrip(k):
     ctx.close()
 
 
-@pytest.mark.parametrize("ext2", [0, 1])
-def test_gpu_strain_collection(ext2):
+@pytest.mark.parametrize("ext2,joint", [(0, -1), (1, -1), (0, 0)])
+def test_gpu_strain_collection(ext2, joint):
     """An index of a genome + 3 strains at 1 % substitutions (fragmented path cover, many
     branching nodes): 300k reads from the collection round-trip exactly, 10k bit-exact vs
     the oracle (bench.py's S91 config at reduced size); also with the two-character rank
-    chunks (ctx option ext2)."""
+    chunks (ctx option ext2), and without joint path runs (ctx option joint; auto turns
+    them on for this cover).  (d, S) of every position of a read sample equals the
+    oracle's matching statistics."""
     genome = nt.synth_genome(1, 2_000_000)
     strains = nt.synth_strains(genome, 3, 3, 10_000)
     texts = [genome] + [strains[i] for i in range(3)]
     ix = nt.Index.build([t.tobytes() for t in texts], 91)
     ctx = nt.GpuContext(0)
     ctx.set_option("ext2", ext2)
+    ctx.set_option("joint", joint)
     ctx.upload(ix)
     assert ctx.get_option("ext2") == ext2
+    assert ctx.get_option("joint") == (1 if joint < 0 else joint)
     assert ctx.get_option("n_paths") > 1000
     coll = np.concatenate(texts)
     n, L = 300_000, 150
@@ -216,6 +222,11 @@ def test_gpu_strain_collection(ext2):
     m = 10_000
     exp, eoff = orc.encode(reads[: m * L], offs[: m + 1])
     assert np.array_equal(recs[: int(roff[m])], exp)
+    d, s = ctx.matching_statistics(reads[:500 * L], offs[:501])
+    for r in range(0, 500, 5):
+        od, olo = orc.ms(reads[r * L:(r + 1) * L].tobytes())
+        assert np.array_equal(d[r * L:(r + 1) * L], od), r
+        assert np.array_equal(s[r * L:(r + 1) * L].astype(np.uint64), olo), r
     ctx.close()
 
 

@@ -205,15 +205,17 @@ def test_emulated_small_k_reference_panic_status(k, glen):
         assert np.array_equal(got, exp) and np.array_equal(goff, eoff)
 
 
+@pytest.mark.parametrize("joint", ["1", "0"])
 @pytest.mark.parametrize("ext2", ["1", "0"])
 @pytest.mark.parametrize("k", [31, 91])
-def test_emulated_strain_collection(k, ext2, monkeypatch):
+def test_emulated_strain_collection(k, ext2, joint, monkeypatch):
     """A genome + 5 strains at 1 % substitutions (multi-node MS intervals over long climbs,
     short unitigs): records equal the oracle's with and without the two-character rank
     lines (NTC_EMU_EXT2), and decode back exactly.  The climbs run as joint path runs over
     the interval's first and last nodes (MsLane::note_single): (d, S) of every position of a
     read sample equals the oracle's matching statistics."""
     monkeypatch.setenv("NTC_EMU_EXT2", ext2)
+    monkeypatch.setenv("NTC_EMU_JOINT", joint)
     g = nt.synth_genome(17, 150_000)
     st = nt.synth_strains(g, 3, 5, 10_000)
     texts = [g] + [st[i] for i in range(5)]
