@@ -319,7 +319,17 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("gloo")  # barriers, max over ranks, parity verdicts
+        # gloo's native "[Gloo] Rank i is connected to ..." lines go to fd 1; stdout must carry
+        # rank 0's JSON line alone, so the native side writes to stderr while the group forms
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo")  # barriers, max over ranks, parity verdicts
+            dist.barrier()
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
     device = 0
     if not args.dry_run:
         ndev = torch.cuda.device_count()  # a box with fewer GPUs than ranks (rehearsal): ranks share

@@ -16,8 +16,8 @@ def _run(args):
     p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, capture_output=True, text=True,
                        timeout=600, env=env, cwd=REPO)
     assert p.returncode == 0, p.stderr[-3000:]
-    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, p.stdout
+    lines = [l for l in p.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), p.stdout  # stdout: the JSON line alone
     return json.loads(lines[0]), p.stderr
 
 
