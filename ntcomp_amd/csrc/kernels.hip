@@ -75,6 +75,76 @@ __device__ __forceinline__ uint32_t pack4(uint32_t w, uint32_t absent_tab, bool 
     return (u | (u >> 12)) & 0xFFu;
 }
 
+#ifndef NTC_PACK16
+#define NTC_PACK16 1  // k_pack: 16 characters per thread (one coalesced uint4 load, one u32 store)
+#endif
+#if NTC_PACK16
+// Thread t packs characters [16t, 16t + 16) into the 32-bit half t of the 2-bit stream (Q
+// word t / 2, low half for even t).  A 16-byte aligned batch start (uniform over the grid)
+// takes the fast path: one aligned uint4 load per lane, a wave reading 1 KB contiguous;
+// otherwise two aligned loads are realigned per byte.  Halves past the batch's last
+// character, up to the end of its last Q word, are written as zero.  `bound` (>= the
+// batch's bases) only sizes the grid; the true count is offs[n] - offs[0].
+__global__ __launch_bounds__(256) void k_pack(Enc4Args a, uint64_t bound) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t x0 = t * 16;
+    const uint64_t total = a.offs[a.n_reads] - a.offs[0];
+    (void)bound;
+    if (t >= 2 * ((total + 31) / 32)) return;
+    uint32_t *Q32 = reinterpret_cast<uint32_t *>(a.Q);
+    if (x0 >= total) {
+        Q32[t] = 0u;
+        return;
+    }
+    const uint8_t *B = a.bases + a.offs[0];
+    const uint32_t absent = a.ix.absent;
+    const uint32_t n = total - x0 < 16 ? (uint32_t)(total - x0) : 16u;
+    if ((((uintptr_t)B) & 15) == 0 && n == 16) {
+        const uint32_t absent_tab = (absent & 1u) | ((absent >> 1) & 1u) << 8 | ((absent >> 2) & 1u) << 16 |
+                                    ((absent >> 3) & 1u) << 24;
+        const uint4 v = *reinterpret_cast<const uint4 *>(B + x0);
+        bool ok = true;
+        Q32[t] = pack4(v.x, absent_tab, ok) | pack4(v.y, absent_tab, ok) << 8 | pack4(v.z, absent_tab, ok) << 16 |
+                 pack4(v.w, absent_tab, ok) << 24;
+        if (!ok) pack_report_bad(a, B, x0, 16, absent);
+        return;
+    }
+    // unaligned start or the last partial chunk: 16-byte blocks never cross a page, so
+    // reading a whole block that holds the batch's last byte stays inside its allocation
+    const uint8_t *end = B + total;
+    const uint8_t *p = B + x0;
+    const uintptr_t al = (uintptr_t)p & ~(uintptr_t)15;
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 15);
+    uint32_t w[8];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const uint8_t *blk = (const uint8_t *)(al + 16 * q);
+        if (blk < end) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(blk);
+            w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+        } else {
+            w[4 * q] = w[4 * q + 1] = w[4 * q + 2] = w[4 * q + 3] = 0x41414141u;
+        }
+    }
+    uint32_t acc = 0;
+    bool bad = false;
+#pragma unroll
+    for (uint32_t c = 0; c < 16; c++) {
+        const uint32_t o = sh + c;
+        const uint32_t word = o >> 2;
+        uint32_t wv = w[0];
+#pragma unroll
+        for (uint32_t q = 1; q < 8; q++) wv = (word == q) ? w[q] : wv;
+        const uint32_t ch = (wv >> (8 * (o & 3))) & 0xFFu;
+        if (c < n) {
+            bad |= !is_acgt(ch) || ((absent >> fast_code(ch)) & 1u);
+            acc |= fast_code(ch) << (2 * c);
+        }
+    }
+    Q32[t] = acc;
+    if (bad) pack_report_bad(a, B, x0, n, absent);
+}
+#else
 // Thread b packs characters [32b, 32b + 32).  `bound` (>= the batch's bases) only sizes
 // the grid; the true count is offs[n] - offs[0].  A 16-byte aligned batch start (uniform
 // over the grid) takes the fast path: two aligned uint4 loads, consecutive lanes reading
@@ -137,6 +207,7 @@ __global__ __launch_bounds__(256) void k_pack(Enc4Args a, uint64_t bound) {
     a.Q[b] = acc;
     if (bad) pack_report_bad(a, B, x0, n, absent);
 }
+#endif
 
 constexpr uint32_t kPoolChunk = 64;
 
@@ -279,6 +350,12 @@ __global__ __launch_bounds__(256, NTC_PARSE_WAVES) void k_parse4(Enc4Args a) {
 }
 
 // record offsets = scanned wave totals + a wave scan of the reads' counts
+#ifndef NTC_EMIT_STAGE
+#define NTC_EMIT_STAGE 1  // k_emit4 gathers a wave's records in LDS and stores them coalesced
+#endif
+#if NTC_EMIT_STAGE
+constexpr uint32_t kEmitStage = 64 * kRecSlot;  // records a wave stages (more: direct stores)
+#endif
 __global__ __launch_bounds__(256) void k_emit4(Enc4Args a, const uint64_t *wave_off, uint64_t *rec_offsets,
                                                uint64_t *out, uint64_t capacity) {
     const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
@@ -302,16 +379,44 @@ __global__ __launch_bounds__(256) void k_emit4(Enc4Args a, const uint64_t *wave_
         const uint32_t t = __shfl_up(inc, o, 64);
         if (lane >= (uint32_t)o) inc += t;
     }
-    if (r >= a.n_reads) return;
     const uint64_t off = woff + (inc - cnt);
-    rec_offsets[r] = off;
-    if (r + 1 == a.n_reads) rec_offsets[r + 1] = off + cnt;
+    if (r < a.n_reads) {
+        rec_offsets[r] = off;
+        if (r + 1 == a.n_reads) rec_offsets[r + 1] = off + cnt;
+    }
+    const uint32_t ns = cnt < kRecSlot ? cnt : kRecSlot;
+#if NTC_EMIT_STAGE
+    // The wave's records are one contiguous range [woff, woff + total) of the output.  Each
+    // lane's records sit ~31 B apart from its neighbours', so stores straight from the lanes
+    // touch every line once per record index; gathered in LDS, the wave stores the range as
+    // consecutive 8-byte words (512 B per instruction).
+    __shared__ uint64_t s_rec[4][kEmitStage];
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t total = __shfl(inc, 63, 64);
+    const bool staged = st == ~0ull && total <= kEmitStage && woff + total <= capacity;  // wave-uniform
+    if (staged && r < a.n_reads) {
+        uint64_t *dst = s_rec[wv] + (inc - cnt);
+#pragma unroll
+        for (uint32_t j = 0; j < kEmitEarly; j++)
+            if (j < ns) dst[j] = early[j];
+        for (uint32_t j = kEmitEarly; j < ns; j++) dst[j] = slot[(uint64_t)j * a.n_reads];
+        if (cnt > kRecSlot) {
+            const uint64_t *spill = a.R + (a.offs[r] - a.offs[0]);
+            for (uint32_t j = kRecSlot; j < cnt; j++) dst[j] = spill[j];
+        }
+    }
+    __syncthreads();
+    if (staged) {
+        for (uint32_t i = lane; i < total; i += 64) out[woff + i] = s_rec[wv][i];
+        return;
+    }
+#endif
+    if (r >= a.n_reads) return;
     if (st != ~0ull) return;  // a read failed: the call reports that, no records
     if (off + cnt > capacity) {
         atomicMin(a.status, (unsigned long long)((r << 8) | (uint64_t)kErrCapacity));
         return;
     }
-    const uint32_t ns = cnt < kRecSlot ? cnt : kRecSlot;
 #pragma unroll
     for (uint32_t j = 0; j < kEmitEarly; j++)
         if (j < ns) out[off + j] = early[j];
@@ -875,7 +980,7 @@ int ms4_blocks_per_cu() {
 
 void launch_encode4(const Enc4Args &a, uint64_t total, uint32_t ms_blocks, hipStream_t s, hipEvent_t ev_ms_begin,
                     hipEvent_t ev_ms_end) {
-    hipLaunchKernelGGL(k_pack, grid_for((total + 31) / 32), dim3(256), 0, s, a, total);
+    hipLaunchKernelGGL(k_pack, grid_for((total + 31) / 32 * (NTC_PACK16 ? 2 : 1)), dim3(256), 0, s, a, total);
     (void)hipEventRecord(ev_ms_begin, s);
     const uint64_t need = (a.n_reads + 255) / 256;
     if (a.ix.joint)
