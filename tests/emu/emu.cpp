@@ -102,6 +102,10 @@ bool load(const ntc_index_view *v, HostIndex &hx, Derived &dv, std::vector<WalkE
     d.tab_bits = bits.data();
     d.filt_f = fbits.empty() ? 0u : filter_level(U);
     d.filt_bits = fbits.empty() ? nullptr : fbits.data();
+    if (const char *ef = getenv("NTC_EMU_FILTER"); ef && atoi(ef) == 0) {  // as the upload's filter=0 (S91 auto)
+        d.filt_f = 0;
+        d.filt_bits = nullptr;
+    }
     d.tab_u = U;
     d.pair_w = nullptr;
     const char *pe = getenv("NTC_EMU_PAIR_BYTES");
