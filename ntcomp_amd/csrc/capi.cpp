@@ -522,7 +522,7 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     }
     // suffix table, levels 1..U, built on the device from the rank lines
     uint32_t U = ctx->tab_u_opt ? std::min<uint32_t>(ctx->tab_u_opt, std::min<uint32_t>(hx.k, kTabMaxU))
-                                : default_tab_u(n, hx.k);
+                                : default_tab_u(n, hx.k, hx.lcs.data());
     const uint32_t F = filter_level(U);
     void *d_tab, *d_bits, *d_fbits = nullptr;
     if ((rc = dalloc(tab_base(U + 1) * sizeof(uint2), &d_tab))) return rc;

@@ -51,7 +51,7 @@ inline uint64_t path_cover_hash(const uint4 *pstream, const uint32_t *colex_at, 
 // dummy[z] = 1 when node z's k-mer contains '$' (BFS from the root, depth < k).
 std::vector<uint8_t> dummy_nodes(const HostIndex &ix, const Derived &dv);
 // Suffix-table depth U for an index of n nodes (encode_core.h "Suffix table").
-uint32_t default_tab_u(uint64_t n, uint32_t k);
+uint32_t default_tab_u(uint64_t n, uint32_t k, const uint8_t *lcs = nullptr);
 // Host build of the suffix table levels 1..U (test emulation; the GPU builds it on device).
 // (bits: presence of level U; fbits: presence of the filter level, or empty).
 void build_tab_host(const DevIndex &d, uint32_t U, std::vector<uint2> &tab, std::vector<uint32_t> &bits,

@@ -447,7 +447,8 @@ constexpr uint32_t kTabShort = 0xFFFFFF00u;  // y >= kTabShort: absent, m = y & 
 constexpr uint32_t kTabPos = 0x80000000u;    // top level, tab_pos: y = kTabPos | path position
                                              // of the single node x (interval [x, x + 1))
 constexpr uint32_t kTabMaxU = 15;            // 4^15 entries x 8 B (8.6 GB) at the top level (tab_u option)
-constexpr uint32_t kTabDefaultMaxU = 14;     // default cap: U = 15 measured +1 % on S91 for 4x the table
+constexpr uint32_t kTabDefaultMaxU = 14;     // default cap, one deeper past kTabMaxDensity (default_tab_u)
+constexpr double kTabMaxDensity = 0.25;      // distinct U-mers / 4^U
 
 NTC_HD uint64_t tab_base(uint32_t u) { return ((1ULL << (2 * u)) - 4) / 3; }
 NTC_HD bool tab_long(uint2 e) { return e.y < kTabShort; }

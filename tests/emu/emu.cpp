@@ -94,7 +94,7 @@ bool load(const ntc_index_view *v, HostIndex &hx, Derived &dv, std::vector<WalkE
         const char *ej = getenv("NTC_EMU_JOINT");
         d.joint = (ej && atoi(ej) == 0) ? 0u : 1u;
     }
-    const uint32_t U = tab_u ? std::min<uint32_t>(tab_u, std::min<uint32_t>(hx.k, kTabMaxU)) : default_tab_u(hx.n, hx.k);
+    const uint32_t U = tab_u ? std::min<uint32_t>(tab_u, std::min<uint32_t>(hx.k, kTabMaxU)) : default_tab_u(hx.n, hx.k, hx.lcs.data());
     d.tab_u = U;
     d.tab_pos = (dv.has_paths && U >= dv.t_jump && hx.n < (1ULL << 31)) ? 1u : 0u;
     build_tab_host(d, U, tab, bits, fbits);
