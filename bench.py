@@ -427,6 +427,7 @@ def main():
                 f"of a {args.genome_bp / 1e6:g} Mbp synthetic genome (+revcomp), k={k}"
                 + (f"; {world} GPUs x {n} = {world * n} reads" if world > 1 else ""))
         cfg = dict(base_cfg, workload=wl_c, index_nodes=index.n, records_per_gpu=n_recs,
+                   suffix_table_u=None if args.dry_run else ctx.get_option("tab_u"),
                    parallelism=f"reads sharded over {world} GPU(s), index replicated, no collective")
         if enc is not None:
             el, kms = enc
@@ -503,6 +504,7 @@ def main():
         if not args.dry_run:
             encode_pass(ctx, sh, check=True)
             s["config"]["records_per_gpu"] = sum(b["n_recs"] for b in sh.batches)
+            s["config"]["suffix_table_u"] = ctx.get_option("tab_u")
             s["config"]["n_paths"] = ctx.get_option("n_paths")
             s["config"]["scan_filter"] = bool(ctx.get_option("filter"))
             s["config"]["joint_runs"] = bool(ctx.get_option("joint"))
