@@ -582,6 +582,9 @@ constexpr uint32_t kScanExact = 4;   // filter candidates tested exactly per SCA
 #ifndef NTC_PAIR_TESTS
 #define NTC_PAIR_TESTS 4  // candidate pairs tested per SCAN with pair words
 #endif
+#ifndef NTC_SEEK_BS
+#define NTC_SEEK_BS 1  // EntryView::seek: binary search instead of a forward scan
+#endif
 constexpr uint32_t kJointPending = 0xFFFFFFFEu;  // joint run wanted, path positions not loaded yet
 
 // ======================================================================================
@@ -754,6 +757,26 @@ struct EntryView {
         // every entry covers >= 1 position, so entry e - (p - x) starts at or before x
         int32_t g = e - (int32_t)(cur.p - x);
         if (g < 0) g = 0;
+#if NTC_SEEK_BS
+        // binary search in [g, e): run entries cover many positions each (joint runs on
+        // strain collections), so the bound g is often far below the answer and a forward
+        // scan from it is a long chain of dependent loads
+        int32_t hi = e;
+        Entry eg{0, 0, 0, 0};
+        bool have = false;
+        while (hi - g > 1) {
+            const int32_t mid = (g + hi) >> 1;
+            const Entry em = at(mid);
+            if (em.p <= x) {
+                g = mid;
+                eg = em;
+                have = true;
+            } else {
+                hi = mid;
+            }
+        }
+        if (!have) eg = at(g);
+#else
         Entry eg = at(g);
         while (g + 1 < e) {
             const Entry nx = at(g + 1);
@@ -761,6 +784,7 @@ struct EntryView {
             g++;
             eg = nx;
         }
+#endif
         e = g;
         cur = eg;
     }
