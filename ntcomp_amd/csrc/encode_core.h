@@ -932,10 +932,10 @@ struct MsLaneT {
     uint32_t len, p, d, l, r, j, ne, mode, hi, lo, l1, r1, bl, bR;
     uint32_t gj, ge;    // last run break: at position ge, node before it at path position gj (ge = 0: none)
     uint32_t vfy;       // the next run first verifies the vfy characters ending at node j
-    // Joint run (note_single): path position of the interval's last node, else kNoJoint.  It
-    // lives in l1, which only the binary-search probes use (written before read in kModeBs);
-    // a separate field costs k_ms4 a wave of occupancy (72 VGPRs is the 7-wave limit).
-#define jy l1
+    // Joint run (note_single): path position of the interval's last node, else 0xFFFFFFFF.
+    // It lives in l1, which only the binary-search probes use (written before read in
+    // kModeBs); a separate field costs k_ms4 a wave of occupancy (72 VGPRs is the 7-wave limit).
+    NTC_HD uint32_t &jy() { return l1; }
     bool try_run;
 
     NTC_HD void start(const DevIndex &ix, uint64_t qo_, uint32_t len_, uint64_t rid_ = 0) {
@@ -948,7 +948,7 @@ struct MsLaneT {
         mode = kModeFirst; lo = r1 = bl = bR = 0;
         hi = kScanW;  // SCAN width cap (hi is free while scanning)
         gj = ge = vfy = 0;
-        jy = 0xFFFFFFFFu;
+        jy() = 0xFFFFFFFFu;
         try_run = false;
     }
     NTC_HD void window(const MsBufs &b, uint32_t from) {
@@ -1052,14 +1052,14 @@ struct MsLaneT {
     // the entries are ordinary run entries on l's path
     NTC_HD void note_single(const DevIndex &ix) {
         j = 0xFFFFFFFFu;
-        jy = 0xFFFFFFFFu;
+        jy() = 0xFFFFFFFFu;
         if (ix.has_paths && r == l + 1 && d >= ix.t_jump) {
             NTC_TOUCH(kTrPon, ix.pos_of_node + l);
             j = ix.pos_of_node[l];
             try_run = j != 0xFFFFFFFFu;
         }
         else if (kJoint && ix.has_paths && r > l + 1 && d >= ix.t_jump && d + 1 < ix.k) {
-            jy = kJointPending;  // both path positions are looked up by the run block (step)
+            jy() = kJointPending;  // both path positions are looked up by the run block (step)
             try_run = true;
         }
     }
@@ -1088,7 +1088,7 @@ struct MsLaneT {
         p = x + 1;
         mode = kModeExt;
         if (ix.tab_pos) {  // the table already holds the path position (d = U >= t_jump)
-            jy = 0xFFFFFFFFu;
+            jy() = 0xFFFFFFFFu;
             j = jj;
             try_run = jj != 0xFFFFFFFFu;
         } else {
@@ -1101,13 +1101,13 @@ struct MsLaneT {
         const uint32_t k = ix.k, U = ix.tab_u;
         const uint64_t *Q = b.Q;
         if (p >= len) return 1;
-        if (kJoint && try_run && jy == kJointPending) {
+        if (kJoint && try_run && jy() == kJointPending) {
             NTC_TOUCH(kTrPon, ix.pos_of_node + l);
             NTC_TOUCH(kTrPon, ix.pos_of_node + r - 1);
             j = ix.pos_of_node[l];
-            jy = ix.pos_of_node[r - 1];
-            if (j == 0xFFFFFFFFu || jy == 0xFFFFFFFFu) {
-                jy = 0xFFFFFFFFu;
+            jy() = ix.pos_of_node[r - 1];
+            if (j == 0xFFFFFFFFu || jy() == 0xFFFFFFFFu) {
+                jy() = 0xFFFFFFFFu;
                 try_run = false;  // on with the extension at p
             }
         }
@@ -1152,11 +1152,11 @@ struct MsLaneT {
                 const uint32_t ib = ~vb ? (uint32_t)__builtin_ctz(~vb) : 32u;
                 if (ib < lb) lb = ib;
                 uint32_t lim = la == 32 ? 32 + lb : la;
-                if (kJoint && jy != 0xFFFFFFFFu) {  // joint run: the interval's last node follows its path too
+                if (kJoint && jy() != 0xFFFFFFFFu) {  // joint run: the interval's last node follows its path too
 #if defined(__HIP_DEVICE_COMPILE__)
                     __asm__ volatile("" ::: "memory");  // after lim: the loads below must not overlap the x path's
 #endif
-                    const uint64_t Ty = (uint64_t)jy + k + m;
+                    const uint64_t Ty = (uint64_t)jy() + k + m;
                     NTC_TOUCH(kTrPst, ix.pstream + (Ty >> 5));
                     NTC_TOUCH(kTrPst, ix.pstream + (Ty >> 5) + 2);
                     const uint4 h0 = ld4<4>(ix.pstream + (Ty >> 5)), h1 = ld4<4>(ix.pstream + (Ty >> 5) + 1),
@@ -1177,7 +1177,7 @@ struct MsLaneT {
                 pre = 0;
                 if (lim < 64) break;
             }
-            if (kJoint && jy != 0xFFFFFFFFu) {
+            if (kJoint && jy() != 0xFFFFFFFFu) {
                 // joint run over a multi-node interval [l, r) (its first and last nodes followed
                 // along their paths): the interval at p + m - 1 is [node at j + m, node at jy + m
                 // + 1) and the extension at p + m goes on from it (see note_path)
@@ -1185,13 +1185,13 @@ struct MsLaneT {
                     put_entry(b, p, j + 1, m, (d + 1 < k ? d + 1 : k) | kRunTag);
                     p += m;
                     d = d + m < k ? d + m : k;
-                    if (p >= len) { jy = 0xFFFFFFFFu; return 1; }
+                    if (p >= len) { jy() = 0xFFFFFFFFu; return 1; }
                     NTC_TOUCH(kTrColex, ix.colex_at + j + m);
-                    NTC_TOUCH(kTrColex, ix.colex_at + jy + m);
+                    NTC_TOUCH(kTrColex, ix.colex_at + jy() + m);
                     l = ix.colex_at[j + m] & 0x7FFFFFFFu;
-                    r = (ix.colex_at[jy + m] & 0x7FFFFFFFu) + 1;
+                    r = (ix.colex_at[jy() + m] & 0x7FFFFFFFu) + 1;
                 }
-                jy = 0xFFFFFFFFu;
+                jy() = 0xFFFFFFFFu;
                 m = 0;  // on into the EXT block below, in this same call
             }
             if (m > 0) {
@@ -1353,7 +1353,7 @@ struct MsLaneT {
                     if (((single >> xi) & 1u) && ix.tab_pos && ge != 0 && x - ge - U <= NTC_GUESS_SLACK &&
                         x >= ge + U && jg < ix.path_len) {
                         j = jg;
-                        jy = 0xFFFFFFFFu;
+                        jy() = 0xFFFFFFFFu;
                         d = U;
                         p = x + 1;
                         vfy = U;
@@ -1586,7 +1586,6 @@ struct MsLaneT {
         return 0;
     }
 };
-#undef jy
 using MsLane = MsLaneT<true>;
 
 // (d, S) of every position of one read (diagnostics: ntc_debug_matching_statistics)
