@@ -119,6 +119,9 @@ bool load(const ntc_index_view *v, HostIndex &hx, Derived &dv, std::vector<WalkE
 }  // namespace
 
 // out[0] = path-cover hash, out[1] = text length, out[2] = paths (host build_paths)
+// the upload's default suffix-table depth (derived.cpp default_tab_u) for n nodes with this LCS
+extern "C" uint32_t emu_default_tab_u(uint64_t n, uint32_t k, const uint8_t *lcs) { return default_tab_u(n, k, lcs); }
+
 extern "C" int emu_path_cover(const ntc_index_view *v, uint64_t *out) {
     HostIndex hx;
     Derived dv;

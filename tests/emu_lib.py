@@ -93,6 +93,15 @@ def emu_path_cover(n, k, rows, C, lcs):
     return int(out[0]), int(out[1]), int(out[2])
 
 
+def emu_default_tab_u(k, lcs):
+    """derived.cpp default_tab_u: the suffix-table depth the upload picks for this LCS array."""
+    lib = emu_lib()
+    lib.emu_default_tab_u.restype = ctypes.c_uint32
+    lib.emu_default_tab_u.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p]
+    lcs = np.ascontiguousarray(lcs, dtype=np.uint8)
+    return int(lib.emu_default_tab_u(len(lcs), k, lcs.ctypes.data))
+
+
 def emu_wave_modes(n, k, rows, C, lcs, bases, offs):
     """k_ms4 wave divergence statistics (tests/emu/emu.cpp emu_wave_modes)"""
     v, keep = make_view(n, k, rows, C, lcs)

@@ -233,3 +233,20 @@ def test_emulated_strain_collection(k, ext2, joint, monkeypatch):
         assert np.array_equal(s[r * L:(r + 1) * L].astype(np.uint64), olo), r
     out, oo = emu_decode(ix.n, k, ix.rows, ix.C, ix.lcs, got)
     assert np.array_equal(out, reads)
+
+
+def test_default_suffix_table_depth_follows_umer_density():
+    """The upload's default depth (derived.cpp default_tab_u): U = min(k, 14, ceil(log4 n) + 2),
+    one level deeper when the distinct 14-mers (nodes whose LCS with their colex predecessor is
+    < 14) exceed 25 % of 4^14, as for a 100 Mbp genome (53 %); a strain collection of as many
+    nodes that shares its 14-mers (S91: 8 %) keeps 14, and U never exceeds k."""
+    from emu_lib import emu_default_tab_u
+    n = 80_000_000  # > 0.25 * 4^14 = 67.1 M
+    dense = np.zeros(n, dtype=np.uint8)  # every node its own 14-mer
+    assert emu_default_tab_u(91, dense) == 15
+    assert emu_default_tab_u(14, dense) == 14
+    shared = np.full(n, 40, dtype=np.uint8)
+    shared[::8] = 0  # 10 M distinct 14-mers: 15 %
+    assert emu_default_tab_u(91, shared) == 14
+    assert emu_default_tab_u(91, np.zeros(10_000_000, dtype=np.uint8)) == 14  # C91-sized: ceil(log4 n) + 2 = 14
+    assert emu_default_tab_u(91, np.zeros(1000, dtype=np.uint8)) == 7
