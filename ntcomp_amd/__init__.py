@@ -39,7 +39,8 @@ EXPORTED = [
     "ntc_decode_status", "ntc_last_timing", "ntc_device_alloc", "ntc_device_free", "ntc_memcpy_h2d",
     "ntc_memcpy_d2h", "ntc_debug_matching_statistics", "ntc_build_index", "ntc_index_free",
     "ntc_index_view_of", "ntc_index_save", "ntc_index_save_as", "ntc_index_load", "ntc_synth_genome", "ntc_synth_strains", "ntc_synth_reads", "ntc_minimizer_keys",
-    "ntc_file_header", "ntc_write_block", "ntc_read_block", "ntc_buffer_free",
+    "ntc_file_header", "ntc_write_block", "ntc_read_block", "ntc_buffer_free", "ntc_pack_block",
+    "ntc_deflate_block", "ntc_pack_blocks_device", "ntc_encode_pack_batch",
     "ntc_fastx_open", "ntc_fastx_next_batch", "ntc_fastx_close", "ntc_fasta_format",
 ]
 
@@ -53,6 +54,20 @@ class NtcError(RuntimeError):
 class IndexView(ctypes.Structure):
     _fields_ = [("n_nodes", ctypes.c_uint64), ("k", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
                 ("rows", ctypes.c_void_p * 4), ("C", ctypes.c_uint64 * 4), ("lcs", ctypes.c_void_p)]
+
+
+class StreamMeta(ctypes.Structure):
+    _fields_ = [("num_u64", ctypes.c_uint64), ("encoded_size", ctypes.c_uint64), ("param", ctypes.c_uint64),
+                ("offset", ctypes.c_uint64)]
+
+
+class BlockMeta(ctypes.Structure):
+    """ntc_block_meta (include/ntcomp_codec.h): the four packed streams of one block."""
+    _fields_ = [("stream", StreamMeta * 4), ("num_records", ctypes.c_uint64), ("n_recs", ctypes.c_uint64),
+                ("status", ctypes.c_int32), ("reserved", ctypes.c_uint32)]
+
+
+DEFLATE_ENGINES = {"zlib": 0, "libdeflate": 1}
 
 
 class Timing(ctypes.Structure):
@@ -129,6 +144,11 @@ def lib():
         "ntc_read_block": (I, [P, u64, ctypes.POINTER(u64), ctypes.POINTER(P), ctypes.POINTER(u64),
                                ctypes.POINTER(u64)]),
         "ntc_buffer_free": (None, [P]),
+        "ntc_pack_block": (I, [P, u64, u64, ctypes.POINTER(BlockMeta), ctypes.POINTER(P), ctypes.POINTER(u64)]),
+        "ntc_deflate_block": (I, [ctypes.POINTER(BlockMeta), P, I, ctypes.POINTER(P), ctypes.POINTER(u64)]),
+        "ntc_pack_blocks_device": (I, [P, P, P, u64, u32, P, u64, P, ctypes.POINTER(u64)]),
+        "ntc_encode_pack_batch": (I, [P, P, P, u64, u32, P, ctypes.POINTER(P), ctypes.POINTER(u64),
+                                      ctypes.POINTER(i64)]),
         "ntc_fastx_open": (I, [ctypes.c_char_p, ctypes.POINTER(P)]),
         "ntc_fastx_next_batch": (I, [P, u64, u64, ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(u64)]),
         "ntc_fastx_close": (None, [P]),
@@ -343,6 +363,39 @@ class GpuContext:
                                                    n_reads, max_read_len, ctypes.c_void_p(d_recs), cap,
                                                    ctypes.c_void_p(d_roffs)), "ntc_encode_batch_device")
 
+    def pack_device(self, d_recs, d_roffs, n_reads, block_reads, d_payload, cap):
+        """GPU packer (ntc_pack_blocks_device) -> (list of BlockMeta, payload bytes used)."""
+        nb = (n_reads + block_reads - 1) // block_reads
+        metas = (BlockMeta * max(nb, 1))()
+        used = ctypes.c_uint64()
+        self._check(self.L.ntc_pack_blocks_device(self.h, ctypes.c_void_p(d_recs), ctypes.c_void_p(d_roffs), n_reads,
+                                                  block_reads, ctypes.c_void_p(d_payload), cap, metas,
+                                                  ctypes.byref(used)), "ntc_pack_blocks_device")
+        return list(metas)[:nb], int(used.value)
+
+    def encode_pack(self, bases, offsets, block_reads=65536):
+        """Reads -> packed blocks (ntc_encode_pack_batch): the records stay in HBM and the
+        GPU packer writes each block's four streams; returns (list of BlockMeta, payload
+        bytes) ready for deflate_block."""
+        bases = np.ascontiguousarray(bases, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        nreads = len(offsets) - 1
+        nb = (nreads + block_reads - 1) // block_reads
+        metas = (BlockMeta * max(nb, 1))()
+        out, used, bad = ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_int64(-1)
+        b = bases if len(bases) else np.zeros(1, dtype=np.uint8)
+        rc = self.L.ntc_encode_pack_batch(self.h, _p(b), _p(offsets), nreads, block_reads, metas, ctypes.byref(out),
+                                          ctypes.byref(used), ctypes.byref(bad))
+        if rc:
+            e = NtcError(rc, self.L.ntc_last_error(self.h).decode(errors="replace"))
+            e.bad_read = bad.value
+            raise e
+        try:
+            payload = ctypes.string_at(out.value, used.value) if used.value else b""
+        finally:
+            self.L.ntc_buffer_free(out)
+        return list(metas)[:nb], payload
+
     def encode_status(self):
         bad, n = ctypes.c_int64(-1), ctypes.c_uint64()
         self._check(self.L.ntc_encode_status(self.h, ctypes.byref(bad), ctypes.byref(n)), "ntc_encode_status")
@@ -436,6 +489,41 @@ def write_block(records, num_records):
     rc = lib().ntc_write_block(_p(recs), len(recs), num_records, ctypes.byref(out), ctypes.byref(n))
     if rc:
         raise NtcError(rc, "ntc_write_block")
+    try:
+        return ctypes.string_at(out.value, n.value)
+    finally:
+        lib().ntc_buffer_free(out)
+
+
+def pack_block(records, num_records):
+    """The part of write_block_to before deflate (split_encoded_dictionary + Rice /
+    minimal-binary coding, encode.rs:59-94,168-229) on the host -> (BlockMeta, payload
+    bytes).  meta.status = NTC_ERR_EMPTY_READ (3) for a block the reference drops."""
+    recs = np.ascontiguousarray(records, dtype=np.uint64)
+    meta, out, n = BlockMeta(), ctypes.c_void_p(), ctypes.c_uint64()
+    rc = lib().ntc_pack_block(_p(recs) if len(recs) else None, len(recs), num_records, ctypes.byref(meta),
+                              ctypes.byref(out), ctypes.byref(n))
+    if rc not in (0, 3):
+        raise NtcError(rc, "ntc_pack_block")
+    try:
+        return meta, (ctypes.string_at(out.value, n.value) if out.value else b"")
+    finally:
+        lib().ntc_buffer_free(out)
+
+
+def stream_payloads(meta, payload):
+    """The four streams' pre-deflate bytes of a packed block."""
+    return [bytes(payload[m.offset:m.offset + 8 * m.encoded_size]) for m in meta.stream]
+
+
+def deflate_block(meta, payload, engine="zlib"):
+    """Headers + gzip members of a packed block (the bytes write_block_to writes)."""
+    buf = np.frombuffer(payload, dtype=np.uint8) if len(payload) else np.zeros(1, dtype=np.uint8)
+    out, n = ctypes.c_void_p(), ctypes.c_uint64()
+    rc = lib().ntc_deflate_block(ctypes.byref(meta), _p(buf), DEFLATE_ENGINES[engine], ctypes.byref(out),
+                                 ctypes.byref(n))
+    if rc:
+        raise NtcError(rc, "ntc_deflate_block")
     try:
         return ctypes.string_at(out.value, n.value)
     finally:

@@ -11,69 +11,79 @@
 //   zip_block_contents                          lib.rs:320-368, decode.rs:41-149
 //   file header (4 x u64 = 32 zero bytes)       lib.rs:29-35,52-73
 //
+// write_block_to = pack (everything before deflate: ntc_pack_block here, or the GPU packer
+// ntc_pack_blocks_device in pack.hip) + deflate (ntc_deflate_block).  The packed streams
+// are pinned by tests/golden/make_codec_golden.py, an independent restatement.
+//
 // Restated dsi-bitstream semantics (not in the container; recalled):
 //   * BufBitWriter<BE, u64 words>: bits MSB-first into u64 words, last word zero-padded;
-//     words stored with to_ne_bytes (little-endian) (encode.rs:107-109).
+//     the writer hands words over as to_be(), encode.rs:107-109 emits to_ne_bytes
+//     (little-endian): on disk each word is big-endian, i.e. the MSB-first bit stream.
 //   * unary(n) = n zeros then a one; rice(n, b) = unary(n >> b) then the low b bits.
 //   * rice::log2_b(p) = ceil(log2(ln(phi) / -ln(1-p))), saturating at 0 (Rust `as usize`).
 //   * minimal_binary(v, max): l = floor(log2 max), limit = 2^(l+1) - max;
 //     v < limit -> v in l bits, else v + limit in l+1 bits.
 //   * gzip member like flate2's GzEncoder: 10-byte header (mtime 0, XFL 0, OS 255), raw
-//     deflate at level 6, CRC32 + ISIZE trailer.  Deflate bytes come from system zlib, so
-//     they inflate identically but are not byte-identical to zlib-rs (parity level F is
-//     unpinned).
+//     deflate at level 6, CRC32 + ISIZE trailer.  Deflate bytes come from system zlib (or
+//     libdeflate), so they inflate identically but are not byte-identical to zlib-rs
+//     (parity level F is unpinned).
+#include <dlfcn.h>
 #include <zlib.h>
 
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
 #include "../../include/ntcomp_codec.h"
+#include "codec_params.h"
 
 namespace {
 
 // ---- bit writer / reader (big-endian bit order in u64 words) -------------------------
-struct BitWriter {
-    std::vector<uint64_t> words;
-    uint64_t cur = 0;
-    int used = 0;  // bits used in cur (from the MSB)
-    void put(uint64_t v, int nbits) {  // the low nbits (<= 64) of v, most significant first
-        if (nbits <= 0) return;
-        if (nbits < 64) v &= (1ULL << nbits) - 1;
+// Writes into a caller-sized word array (exact sizes come from a counting pass).
+struct BitSink {
+    uint64_t *w;
+    uint64_t n = 0;    // complete words written
+    uint64_t acc = 0;  // bits in progress, from the MSB
+    int used = 0;      // 0..63
+    explicit BitSink(uint64_t *words) : w(words) {}
+    inline void put(uint64_t v, int nb) {  // v < 2^nb, nb <= 64
+        if (nb <= 0) return;
         const int room = 64 - used;
-        if (nbits <= room) {
-            cur |= (room == nbits) ? v : (v << (room - nbits));
-            used += nbits;
+        if (nb < room) {
+            acc |= v << (room - nb);
+            used += nb;
         } else {
-            const int lo = nbits - room;  // 1..63
-            cur |= v >> lo;
-            words.push_back(cur);
-            cur = v << (64 - lo);
+            const int lo = nb - room;  // 0..63 bits spill into the next word
+            w[n++] = acc | (lo ? v >> lo : v);
+            acc = lo ? v << (64 - lo) : 0;
             used = lo;
         }
-        if (used == 64) {
-            words.push_back(cur);
-            cur = 0;
-            used = 0;
-        }
     }
-    void unary(uint64_t n) {
-        while (n >= 64) {
-            put(0, 64);
-            n -= 64;
+    inline void zeros(uint64_t z) {  // z zero bits
+        uint64_t t = (uint64_t)used + z;
+        if (t >= 64) {
+            w[n++] = acc;
+            acc = 0;
+            t -= 64;
+            while (t >= 64) {
+                w[n++] = 0;
+                t -= 64;
+            }
         }
-        if (n) put(0, (int)n);
-        put(1, 1);
+        used = (int)t;
     }
-    std::vector<uint64_t> finish() {
+    uint64_t finish() {
         if (used) {
-            words.push_back(cur);
-            cur = 0;
+            w[n++] = acc;
+            acc = 0;
             used = 0;
         }
-        return words;
+        return n;
     }
 };
 
@@ -125,46 +135,8 @@ struct BitReader {
 
 int ilog2(uint64_t x) { return 63 - __builtin_clzll(x); }
 
-uint64_t rice_log2_b(double p) {
-    const double phi = (std::sqrt(5.0) + 1.0) / 2.0;
-    double v = std::ceil(std::log2(std::log(phi) / -std::log1p(-p)));
-    if (!(v > 0)) return 0;  // NaN and negatives saturate to 0 like Rust's `as usize`
-    if (v > 63) return 63;
-    return (uint64_t)v;
-}
-
-std::vector<uint64_t> rice_encode(const std::vector<uint64_t> &ints, uint64_t &param) {
-    long double sum = 0;
-    for (uint64_t x : ints) sum += (long double)x;
-    // encode.rs:62: inv_mean = exp(ln(len) - ln(sum))
-    double inv_mean = std::exp(std::log((double)ints.size()) - std::log((double)sum));
-    param = rice_log2_b(inv_mean);
-    BitWriter bw;
-    for (uint64_t n : ints) {
-        bw.unary(n >> param);
-        if (param) bw.put(n & ((1ULL << param) - 1), (int)param);
-    }
-    return bw.finish();
-}
-
-bool minimal_binary_encode(const std::vector<uint64_t> &ints, std::vector<uint64_t> &out, uint64_t &param) {
-    if (ints.empty()) return false;  // encode.rs:80 EncodeError (block dropped, Appendix B.3)
-    uint64_t mx = 0;
-    for (uint64_t x : ints) mx = x > mx ? x : mx;
-    param = mx + 2;
-    const int l = ilog2(param);
-    const uint64_t limit = (2ULL << l) - param;
-    BitWriter bw;
-    for (uint64_t x : ints) {
-        uint64_t v = x + 1;
-        if (v < limit) bw.put(v, l);
-        else bw.put(v + limit, l + 1);
-    }
-    out = bw.finish();
-    return true;
-}
-
 bool rice_decode(const std::vector<uint64_t> &w, uint64_t n, uint64_t param, std::vector<uint64_t> &out) {
+    if (param > 63) return false;
     BitReader br(w.data(), w.size());
     out.resize(n);
     for (uint64_t i = 0; i < n; i++) {
@@ -179,7 +151,7 @@ bool minimal_binary_decode(const std::vector<uint64_t> &w, uint64_t n, uint64_t 
     if (param < 1) return n == 0;
     BitReader br(w.data(), w.size());
     const int l = ilog2(param);
-    const uint64_t limit = (2ULL << l) - param;
+    const uint64_t limit = (l == 63 ? 0 : (2ULL << l)) - param;
     out.resize(n);
     for (uint64_t i = 0; i < n; i++) {
         uint64_t v;
@@ -195,25 +167,76 @@ bool minimal_binary_decode(const std::vector<uint64_t> &w, uint64_t n, uint64_t 
     return true;
 }
 
-// ---- gzip (flate2 GzEncoder-shaped member) ---------------------------------------------
-bool gzip_bytes(const uint8_t *data, size_t n, std::vector<uint8_t> &out) {
-    const uint8_t hdr[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, 0, 0xff};
-    out.assign(hdr, hdr + 10);
+// ---- deflate engines -------------------------------------------------------------------
+bool zlib_deflate(const uint8_t *data, size_t n, std::vector<uint8_t> &out, size_t at) {
     z_stream zs;
     std::memset(&zs, 0, sizeof(zs));
     if (deflateInit2(&zs, 6, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return false;
-    size_t bound = deflateBound(&zs, (uLong)n) + 16;
-    out.resize(10 + bound);
+    const size_t bound = deflateBound(&zs, (uLong)n) + 16;
+    out.resize(at + bound);
     zs.next_in = const_cast<Bytef *>(data);
     zs.avail_in = (uInt)n;
-    zs.next_out = out.data() + 10;
+    zs.next_out = out.data() + at;
     zs.avail_out = (uInt)bound;
-    int rc = deflate(&zs, Z_FINISH);
-    size_t produced = bound - zs.avail_out;
+    const int rc = deflate(&zs, Z_FINISH);
+    const size_t produced = bound - zs.avail_out;
     deflateEnd(&zs);
     if (rc != Z_STREAM_END) return false;
-    out.resize(10 + produced);
-    uint32_t crc = (uint32_t)crc32(0L, data, (uInt)n), isize = (uint32_t)n;
+    out.resize(at + produced);
+    return true;
+}
+
+// libdeflate.so.0 (dlopen; the image ships the runtime library without headers).  One
+// compressor per thread: libdeflate compressors are not thread-safe.
+struct LibDeflate {
+    void *(*alloc_c)(int) = nullptr;
+    void (*free_c)(void *) = nullptr;
+    size_t (*deflate_c)(void *, const void *, size_t, void *, size_t) = nullptr;
+    size_t (*bound_c)(void *, size_t) = nullptr;
+    bool ok = false;
+    LibDeflate() {
+        void *h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        alloc_c = (void *(*)(int))dlsym(h, "libdeflate_alloc_compressor");
+        free_c = (void (*)(void *))dlsym(h, "libdeflate_free_compressor");
+        deflate_c = (size_t(*)(void *, const void *, size_t, void *, size_t))dlsym(h, "libdeflate_deflate_compress");
+        bound_c = (size_t(*)(void *, size_t))dlsym(h, "libdeflate_deflate_compress_bound");
+        ok = alloc_c && free_c && deflate_c && bound_c;
+    }
+};
+LibDeflate &libdeflate() {
+    static LibDeflate L;
+    return L;
+}
+struct ThreadCompressor {
+    void *c = nullptr;
+    ~ThreadCompressor() {
+        if (c) libdeflate().free_c(c);
+    }
+};
+thread_local ThreadCompressor tl_compressor;
+
+bool libdeflate_deflate(const uint8_t *data, size_t n, std::vector<uint8_t> &out, size_t at) {
+    LibDeflate &L = libdeflate();
+    if (!L.ok) return false;
+    if (!tl_compressor.c && !(tl_compressor.c = L.alloc_c(6))) return false;
+    const size_t bound = L.bound_c(tl_compressor.c, n);
+    out.resize(at + bound);
+    const size_t got = L.deflate_c(tl_compressor.c, data, n, out.data() + at, bound);
+    if (!got && n) return false;
+    out.resize(at + got);
+    return true;
+}
+
+// one gzip member (flate2 GzEncoder shape) appended to out
+bool gzip_append(const uint8_t *data, size_t n, int engine, std::vector<uint8_t> &out) {
+    static const uint8_t hdr[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, 0, 0xff};
+    const size_t start = out.size();
+    out.insert(out.end(), hdr, hdr + 10);
+    const bool ok = engine == NTC_DEFLATE_LIBDEFLATE ? libdeflate_deflate(data, n, out, start + 10)
+                                                     : zlib_deflate(data, n, out, start + 10);
+    if (!ok) return false;
+    const uint32_t crc = (uint32_t)crc32(0L, data, (uInt)n), isize = (uint32_t)n;
     for (int i = 0; i < 4; i++) out.push_back((uint8_t)(crc >> (8 * i)));
     for (int i = 0; i < 4; i++) out.push_back((uint8_t)(isize >> (8 * i)));
     return true;
@@ -290,51 +313,24 @@ uint64_t as_2bit(const uint8_t *codes, size_t n) {
     return v;
 }
 
-// encode.rs:96-127
-bool compress_block(const std::vector<uint64_t> &data, uint64_t num_records, bool rice, std::vector<uint8_t> &out) {
-    std::vector<uint64_t> words;
-    uint64_t param = 0;
-    if (rice) {
-        words = rice_encode(data, param);
-    } else if (!minimal_binary_encode(data, words, param)) {
-        return false;
-    }
-    // Words hold the bitstream MSB-first.  dsi-bitstream's BE BufBitWriter hands each word to
-    // the word writer as to_be(), and encode.rs:107-109 then emits to_ne_bytes (little-endian
-    // on x86): the bytes on disk are the MSB-first bitstream, i.e. each word big-endian
-    // [ext dsi-bitstream 0.5.0, recalled; SURVEY.md A.4].  Parity unpinned vs the reference
-    // (no reference-written encoded.dat exists offline).
-    std::vector<uint8_t> bytes(words.size() * 8);
-    for (size_t i = 0; i < words.size(); i++)
-        for (int b = 0; b < 8; b++) bytes[i * 8 + b] = (uint8_t)(words[i] >> (8 * (7 - b)));
-    std::vector<uint8_t> gz;
-    if (!gzip_bytes(bytes.data(), bytes.size(), gz)) return false;
-    BlockHeader h{};
-    h.block_size = (uint32_t)gz.size();
-    h.num_records = (uint32_t)num_records;
-    h.num_u64 = (uint32_t)data.size();
-    h.encoded_size = (uint32_t)words.size();
-    h.rice_param = param;
-    h.bitpacker_exponent = 8;
-    out.clear();
-    write_header(out, h);
-    out.insert(out.end(), gz.begin(), gz.end());
-    return true;
-}
+inline uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
 
 bool decompress_block(const uint8_t *payload, const BlockHeader &h, bool rice, std::vector<uint64_t> &out) {
     std::vector<uint8_t> bytes;
     if (!gunzip_bytes(payload, h.block_size, bytes)) return false;
     std::vector<uint64_t> words(bytes.size() / 8);
-    for (size_t i = 0; i < words.size(); i++) {  // big-endian words (see compress_block)
-        uint64_t w = 0;
-        for (int b = 0; b < 8; b++) w = (w << 8) | bytes[8 * i + b];
-        words[i] = w;
+    for (size_t i = 0; i < words.size(); i++) {  // big-endian words (see pack_block)
+        uint64_t w;
+        std::memcpy(&w, bytes.data() + 8 * i, 8);
+        words[i] = bswap64(w);
     }
-    if (words.size() != h.encoded_size) return false;  // decode.rs:319-321
+    if (words.size() != h.encoded_size) return false;  // decode.rs:90-92
     return rice ? rice_decode(words, h.num_u64, h.rice_param, out)
                 : minimal_binary_decode(words, h.num_u64, h.rice_param, out);
 }
+
+// Rice code length of v with parameter p
+inline uint64_t rice_bits(uint64_t v, int p) { return (v >> p) + 1 + (uint64_t)p; }
 
 }  // namespace
 
@@ -342,47 +338,179 @@ extern "C" {
 
 void ntc_file_header(uint8_t out[32]) { std::memset(out, 0, 32); }
 
+// split_encoded_dictionary (encode.rs:168-229) + rice / minimal binary coding
+// (encode.rs:59-94), words written as compress_block hands them to deflate.
+int ntc_pack_block(const uint64_t *recs, uint64_t n_recs, uint64_t num_records, ntc_block_meta *meta,
+                   uint8_t **payload, uint64_t *payload_len) {
+    if (!meta || !payload || !payload_len || (n_recs && !recs)) return NTC_ERR_INVALID_ARG;
+    *payload = nullptr;
+    *payload_len = 0;
+    std::memset(meta, 0, sizeof(*meta));
+    meta->num_records = num_records;
+    meta->n_recs = n_recs;
+    if (n_recs == 0) return meta->status = NTC_ERR_EMPTY_READ;  // split_encoded_dictionary EncodeError
+    // pass 1: stream totals
+    uint64_t n_long = 0, max1 = 0, sum2 = 0, sum3 = 0, T = 0;
+    for (uint64_t i = 0; i < n_recs; i++) {
+        const uint64_t w = recs[i], flag = w >> 56;
+        sum3 += flag;
+        if ((flag & 2) == 0) {
+            n_long++;
+            const uint64_t c = w & 0xFFFFFFFFULL;
+            max1 = c > max1 ? c : max1;
+            sum2 += (w >> 32) & 0xFFFFFFULL;
+        } else {
+            T += flag >> 2;
+        }
+    }
+    // s4 chunk values: the short bases in 31-base as_2bit chunks.  A short record's bases
+    // are bits 0-55 (encode.rs:216-221: from_2bit of bytes 0..7); from_2bit panics past 32
+    // bases, so a longer length is a malformed block here.
+    std::vector<uint64_t> s4((T + 30) / 31);
+    uint64_t max4 = 0;
+    {
+        uint64_t chunk = 0, nchunk = 0;
+        int have = 0;  // bases in chunk
+        for (uint64_t i = 0; i < n_recs; i++) {
+            const uint64_t w = recs[i], flag = w >> 56;
+            if ((flag & 2) == 0) continue;
+            int len = (int)(flag >> 2);
+            if (len > 32) return meta->status = NTC_ERR_FORMAT;
+            uint64_t bits = w & 0x00FFFFFFFFFFFFFFULL;
+            if (len < 28) bits &= (1ULL << (2 * len)) - 1;
+            while (len) {
+                const int take = len < 31 - have ? len : 31 - have;  // <= 31
+                chunk |= (bits & ((1ULL << (2 * take)) - 1)) << (2 * have);
+                bits >>= 2 * take;
+                have += take;
+                len -= take;
+                if (have == 31) {
+                    s4[nchunk++] = chunk;
+                    max4 = chunk > max4 ? chunk : max4;
+                    chunk = 0;
+                    have = 0;
+                }
+            }
+        }
+        if (have) {
+            s4[nchunk++] = chunk;
+            max4 = chunk > max4 ? chunk : max4;
+        }
+    }
+    // write_block_to computes all four before writing: an empty minimal-binary stream errs
+    // and the block is dropped (lib.rs:242-250, App. B.3)
+    if (n_long == 0 || T == 0) return meta->status = NTC_ERR_EMPTY_READ;
+    const int p2 = ntc_rice_log2_b(n_long, sum2), p3 = ntc_rice_log2_b(n_recs, sum3);
+    const uint64_t m1 = max1 + 2, m4 = max4 + 2;
+    const int l1 = ilog2(m1), l4 = ilog2(m4);
+    const uint64_t lim1 = (2ULL << l1) - m1, lim4 = (l4 == 63 ? 0 : (2ULL << l4)) - m4;
+    // pass 2: exact code lengths
+    uint64_t b1 = 0, b2 = 0, b3 = 0, b4 = 0;
+    for (uint64_t i = 0; i < n_recs; i++) {
+        const uint64_t w = recs[i], flag = w >> 56;
+        b3 += rice_bits(flag, p3);
+        if ((flag & 2) == 0) {
+            b1 += (uint64_t)l1 + ((w & 0xFFFFFFFFULL) + 1 >= lim1);
+            b2 += rice_bits((w >> 32) & 0xFFFFFFULL, p2);
+        }
+    }
+    for (uint64_t v : s4) b4 += (uint64_t)l4 + (v + 1 >= lim4);
+    const uint64_t wn[4] = {(b1 + 63) / 64, (b2 + 63) / 64, (b3 + 63) / 64, (b4 + 63) / 64};
+    const uint64_t total_words = wn[0] + wn[1] + wn[2] + wn[3];
+    uint64_t *words = (uint64_t *)std::malloc(total_words * 8 + 8);
+    if (!words) return NTC_ERR_CAPACITY;
+    uint64_t off = 0;
+    const uint64_t params[4] = {m1, (uint64_t)p2, (uint64_t)p3, m4};
+    const uint64_t counts[4] = {n_long, n_long, n_recs, (uint64_t)s4.size()};
+    for (int s = 0; s < 4; s++) {
+        meta->stream[s].num_u64 = counts[s];
+        meta->stream[s].encoded_size = wn[s];
+        meta->stream[s].param = params[s];
+        meta->stream[s].offset = off * 8;
+        off += wn[s];
+    }
+    // pass 3: codes
+    BitSink o1(words), o2(words + wn[0]), o3(words + wn[0] + wn[1]), o4(words + wn[0] + wn[1] + wn[2]);
+    const uint64_t mask2 = (1ULL << p2) - 1, mask3 = (1ULL << p3) - 1;
+    for (uint64_t i = 0; i < n_recs; i++) {
+        const uint64_t w = recs[i], flag = w >> 56;
+        o3.zeros(flag >> p3);
+        o3.put(((uint64_t)1 << p3) | (flag & mask3), p3 + 1);
+        if ((flag & 2) == 0) {
+            const uint64_t v = (w & 0xFFFFFFFFULL) + 1;
+            if (v < lim1) o1.put(v, l1);
+            else o1.put(v + lim1, l1 + 1);
+            const uint64_t len = (w >> 32) & 0xFFFFFFULL;
+            o2.zeros(len >> p2);
+            o2.put(((uint64_t)1 << p2) | (len & mask2), p2 + 1);
+        }
+    }
+    for (uint64_t c : s4) {
+        const uint64_t v = c + 1;
+        if (v < lim4) o4.put(v, l4);
+        else o4.put(v + lim4, l4 + 1);  // v + lim4 < 2^(l4+1) <= 2^63: fits
+    }
+    const uint64_t got[4] = {o1.finish(), o2.finish(), o3.finish(), o4.finish()};
+    for (int s = 0; s < 4; s++)
+        if (got[s] != wn[s]) {
+            std::free(words);
+            return NTC_ERR_FORMAT;  // internal size mismatch (never expected)
+        }
+    for (uint64_t i = 0; i < total_words; i++) words[i] = bswap64(words[i]);  // on-disk byte order
+    *payload = (uint8_t *)words;
+    *payload_len = total_words * 8;
+    return meta->status = NTC_OK;
+}
+
+// compress_block's header + deflate_bytes for each stream (encode.rs:96-127)
+int ntc_deflate_block(const ntc_block_meta *meta, const uint8_t *payload, int engine, uint8_t **out,
+                      uint64_t *out_len) {
+    if (!meta || !out || !out_len) return NTC_ERR_INVALID_ARG;
+    *out = nullptr;
+    *out_len = 0;
+    if (meta->status != NTC_OK) return meta->status;
+    if (!payload) return NTC_ERR_INVALID_ARG;
+    if (engine != NTC_DEFLATE_ZLIB && engine != NTC_DEFLATE_LIBDEFLATE) return NTC_ERR_INVALID_ARG;
+    if (engine == NTC_DEFLATE_LIBDEFLATE && !libdeflate().ok) return NTC_ERR_UNSUPPORTED;
+    std::vector<uint8_t> buf;
+    uint64_t est = 0;
+    for (int s = 0; s < 4; s++) est += meta->stream[s].encoded_size * 8 + 64;
+    buf.reserve(est + est / 16);
+    for (int s = 0; s < 4; s++) {
+        const ntc_stream_meta &m = meta->stream[s];
+        const size_t hpos = buf.size();
+        buf.resize(hpos + 32);
+        if (!gzip_append(payload + m.offset, m.encoded_size * 8, engine, buf)) return NTC_ERR_FORMAT;
+        BlockHeader h{};
+        h.block_size = (uint32_t)(buf.size() - hpos - 32);
+        h.num_records = (uint32_t)meta->num_records;
+        h.num_u64 = (uint32_t)m.num_u64;
+        h.encoded_size = (uint32_t)m.encoded_size;
+        h.rice_param = m.param;
+        h.bitpacker_exponent = 8;
+        std::vector<uint8_t> hb;
+        write_header(hb, h);
+        std::memcpy(buf.data() + hpos, hb.data(), 32);
+    }
+    uint8_t *o = (uint8_t *)std::malloc(buf.size() ? buf.size() : 1);
+    if (!o) return NTC_ERR_CAPACITY;
+    std::memcpy(o, buf.data(), buf.size());
+    *out = o;
+    *out_len = buf.size();
+    return NTC_OK;
+}
+
 int ntc_write_block(const uint64_t *recs, uint64_t n_recs, uint64_t num_records, uint8_t **out, uint64_t *out_len) {
     if (!out || !out_len || (n_recs && !recs)) return NTC_ERR_INVALID_ARG;
     *out = nullptr;
     *out_len = 0;
-    if (n_recs == 0) return NTC_ERR_EMPTY_READ;  // split_encoded_dictionary EncodeError
-    // split_encoded_dictionary (encode.rs:168-229)
-    std::vector<uint64_t> d1, d2, d3;
-    std::vector<uint8_t> tmp;
-    d3.reserve(n_recs);
-    for (uint64_t i = 0; i < n_recs; i++) {
-        const uint64_t w = recs[i];
-        const uint8_t flag = (uint8_t)(w >> 56);
-        d3.push_back(flag);
-        if ((flag & 2) == 0) {
-            d1.push_back(w & 0xFFFFFFFFULL);
-            d2.push_back((w >> 32) & 0xFFFFFFULL);
-        } else {
-            const uint32_t len = flag >> 2;
-            for (uint32_t j = 0; j < len; j++) tmp.push_back((uint8_t)((w >> (2 * j)) & 3));
-        }
-    }
-    std::vector<uint64_t> d4;
-    for (size_t a = 0; a < tmp.size(); a += 31) d4.push_back(as_2bit(tmp.data() + a, std::min<size_t>(31, tmp.size() - a)));
-    std::vector<uint8_t> b1, b2, b3, b4;
-    // write_block_to (lib.rs:232-252): all four are built before anything is written; an
-    // empty minimal-binary stream is an error and the whole block is dropped (B.3)
-    if (!compress_block(d1, num_records, false, b1)) return NTC_ERR_EMPTY_READ;
-    if (!compress_block(d2, num_records, true, b2)) return NTC_ERR_FORMAT;
-    if (!compress_block(d3, num_records, true, b3)) return NTC_ERR_FORMAT;
-    if (!compress_block(d4, num_records, false, b4)) return NTC_ERR_EMPTY_READ;
-    const uint64_t total = b1.size() + b2.size() + b3.size() + b4.size();
-    uint8_t *buf = (uint8_t *)std::malloc(total ? total : 1);
-    if (!buf) return NTC_ERR_CAPACITY;
-    uint64_t o = 0;
-    for (auto *b : {&b1, &b2, &b3, &b4}) {
-        std::memcpy(buf + o, b->data(), b->size());
-        o += b->size();
-    }
-    *out = buf;
-    *out_len = total;
-    return NTC_OK;
+    ntc_block_meta meta;
+    uint8_t *payload = nullptr;
+    uint64_t plen = 0;
+    int rc = ntc_pack_block(recs, n_recs, num_records, &meta, &payload, &plen);
+    if (rc == NTC_OK) rc = ntc_deflate_block(&meta, payload, NTC_DEFLATE_ZLIB, out, out_len);
+    std::free(payload);
+    return rc;
 }
 
 int ntc_read_block(const uint8_t *data, uint64_t len, uint64_t *consumed, uint64_t **recs, uint64_t *n_recs,

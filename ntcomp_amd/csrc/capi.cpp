@@ -13,7 +13,9 @@
 #include <vector>
 
 #include "../../include/ntcomp_gpu.h"
+#include "../../include/ntcomp_codec.h"
 #include "../../include/ntcomp_host.h"
+#include "codec_params.h"
 #include "derived.h"
 #include "kernels.h"
 #include "ntc_internal.h"
@@ -68,6 +70,8 @@ struct ntc_ctx {
     uint64_t n_paths = 0, path_text_len = 0;
     int64_t upload_host_us = 0, upload_total_us = 0;  // last ntc_index_upload: host derive / total
     uint64_t max_pass_bases = 1ULL << 30;  // host-buffer calls split into device passes of at most this
+    double last_pack_ms = 0;               // last ntc_pack_blocks_device: both packer kernels
+    hipEvent_t pack_ev[3] = {nullptr, nullptr, nullptr};
 };
 
 namespace {
@@ -77,7 +81,8 @@ constexpr uint64_t kCounterBytes = 8 * 64;  // work queue heads (kernels.hip Wav
 enum WsSlot {
     WS_D = 0, WS_S, WS_F, WS_R, WS_RECCOUNT, WS_SCANTMP, WS_TILEBASE, WS_TILEROWS,
     WS_STAGE_BASES, WS_STAGE_OFFS, WS_STAGE_RECS, WS_E, WS_DEC_A, WS_DEC_B, WS_DEC_C,
-    WS_DEC_D, WS_Q, WS_E3, WS_NE, WS_COUNTER, WS_R2, WS_ED, WS_WAVECNT
+    WS_DEC_D, WS_Q, WS_E3, WS_NE, WS_COUNTER, WS_R2, WS_ED, WS_WAVECNT, WS_PACK_CHUNKS, WS_PACK_META,
+    WS_PACK_PAYLOAD
 };
 
 #define HIP_TRY(ctx, expr)                                                                   \
@@ -283,6 +288,110 @@ int read_status(ntc_ctx *ctx, int64_t *bad_index) {
     return code;
 }
 
+
+// GPU packer (pack.hip) over the records of n_reads reads in HBM: block b = reads
+// [b * block_reads, ...).  Pass 1 on the device, Rice parameters and payload layout on the
+// host (glibc f64 math, codec_params.h), pass 2 on the device.  Synchronous.
+int pack_blocks_impl(ntc_ctx *ctx, const uint64_t *d_recs, const uint64_t *d_roffs, uint64_t n_reads,
+                     uint32_t block_reads, uint8_t *d_payload, uint64_t payload_capacity, ntc_block_meta *meta,
+                     uint64_t *payload_bytes) {
+    *payload_bytes = 0;
+    const uint64_t n_blocks = (n_reads + block_reads - 1) / block_reads;
+    if (n_blocks == 0) return NTC_OK;
+    for (int i = 0; i < 3; i++)
+        if (!ctx->pack_ev[i]) HIP_TRY(ctx, hipEventCreate(&ctx->pack_ev[i]));
+    uint64_t ends[2] = {0, 0};
+    HIP_TRY(ctx, hipMemcpyAsync(&ends[0], d_roffs, 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(&ends[1], d_roffs + n_reads, 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (ends[1] < ends[0]) return set_err(ctx, NTC_ERR_INVALID_ARG, "record offsets decrease");
+    void *d_chunks, *d_meta;
+    int rc;
+    // chunks of block b at rec_begin + b (at most n_recs + 1 chunks per block)
+    if ((rc = ensure(ctx, WS_PACK_CHUNKS, (ends[1] + n_blocks + 1) * 8, &d_chunks))) return rc;
+    const uint64_t meta_bytes = n_blocks * (sizeof(PackStats) + sizeof(PackParams) + 32);
+    if ((rc = ensure(ctx, WS_PACK_META, meta_bytes, &d_meta))) return rc;
+    PackStats *d_stats = (PackStats *)d_meta;
+    PackParams *d_params = (PackParams *)(d_stats + n_blocks);
+    uint64_t *d_bits = (uint64_t *)(d_params + n_blocks);
+    HIP_TRY(ctx, hipEventRecord(ctx->pack_ev[0], ctx->stream));
+    launch_pack_stats(d_recs, d_roffs, n_reads, block_reads, n_blocks, (uint64_t *)d_chunks, d_stats, ctx->stream);
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipEventRecord(ctx->pack_ev[1], ctx->stream));
+    std::vector<PackStats> st(n_blocks);
+    std::vector<PackParams> pp(n_blocks);
+    HIP_TRY(ctx, hipMemcpyAsync(st.data(), d_stats, n_blocks * sizeof(PackStats), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    float ms1 = 0;
+    HIP_TRY(ctx, hipEventElapsedTime(&ms1, ctx->pack_ev[0], ctx->pack_ev[1]));
+    uint64_t words = 0;  // payload words so far (each stream at its exact upper bound)
+    for (uint64_t b = 0; b < n_blocks; b++) {
+        const PackStats &S = st[b];
+        PackParams &P = pp[b];
+        ntc_block_meta &M = meta[b];
+        std::memset(&M, 0, sizeof(M));
+        std::memset(&P, 0, sizeof(P));
+        const uint64_t r0 = b * block_reads;
+        M.num_records = std::min<uint64_t>(block_reads, n_reads - r0);
+        M.n_recs = S.n_recs;
+        M.status = NTC_OK;
+        if (S.bad) M.status = NTC_ERR_FORMAT;  // a short record past 32 bases (from_2bit panics)
+        else if (S.n_recs == 0 || S.n_long == 0 || S.T == 0) M.status = NTC_ERR_EMPTY_READ;  // App. B.3
+        if (M.status != NTC_OK) {
+            P.skip = 1;
+            continue;
+        }
+        const uint64_t m1 = S.max1 + 2, m4 = S.max4 + 2;
+        P.l1 = 63 - __builtin_clzll(m1);
+        P.l4 = 63 - __builtin_clzll(m4);
+        P.lim1 = (2ULL << P.l1) - m1;
+        P.lim4 = (2ULL << P.l4) - m4;  // l4 <= 62
+        P.p2 = ntc_rice_log2_b(S.n_long, S.sum2);
+        P.p3 = ntc_rice_log2_b(S.n_recs, S.sum3);
+        const uint64_t nch = (S.T + 30) / 31;
+        const uint64_t bound[4] = {S.n_long * (uint64_t)(P.l1 + 1),
+                                   S.n_long * (uint64_t)(1 + P.p2) + (S.sum2 >> P.p2),
+                                   S.n_recs * (uint64_t)(1 + P.p3) + (S.sum3 >> P.p3),
+                                   nch * (uint64_t)(P.l4 + 1)};
+        const uint64_t params[4] = {m1, (uint64_t)P.p2, (uint64_t)P.p3, m4};
+        const uint64_t counts[4] = {S.n_long, S.n_long, S.n_recs, nch};
+        for (int k = 0; k < 4; k++) {
+            P.off[k] = words;
+            M.stream[k].offset = words * 8;
+            M.stream[k].encoded_size = (bound[k] + 63) / 64;  // refined after pass 2
+            M.stream[k].param = params[k];
+            M.stream[k].num_u64 = counts[k];
+            words += (bound[k] + 63) / 64 + 1;
+        }
+    }
+    *payload_bytes = words * 8;
+    if (words * 8 > payload_capacity) return set_err(ctx, NTC_ERR_CAPACITY, "payload_capacity too small");
+    HIP_TRY(ctx, hipMemsetAsync(d_payload, 0, words * 8, ctx->stream));  // fallback tiles OR into zeros
+    HIP_TRY(ctx, hipMemcpyAsync(d_params, pp.data(), n_blocks * sizeof(PackParams), hipMemcpyHostToDevice,
+                                ctx->stream));
+    HIP_TRY(ctx, hipEventRecord(ctx->pack_ev[2], ctx->stream));
+    launch_pack_write(d_recs, (const uint64_t *)d_chunks, d_stats, d_params, n_blocks, (uint64_t *)d_payload, d_bits,
+                      ctx->stream);
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipEventRecord(ctx->pack_ev[1], ctx->stream));
+    std::vector<uint64_t> bits(n_blocks * 4);
+    HIP_TRY(ctx, hipMemcpyAsync(bits.data(), d_bits, n_blocks * 32, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    float ms2 = 0;
+    HIP_TRY(ctx, hipEventElapsedTime(&ms2, ctx->pack_ev[2], ctx->pack_ev[1]));
+    ctx->last_pack_ms = (double)ms1 + (double)ms2;
+    for (uint64_t b = 0; b < n_blocks; b++) {
+        if (meta[b].status != NTC_OK) continue;
+        for (int k = 0; k < 4; k++) {
+            const uint64_t w = (bits[b * 4 + k] + 63) / 64;
+            if (w > meta[b].stream[k].encoded_size)
+                return set_err(ctx, NTC_ERR_FORMAT, "packer exceeded its stream bound");  // never expected
+            meta[b].stream[k].encoded_size = w;
+        }
+    }
+    return NTC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -330,6 +439,8 @@ void ntc_ctx_destroy(ntc_ctx *ctx) {
     if (ctx->d_status) (void)hipFree(ctx->d_status);
     if (ctx->h_box) (void)hipHostFree(ctx->h_box);
     for (auto &e : ctx->ev)
+        if (e) (void)hipEventDestroy(e);
+    for (auto &e : ctx->pack_ev)
         if (e) (void)hipEventDestroy(e);
     if (ctx->stream && ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -635,6 +746,7 @@ int ntc_ctx_get_option(const ntc_ctx *ctx, const char *key, int64_t *value) {
     else if (std::strcmp(key, "upload_host_us") == 0) *value = ctx->upload_host_us;
     else if (std::strcmp(key, "max_pass_bases") == 0) *value = (int64_t)ctx->max_pass_bases;
     else if (std::strcmp(key, "upload_total_us") == 0) *value = ctx->upload_total_us;
+    else if (std::strcmp(key, "pack_us") == 0) *value = (int64_t)(ctx->last_pack_ms * 1000.0);
     else return NTC_ERR_INVALID_ARG;
     return NTC_OK;
 }
@@ -939,6 +1051,75 @@ int ntc_decode_batch(ntc_ctx *ctx, const uint64_t *recs, uint64_t n_recs, uint8_
         bases_done += pb;
         a0 = a1;
     }
+    return NTC_OK;
+}
+
+int ntc_pack_blocks_device(ntc_ctx *ctx, const uint64_t *d_recs, const uint64_t *d_rec_offsets,
+                           uint64_t n_reads, uint32_t block_reads, uint8_t *d_payload,
+                           uint64_t payload_capacity, ntc_block_meta *meta, uint64_t *payload_bytes) {
+    if (!ctx || !d_rec_offsets || !meta || !payload_bytes || block_reads == 0 || (n_reads && (!d_recs || !d_payload)))
+        return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument or block_reads = 0");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    return pack_blocks_impl(ctx, d_recs, d_rec_offsets, n_reads, block_reads, d_payload, payload_capacity, meta,
+                            payload_bytes);
+}
+
+int ntc_encode_pack_batch(ntc_ctx *ctx, const uint8_t *bases, const uint64_t *read_offsets, uint64_t n_reads,
+                          uint32_t block_reads, ntc_block_meta *meta, uint8_t **payload, uint64_t *payload_bytes,
+                          int64_t *bad_read) {
+    if (bad_read) *bad_read = -1;
+    if (!ctx || !read_offsets || !meta || !payload || !payload_bytes || block_reads == 0 || (n_reads && !bases))
+        return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument or block_reads = 0");
+    *payload = nullptr;
+    *payload_bytes = 0;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (!ctx->has_index) return set_err(ctx, NTC_ERR_NO_INDEX, "no index uploaded");
+    if (ctx->encode_variant != 4) return set_err(ctx, NTC_ERR_UNSUPPORTED, "encode_pack needs encode_variant 4");
+    for (uint64_t r = 0; r < n_reads; r++)
+        if (read_offsets[r + 1] < read_offsets[r])
+            return set_err(ctx, NTC_ERR_INVALID_ARG, "read offsets must be non-decreasing");
+    if (n_reads == 0) return NTC_OK;
+    const uint64_t o0 = read_offsets[0], total = read_offsets[n_reads] - o0;
+    std::vector<uint64_t> offs(n_reads + 1);
+    for (uint64_t r = 0; r <= n_reads; r++) offs[r] = read_offsets[r] - o0;
+    void *d_bases, *d_offs, *d_recs, *d_payload;
+    int rc;
+    if ((rc = ensure(ctx, WS_STAGE_BASES, total + 64, &d_bases))) return rc;
+    if ((rc = ensure(ctx, WS_STAGE_OFFS, (n_reads + 1) * 8 * 2, &d_offs))) return rc;
+    if ((rc = ensure(ctx, WS_STAGE_RECS, (total + 1) * 8, &d_recs))) return rc;
+    uint64_t *d_roffs = (uint64_t *)d_offs + (n_reads + 1);
+    if (total) HIP_TRY(ctx, hipMemcpyAsync(d_bases, bases + o0, total, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(d_offs, offs.data(), (n_reads + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+    rc = encode4_impl(ctx, (const uint8_t *)d_bases, (const uint64_t *)d_offs, n_reads, total, (uint64_t *)d_recs,
+                      total + 1, d_roffs);
+    if (rc) return rc;
+    int64_t bad = -1;
+    if ((rc = read_status(ctx, &bad))) {
+        if (bad_read) *bad_read = bad;
+        return rc;
+    }
+    // the payload never exceeds the records' 8 B each plus per-stream rounding, except for
+    // malformed unary runs: size the device buffer for that and let the packer check
+    const uint64_t n_blocks = (n_reads + block_reads - 1) / block_reads;
+    uint64_t nrec = 0;
+    HIP_TRY(ctx, hipMemcpy(&nrec, d_roffs + n_reads, 8, hipMemcpyDeviceToHost));
+    uint64_t cap = nrec * 10 + n_blocks * 64 + 64, used = 0;
+    for (int attempt = 0;; attempt++) {
+        if ((rc = ensure(ctx, WS_PACK_PAYLOAD, cap, &d_payload))) return rc;
+        rc = pack_blocks_impl(ctx, (const uint64_t *)d_recs, d_roffs, n_reads, block_reads, (uint8_t *)d_payload,
+                              ctx->ws[WS_PACK_PAYLOAD].bytes, meta, &used);
+        if (rc != NTC_ERR_CAPACITY || attempt) break;
+        cap = used;  // exact requirement from the first pass
+    }
+    if (rc) return rc;
+    uint8_t *h = (uint8_t *)std::malloc(used ? used : 1);
+    if (!h) return set_err(ctx, NTC_ERR_CAPACITY, "host payload allocation");
+    if (used && hipMemcpy(h, d_payload, used, hipMemcpyDeviceToHost) != hipSuccess) {
+        std::free(h);
+        return set_err(ctx, NTC_ERR_HIP, "payload copy");
+    }
+    *payload = h;
+    *payload_bytes = used;
     return NTC_OK;
 }
 

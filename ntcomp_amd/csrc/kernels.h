@@ -84,6 +84,23 @@ struct DecWalkArgs {
     unsigned long long *status;
 };
 
+// GPU block packer (pack.hip): per 65,536-read block, stream totals, then the four coded
+// streams of write_block_to (src/lib.rs:232-252) before deflate
+struct PackStats {
+    uint64_t n_recs, n_long, max1, sum2, sum3, T, max4, bad, rec_begin;
+};
+struct PackParams {
+    uint64_t off[4];      // word offsets of s1..s4 in the payload
+    uint64_t lim1, lim4;  // minimal-binary limits 2^(l+1) - max
+    int32_t p2, p3, l1, l4;
+    uint32_t skip, pad;   // skip: the block is dropped (App. B.3) or malformed
+};
+void launch_pack_stats(const uint64_t *recs, const uint64_t *roffs, uint64_t n_reads, uint32_t block_reads,
+                       uint64_t n_blocks, uint64_t *chunks, PackStats *stats, hipStream_t s);
+void launch_pack_write(const uint64_t *recs, const uint64_t *chunks, const PackStats *stats,
+                       const PackParams *params, uint64_t n_blocks, uint64_t *payload, uint64_t *bits_out,
+                       hipStream_t s);
+
 void launch_encode(const EncodeArgs &a, hipStream_t s);
 void launch_encode4(const Enc4Args &a, uint64_t total, uint32_t ms_blocks, hipStream_t s,
                     hipEvent_t ev_ms_begin, hipEvent_t ev_ms_end);
