@@ -55,6 +55,16 @@ int ntc_fastx_open(const char *path, ntc_fastx **out);
 int ntc_fastx_next_batch(ntc_fastx *fx, uint64_t max_reads, uint64_t max_bases, const uint8_t **bases,
                          const uint64_t **offsets, uint64_t *n_reads);
 void ntc_fastx_close(ntc_fastx *fx);
+/* The same batch written into caller buffers (e.g. pinned host memory for the H2D copy):
+ * bases_capacity bytes, offsets[max_reads + 1].  NTC_ERR_CAPACITY if the bases do not fit. */
+int ntc_fastx_next_batch_into(ntc_fastx *fx, uint64_t max_reads, uint64_t max_bases, uint8_t *bases,
+                              uint64_t bases_capacity, uint64_t *offsets, uint64_t *n_reads);
+/* Plain FASTQ files are memory-mapped and each batch is parsed by this many threads
+ * (default ntc_host_threads()); other inputs decode on one producer thread.          */
+int ntc_fastx_set_threads(ntc_fastx *fx, int n_threads);
+/* CPUs this process may use: NTC_THREADS if set, else min(affinity mask, cgroup v2 CPU
+ * quota) -- the thread count of every host pool (FASTX parse, block deflate).         */
+int ntc_host_threads(void);
 /* decode output (src/main.rs:203-209): ">seq.{first_id + r}\n{read r}\n" for each read;
  * *out is freed with ntc_buffer_free (include/ntcomp_codec.h).                         */
 int ntc_fasta_format(const uint8_t *bases, const uint64_t *offsets, uint64_t n_reads, uint64_t first_id,

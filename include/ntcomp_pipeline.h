@@ -1,0 +1,52 @@
+/*
+ * ntcomp_pipeline.h -- the CLI's native file-to-file drivers (libntcomp_gpu.so).
+ *
+ *   ntc_encode_file   src/main.rs:141-181 (`ntcomp encode -i P reads > encoded.dat`):
+ *                     FASTX batches -> GPU encode + block packer on every context ->
+ *                     deflate on the host pool -> file header + blocks, in file order.
+ *
+ * Behaviour kept from the reference: blocks of 65,536 reads (main.rs:152), the last block's
+ * header carries num_records % 65,536 (main.rs:176), a block with no long or no short
+ * record is not written (write_block_to errs and main.rs:170 drops it).
+ * Errors are status codes (the reference panics or, for bases absent from the index, never
+ * terminates): the first failing read's file index is in stats->bad_read.
+ */
+#ifndef NTCOMP_PIPELINE_H
+#define NTCOMP_PIPELINE_H
+
+#include <stdint.h>
+
+#include "ntcomp_gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ntc_pipeline_opts {
+    int32_t threads;          /* host pool (parse, deflate); <= 0: ntc_host_threads()        */
+    int32_t blocks_per_batch; /* 65,536-read blocks per GPU call; <= 0: 16                    */
+    uint64_t batch_bases;     /* bases per pinned batch buffer; 0: 256 Mi (grows for long reads) */
+    int32_t deflate_engine;   /* NTC_DEFLATE_ZLIB (0) or NTC_DEFLATE_LIBDEFLATE (1)           */
+    int32_t reserved;
+} ntc_pipeline_opts;
+
+typedef struct ntc_pipeline_stats {
+    uint64_t reads, bases, blocks, dropped_blocks, bytes_out;
+    double parse_s, gpu_s, deflate_s, write_s; /* thread-seconds per stage                  */
+    double wall_s;
+    double alloc_s, first_batch_s, reader_done_s, gpu_done_s; /* timeline from the call's start */
+    int32_t threads;
+    int32_t reserved;
+    int64_t bad_read;                          /* file index of the failing read, or -1     */
+    char error[256];
+} ntc_pipeline_stats;
+
+/* ctxs: n_ctx contexts with the index uploaded (one per GPU; two on one device are allowed).
+ * Writes encoded.dat to out_fd (not closed).                                              */
+int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int out_fd, const ntc_pipeline_opts *opts,
+                    ntc_pipeline_stats *stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

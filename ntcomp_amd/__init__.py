@@ -41,7 +41,8 @@ EXPORTED = [
     "ntc_index_view_of", "ntc_index_save", "ntc_index_save_as", "ntc_index_load", "ntc_synth_genome", "ntc_synth_strains", "ntc_synth_reads", "ntc_minimizer_keys",
     "ntc_file_header", "ntc_write_block", "ntc_read_block", "ntc_buffer_free", "ntc_pack_block",
     "ntc_deflate_block", "ntc_pack_blocks_device", "ntc_encode_pack_batch",
-    "ntc_fastx_open", "ntc_fastx_next_batch", "ntc_fastx_close", "ntc_fasta_format",
+    "ntc_fastx_open", "ntc_fastx_next_batch", "ntc_fastx_close", "ntc_fasta_format", "ntc_fastx_next_batch_into",
+    "ntc_fastx_set_threads", "ntc_host_threads", "ntc_encode_file",
 ]
 
 
@@ -68,6 +69,20 @@ class BlockMeta(ctypes.Structure):
 
 
 DEFLATE_ENGINES = {"zlib": 0, "libdeflate": 1}
+
+
+class PipelineOpts(ctypes.Structure):
+    _fields_ = [("threads", ctypes.c_int32), ("blocks_per_batch", ctypes.c_int32), ("batch_bases", ctypes.c_uint64),
+                ("deflate_engine", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class PipelineStats(ctypes.Structure):
+    _fields_ = [("reads", ctypes.c_uint64), ("bases", ctypes.c_uint64), ("blocks", ctypes.c_uint64),
+                ("dropped_blocks", ctypes.c_uint64), ("bytes_out", ctypes.c_uint64), ("parse_s", ctypes.c_double),
+                ("gpu_s", ctypes.c_double), ("deflate_s", ctypes.c_double), ("write_s", ctypes.c_double),
+                ("wall_s", ctypes.c_double), ("alloc_s", ctypes.c_double), ("first_batch_s", ctypes.c_double),
+                ("reader_done_s", ctypes.c_double), ("gpu_done_s", ctypes.c_double), ("threads", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("bad_read", ctypes.c_int64), ("error", ctypes.c_char * 256)]
 
 
 class Timing(ctypes.Structure):
@@ -152,6 +167,10 @@ def lib():
         "ntc_fastx_open": (I, [ctypes.c_char_p, ctypes.POINTER(P)]),
         "ntc_fastx_next_batch": (I, [P, u64, u64, ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(u64)]),
         "ntc_fastx_close": (None, [P]),
+        "ntc_fastx_next_batch_into": (I, [P, u64, u64, P, u64, P, ctypes.POINTER(u64)]),
+        "ntc_fastx_set_threads": (I, [P, I]),
+        "ntc_host_threads": (I, []),
+        "ntc_encode_file": (I, [P, I, ctypes.c_char_p, I, ctypes.POINTER(PipelineOpts), ctypes.POINTER(PipelineStats)]),
         "ntc_fasta_format": (I, [P, P, u64, u64, ctypes.POINTER(P), ctypes.POINTER(u64)]),
     }
     for name, (res, args) in sig.items():
@@ -548,6 +567,29 @@ def read_block(data):
 
 
 # ---- FASTX ingest ---------------------------------------------------------------------
+def encode_file(ctxs, in_path, out_fd, threads=0, blocks_per_batch=16, batch_bases=0, deflate="zlib"):
+    """`ntcomp encode` file to file (ntc_encode_file, include/ntcomp_pipeline.h): FASTX ->
+    GPU encode + block packer on every context -> deflate pool -> encoded.dat on out_fd.
+    Returns the per-stage stats as a dict; raises NtcError (with .bad_read)."""
+    arr = (ctypes.c_void_p * len(ctxs))(*[c.h.value for c in ctxs])
+    o = PipelineOpts(threads, blocks_per_batch, batch_bases, DEFLATE_ENGINES[deflate], 0)
+    st = PipelineStats()
+    rc = lib().ntc_encode_file(arr, len(ctxs), os.fsencode(in_path), out_fd, ctypes.byref(o), ctypes.byref(st))
+    d = {k: (getattr(st, k).decode(errors="replace") if k == "error" else getattr(st, k))
+         for k, _ in PipelineStats._fields_ if k != "reserved"}
+    if rc:
+        e = NtcError(rc, d["error"])
+        e.bad_read = d["bad_read"]
+        e.stats = d
+        raise e
+    return d
+
+
+def host_threads():
+    """CPUs this process may use (NTC_THREADS, else min(affinity, cgroup CPU quota))."""
+    return int(lib().ntc_host_threads())
+
+
 class FastxReader:
     """needletail::parse_fastx_file + normalize(true) (src/main.rs:51-62, 158-163): plain or
     gzip FASTA/FASTQ -> batches of (bases, read offsets) as numpy arrays (copies)."""

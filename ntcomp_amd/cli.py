@@ -4,9 +4,11 @@ Mirrors the reference CLI (src/cli.rs:27-93, src/main.rs:91-211) with the hot pa
 the GPU: FASTX ingest in C++ (needletail parse + normalize(true) restated), encode /
 decode through libntcomp_gpu.so, blocks of 65,536 reads (main.rs:152) in the encoded.dat
 layout (file header lib.rs:52-67, write_block_to lib.rs:232-252), decode output
-">seq.N" (main.rs:203-209).  Pipelined: FASTX parse runs a batch ahead on its own
-thread, block compression / unzip and FASTA formatting on a thread pool (ctypes releases
-the GIL), each GPU context on its own driver thread; blocks are written in file order.
+">seq.N" (main.rs:203-209).  Encode runs the native pipeline (ntc_encode_file,
+include/ntcomp_pipeline.h): FASTX batches into pinned buffers, GPU encode + block packer
+per context, deflate on the host pool, blocks in file order.  Decode: blocks unzip on a
+thread pool (ctypes releases the GIL), batches decode on the GPU contexts, FASTA
+formatting on the pool, output in file order.
 
 Index files: <prefix>.sbwt / <prefix>.lcs in this library's own layout (the sbwt 0.3.11
 byte layout is unavailable offline -- DESIGN.md section 8).
@@ -95,11 +97,12 @@ def cmd_build(args):
     ix.save(args.output_prefix, layout=args.index_format)
 
 
-def _open_gpus(index, n, st=None):
-    """One context per GPU, each holding its own copy of the index."""
+def _open_gpus(index, devices, st=None):
+    """One context per entry of devices, each holding its own copy of the index (SURVEY.md
+    8(e)); an int n means devices 0..n-1."""
     import ntcomp_amd as nt
     ctxs = []
-    for d in range(n):
+    for d in (range(devices) if isinstance(devices, int) else devices):
         c = (st.wrap("gpu_init", nt.GpuContext) if st else nt.GpuContext)(d)
         (st.wrap("index_upload", c.upload) if st else c.upload)(index)
         if st and st.on:
@@ -108,96 +111,42 @@ def _open_gpus(index, n, st=None):
     return ctxs
 
 
+def _devices(args):
+    """--devices 0,0,1 (contexts, several may share a GPU) or --gpus N (devices 0..N-1)."""
+    if getattr(args, "devices", None):
+        return [int(x) for x in args.devices.split(",") if x.strip() != ""]
+    return list(range(args.gpus))
+
+
 def cmd_encode(args):
+    """main.rs:141-181 through the native pipeline (ntc_encode_file): FASTX parse on the
+    host pool, GPU encode + block packer per context, deflate on the host pool, blocks
+    written in file order."""
     import ntcomp_amd as nt
     st = _Stats(args.stats)
     log("Loading SBWT index...")
     index = st.wrap("index_load", nt.Index.load)(args.index_prefix)
-    ctxs = _open_gpus(index, args.gpus, st)
-    out = sys.stdout.buffer
-    out.write(nt.file_header())
+    ctxs = _open_gpus(index, _devices(args), st)
     log("Encoding fastX data...")
-    pool = cf.ThreadPoolExecutor(max_workers=args.threads)
-    gpu_pools = [cf.ThreadPoolExecutor(max_workers=1) for _ in ctxs]  # one driver thread per context
-    pending = []  # compressed blocks, in file order
-
-    def flush(wait_all=False):
-        while pending and (wait_all or pending[0].done() or len(pending) > 4 * args.threads):
-            data = pending.pop(0).result()
-            if data is not None:
-                out.write(data)
-
-    write_block = st.wrap("compress", nt.write_block)
-
-    def compress(recs, nreads):
-        try:
-            return write_block(recs, nreads)
-        except nt.NtcError as e:
-            if e.code == 3:  # a stream with no records: write_block_to errs, the
-                log("warning: block dropped (no long or no short records; main.rs:170 ignores the error)")
-                return None  # reference drops the block
-            raise
-
-    carry_recs, carry_counts = [], []  # records of reads not yet in a full block
-    rd = nt.FastxReader(args.query_file)
-    batch_reads = BLOCK_READS * args.blocks_per_batch
-    # FASTX parse runs one batch ahead on its own thread (the C reader releases the GIL)
-    reader = cf.ThreadPoolExecutor(max_workers=1)
-
-    next_batch = st.wrap("parse", lambda: rd.batch(max_reads=batch_reads, max_bases=batch_reads * 1024))
-    encode_on = st.wrap("gpu_encode", lambda ctx, bases, offs: ctx.encode(bases, offs))
-
-    jobs = []  # GPU encodes in flight, in file order
-    gi = 0
-    nxt = reader.submit(next_batch)
-    while True:
-        x = nxt.result()
-        if x is None:
-            break
-        nxt = reader.submit(next_batch)
-        bases, offs = x
-        jobs.append(gpu_pools[gi % len(ctxs)].submit(encode_on, ctxs[gi % len(ctxs)], bases, offs))
-        gi += 1
-        while len(jobs) > len(ctxs) or (jobs and jobs[0].done()):
-            _emit(jobs.pop(0).result(), carry_recs, carry_counts, pool, pending, compress)
-            flush()
-    for j in jobs:
-        _emit(j.result(), carry_recs, carry_counts, pool, pending, compress)
-        flush()
-    if carry_counts:
-        counts = np.concatenate(carry_counts)
-        recs = np.concatenate(carry_recs) if carry_recs else np.zeros(0, np.uint64)
-        pending.append(pool.submit(compress, recs, len(counts)))
-    flush(wait_all=True)
+    out = sys.stdout.buffer
     out.flush()
-    reader.shutdown()
-    rd.close()
-    for c in ctxs:
-        c.close()
-    st.report(command="encode", gpus=len(ctxs))
-
-
-def _emit(result, carry_recs, carry_counts, pool, pending, compress):
-    recs, roff = result
-    counts = np.diff(roff)
-    carry_recs.append(recs)
-    carry_counts.append(counts)
-    total = sum(len(c) for c in carry_counts)
-    if total < BLOCK_READS:
-        return
-    allc = np.concatenate(carry_counts)
-    allr = np.concatenate(carry_recs)
-    ends = np.concatenate([[0], np.cumsum(allc, dtype=np.uint64)])
-    nfull = len(allc) // BLOCK_READS
-    for b in range(nfull):
-        a0, a1 = int(ends[b * BLOCK_READS]), int(ends[(b + 1) * BLOCK_READS])
-        pending.append(pool.submit(compress, allr[a0:a1], BLOCK_READS))
-    rest = nfull * BLOCK_READS
-    carry_recs.clear()
-    carry_counts.clear()
-    if rest < len(allc):
-        carry_recs.append(allr[int(ends[rest]):])
-        carry_counts.append(allc[rest:])
+    try:
+        res = st.wrap("pipeline", nt.encode_file)(ctxs, args.query_file, out.fileno(), threads=args.threads,
+                                                  blocks_per_batch=args.blocks_per_batch, deflate=args.deflate)
+    except nt.NtcError as e:
+        bad = getattr(e, "bad_read", -1)
+        raise SystemExit(f"ntcomp encode: {e}" + (f" (read {bad + 1})" if bad is not None and bad >= 0 else ""))
+    finally:
+        for c in ctxs:
+            c.close()
+    if res["dropped_blocks"]:
+        log(f"warning: {res['dropped_blocks']} block(s) dropped (no long or no short records; "
+            "main.rs:170 ignores write_block_to's error, SURVEY App. B.3)")
+    if st.on:
+        for k in ("parse_s", "gpu_s", "deflate_s", "write_s"):
+            st.acc[k[:-2]] = res[k]
+    st.report(command="encode", gpus=len(ctxs), threads=res["threads"], reads=res["reads"], blocks=res["blocks"],
+              dropped_blocks=res["dropped_blocks"], pipeline_wall_s=round(res["wall_s"], 3), deflate=args.deflate)
 
 
 def _block_extents(data, pos):
@@ -223,7 +172,7 @@ def cmd_decode(args):
     import ntcomp_amd as nt
     st = _Stats(args.stats)
     index = st.wrap("index_load", nt.Index.load)(args.index_prefix)
-    ctxs = _open_gpus(index, args.gpus, st)
+    ctxs = _open_gpus(index, _devices(args), st)
     read_block = st.wrap("unzip", nt.read_block)
     fasta_format = st.wrap("format", nt.fasta_format)
     gpu_decode = st.wrap("gpu_decode", lambda ctx, r: ctx.decode(r))
@@ -306,17 +255,26 @@ def main(argv=None):
     e.add_argument("query_file", help="Query file with sequence data.")
     e.add_argument("-i", "--index", dest="index_prefix", required=True, help="Prefix for prebuilt <prefix>.sbwt and <prefix>.lcs")
     e.add_argument("--gpus", type=int, default=1, help="GPUs to encode on (batches dealt round-robin).")
-    e.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 4), help="block compression threads")
+    e.add_argument("--devices", help="comma-separated device list, one context each (e.g. 0,0 shares GPU 0); "
+                                     "overrides --gpus")
+    e.add_argument("--threads", type=int, default=0,
+                   help="host pool for FASTQ parse and deflate (0: CPUs available to the process)")
     e.add_argument("--blocks-per-batch", type=int, default=16, help="65,536-read blocks per GPU call")
+    e.add_argument("--deflate", choices=["zlib", "libdeflate"], default="zlib",
+                   help="gzip engine for the block streams (level 6 both; the bytes differ, the content does not)")
     e.add_argument("--stats", action="store_true", help="print per-stage seconds to stderr")
     d = sub.add_parser("decode", help="Decode data written with Encode")
     d.add_argument("input_path", help="File with encoded fastX data.")
     d.add_argument("-i", "--index", dest="index_prefix", required=True, help="Prefix for prebuilt <prefix>.sbwt and <prefix>.lcs")
     d.add_argument("--gpus", type=int, default=1, help="GPUs to decode on (batches dealt round-robin).")
-    d.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 4), help="block unzip / format threads")
+    d.add_argument("--devices", help="comma-separated device list, one context each; overrides --gpus")
+    d.add_argument("--threads", type=int, default=0, help="block unzip / format threads (0: CPUs available)")
     d.add_argument("--blocks-per-batch", type=int, default=16, help="blocks per GPU call")
     d.add_argument("--stats", action="store_true", help="print per-stage seconds to stderr")
     args = ap.parse_args(argv)
+    if getattr(args, "threads", None) == 0:
+        import ntcomp_amd as nt
+        args.threads = nt.host_threads()
     if args.command == "build":
         cmd_build(args)
     elif args.command == "encode":

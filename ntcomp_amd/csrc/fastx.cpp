@@ -18,6 +18,11 @@
 // normalisation into one growing buffer), so a gzip input is bound by inflate alone.
 #include <dlfcn.h>
 #include <emmintrin.h>
+#include <fcntl.h>
+#include <sched.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -28,6 +33,8 @@
 #include <cstring>
 #include <deque>
 #include <mutex>
+#include <new>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -59,6 +66,141 @@ void init_norm() {
     norm_init = true;
 }
 
+// growable byte buffer without zero-fill (std::vector::resize would touch every new byte)
+struct RawBuf {
+    uint8_t *p = nullptr;
+    size_t cap = 0;
+    RawBuf() = default;
+    RawBuf(const RawBuf &) = delete;
+    RawBuf &operator=(const RawBuf &) = delete;
+    RawBuf(RawBuf &&o) noexcept : p(o.p), cap(o.cap) { o.p = nullptr, o.cap = 0; }
+    ~RawBuf() { std::free(p); }
+    uint8_t *data() { return p; }
+    size_t size() const { return cap; }
+    // room for n bytes, keeping the first keep
+    void reserve_keep(size_t n, size_t keep) {
+        if (n <= cap) return;
+        size_t want = std::max(n, cap + cap / 2);
+        uint8_t *q;
+        if (want >= (8u << 20)) {  // large: 2 MB aligned, transparent huge pages (512x fewer faults)
+            want = (want + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+            q = (uint8_t *)std::aligned_alloc(2u << 20, want);
+            if (q) madvise(q, want, MADV_HUGEPAGE);
+        } else {
+            q = (uint8_t *)std::malloc(want);
+        }
+        if (!q) throw std::bad_alloc();
+        if (keep) std::memcpy(q, p, keep);
+        std::free(p);
+        p = q;
+        cap = want;
+    }
+};
+
+// normalize(true) of n bytes into d (d has room for n); returns the bytes kept
+size_t norm_copy(const char *s, size_t n, uint8_t *d) {
+    size_t i = 0, j = 0;
+    // fast path: 16 bytes at a time while every byte is already one of A C G T
+    const __m128i cA = _mm_set1_epi8('A'), cC = _mm_set1_epi8('C'), cG = _mm_set1_epi8('G'), cT = _mm_set1_epi8('T');
+    for (; i + 16 <= n; i += 16) {
+        const __m128i x = _mm_loadu_si128((const __m128i *)(s + i));
+        const __m128i ok = _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(x, cA), _mm_cmpeq_epi8(x, cC)),
+                                        _mm_or_si128(_mm_cmpeq_epi8(x, cG), _mm_cmpeq_epi8(x, cT)));
+        if (_mm_movemask_epi8(ok) == 0xFFFF) {
+            _mm_storeu_si128((__m128i *)(d + j), x);
+            j += 16;
+            continue;
+        }
+        for (size_t t = i; t < i + 16; t++) {  // this block holds something else
+            const uint8_t v = norm_table[(uint8_t)s[t]];
+            d[j] = v;
+            j += v != 0;
+        }
+    }
+    for (; i < n; i++) {
+        const uint8_t v = norm_table[(uint8_t)s[i]];
+        d[j] = v;
+        j += v != 0;
+    }
+    return j;
+}
+
+// line length without a trailing '\r' (needletail strips CRLF endings)
+inline size_t line_len(const char *b, const char *e) { return (size_t)(e - b) - (e > b && e[-1] == '\r'); }
+
+// ---- plain FASTQ through mmap, parsed in parallel -------------------------------------
+// A batch's byte range is cut into T pieces at record starts (a line beginning with '@'
+// whose next-but-one line begins with '+': a quality line that begins with '@' is followed
+// by a header and a sequence line, so it never qualifies); each piece is parsed by its own
+// thread, and every piece must end exactly where the next begins, else the range is parsed
+// again by one thread.  Same records, same errors as the streaming parser.
+struct FqPiece {
+    RawBuf bases;
+    std::vector<uint64_t> ends;    // per record: bases up to and including it
+    std::vector<uint64_t> starts;  // per record: byte position of its '@'
+    size_t stop = 0;               // byte position after the last record parsed (blank lines skipped)
+    int err = 0;                   // 0 ok, NTC_ERR_FORMAT
+};
+
+// records starting in [from, limit) of p[0..n); a record may run past limit
+void parse_fq_range(const char *p, size_t n, size_t from, size_t limit, FqPiece &o) {
+    size_t pos = from;
+    o.ends.clear();
+    o.starts.clear();
+    o.err = 0;
+    uint64_t nb = 0;
+    for (;;) {
+        while (pos < n && (p[pos] == '\n' || p[pos] == '\r')) pos++;
+        if (pos >= limit || pos >= n) break;
+        if (p[pos] != '@') {
+            o.err = NTC_ERR_FORMAT;
+            break;
+        }
+        const char *e = p + n;
+        const char *h = (const char *)std::memchr(p + pos, '\n', n - pos);
+        const char *se = h ? (const char *)std::memchr(h + 1, '\n', (size_t)(e - h - 1)) : nullptr;
+        const char *pe = se ? (const char *)std::memchr(se + 1, '\n', (size_t)(e - se - 1)) : nullptr;
+        if (!pe) {  // truncated record
+            o.err = NTC_ERR_FORMAT;
+            break;
+        }
+        const char *qe = (const char *)std::memchr(pe + 1, '\n', (size_t)(e - pe - 1));
+        if (!qe) qe = e;  // the last line may lack its newline
+        if (se[1] != '+' || line_len(h + 1, se) != line_len(pe + 1, qe)) {
+            o.err = NTC_ERR_FORMAT;
+            break;
+        }
+        const size_t L = (size_t)(se - h - 1);
+        o.bases.reserve_keep(nb + L + (1u << 16), nb);
+        nb += norm_copy(h + 1, L, o.bases.data() + nb);
+        o.starts.push_back(pos);
+        o.ends.push_back(nb);
+        pos = (size_t)(qe - p) + (qe < e);
+    }
+    while (pos < n && (p[pos] == '\n' || p[pos] == '\r')) pos++;
+    o.stop = pos;
+}
+
+// first record start at or after c and before limit (limit if none)
+size_t fq_record_start(const char *p, size_t n, size_t c, size_t limit) {
+    if (c > 0 && p[c - 1] != '\n') {
+        const char *nl = (const char *)std::memchr(p + c, '\n', n - c);
+        if (!nl) return limit;
+        c = (size_t)(nl - p) + 1;
+    }
+    while (c < limit) {
+        if (p[c] == '@') {
+            const char *l1 = (const char *)std::memchr(p + c, '\n', n - c);
+            const char *l2 = l1 ? (const char *)std::memchr(l1 + 1, '\n', n - (size_t)(l1 + 1 - p)) : nullptr;
+            if (l2 && l2 + 1 < p + n && l2[1] == '+') return c;
+        }
+        const char *nl = (const char *)std::memchr(p + c, '\n', n - c);
+        if (!nl) return limit;
+        c = (size_t)(nl - p) + 1;
+    }
+    return limit;
+}
+
 constexpr size_t kChunk = 8u << 20;
 constexpr size_t kRing = 4;
 
@@ -72,7 +214,15 @@ struct GzReader : ByteReader {  // plain or gzip (zlib's transparent gz* reader)
     gzFile f;
     explicit GzReader(gzFile file) : f(file) {}
     ~GzReader() override { gzclose(f); }
-    int read(char *dst, unsigned n) override { return gzread(f, dst, n); }
+    int read(char *dst, unsigned n) override {
+        const int got = gzread(f, dst, n);
+        if (got <= 0) {  // gzread reports a truncated member as a clean end: ask gzerror
+            int err = Z_OK;
+            gzerror(f, &err);
+            if (err != Z_OK) return -1;
+        }
+        return got;
+    }
 };
 
 // Stream decoders over a FILE*: feed kIn-byte blocks of the compressed file to a decoder
@@ -263,23 +413,35 @@ struct ZstdCodec {
     }
 };
 
-// gzip through libdeflate (libdeflate.so.0, ~4x zlib's inflate rate on this image): whole
-// members at once, so the compressed file is read into memory and each member inflates into
-// one buffer (a BGZF member's size is in its header; otherwise the output size is guessed
-// from the last ISIZE, mod 2^32, and grown on LIBDEFLATE_INSUFFICIENT_SPACE).  Used for
-// files up to kDeflateMaxFile compressed bytes; larger ones stream through zlib.
-constexpr uint64_t kDeflateMaxFile = 2ull << 30;
+// gzip through libdeflate (libdeflate.so.0, ~4x zlib's inflate rate on this image).
+//  * BGZF (bgzip: members of <= 64 KB carrying their size): the compressed file streams
+//    through a bounded window (kWindow) and runs of up to kBatch members inflate in
+//    parallel into one buffer at the offsets their ISIZE trailers give.
+//  * Other gzip files up to kWholeMax compressed bytes: read whole, each member inflated
+//    into one buffer sized from its ISIZE guess (the last member's ISIZE, mod 2^32), capped
+//    at kOutCap; a member that does not fit, or any libdeflate failure, hands the stream
+//    to zlib's gzread from the same point (the bytes already delivered are skipped), so a
+//    valid file never fails here.  Larger gzip files stream through zlib directly.
+//  * Bytes after the last member that are not a gzip member end the input, as gzread does.
+constexpr uint64_t kWholeMax = 256ull << 20;
+constexpr uint64_t kOutCap = 2ull << 30;
+constexpr size_t kWindow = 32u << 20;
 struct DeflateReader : ByteReader {
     void *(*alloc_fn)() = nullptr;
     void (*free_fn)(void *) = nullptr;
     int (*gz_fn)(void *, const void *, size_t, void *, size_t, size_t *, size_t *) = nullptr;
     void *dec = nullptr;
-    std::vector<unsigned char> comp;
-    size_t ci = 0;  // next member
+    std::string path;
+    FILE *f = nullptr;
+    bool bgzf = false, in_eof = false;
+    std::vector<unsigned char> comp;  // whole file, or the BGZF window [ci, comp_end)
+    size_t ci = 0, comp_end = 0;
     char *out = nullptr;
     size_t out_n = 0, out_pos = 0, cap = 0;
+    uint64_t delivered = 0, members = 0;
+    GzReader *zfall = nullptr;  // zlib takes over after a libdeflate failure
     bool ok = false;
-    DeflateReader(FILE *f, uint64_t size) {
+    DeflateReader(const char *p, FILE *file, uint64_t size, bool is_bgzf) : path(p), f(file), bgzf(is_bgzf) {
         void *h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
         if (h) {
             alloc_fn = (void *(*)())dlsym(h, "libdeflate_alloc_decompressor");
@@ -287,43 +449,83 @@ struct DeflateReader : ByteReader {
             gz_fn = (int (*)(void *, const void *, size_t, void *, size_t, size_t *, size_t *))dlsym(
                 h, "libdeflate_gzip_decompress_ex");
         }
-        if (alloc_fn && free_fn && gz_fn && (dec = alloc_fn())) {
+        if (!(alloc_fn && free_fn && gz_fn && (dec = alloc_fn()))) return;
+        if (bgzf) {
+            comp.resize(kWindow);
+            ok = true;
+        } else {
             comp.resize(size);
             ok = std::fread(comp.data(), 1, size, f) == size;
+            comp_end = size;
+            in_eof = true;
         }
-        std::fclose(f);
     }
     ~DeflateReader() override {
         if (dec) free_fn(dec);
         for (void *d : pool) free_fn(d);
         std::free(out);
+        delete zfall;
+        if (f) std::fclose(f);
     }
     static uint32_t le32(const unsigned char *p) { return p[0] | p[1] << 8 | p[2] << 16 | (uint32_t)p[3] << 24; }
     // BGZF member at m (left bytes on): its size, or 0 when it is not one
     static size_t bgzf_size(const unsigned char *m, size_t left) {
-        if (left < 26 || m[0] != 0x1F || m[1] != 0x8B || !(m[3] & 4) || (m[10] | m[11] << 8) < 6 || m[12] != 'B' ||
+        if (left < 18 || m[0] != 0x1F || m[1] != 0x8B || !(m[3] & 4) || (m[10] | m[11] << 8) < 6 || m[12] != 'B' ||
             m[13] != 'C')
             return 0;
         const size_t bsize = (size_t)(m[16] | m[17] << 8) + 1;
-        return bsize >= 26 && bsize <= left ? bsize : 0;
+        return bsize >= 26 ? bsize : 0;
     }
-    // BGZF: the next run of up to kBatch members, inflated in parallel into out at the offsets
-    // their ISIZE trailers give (bgzip's 64 KB members are independent).  1 done, 0 not BGZF here
-    // (or a single member), -1 error
+    // BGZF window: keep [ci, comp_end) and top it up from the file
+    bool refill() {
+        if (in_eof) return true;
+        if (ci) {
+            std::memmove(comp.data(), comp.data() + ci, comp_end - ci);
+            comp_end -= ci;
+            ci = 0;
+        }
+        while (comp_end < comp.size()) {
+            const size_t got = std::fread(comp.data() + comp_end, 1, comp.size() - comp_end, f);
+            if (got == 0) {
+                if (std::ferror(f)) return false;
+                in_eof = true;
+                break;
+            }
+            comp_end += got;
+        }
+        return true;
+    }
+    // The next run of up to kBatch BGZF members, inflated in parallel (bgzip's members are
+    // independent).  1 done, 0 no member here, -1 error
     static constexpr size_t kBatch = 256;
     std::vector<void *> pool;
     int next_bgzf_batch() {
         std::vector<size_t> at, sz, off(1, 0);
-        size_t c = ci;
-        while (at.size() < kBatch && c < comp.size()) {
-            const size_t b = bgzf_size(comp.data() + c, comp.size() - c);
-            if (!b) break;
-            at.push_back(c);
-            sz.push_back(b);
-            off.push_back(off.back() + le32(comp.data() + c + b - 4));
-            c += b;
+        for (int pass = 0; pass < 2; pass++) {
+            at.clear();
+            sz.clear();
+            off.assign(1, 0);
+            size_t c = ci;
+            bool short_window = false;
+            while (at.size() < kBatch && c < comp_end) {
+                const size_t b = bgzf_size(comp.data() + c, comp_end - c);
+                if (!b) break;
+                if (b > comp_end - c) {  // the member runs past the window
+                    short_window = true;
+                    break;
+                }
+                at.push_back(c);
+                sz.push_back(b);
+                off.push_back(off.back() + le32(comp.data() + c + b - 4));
+                c += b;
+            }
+            if (pass == 0 && (at.size() < kBatch && (short_window || c == comp_end)) && !in_eof) {
+                if (!refill()) return -1;
+                continue;
+            }
+            break;
         }
-        if (at.size() < 2) return 0;
+        if (at.empty()) return 0;
         if (off.back() + 1 > cap) {
             std::free(out);
             cap = std::max<size_t>(off.back() + 1, kBatch << 16);
@@ -349,32 +551,35 @@ struct DeflateReader : ByteReader {
             }
         };
         std::vector<std::thread> th;
-        for (unsigned t = 1; t < T; t++) th.emplace_back(work, t);
+        for (unsigned t = 1; t < T && t < at.size(); t++) th.emplace_back(work, t);
         work(0);
         for (auto &x : th) x.join();
         if (bad) return -1;
-        ci = c;
+        ci = at.back() + sz.back();
+        members += at.size();
         out_n = off.back();
         out_pos = 0;
         return 1;
     }
-    // the member at ci into out: 1 done, 0 no member left, -1 error
+    // the member at ci into out: 1 done, 0 end of input, -1 error (zlib takes over)
     int next_member() {
-        const size_t left = comp.size() - ci;
-        if (left == 0) return 0;
-        const int rb = next_bgzf_batch();
-        if (rb != 0) return rb;
-        const unsigned char *m = comp.data() + ci;
-        if (left < 18 || m[0] != 0x1F || m[1] != 0x8B) return -1;
-        uint64_t want;
-        if (const size_t bsize = bgzf_size(m, left)) {  // BGZF: the member's size, its ISIZE exact
-            want = le32(m + bsize - 4);
-        } else {
-            // the last member's ISIZE + j 2^32 >= what is left (inflated >= its input - headers)
-            want = le32(comp.data() + comp.size() - 4);
-            while (want + 64 < left) want += 1ull << 32;
+        if (bgzf) {
+            if (comp_end - ci < 26 && !in_eof && !refill()) return -1;
+            if (ci == comp_end) return 0;
+            const int rb = next_bgzf_batch();
+            if (rb != 0) return rb;
+            // not a BGZF member here: the rest goes through zlib
+            return -1;
         }
+        const size_t left = comp_end - ci;
+        if (left == 0) return 0;
+        const unsigned char *m = comp.data() + ci;
+        if (left < 18 || m[0] != 0x1F || m[1] != 0x8B) return members ? 0 : -1;  // trailing bytes end it
+        // the last member's ISIZE + j 2^32 >= what is left (inflated >= its input - headers)
+        uint64_t want = le32(comp.data() + comp_end - 4);
+        while (want + 64 < left) want += 1ull << 32;
         for (;;) {
+            if (want > kOutCap) return -1;
             if (want + 1 > cap) {
                 std::free(out);
                 cap = want + 1;
@@ -385,21 +590,42 @@ struct DeflateReader : ByteReader {
             const int rc = gz_fn(dec, m, left, out, cap, &in_used, &got);
             if (rc == 0) {
                 ci += in_used;
+                members++;
                 out_n = got;
                 out_pos = 0;
                 return 1;
             }
-            // 3 = INSUFFICIENT_SPACE (a multi-member file's earlier, larger member): grow
-            if (rc != 3 || want > (uint64_t)left * 1100 + (1u << 20)) return -1;
+            if (rc != 3) return -1;  // 3 = INSUFFICIENT_SPACE: an earlier, larger member
             want = want * 2 + (1u << 20);
         }
     }
-    int read(char *dst, unsigned n) override {  // fills dst across (BGZF's 64 KB) members
+    // hand the rest of the stream to zlib: reopen, skip what was delivered
+    bool to_zlib() {
+        gzFile g = gzopen(path.c_str(), "rb");
+        if (!g) return false;
+        gzbuffer(g, 1u << 20);
+        zfall = new GzReader(g);
+        std::vector<char> skip(1u << 20);
+        uint64_t left = delivered;
+        while (left) {
+            const int got = zfall->read(skip.data(), (unsigned)std::min<uint64_t>(left, skip.size()));
+            if (got <= 0) return false;
+            left -= (uint64_t)got;
+        }
+        return true;
+    }
+    int read(char *dst, unsigned n) override {  // fills dst across members
+        if (zfall) return zfall->read(dst, n);
         unsigned done = 0;
         while (done < n) {
             if (out_pos == out_n) {
                 const int rc = next_member();
-                if (rc < 0) return -1;
+                if (rc < 0) {
+                    if (!to_zlib()) return -1;
+                    const int more = zfall->read(dst + done, n - done);
+                    if (more < 0) return -1;
+                    return (int)(done + (unsigned)more);
+                }
                 if (rc == 0) break;
                 continue;
             }
@@ -407,6 +633,7 @@ struct DeflateReader : ByteReader {
             std::memcpy(dst + done, out + out_pos, t);
             out_pos += t;
             done += (unsigned)t;
+            delivered += t;
         }
         return (int)done;
     }
@@ -436,12 +663,15 @@ ByteReader *open_reader(const char *path, int *rc) {
         if (!z->ok) { delete z; *rc = NTC_ERR_UNSUPPORTED; return nullptr; }
         r = z;
     } else {
-        if (got >= 3 && m[0] == 0x1F && m[1] == 0x8B && m[2] == 8) {
+        if (got >= 3 && m[0] == 0x1F && m[1] == 0x8B && m[2] == 8 && !std::getenv("NTC_FASTX_ZLIB")) {
+            unsigned char h[18] = {0};
+            const size_t hn = std::fread(h, 1, 18, f);
             std::fseek(f, 0, SEEK_END);
             const long size = std::ftell(f);
             std::rewind(f);
-            if (size > 0 && (uint64_t)size <= kDeflateMaxFile && !std::getenv("NTC_FASTX_ZLIB")) {
-                auto *d = new DeflateReader(f, (uint64_t)size);  // closes f
+            const bool bgzf = hn == 18 && DeflateReader::bgzf_size(h, 18) != 0;
+            if (size > 0 && (bgzf || (uint64_t)size <= kWholeMax)) {
+                auto *d = new DeflateReader(path, f, (uint64_t)size, bgzf);  // owns f
                 if (d->ok) return d;
                 delete d;
                 f = nullptr;
@@ -524,6 +754,12 @@ struct ChunkSource {
 }  // namespace
 
 struct ntc_fastx {
+    // plain FASTQ: the file mapped, parsed in parallel pieces (parse_fq_range)
+    const char *mm = nullptr;
+    size_t mm_n = 0, mm_pos = 0;
+    double avg_rec = 0;  // bytes per record so far
+    int threads = 1;
+    std::vector<FqPiece> pieces;
     ByteReader *f = nullptr;
     ChunkSource *src = nullptr;
     std::vector<char> buf;  // unparsed bytes live in [pos, end)
@@ -533,10 +769,113 @@ struct ntc_fastx {
     int format = 0;  // '>' FASTA, '@' FASTQ
     bool have_pending = false;  // FASTA: the next record's '>' line was already consumed
     // current batch
-    std::vector<uint8_t> bases;
+    RawBuf bases;
     size_t nb = 0;
     std::vector<uint64_t> offsets;
 
+    // one batch from the mapping: up to max_reads reads / about max_bases bases
+    int mm_batch(uint64_t max_reads, uint64_t max_bases, uint8_t *dst, uint64_t dst_cap, uint64_t *dst_offs) {
+        uint64_t reads = 0;
+        nb = 0;
+        while (reads < max_reads && nb < max_bases && mm_pos < mm_n) {
+            const uint64_t want = max_reads - reads;
+            if (avg_rec <= 0) {  // probe the record size on a few records
+                FqPiece probe;
+                parse_fq_range(mm, mm_n, mm_pos, std::min(mm_n, mm_pos + (64u << 10)), probe);
+                avg_rec = probe.starts.size() > 1 ? (double)(probe.starts.back() - probe.starts[0]) /
+                                                        (double)(probe.starts.size() - 1)
+                                                  : 512.0;
+            }
+            const size_t region = (size_t)std::min<double>((double)(mm_n - mm_pos),
+                                                           (double)want * avg_rec * 1.02 + (256u << 10));
+            const size_t lim = mm_pos + region;
+            const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)threads, region >> 20));
+            if ((int)pieces.size() < T) pieces.resize((size_t)T);
+            std::vector<size_t> cut((size_t)T + 1);
+            cut[0] = mm_pos;
+            cut[(size_t)T] = lim;
+            for (int t = 1; t < T; t++)
+                cut[(size_t)t] = std::max(cut[(size_t)t - 1], fq_record_start(mm, mm_n, mm_pos + region * (size_t)t / (size_t)T, lim));
+            // size every piece's buffers here: allocating inside the workers serialises them on
+            // the address-space lock that their page faults need too
+            for (int t = 0; t < T; t++) {
+                const size_t bytes = cut[(size_t)t + 1] - cut[(size_t)t];
+                const size_t recs = (size_t)((double)bytes / std::max(avg_rec, 16.0) * 1.25) + 1024;
+                pieces[(size_t)t].bases.reserve_keep(bytes / 2 + (1u << 20), 0);
+                pieces[(size_t)t].ends.reserve(recs);
+                pieces[(size_t)t].starts.reserve(recs);
+            }
+            auto work = [&](int t) { parse_fq_range(mm, mm_n, cut[(size_t)t], cut[(size_t)t + 1], pieces[(size_t)t]); };
+            std::vector<std::thread> th;
+            for (int t = 1; t < T; t++) th.emplace_back(work, t);
+            work(0);
+            for (auto &x : th) x.join();
+            int np = T;
+            for (int t = 0; t + 1 < T; t++)
+                if (pieces[(size_t)t].err || pieces[(size_t)t].stop != cut[(size_t)t + 1]) {
+                    np = -1;  // a piece did not end where the next begins: parse [mm_pos, lim) in one
+                    break;
+                }
+            if (np < 0) {
+                np = 1;
+                parse_fq_range(mm, mm_n, mm_pos, lim, pieces[0]);
+            }
+            // take records in order up to the limits; the first record not taken restarts there
+            size_t next_pos = pieces[(size_t)np - 1].stop;
+            int err = 0;
+            std::vector<uint64_t> take((size_t)np, 0), base0((size_t)np, 0), boff((size_t)np, 0);
+            for (int t = 0; t < np; t++) {
+                FqPiece &pc = pieces[(size_t)t];
+                base0[(size_t)t] = reads;
+                boff[(size_t)t] = nb;
+                uint64_t k = 0;
+                while (k < pc.ends.size() && reads + k < max_reads && nb + (k ? pc.ends[k - 1] : 0) < max_bases) k++;
+                take[(size_t)t] = k;
+                reads += k;
+                nb += k ? pc.ends[k - 1] : 0;
+                if (k < pc.ends.size()) {
+                    next_pos = pc.starts[k];
+                    np = t + 1;
+                    break;
+                }
+                if (pc.err) {
+                    err = pc.err;
+                    np = t + 1;
+                    break;
+                }
+            }
+            // copy out in parallel
+            if (!dst) {
+                bases.reserve_keep(nb + 64, boff[0]);
+                if (offsets.size() < reads + 1) offsets.resize(reads + 1);
+            } else if (nb > dst_cap) {
+                return NTC_ERR_CAPACITY;
+            }
+            uint8_t *B = dst ? dst : bases.data();
+            uint64_t *O = dst ? dst_offs : offsets.data();
+            O[0] = 0;
+            auto copy = [&](int t) {
+                FqPiece &pc = pieces[(size_t)t];
+                const uint64_t k = take[(size_t)t];
+                if (!k) return;
+                std::memcpy(B + boff[(size_t)t], pc.bases.data(), pc.ends[k - 1]);
+                for (uint64_t i = 0; i < k; i++) O[base0[(size_t)t] + i + 1] = boff[(size_t)t] + pc.ends[i];
+            };
+            th.clear();
+            for (int t = 1; t < np; t++) th.emplace_back(copy, t);
+            copy(0);
+            for (auto &x : th) x.join();
+
+            if (err) return err;
+            const size_t used = next_pos - mm_pos;
+            mm_pos = next_pos;
+            if (reads) avg_rec = 0.5 * avg_rec + 0.5 * (double)used / (double)std::max<uint64_t>(1, reads - base0[0]);
+            if (used == 0) break;  // nothing parsed (end of data)
+        }
+        mm_reads = reads;
+        return NTC_OK;
+    }
+    uint64_t mm_reads = 0;
     // append the next chunk behind the unparsed tail; false at end of input (a missing
     // final newline is supplied once so the last line always ends in '\n')
     bool fill() {
@@ -564,33 +903,8 @@ struct ntc_fastx {
         return (const char *)std::memchr(buf.data() + from, '\n', end - from);
     }
     void append_seq(const char *s, size_t n) {
-        if (nb + n > bases.size()) bases.resize(std::max(bases.size() * 2, nb + n + (1u << 20)));
-        uint8_t *d = bases.data() + nb;
-        size_t i = 0, j = 0;
-        // fast path: 16 bytes at a time while every byte is already one of A C G T
-        const __m128i cA = _mm_set1_epi8('A'), cC = _mm_set1_epi8('C'), cG = _mm_set1_epi8('G'),
-                      cT = _mm_set1_epi8('T');
-        for (; i + 16 <= n; i += 16) {
-            const __m128i x = _mm_loadu_si128((const __m128i *)(s + i));
-            const __m128i ok = _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(x, cA), _mm_cmpeq_epi8(x, cC)),
-                                            _mm_or_si128(_mm_cmpeq_epi8(x, cG), _mm_cmpeq_epi8(x, cT)));
-            if (_mm_movemask_epi8(ok) == 0xFFFF) {
-                _mm_storeu_si128((__m128i *)(d + j), x);
-                j += 16;
-                continue;
-            }
-            for (size_t t = i; t < i + 16; t++) {  // this block holds something else
-                const uint8_t v = norm_table[(uint8_t)s[t]];
-                d[j] = v;
-                j += v != 0;
-            }
-        }
-        for (; i < n; i++) {
-            const uint8_t v = norm_table[(uint8_t)s[i]];
-            d[j] = v;
-            j += v != 0;
-        }
-        nb += j;
+        bases.reserve_keep(nb + n + (1u << 20), nb);
+        nb += norm_copy(s, n, bases.data() + nb);
     }
     // next FASTQ record's sequence appended; 0 ok, 1 end of input, <0 format error
     int next_fastq() {
@@ -609,7 +923,7 @@ struct ntc_fastx {
                 if (!fill()) return -1;  // truncated record
                 continue;
             }
-            if (se[1] != '+') return -1;
+            if (se[1] != '+' || line_len(h + 1, se) != line_len(pe + 1, qe)) return -1;  // needletail: equal lengths
             append_seq(h + 1, (size_t)(se - h - 1));
             pos = (size_t)(qe - buf.data()) + 1;
             return 0;
@@ -663,10 +977,75 @@ struct ntc_fastx {
 
 extern "C" {
 
+int ntc_host_threads(void) {
+    static int cached = 0;
+    if (cached) return cached;
+    int n = 0;
+    if (const char *v = std::getenv("NTC_THREADS")) n = std::atoi(v);
+    if (n <= 0) {
+        cpu_set_t set;
+        n = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : (int)std::thread::hardware_concurrency();
+        if (FILE *f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {  // cgroup v2 CPU quota
+            char q[32] = {0};
+            unsigned long long period = 0;
+            if (std::fscanf(f, "%31s %llu", q, &period) == 2 && std::strcmp(q, "max") != 0 && period) {
+                const unsigned long long quota = std::strtoull(q, nullptr, 10);
+                const int lim = (int)((quota + period - 1) / period);
+                if (lim > 0 && lim < n) n = lim;
+            }
+            std::fclose(f);
+        }
+    }
+    cached = std::max(1, n);
+    return cached;
+}
+
+int ntc_fastx_set_threads(ntc_fastx *fx, int n_threads) {
+    if (!fx) return NTC_ERR_INVALID_ARG;
+    fx->threads = n_threads > 0 ? n_threads : ntc_host_threads();
+    return NTC_OK;
+}
+
+// A plain (uncompressed) FASTQ file is mapped and parsed in parallel; anything else streams.
+static ntc_fastx *open_mapped_fastq(const char *path) {
+    const int fd = ::open(path, O_RDONLY);
+    if (fd < 0) return nullptr;
+    struct stat st;
+    if (fstat(fd, &st) != 0 || !S_ISREG(st.st_mode) || st.st_size < 4) {
+        ::close(fd);
+        return nullptr;
+    }
+    const size_t n = (size_t)st.st_size;
+    const unsigned char *m = (const unsigned char *)mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+    ::close(fd);
+    if (m == MAP_FAILED) return nullptr;
+    const bool compressed = (m[0] == 0x1F && m[1] == 0x8B) || (m[0] == 'B' && m[1] == 'Z' && m[2] == 'h') ||
+                            (m[0] == 0xFD && m[1] == '7') || (m[0] == 0x28 && m[1] == 0xB5);
+    size_t i = 0;
+    while (i < n && (m[i] == '\n' || m[i] == '\r' || m[i] == ' ')) i++;
+    if (compressed || i == n || m[i] != '@') {
+        munmap((void *)m, n);
+        return nullptr;
+    }
+    madvise((void *)m, n, MADV_SEQUENTIAL);
+    auto *fx = new ntc_fastx();
+    fx->mm = (const char *)m;
+    fx->mm_n = n;
+    fx->mm_pos = 0;
+    fx->format = '@';
+    fx->threads = ntc_host_threads();
+    return fx;
+}
+
 int ntc_fastx_open(const char *path, ntc_fastx **out) {
     if (!path || !out) return NTC_ERR_INVALID_ARG;
     *out = nullptr;
     init_norm();
+    if (!std::getenv("NTC_FASTX_STREAM"))
+        if (ntc_fastx *fx = open_mapped_fastq(path)) {
+            *out = fx;
+            return NTC_OK;
+        }
     int orc = NTC_OK;
     ByteReader *f = open_reader(path, &orc);
     if (!f) return orc;
@@ -697,6 +1076,15 @@ int ntc_fastx_open(const char *path, ntc_fastx **out) {
 int ntc_fastx_next_batch(ntc_fastx *fx, uint64_t max_reads, uint64_t max_bases, const uint8_t **bases,
                          const uint64_t **offsets, uint64_t *n_reads) {
     if (!fx || !bases || !offsets || !n_reads || max_reads == 0) return NTC_ERR_INVALID_ARG;
+    if (fx->mm) {
+        const int rc = fx->mm_batch(max_reads, max_bases, nullptr, 0, nullptr);
+        if (rc) return rc;
+        if (fx->offsets.empty()) fx->offsets.assign(1, 0);
+        *bases = fx->bases.data();
+        *offsets = fx->offsets.data();
+        *n_reads = fx->mm_reads;
+        return NTC_OK;
+    }
     fx->nb = 0;
     fx->offsets.assign(1, 0);
     fx->offsets.reserve(max_reads + 1);
@@ -737,8 +1125,36 @@ int ntc_fasta_format(const uint8_t *bases, const uint64_t *offsets, uint64_t n_r
     return NTC_OK;
 }
 
+int ntc_fastx_next_batch_into(ntc_fastx *fx, uint64_t max_reads, uint64_t max_bases, uint8_t *bases,
+                              uint64_t bases_capacity, uint64_t *offsets, uint64_t *n_reads) {
+    if (!fx || !bases || !offsets || !n_reads || max_reads == 0) return NTC_ERR_INVALID_ARG;
+    *n_reads = 0;
+    if (fx->mm) {
+        const int rc = fx->mm_batch(max_reads, max_bases, bases, bases_capacity, offsets);
+        if (rc) return rc;
+        *n_reads = fx->mm_reads;
+        if (!fx->mm_reads) offsets[0] = 0;
+        return NTC_OK;
+    }
+    const uint8_t *b;
+    const uint64_t *o;
+    uint64_t n;
+    const int rc = ntc_fastx_next_batch(fx, max_reads, max_bases, &b, &o, &n);
+    if (rc) return rc;
+    if (o[n] > bases_capacity) return NTC_ERR_CAPACITY;
+    std::memcpy(bases, b, o[n]);
+    std::memcpy(offsets, o, (n + 1) * 8);
+    *n_reads = n;
+    return NTC_OK;
+}
+
 void ntc_fastx_close(ntc_fastx *fx) {
     if (!fx) return;
+    if (fx->mm) {
+        munmap((void *)fx->mm, fx->mm_n);
+        delete fx;
+        return;
+    }
     delete fx->src;  // joins the producer before the file goes away
     delete fx->f;
     delete fx;

@@ -23,15 +23,20 @@ def main():
     ap.add_argument("--gzip", action="store_true", help="gzip the FASTQ (level 1)")
     ap.add_argument("--bgzf", action="store_true", help="with --gzip: BGZF members (bgzip layout) instead of one member")
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--devices", help="CLI --devices list (several contexts may share a GPU)")
+    ap.add_argument("--deflate", default="zlib", choices=["zlib", "libdeflate"])
+    ap.add_argument("--keep", action="store_true", help="reuse an existing FASTQ + index in --dir")
+    ap.add_argument("--reps", type=int, default=3, help="runs per timing (the best counts)")
     a = ap.parse_args()
-    a.gpus_arg = ["--gpus", str(a.gpus)]
+    a.gpus_arg = ["--devices", a.devices] if a.devices else ["--gpus", str(a.gpus)]
     import numpy as np
     import ntcomp_amd as nt
     os.makedirs(a.dir, exist_ok=True)
     genome = nt.synth_genome(1, a.genome_bp)
-    ix = nt.Index.build([genome.tobytes()], a.k, threads=16)
     prefix = os.path.join(a.dir, "idx")
-    ix.save(prefix)
+    if not (a.keep and os.path.exists(prefix + ".sbwt")):
+        ix = nt.Index.build([genome.tobytes()], a.k, threads=16)
+        ix.save(prefix)
     L, n = a.read_len, a.reads
     reads = nt.synth_reads(genome, 2, 0, n, L, 10_000, threads=16)
     fq = os.path.join(a.dir, "reads.fq" + (".gz" if a.gzip else ""))
@@ -43,7 +48,9 @@ def main():
     plus = np.frombuffer(b"+\n", dtype=np.uint8)[None, :].repeat(n, 0)
     head = np.frombuffer(b"@r\n", dtype=np.uint8)[None, :].repeat(n, 0)
     rec = np.concatenate([head, body, nl, plus, qual, nl], axis=1).tobytes()
-    if a.gzip and a.bgzf:
+    if a.keep and os.path.exists(fq):
+        pass
+    elif a.gzip and a.bgzf:
         import struct
         import zlib
 
@@ -66,27 +73,39 @@ def main():
     print(f"fastq {len(rec) / 1e9:.2f} GB written in {time.time() - t0:.1f}s", file=sys.stderr)
     enc, dec = os.path.join(a.dir, "enc.dat"), os.path.join(a.dir, "dec.fa")
     cmd = [sys.executable, "-m", "ntcomp_amd"]
-    # fixed cost of one CLI process (interpreter, index load, GPU init + upload): encode an
-    # empty FASTQ and decode its (header-only) output
+
+    def stats_line(err):
+        for line in reversed(err.decode(errors="replace").splitlines()):
+            if line.startswith("{"):
+                return json.loads(line)
+        return None
+
+    def run_encode(src, dst):
+        t0 = time.time()
+        with open(dst, "wb") as f:
+            r = subprocess.run(cmd + ["encode", "-i", prefix, src, "--stats", "--deflate", a.deflate] + a.gpus_arg,
+                               stdout=f, stderr=subprocess.PIPE, check=True, cwd=REPO)
+        return time.time() - t0, stats_line(r.stderr)
+
+    def run_decode(src, dst):
+        t0 = time.time()
+        with open(dst, "wb") as f:
+            r = subprocess.run(cmd + ["decode", "-i", prefix, src, "--stats"] + a.gpus_arg, stdout=f,
+                               stderr=subprocess.PIPE, check=True, cwd=REPO)
+        return time.time() - t0, stats_line(r.stderr)
+
+    # fixed cost of one CLI process (interpreter, index load, GPU init + upload, pipeline
+    # buffers): encode an empty FASTQ and decode its (header-only) output.  Every timing is
+    # the best of --reps runs (process start-up varies by ~0.1 s on a fresh box).
     empty = os.path.join(a.dir, "empty.fq")
     open(empty, "wb").close()
-    t0 = time.time()
-    with open(os.path.join(a.dir, "empty.dat"), "wb") as f:
-        subprocess.run(cmd + ["encode", "-i", prefix, empty] + a.gpus_arg, stdout=f, check=True, cwd=REPO)
-    t_fixed_enc = time.time() - t0
-    t0 = time.time()
-    with open(os.path.join(a.dir, "empty.fa"), "wb") as f:
-        subprocess.run(cmd + ["decode", "-i", prefix, os.path.join(a.dir, "empty.dat")] + a.gpus_arg, stdout=f,
-                       check=True, cwd=REPO)
-    t_fixed_dec = time.time() - t0
-    t0 = time.time()
-    with open(enc, "wb") as f:
-        subprocess.run(cmd + ["encode", "-i", prefix, fq, "--stats"] + a.gpus_arg, stdout=f, check=True, cwd=REPO)
-    te = time.time() - t0
-    t0 = time.time()
-    with open(dec, "wb") as f:
-        subprocess.run(cmd + ["decode", "-i", prefix, enc, "--stats"] + a.gpus_arg, stdout=f, check=True, cwd=REPO)
-    td = time.time() - t0
+    t_fixed_enc = min(run_encode(empty, os.path.join(a.dir, "empty.dat"))[0] for _ in range(a.reps))
+    t_fixed_dec = min(run_decode(os.path.join(a.dir, "empty.dat"), os.path.join(a.dir, "empty.fa"))[0]
+                      for _ in range(a.reps))
+    runs = [run_encode(fq, enc) for _ in range(a.reps)]
+    te, enc_stats = min(runs, key=lambda x: x[0])
+    runs = [run_decode(enc, dec) for _ in range(a.reps)]
+    td, dec_stats = min(runs, key=lambda x: x[0])
     ok = open(dec, "rb").read().split(b"\n")[1::2]
     same = b"".join(ok) == reads.tobytes()
     bases = n * L
@@ -96,10 +115,25 @@ def main():
                       "encode_s": round(te, 3), "encode_mbases_s": round(bases / te / 1e6, 1),
                       "encoded_bytes": os.path.getsize(enc), "bits_per_base": round(8 * os.path.getsize(enc) / bases, 4),
                       "decode_s": round(td, 3), "decode_mbases_s": round(bases / td / 1e6, 1),
-                      "gpus": a.gpus, "fixed_s": {"encode": round(t_fixed_enc, 3), "decode": round(t_fixed_dec, 3)},
+                      "gpus": a.gpus, "reps": a.reps,
+                      "pipeline_mbases_s": {"encode": round(bases / enc_stats["pipeline_wall_s"] / 1e6, 1)
+                                            if enc_stats and enc_stats.get("pipeline_wall_s") else None},
+                      "fixed_s": {"encode": round(t_fixed_enc, 3), "decode": round(t_fixed_dec, 3)},
                       "streaming_mbases_s": {"encode": round(bases / max(te - t_fixed_enc, 1e-9) / 1e6, 1),
                                              "decode": round(bases / max(td - t_fixed_dec, 1e-9) / 1e6, 1)},
-                      "round_trip_exact": same}))
+                      "round_trip_exact": same, "deflate": a.deflate,
+                      "host": {"cpu": _cpu_model(), "threads": nt.host_threads()},
+                      "encode_stages": enc_stats, "decode_stages": dec_stats}))
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 if __name__ == "__main__":

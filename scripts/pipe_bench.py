@@ -1,0 +1,43 @@
+#!/usr/bin/env python3
+"""ntc_encode_file timeline on a FASTQ (no CLI process around it): per-stage thread-seconds
+and when the reader / GPU finished, for sizing the host pipeline."""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dir", default="/tmp/ntc_e2e")
+    ap.add_argument("--deflate", default="libdeflate")
+    ap.add_argument("--bpb", type=int, nargs="+", default=[16])
+    ap.add_argument("--threads", type=int, nargs="+", default=[0])
+    ap.add_argument("--reps", type=int, default=2)
+    a = ap.parse_args()
+    import ntcomp_amd as nt
+    ix = nt.Index.load(os.path.join(a.dir, "idx"))
+    ctx = nt.GpuContext(0)
+    ctx.upload(ix)
+    fq = os.path.join(a.dir, "reads.fq")
+    for bpb in a.bpb:
+        for th in a.threads:
+            for rep in range(a.reps):
+                t0 = time.time()
+                with open(os.path.join(a.dir, "pipe.dat"), "wb") as f:
+                    st = nt.encode_file([ctx], fq, f.fileno(), threads=th, blocks_per_batch=bpb, deflate=a.deflate)
+                w = time.time() - t0
+                st.pop("error")
+                print(json.dumps({"bpb": bpb, "threads": th, "rep": rep, "wall": round(w, 3),
+                                  "gbases_s": round(st["bases"] / w / 1e9, 3),
+                                  **{k: (round(v, 3) if isinstance(v, float) else v) for k, v in st.items()}}),
+                      flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -23,6 +23,7 @@
 #include "ntcomp_codec.h"
 #include "ntcomp_gpu.h"
 #include "ntcomp_host.h"
+#include "ntcomp_pipeline.h"
 
 /* #[repr(C)] NtcIndexView: u64, u32, u32, [*const u64; 4], [u64; 4], *const u8 */
 _Static_assert(sizeof(void *) == 8, "64-bit target");
@@ -44,6 +45,16 @@ _Static_assert(offsetof(ntc_block_meta, stream) == 0 && offsetof(ntc_block_meta,
                    offsetof(ntc_block_meta, n_recs) == 136 && offsetof(ntc_block_meta, status) == 144 &&
                    offsetof(ntc_block_meta, reserved) == 148 && sizeof(ntc_block_meta) == 152,
                "ntc_block_meta");
+/* #[repr(C)] NtcPipelineOpts: i32, i32, u64, i32, i32; NtcPipelineStats: 5 x u64, 9 x f64, i32,
+ * i32, i64, [c_char; 256] */
+_Static_assert(offsetof(ntc_pipeline_opts, batch_bases) == 8 && offsetof(ntc_pipeline_opts, deflate_engine) == 16 &&
+                   sizeof(ntc_pipeline_opts) == 24,
+               "ntc_pipeline_opts");
+_Static_assert(offsetof(ntc_pipeline_stats, parse_s) == 40 && offsetof(ntc_pipeline_stats, wall_s) == 72 &&
+                   offsetof(ntc_pipeline_stats, alloc_s) == 80 && offsetof(ntc_pipeline_stats, threads) == 112 &&
+                   offsetof(ntc_pipeline_stats, bad_read) == 120 && offsetof(ntc_pipeline_stats, error) == 128 &&
+                   sizeof(ntc_pipeline_stats) == 384,
+               "ntc_pipeline_stats");
 /* the status enum crosses the boundary as a C int (Rust: c_int) */
 _Static_assert(sizeof(ntc_status) == sizeof(int), "ntc_status");
 

@@ -1,5 +1,5 @@
 """The C ABI library loads on a CPU-only machine and exports every symbol that
-include/ntcomp_gpu.h and include/ntcomp_host.h declare (no GPU compute here)."""
+include/*.h declare (no GPU compute here)."""
 import ctypes
 import os
 import re
@@ -12,7 +12,7 @@ from oracle_lib import REPO
 
 def declared_symbols():
     names = set()
-    for h in ("ntcomp_gpu.h", "ntcomp_host.h", "ntcomp_codec.h"):
+    for h in ("ntcomp_gpu.h", "ntcomp_host.h", "ntcomp_codec.h", "ntcomp_pipeline.h"):
         src = open(os.path.join(REPO, "include", h)).read()
         names |= set(re.findall(r"\b(ntc_[a-z0-9_]+)\s*\(", src))
     return names

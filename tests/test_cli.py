@@ -131,6 +131,58 @@ def test_fastx_random_records_across_chunks(tmp_path, monkeypatch, fmt, gz):
     assert got == expect
 
 
+@pytest.mark.parametrize("threads", [1, 3, 16])
+def test_fastx_mapped_parallel_equals_streaming(tmp_path, monkeypatch, threads):
+    """Plain FASTQ is memory-mapped and each batch parsed in parallel pieces cut at record
+    starts (fastx.cpp parse_fq_range); batches, records and bases must equal the streaming
+    parser's (NTC_FASTX_STREAM=1), including quality lines that begin with '@' or '+',
+    CRLF endings, blank lines between records and a last line without a newline."""
+    rng = np.random.default_rng(11)
+    parts = []
+    for i in range(60_000):
+        L = int(rng.integers(0, 400)) if i % 97 else 0
+        seq = np.frombuffer(b"ACGTacgtN", np.uint8)[rng.integers(0, 9, L)].tobytes()
+        qual = np.frombuffer(b"@+I#5", np.uint8)[rng.integers(0, 5, L)].tobytes()
+        eol = b"\r\n" if i % 7 == 0 else b"\n"
+        parts.append(b"@r%d x%s%s%s+%s%s%s" % (i, eol, seq, eol, eol, qual, eol) + (b"\n" if i % 13 == 0 else b""))
+    data = b"".join(parts).rstrip(b"\n")
+    path = tmp_path / "p.fq"
+    path.write_bytes(data)
+
+    def batches(stream):
+        if stream:
+            monkeypatch.setenv("NTC_FASTX_STREAM", "1")
+        else:
+            monkeypatch.delenv("NTC_FASTX_STREAM", raising=False)
+        rd = nt.FastxReader(str(path))
+        if not stream:
+            assert nt.lib().ntc_fastx_set_threads(rd.h, threads) == 0
+        out = []
+        while True:
+            x = rd.batch(max_reads=7777, max_bases=1 << 21)
+            if x is None:
+                break
+            out.append((x[0].tobytes(), x[1].tolist()))
+        rd.close()
+        return out
+
+    a, b = batches(False), batches(True)
+    assert len(a) == len(b) and a == b
+    assert sum(len(o) - 1 for _, o in a) == 60_000
+
+
+def test_fastx_fastq_quality_length_must_match(tmp_path):
+    """needletail rejects a record whose quality and sequence lengths differ (the reference
+    then panics in read_from_fastx_parser, main.rs:46): NTC_ERR_FORMAT, mapped or streamed."""
+    for name, data in (("plain.fq", b"@a\nACGT\n+\nIII\n"), ("z.fq.gz", gzip.compress(b"@a\nACGT\n+\nIIIII\n"))):
+        p = tmp_path / name
+        p.write_bytes(data)
+        rd = nt.FastxReader(str(p))
+        with pytest.raises(nt.NtcError) as e:
+            rd.batch()
+        assert e.value.code == 8
+
+
 def _bgzf_member(chunk):
     import struct
     import zlib
@@ -176,6 +228,28 @@ def test_fastx_truncated_and_corrupt_compression(tmp_path):
             for _ in nt.FastxReader(str(tmp_path / name)):
                 pass
         assert e.value.code == 9
+
+
+def test_fastx_gzip_padding_and_mixed_members(tmp_path):
+    """zlib's gzread ignores bytes after the last member (e.g. zero padding) and reads any
+    mix of members; the libdeflate readers must agree: padding ends the input, and a
+    non-BGZF member after BGZF ones hands the rest to zlib (delivered bytes skipped)."""
+    recs = [b"@r%d\n%s\n+\n%s\n" % (i, b"ACGT" * (1 + i % 9), b"I" * (4 * (1 + i % 9))) for i in range(30000)]
+    data = b"".join(recs)
+    exp = [r.split(b"\n")[1] for r in recs]
+    half = len(data) // 2
+    cases = {
+        "pad.fq.gz": gzip.compress(data, 1) + b"\0" * 4096,
+        "multipad.fq.gz": gzip.compress(data[:half], 1) + gzip.compress(data[half:], 1) + b"\0" * 16,
+        "mixed.fq.gz": b"".join(_bgzf_member(data[i:i + 65280]) for i in range(0, half, 65280)) +
+        gzip.compress(data[((half + 65279) // 65280) * 65280:], 1),
+    }
+    for name, blob in cases.items():
+        (tmp_path / name).write_bytes(blob)
+        got = []
+        for b, o in nt.FastxReader(str(tmp_path / name)):
+            got += [b[int(o[r]):int(o[r + 1])].tobytes() for r in range(len(o) - 1)]
+        assert got == exp, name
 
 
 def test_fasta_format():
