@@ -106,7 +106,9 @@ int ntc_ctx_synchronize(ntc_ctx *ctx);
  * pre-filter), "ext2" (0 / 1: two-character rank chunks), "pair_bytes" (0 / 1), same rules.
  * Read-only: "n_paths", "path_text_len" (the path cover built on the device at upload),
  * "path_hash" (test hook: FNV-1a of the cover arrays, derived.h path_cover_hash),
- * "tab_u" (after an upload: the depth in use), "upload_host_us" / "upload_total_us"
+ * "tab_u" (after an upload: the depth in use), "tab_u_fallback" (1: the default depth 15
+ * did not fit in free HBM, 14 was used), "pack_us" (last GPU block packer call, both
+ * kernels), "upload_host_us" / "upload_total_us"
  * (last upload: host-side derivation / whole call).  Env NTC_ENCODE_VARIANT sets the
  * default variant at ntc_ctx_create.                                                 */
 int ntc_ctx_set_option(ntc_ctx *ctx, const char *key, int64_t value);

@@ -585,6 +585,15 @@ def encode_file(ctxs, in_path, out_fd, threads=0, blocks_per_batch=16, batch_bas
     return d
 
 
+def libdeflate_available():
+    """libdeflate.so.0 loads on this host (the block codec's fast deflate engine)."""
+    try:
+        ctypes.CDLL("libdeflate.so.0")
+        return True
+    except OSError:
+        return False
+
+
 def host_threads():
     """CPUs this process may use (NTC_THREADS, else min(affinity, cgroup CPU quota))."""
     return int(lib().ntc_host_threads())

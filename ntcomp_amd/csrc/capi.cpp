@@ -61,6 +61,7 @@ struct ntc_ctx {
     int num_cus = 0;
     Enc4Args last4{};
     uint32_t tab_u_opt = 0;  // suffix-table depth for the next upload (0 = default_tab_u)
+    int tab_u_fallback = 0;  // last upload: the default depth did not fit, U = 14 was used
     int pair_bytes_opt = 1;  // build the SCAN pair bytes at the next upload (0: bitmap tests, A/B)
     int filter_opt = -1;     // SCAN pre-filter at the next upload: -1 auto (off when saturated), 0 off, 1 on
     int64_t filter_density_ppm = -1;  // presence density of the filter level at the last upload
@@ -634,9 +635,29 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     // suffix table, levels 1..U, built on the device from the rank lines
     uint32_t U = ctx->tab_u_opt ? std::min<uint32_t>(ctx->tab_u_opt, std::min<uint32_t>(hx.k, kTabMaxU))
                                 : default_tab_u(n, hx.k, hx.lcs.data());
-    const uint32_t F = filter_level(U);
+    ctx->tab_u_fallback = 0;
+    if (!ctx->tab_u_opt && U > 14) {
+        // the density rule's deeper table (U = 15: 11.5 GB against 2.9 GB) only where it fits
+        // beside what the device already holds plus an encode workspace (ranks may share a GPU)
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
+            (uint64_t)free_b < tab_base(U + 1) * sizeof(uint2) + (64ull << 30)) {
+            U = 14;
+            ctx->tab_u_fallback = 1;
+        }
+    }
     void *d_tab, *d_bits, *d_fbits = nullptr;
-    if ((rc = dalloc(tab_base(U + 1) * sizeof(uint2), &d_tab))) return rc;
+    if (hipMalloc(&d_tab, tab_base(U + 1) * sizeof(uint2)) != hipSuccess) {
+        (void)hipGetLastError();
+        if (ctx->tab_u_opt || U <= 14) return set_err(ctx, NTC_ERR_HIP, "suffix table allocation failed");
+        U = 14;  // allocation failed at the deeper level: fall back (results never depend on U)
+        ctx->tab_u_fallback = 1;
+        if ((rc = dalloc(tab_base(U + 1) * sizeof(uint2), &d_tab))) return rc;
+    } else {
+        ctx->index_mem.push_back(d_tab);
+        ctx->index_bytes += tab_base(U + 1) * sizeof(uint2);
+    }
+    const uint32_t F = filter_level(U);
     if ((rc = dalloc(tab_bits_words(U) * 4, &d_bits))) return rc;
     if (F && (rc = dalloc(tab_bits_words(F) * 4, &d_fbits))) return rc;
     d.tab = (const uint2 *)d_tab;
@@ -746,6 +767,7 @@ int ntc_ctx_get_option(const ntc_ctx *ctx, const char *key, int64_t *value) {
     else if (std::strcmp(key, "upload_host_us") == 0) *value = ctx->upload_host_us;
     else if (std::strcmp(key, "max_pass_bases") == 0) *value = (int64_t)ctx->max_pass_bases;
     else if (std::strcmp(key, "upload_total_us") == 0) *value = ctx->upload_total_us;
+    else if (std::strcmp(key, "tab_u_fallback") == 0) *value = ctx->tab_u_fallback;
     else if (std::strcmp(key, "pack_us") == 0) *value = (int64_t)(ctx->last_pack_ms * 1000.0);
     else return NTC_ERR_INVALID_ARG;
     return NTC_OK;

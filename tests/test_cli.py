@@ -306,7 +306,7 @@ def test_cli_encode_decode_end_to_end(tmp_path):
             f.write(b"@r%d\n" % i + s + b"\n+\n" + b"I" * L + b"\n")
     enc = tmp_path / "enc.dat"
     with open(enc, "wb") as f:
-        _cli("encode", "-i", str(tmp_path / "idx"), "--blocks-per-batch", "1", str(fq), stdout=f)
+        _cli("encode", "-i", str(tmp_path / "idx"), "--blocks-per-batch", "1", "--deflate", "zlib", str(fq), stdout=f)
     # container from the oracle's records, block by block (main.rs:162-177)
     ix = nt.Index.load(str(tmp_path / "idx"))
     orc = OracleIndex(ix.n, 31, ix.rows, ix.C, ix.lcs)

@@ -96,7 +96,8 @@ def test_cli_two_contexts_on_one_gpu_and_deflate_engines(setup, tmp_path):
     fq = tmp_path / "r.fq"
     write_fastq(fq, reads, L)
     files = {}
-    for tag, extra in (("one", []), ("two", ["--devices", "0,0"]), ("ld", ["--deflate", "libdeflate"])):
+    for tag, extra in (("one", ["--deflate", "zlib"]), ("two", ["--devices", "0,0", "--deflate", "zlib"]),
+                       ("ld", ["--deflate", "libdeflate"])):
         with open(tmp_path / f"{tag}.dat", "wb") as f:
             _cli("encode", "-i", str(d / "idx"), str(fq), "--blocks-per-batch", "1", *extra, stdout=f)
         files[tag] = (tmp_path / f"{tag}.dat").read_bytes()
