@@ -475,7 +475,8 @@ NTC_HD void tab_interval(const DevIndex &ix, uint2 te, uint32_t &l, uint32_t &r,
 // Pair word of the (U-1)-mer M (by key), from level U of the suffix table:
 //   bit a      the U-mer a.M is present (long),
 //   bit 4 + c  the U-mer M.c is present,
-//   bit 8 + a  the U-mer a.M is present and its interval is a single node.
+//   bit 8 + a  the U-mer a.M is present and its interval is a single node,
+//   bit 12 + c the U-mer M.c is present and its interval is a single node.
 // For M = the (U-1)-mer ending at y, a = the character before M and c = the one after it,
 // one word says whether the U-mers ending at y AND y + 1 are present (one cache line per
 // SCAN pair test instead of two bitmap lines).  4^(U-1) x 2 bytes.
@@ -489,7 +490,10 @@ NTC_HD uint32_t pair_word(const uint2 *top, uint32_t U, uint64_t M) {
         const uint2 e = top[a | (M << 2)];
         w |= ((uint32_t)tab_long(e) << a) | ((uint32_t)tab_single(e) << (8 + a));
     }
-    for (uint32_t c = 0; c < 4; c++) w |= (uint32_t)tab_long(top[M | ((uint64_t)c << (2 * (U - 1)))]) << (4 + c);
+    for (uint32_t c = 0; c < 4; c++) {
+        const uint2 e = top[M | ((uint64_t)c << (2 * (U - 1)))];
+        w |= ((uint32_t)tab_long(e) << (4 + c)) | ((uint32_t)tab_single(e) << (12 + c));
+    }
     return w;
 }
 
@@ -580,7 +584,10 @@ constexpr uint32_t kScanExact = 4;   // filter candidates tested exactly per SCA
 #define NTC_CHAIN 1
 #endif
 #ifndef NTC_PAIR_TESTS
-#define NTC_PAIR_TESTS 4  // candidate pairs tested per SCAN with pair words
+#define NTC_PAIR_TESTS 4  // pair words loaded per SCAN
+#endif
+#ifndef NTC_PAIR_STRIDE
+#define NTC_PAIR_STRIDE 1  // SCAN pair words at non-overlapping positions: 1 in the joint-run build, 2 always, 0 never
 #endif
 #ifndef NTC_SEEK_BS
 #define NTC_SEEK_BS 1  // EntryView::seek: binary search instead of a forward scan
@@ -1305,40 +1312,85 @@ struct MsLaneT {
             }
 #endif
             if (ix.pair_w) {
-                // exact test of the first candidate PAIRS (y and y + 1 both pass the filter),
-                // one pair byte each; the first pair that is long-long is the SCAN's answer
-                const uint32_t cp = cand & (cand >> 1);
-                uint32_t untested = cp;
-#pragma unroll
-                for (uint32_t t = 0; t < NTC_PAIR_TESTS; t++) untested &= untested - 1;
-                const uint32_t tested = cp ^ untested;
-                // one unconditional load per slot (a missing pair repeats position p), all
-                // issued before the first use
-                // A slot without a candidate repeats the first candidate's word (the same line,
-                // no further request past L2); with no candidate at all every slot reads word 0,
-                // one line all lanes share, instead of a pair word nobody needs
+                // Pair word of the (U-1)-mer ending at y: whether y AND y + 1 are long.
+                //  * stride (genome collections, the k_ms4 build with joint runs): words go to
+                //    non-overlapping positions -- the smallest position not yet known among those
+                //    in a candidate pair (both pass the filter; with the filter off, every
+                //    position), then the next unknown one, ...  A run of candidates costs one word
+                //    per TWO positions, and a long pair straddling two words is read off both
+                //    (S91: 20.5 -> 12.9 pair-word lines per read, emulator trace).
+                //  * otherwise one word per candidate pair, the first NTC_PAIR_TESTS pairs (C91:
+                //    candidates are sparse after the filter, and the lighter code keeps k_ms4 at
+                //    7 waves).
+                // Every load is issued before the first use.  A slot without a word repeats the
+                // first one's (the same line, no further request past L2); with no candidate at
+                // all every slot reads word 0, one line all lanes share.
+                constexpr bool kStride = NTC_PAIR_STRIDE == 2 || (NTC_PAIR_STRIDE == 1 && kJoint);
+                const uint32_t cp = cand & (cand >> 1);  // candidate pair starts (<= W - 2)
                 uint32_t slot[NTC_PAIR_TESTS], pbv[NTC_PAIR_TESTS];
-                uint32_t rem = tested;
-                const uint32_t first = tested ? (uint32_t)__builtin_ctz(tested) : 0u;
-                const uint64_t M0 = tested ? key_at(p + first, U - 1) : 0u;
+                uint32_t hit = 0, single = 0, open = 0, keep = cand;
+                if constexpr (kStride) {
+                    uint32_t todo = cp | (cp << 1), starts = 0;
+                    const uint32_t first = cp ? (uint32_t)__builtin_ctz(cp) : 0u;
 #pragma unroll
-                for (uint32_t t = 0; t < NTC_PAIR_TESTS; t++) {
-                    slot[t] = rem ? (uint32_t)__builtin_ctz(rem) : first;
-                    const uint64_t M = rem ? key_at(p + slot[t], U - 1) : M0;
-                    rem &= rem - 1;
-                    if ((tested >> slot[t]) & 1u) NTC_TOUCH(kTrBits, ix.pair_w + M);
-                    pbv[t] = ld_hint<32>(ix.pair_w + M);
-                }
-                uint32_t hit = 0, single = 0;
+                    for (uint32_t t = 0; t < NTC_PAIR_TESTS; t++) {
+                        const uint32_t sx = todo ? (uint32_t)__builtin_ctz(todo) : 32u;
+                        const bool real = sx + 2 <= W;  // y + 1 inside the window
+                        slot[t] = real ? sx : first;
+                        starts |= real ? 1u << sx : 0u;
+                        todo &= real ? ~(3u << sx) : 0u;
+                    }
+                    const uint64_t M0 = cp ? key_at(p + first, U - 1) : 0u;
 #pragma unroll
-                for (uint32_t t = 0; t < NTC_PAIR_TESTS; t++) {
-                    const uint32_t y = p + slot[t];
-                    const uint32_t a = (uint32_t)(qw >> (2 * (y + 1 - U - qb))) & 3u;
-                    const uint32_t c = (uint32_t)(qw >> (2 * (y + 1 - qb))) & 3u;
-                    hit |= ((pbv[t] >> a) & (pbv[t] >> (4 + c)) & 1u) << slot[t];
-                    single |= ((pbv[t] >> (8 + a)) & 1u) << slot[t];
+                    for (uint32_t t = 0; t < NTC_PAIR_TESTS; t++) {
+                        const uint64_t M = ((starts >> slot[t]) & 1u) ? key_at(p + slot[t], U - 1) : M0;
+                        if ((starts >> slot[t]) & 1u) NTC_TOUCH(kTrBits, ix.pair_w + M);
+                        pbv[t] = ld_hint<32>(ix.pair_w + M);
+                    }
+                    uint32_t longm = 0, known = 0;
+#pragma unroll
+                    for (uint32_t t = 0; t < NTC_PAIR_TESTS; t++) {
+                        const uint32_t y = p + slot[t];
+                        const uint32_t real = (starts >> slot[t]) & 1u;
+                        const uint32_t a = (uint32_t)(qw >> (2 * (y + 1 - U - qb))) & 3u;
+                        const uint32_t c = (uint32_t)(qw >> (2 * (y + 1 - qb))) & 3u;
+                        const uint32_t w = real ? pbv[t] : 0u;
+                        longm |= (((w >> a) & 1u) << slot[t]) | (((w >> (4 + c)) & 1u) << (slot[t] + 1));
+                        single |= (((w >> (8 + a)) & 1u) << slot[t]) | (((w >> (12 + c)) & 1u) << (slot[t] + 1));
+                        known |= (real * 3u) << slot[t];
+                    }
+                    hit = longm & (longm >> 1);
+                    // undecided candidate pairs: neither position known short, not both known
+                    const uint32_t kshort = known & ~longm;
+                    open = cp & ~kshort & ~(kshort >> 1) & ~(known & (known >> 1));
+                    keep = cand & ~kshort;
+                } else {
+                    uint32_t untested = cp;
+#pragma unroll
+                    for (uint32_t t = 0; t < NTC_PAIR_TESTS; t++) untested &= untested - 1;
+                    const uint32_t tested = cp ^ untested;
+                    uint32_t rem = tested;
+                    const uint32_t first = tested ? (uint32_t)__builtin_ctz(tested) : 0u;
+                    const uint64_t M0 = tested ? key_at(p + first, U - 1) : 0u;
+#pragma unroll
+                    for (uint32_t t = 0; t < NTC_PAIR_TESTS; t++) {
+                        slot[t] = rem ? (uint32_t)__builtin_ctz(rem) : first;
+                        const uint64_t M = rem ? key_at(p + slot[t], U - 1) : M0;
+                        rem &= rem - 1;
+                        if ((tested >> slot[t]) & 1u) NTC_TOUCH(kTrBits, ix.pair_w + M);
+                        pbv[t] = ld_hint<32>(ix.pair_w + M);
+                    }
+#pragma unroll
+                    for (uint32_t t = 0; t < NTC_PAIR_TESTS; t++) {
+                        const uint32_t y = p + slot[t];
+                        const uint32_t a = (uint32_t)(qw >> (2 * (y + 1 - U - qb))) & 3u;
+                        const uint32_t c = (uint32_t)(qw >> (2 * (y + 1 - qb))) & 3u;
+                        hit |= ((pbv[t] >> a) & (pbv[t] >> (4 + c)) & 1u) << slot[t];
+                        single |= ((pbv[t] >> (8 + a)) & 1u) << slot[t];
+                    }
+                    hit &= tested;
+                    open = untested;  // resume at the first untested candidate pair
                 }
-                hit &= tested;
                 if (hit) {
                     const uint32_t xi = (uint32_t)__builtin_ctz(hit);
                     const uint32_t x = p + xi;  // x, x + 1 long, x - 1 short
@@ -1366,12 +1418,12 @@ struct MsLaneT {
                     NTC_TOUCH(kTrTabU, ix.tab + tab_base(U) + key_at(x, U));
                     return enter_pair(ix, b, x, load2_stream(ix.tab + tab_base(U) + key_at(x, U)));
                 }
-                if (untested) {  // resume at the first untested candidate pair
-                    p += (uint32_t)__builtin_ctz(untested);
+                if (open) {
+                    p += (uint32_t)__builtin_ctz(open);
                     return 0;
                 }
                 if (p + W >= len) { p = len; return 1; }
-                p += W - ((cand >> (W - 1)) & 1u);  // a passing last position may start a pair
+                p += W - ((keep >> (W - 1)) & 1u);  // a possibly long last position may start a pair
                 return 0;
             }
 #if NTC_SCAN_MODE == 2

@@ -60,3 +60,24 @@ def test_emulated_kernel_equals_oracle_on_random_cases(seed, k, glen, n_reads, m
     assert np.array_equal(got, exp)
     out, oo = emu_decode(ix.n, k, ix.rows, ix.C, ix.lcs, got)
     assert np.array_equal(out, bases) and np.array_equal(oo, offs)
+
+
+@settings(max_examples=max(50, N_EXAMPLES // 2), deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(seed=st.integers(0, 2**32 - 1), k=st.integers(11, 127), glen=st.integers(300, 6000),
+       n_reads=st.integers(1, 60), max_len=st.integers(1, 400), err=st.sampled_from([0.005, 0.02, 0.08]),
+       repeat=st.booleans())
+def test_emulated_kernel_without_scan_filter_equals_oracle(seed, k, glen, n_reads, max_len, err, repeat):
+    """SCAN with the pre-filter off (the upload's auto mode for dense indexes such as S91):
+    every position is a candidate and the pair words alone decide (two positions per word)."""
+    ix, bases, offs = _case(seed, k, glen, n_reads, max_len, err, repeat)
+    orc = OracleIndex(ix.n, k, ix.rows, ix.C, ix.lcs)
+    rc, bad = orc.try_encode(bases, offs)
+    if rc < 0:
+        return
+    exp, eoff = orc.encode(bases, offs)
+    os.environ["NTC_EMU_FILTER"] = "0"
+    try:
+        got, goff = emu_encode(ix.n, k, ix.rows, ix.C, ix.lcs, bases, offs)
+    finally:
+        del os.environ["NTC_EMU_FILTER"]
+    assert np.array_equal(goff, eoff) and np.array_equal(got, exp)
