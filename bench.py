@@ -18,8 +18,12 @@ Workload:
         strains at 1 % substitutions (reference-based compression of a strain collection,
         README.md:2): 70 M nodes, a fragmented path cover.
 A step = one pass of the hot path over the rank's whole shard, in device calls of at most
---batch-reads reads (10M), inputs already resident in HBM.  The top-level line is C91 encode;
-"decode" and "strains" carry D91 and S91 with their own rooflines and parity.
+--batch-reads reads (10M), inputs already resident in HBM.  C91 and D91 keep --inflight (2)
+calls in flight on as many contexts of the rank's GPU (each with its own index copy,
+stream and output buffers; a context takes a call only after its previous one is
+finalized), so the next call's kernels fill the current one's drain; S91 runs one call at
+a time.  The top-level line is C91 encode; "decode" and "strains" carry D91 and S91 with
+their own rooflines and parity.
 
 roofline: bytes past L2 per launch of the dominant kernel (k_ms4 / k_dec_rec), from the
 rocprofv3 PMC passes of THIS device build (profiles/pmc_traffic.json, keyed by the device
@@ -67,6 +71,10 @@ def parse_args(argv=None):
     ap.add_argument("--k", type=int, default=91)
     ap.add_argument("--reads-per-gpu", type=int, default=None, help="default 10M at N=1, 25M at N>1 (C91x8)")
     ap.add_argument("--batch-reads", type=int, default=10_000_000, help="reads per device call")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="device calls in flight per GPU: contexts on the rank's GPU (each with its own index "
+                         "copy, stream and output buffers) take the calls in turn; a context is reused only after "
+                         "its previous call is finalized (status + that launch's kernel time)")
     ap.add_argument("--read-len", type=int, default=150)
     ap.add_argument("--err-ppm", type=int, default=10_000)
     ap.add_argument("--genome-bp", type=int, default=5_000_000)
@@ -164,7 +172,8 @@ def roofline(kname, kernel_ms, kernel_ms_min, units, unit_name, pmc, pmc_note, w
                               "frac": round(rate / roof, 4)}
         r["pmc_profile_kernel_ms"] = round(kd.get("avg_ns", 0) / 1e6 * scale, 4)
     r["note"] = ("achieved = bytes past L2 per launch (rocprofv3 PMC of this device build, each request at its "
-                 "own 32/64/128 B size, plus writes; " + pmc_note + ") / live HIP-event kernel time")
+                 "own 32/64/128 B size, plus writes; " + pmc_note + ") / live HIP-event kernel time of isolated "
+                 "launches (one call in flight, after the timed region)")
     if extra:
         r.update(extra)
     return r
@@ -180,7 +189,7 @@ def minimizer_order(nt, reads, n, L, threads):
 class Shard:
     """One rank's reads of one workload, in device batches."""
 
-    def __init__(self, nt, ctx, text, first, n, L, err, batch, threads, dry, presort=False):
+    def __init__(self, nt, ctx, text, first, n, L, err, batch, threads, dry, presort=False, n_out=1):
         import numpy as np
         self.L, self.n, self.first = L, n, first
         self.batches = []
@@ -195,7 +204,7 @@ class Shard:
                 offs = np.arange(0, nb * L + 1, L, dtype=np.uint64)
                 cap = nb * L // 4 + 64
                 b.update(d_bases=ctx.alloc(reads.nbytes), d_offs=ctx.alloc(offs.nbytes), cap=cap,
-                         d_recs=ctx.alloc(cap * 8), d_roffs=ctx.alloc(offs.nbytes))
+                         out=[{"d_recs": ctx.alloc(cap * 8), "d_roffs": ctx.alloc(offs.nbytes)} for _ in range(n_out)])
                 ctx.h2d(b["d_bases"], reads)
                 ctx.h2d(b["d_offs"], offs)
             self.batches.append(b)
@@ -204,58 +213,100 @@ class Shard:
 
     def free(self, ctx):
         for b in self.batches:
-            for key in ("d_bases", "d_offs", "d_recs", "d_roffs", "d_out", "d_ooffs"):
-                if b.get(key):
-                    ctx.free(b[key])
-                    b[key] = None
+            for o in [b] + b.get("out", []):
+                for key in ("d_bases", "d_offs", "d_recs", "d_roffs", "d_out", "d_ooffs"):
+                    if o.get(key):
+                        ctx.free(o[key])
+                        o[key] = None
 
 
-def encode_pass(ctx, sh, check=False):
-    ms = []
-    for b in sh.batches:
-        ctx.encode_device(b["d_bases"], b["d_offs"], b["n"], sh.L, b["d_recs"], b["cap"], b["d_roffs"])
-        got = ctx.encode_status()
-        if check:
-            b["n_recs"] = got
-        elif got != b["n_recs"]:
-            raise RuntimeError(f"record count changed between passes: {got} vs {b['n_recs']}")
-        ms.append(ctx.timing()["main_ms"])
-    return ms
+class Pipe:
+    """Device calls of one kind kept in flight over the contexts of one GPU (--inflight):
+    call i goes to context i % n with that context's output buffers, and a context takes a
+    new call only after its previous one is finalized -- status checked and the launch's
+    dominant-kernel time (HIP events on that context's stream) recorded.  With two
+    contexts the next call's kernels fill the drain of the current one."""
 
+    def __init__(self, ctxs, kind):
+        self.ctxs, self.kind = ctxs, kind
+        self.pending = [None] * len(ctxs)
+        self.i = 0
+        self.kms = []
 
-def decode_pass(ctx, sh):
-    ms = []
-    for b in sh.batches:
-        if not b.get("d_out"):
-            b["d_out"], b["d_ooffs"] = ctx.alloc(b["bases"] + 64), ctx.alloc((b["n"] + 1) * 8)
-        ctx.decode_device(b["d_recs"], b["n_recs"], b["d_out"], b["bases"] + 64, b["d_ooffs"], b["n"] + 1)
-        if ctx.decode_status() != (b["n"], b["bases"]):
+    def issue(self, sh, b, check=False):
+        c = self.i % len(self.ctxs)
+        self.i += 1
+        self.finish(c)
+        ctx, o = self.ctxs[c], b["out"][c]
+        if self.kind == "encode":
+            ctx.encode_device(b["d_bases"], b["d_offs"], b["n"], sh.L, o["d_recs"], b["cap"], o["d_roffs"])
+        else:
+            if not o.get("d_out"):
+                o["d_out"], o["d_ooffs"] = ctx.alloc(b["bases"] + 64), ctx.alloc((b["n"] + 1) * 8)
+            ctx.decode_device(o["d_recs"], b["n_recs"], o["d_out"], b["bases"] + 64, o["d_ooffs"], b["n"] + 1)
+        self.pending[c] = (b, check)
+
+    def finish(self, c):
+        if self.pending[c] is None:
+            return
+        b, check = self.pending[c]
+        self.pending[c] = None
+        ctx = self.ctxs[c]
+        if self.kind == "encode":
+            got = ctx.encode_status()
+            if check:
+                b["n_recs"] = got
+            elif got != b["n_recs"]:
+                raise RuntimeError(f"record count changed between passes: {got} vs {b['n_recs']}")
+        elif ctx.decode_status() != (b["n"], b["bases"]):
             raise RuntimeError(f"decode status {ctx.decode_status()} != {(b['n'], b['bases'])}")
-        ms.append(ctx.timing()["main_ms"])
-    return ms
+        self.kms.append(ctx.timing()["main_ms"])
+
+    def drain(self):
+        for k in range(len(self.ctxs)):
+            self.finish((self.i + k) % len(self.ctxs))
 
 
-def timed(fn, steps, warmup, barrier, sync, dist):
+def encode_all_outputs(ctxs, sh):
+    """every context's output buffers hold every batch's records (for decode and checks)"""
+    for c, ctx in enumerate(ctxs):
+        for b in sh.batches:
+            o = b["out"][c]
+            ctx.encode_device(b["d_bases"], b["d_offs"], b["n"], sh.L, o["d_recs"], b["cap"], o["d_roffs"])
+            got = ctx.encode_status()
+            if b.get("n_recs") is not None and got != b["n_recs"]:
+                raise RuntimeError(f"context {c}: {got} records, expected {b['n_recs']}")
+            b["n_recs"] = got
+
+
+def timed(pipe, sh, steps, warmup, barrier, sync, dist):
+    """W untimed steps, then K steps between barrier + sync; a step = one call per batch of
+    the shard through the pipe.  -> (max over ranks of the elapsed time, kernel ms per call)"""
     from ntcomp_amd import shard as shard_mod
     for _ in range(warmup):
-        fn()
+        for b in sh.batches:
+            pipe.issue(sh, b)
+    pipe.drain()
     barrier()
     sync()
+    pipe.kms = []
     t0 = time.perf_counter()
-    kms = []
     for _ in range(steps):
-        kms += fn()
+        for b in sh.batches:
+            pipe.issue(sh, b)
+    pipe.drain()
     sync()
     el = time.perf_counter() - t0
     barrier()
-    return shard_mod.max_over_ranks(el, dist), kms
+    return shard_mod.max_over_ranks(el, dist), list(pipe.kms)
 
 
 def records_of(ctx, b, a_read, b_read):
     import numpy as np
-    ro = ctx.d2h(np.zeros(b["n"] + 1, dtype=np.uint64), b["d_roffs"])
+    o = b["out"][0]
+    ro = ctx.d2h(np.zeros(b["n"] + 1, dtype=np.uint64), o["d_roffs"])
     lo, hi = int(ro[a_read]), int(ro[b_read])
-    recs = ctx.d2h(np.zeros(hi - lo, dtype=np.uint64), b["d_recs"] + 8 * lo) if hi > lo else np.zeros(0, np.uint64)
+    recs = ctx.d2h(np.zeros(hi - lo, dtype=np.uint64), o["d_recs"] + 8 * lo) if hi > lo else np.zeros(0, np.uint64)
     return recs, ro
 
 
@@ -293,9 +344,10 @@ def check_shard(ctx, orc, sh, seconds, full_decode, pin, dry):
             res["reads_checked"] += done
             res.setdefault("spans", []).append(done)
             res["cpu_encode_s"] += spent
-            if full_decode and not dry and b.get("d_out"):
-                out = ctx.d2h(np.zeros(b["bases"], dtype=np.uint8), b["d_out"])
-                oo = ctx.d2h(np.zeros(b["n"] + 1, dtype=np.uint64), b["d_ooffs"])
+            o = b["out"][0] if b.get("out") else {}
+            if full_decode and not dry and o.get("d_out"):
+                out = ctx.d2h(np.zeros(b["bases"], dtype=np.uint8), o["d_out"])
+                oo = ctx.d2h(np.zeros(b["n"] + 1, dtype=np.uint64), o["d_ooffs"])
                 ok = bool(np.array_equal(out, b["reads"])) and bool(
                     np.array_equal(oo, np.arange(0, b["bases"] + 1, L, dtype=np.uint64)))
                 res["decode_ok"] = ok if res["decode_ok"] is None else (res["decode_ok"] and ok)
@@ -385,9 +437,9 @@ def main():
     ctx = None
 
     def sync():
-        if ctx is not None:
-            ctx.synchronize()
-            torch.cuda.synchronize()
+        for c in ctxs:
+            c.synchronize()
+        torch.cuda.synchronize()
 
     def gather(obj):
         if dist is None:
@@ -408,19 +460,25 @@ def main():
     line = {}
     t_start = time.time()
 
-    def setup_index(texts, label):
+    ctxs = []
+
+    def setup_index(texts, label, n_ctx):
         nonlocal ctx
         t0 = time.time()
         index = nt.Index.build([t.tobytes() for t in texts], k, threads=nthreads)
         log(f"[rank {rank}] {label} index k={k} n={index.n} built in {time.time() - t0:.1f}s")
         if not args.dry_run:
             if ctx is None:
-                ctx = nt.GpuContext(device)
-                for kv in args.opt:
-                    key, val = kv.split("=")
-                    ctx.set_option(key, int(val))
+                for _ in range(max(1, args.inflight)):
+                    c = nt.GpuContext(device)
+                    for kv in args.opt:
+                        key, val = kv.split("=")
+                        c.set_option(key, int(val))
+                    ctxs.append(c)
+                ctx = ctxs[0]
             t0 = time.time()
-            ctx.upload(index)
+            for c in ctxs[:n_ctx]:
+                c.upload(index)
             log(f"[rank {rank}] upload {time.time() - t0:.1f}s, {ctx.get_option('n_paths')} paths, SCAN filter "
                 f"{'on' if ctx.get_option('filter') else 'off'} (density {ctx.get_option('filter_density_ppm') / 1e4:.1f} %)")
         return index
@@ -431,20 +489,29 @@ def main():
 
     # ---- C91 encode / D91 decode -------------------------------------------------
     if "encode" in configs or "decode" in configs:
-        index = setup_index([genome], "C")
+        index = setup_index([genome], "C", len(ctxs) or max(1, args.inflight))
         sh = Shard(nt, ctx, genome, first, n, L, args.err_ppm, args.batch_reads, nthreads, args.dry_run,
-                   args.presort)
+                   args.presort, n_out=len(ctxs))
         log(f"[rank {rank}] reads {first}..{first + n} in {len(sh.batches)} batch(es)")
         orc = OracleIndex(index.n, k, index.rows, index.C, index.lcs)
         n_recs = None
         if not args.dry_run:
-            encode_pass(ctx, sh, check=True)
+            encode_all_outputs(ctxs, sh)
             n_recs = sum(b["n_recs"] for b in sh.batches)
         enc = dec = None
+        iso = {}  # kernel ms of isolated launches (one context, one call at a time): the roofline's
+        # denominator -- with calls in flight, a launch shares the GPU with the other context's
+        # kernels and its event time measures both
+        n_iso = max(3, len(sh.batches))
         if "encode" in configs and not args.dry_run:
-            enc = timed(lambda: encode_pass(ctx, sh), args.steps, args.warmup, barrier, sync, dist)
+            enc = timed(Pipe(ctxs, "encode"), sh, args.steps, args.warmup, barrier, sync, dist)
+            iso["encode"] = timed(Pipe(ctxs[:1], "encode"), sh, n_iso, 0, barrier, sync, dist)[1] \
+                if len(ctxs) > 1 else enc[1]
+            encode_all_outputs(ctxs, sh)  # the timed calls alternate contexts: refresh every output
         if "decode" in configs and not args.dry_run:
-            dec = timed(lambda: decode_pass(ctx, sh), args.steps, args.warmup, barrier, sync, dist)
+            dec = timed(Pipe(ctxs, "decode"), sh, args.steps, args.warmup, barrier, sync, dist)
+            iso["decode"] = timed(Pipe(ctxs[:1], "decode"), sh, n_iso, 0, barrier, sync, dist)[1] \
+                if len(ctxs) > 1 else dec[1]
         pin = world == 1
         secs = args.cpu_seconds if (world == 1 and not args.no_cpu) else (0 if args.no_cpu else 2.0)
         chk = check_shard(ctx, orc, sh, secs, dec is not None, pin, args.dry_run) if secs > 0 else None
@@ -473,13 +540,16 @@ def main():
                 + (f"; {world} GPUs x {n} = {world * n} reads" if world > 1 else ""))
         cfg = dict(base_cfg, workload=wl_c, index_nodes=index.n, records_per_gpu=n_recs,
                    suffix_table_u=None if args.dry_run else ctx.get_option("tab_u"),
-                   parallelism=f"reads sharded over {world} GPU(s), index replicated, no collective")
+                   parallelism=f"reads sharded over {world} GPU(s), index replicated, no collective",
+                   inflight=len(ctxs) or None)
         if enc is not None:
             el, kms = enc
             b0 = sh.batches[0]
-            kavg, kmin = launch_ms(kms, [b["n"] for b in sh.batches], b0["n"])
+            kavg, kmin = launch_ms(iso["encode"], [b["n"] for b in sh.batches], b0["n"])
+            kin = launch_ms(kms, [b["n"] for b in sh.batches], b0["n"])[0]
             rl = roofline("k_ms4", kavg, kmin, b0["n"], "read", pmc, pmc_note, f"C{k}",
-                          {"reference_work_avoided": round(
+                          {"kernel_ms_inflight": round(kin, 4), "isolated_launches": len(iso["encode"]),
+                           "reference_work_avoided": round(
                               b0["bases"] * (1 + 2 * 64) / (kavg / 1e3) / 1e9 / HBM_PEAK_GBPS, 3),
                            "reference_work_note": "SURVEY 8(d) B_enc (1 B + two 64 B rank lines per base) / "
                                                   "kernel time / peak: the reference algorithm's bytes this "
@@ -498,7 +568,8 @@ def main():
         if dec is not None:
             el, kms = dec
             b0 = sh.batches[0]
-            kavg, kmin = launch_ms(kms, [b["bases"] for b in sh.batches], b0["bases"])
+            kavg, kmin = launch_ms(iso["decode"], [b["bases"] for b in sh.batches], b0["bases"])
+            kin = launch_ms(kms, [b["bases"] for b in sh.batches], b0["bases"])[0]
             dcpu = None
             if chk and chk["cpu_decode_s"] > 0 and world == 1:
                 dcpu = {"value": round(chk["cpu_decode_bases"] / chk["cpu_decode_s"] / 1e6, 3), "unit": "Mbases/s",
@@ -509,7 +580,8 @@ def main():
                  "ms_per_step": round(el / args.steps * 1e3, 3),
                  "config": {"workload": f"D{k}: decode of the C{k} records ({n_recs} records, {n} reads per GPU) "
                                         f"-> bases via the inverse-SBWT walk, k={k}"},
-                 "roofline": roofline("k_dec_rec", kavg, kmin, b0["bases"], "base", pmc, pmc_note, f"D{k}"),
+                 "roofline": roofline("k_dec_rec", kavg, kmin, b0["bases"], "base", pmc, pmc_note, f"D{k}",
+                                      {"kernel_ms_inflight": round(kin, 4), "isolated_launches": len(iso["decode"])}),
                  "cpu_baseline": dcpu,
                  "parity": {"round_trip_exact_all_ranks": all(v["check"]["decode_ok"] for v in verdicts)
                             if chk else None, "bases_checked_per_rank": n * L if chk else None},
@@ -536,31 +608,33 @@ def main():
     if "strains" in configs:
         strains = nt.synth_strains(genome, 3, args.strains, args.strain_snp_ppm)
         texts = [genome] + [strains[i] for i in range(args.strains)]
-        index = setup_index(texts, "S")
+        index = setup_index(texts, "S", 1)
+        sctx = ctxs[:1]  # S91 runs one call at a time: two in flight measured 3 % slower (k_ms4 is
+        # already at 0.89 of the line rate there, and two persistent grids only compete)
         coll = np.concatenate(texts)
         ns = args.strain_reads if world == 1 else min(args.strain_reads, n)
         fs, ns = shard_mod.read_range(rank, world, ns)
         sh = Shard(nt, ctx, coll, fs, ns, L, args.err_ppm, args.batch_reads, nthreads, args.dry_run,
-                   args.presort)
+                   args.presort, n_out=len(sctx))
         orc = OracleIndex(index.n, k, index.rows, index.C, index.lcs)
         s = {"config": {"workload": f"S{k}: {ns} x {L}bp reads ({args.err_ppm / 1e4:g}% subst, 50% revcomp) drawn "
                                     f"from a collection of the {args.genome_bp / 1e6:g} Mbp genome + {args.strains} "
                                     f"strains at {args.strain_snp_ppm / 1e4:g}% substitutions, SBWT k={k} (+revcomp)",
                         "index_nodes": index.n}}
         if not args.dry_run:
-            encode_pass(ctx, sh, check=True)
+            encode_all_outputs(sctx, sh)
             s["config"]["records_per_gpu"] = sum(b["n_recs"] for b in sh.batches)
             s["config"]["suffix_table_u"] = ctx.get_option("tab_u")
             s["config"]["n_paths"] = ctx.get_option("n_paths")
             s["config"]["scan_filter"] = bool(ctx.get_option("filter"))
             s["config"]["joint_runs"] = bool(ctx.get_option("joint"))
-            el, kms = timed(lambda: encode_pass(ctx, sh), args.steps, args.warmup, barrier, sync, dist)
+            el, kms = timed(Pipe(sctx, "encode"), sh, args.steps, args.warmup, barrier, sync, dist)
             b0 = sh.batches[0]
             kavg, kmin = launch_ms(kms, [b["n"] for b in sh.batches], b0["n"])
             s.update(value=round(sh.bases * world * args.steps / el / 1e6, 2), unit="Mbases/s",
                      ms_per_step=round(el / args.steps * 1e3, 3),
                      roofline=roofline("k_ms4", kavg, kmin, b0["n"], "read", pmc, pmc_note, f"S{k}"))
-            el, kms = timed(lambda: decode_pass(ctx, sh), args.steps, args.warmup, barrier, sync, dist)
+            el, kms = timed(Pipe(sctx, "decode"), sh, args.steps, args.warmup, barrier, sync, dist)
             kavg, kmin = launch_ms(kms, [b["bases"] for b in sh.batches], b0["bases"])
             s["decode"] = {"value": round(sh.bases * world * args.steps / el / 1e6, 2), "unit": "Mbases/s",
                            "ms_per_step": round(el / args.steps * 1e3, 3),
@@ -588,8 +662,8 @@ def main():
     if rank == 0:
         line["wall_s"] = round(time.time() - t_start, 1)
         print(json.dumps(line), flush=True)
-    if ctx is not None:
-        ctx.close()
+    for c in ctxs:
+        c.close()
     if dist is not None:
         dist.destroy_process_group()
 

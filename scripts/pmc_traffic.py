@@ -10,8 +10,13 @@ Per workload and kernel, the mean per launch of:
   dram_read_bytes = 32 * TCC_EA0_RDREQ_DRAM_32B
   fetch_size_bytes = the rocprofv3 FETCH_SIZE expression for gfx950 from the same counters
 Kernel durations come from the kernel-trace pass of the default bench command, split into
-its workloads by dispatch order (C91: 1 + W + K k_ms4 launches, then D91: W + K k_dec_rec,
-then S91 / SD91 the same again).
+its workloads by dispatch order (bench.py with --inflight I contexts):
+  C91 encode calls: I (every context's outputs) + W + K (timed, I in flight) + N isolated
+      (one at a time, I > 1 only: the roofline's denominator) + I (outputs refreshed)
+  D91 decode calls: W + K (timed) + N isolated (I > 1 only)
+  S91: 1 + W + K encode calls, SD91: W + K decode calls (one context)
+avg_ns is the isolated launches' mean (the timed ones where I = 1); avg_ns_inflight the
+timed launches' mean.
 
 usage: pmc_traffic.py PROF_DIR OUT_JSON OUT_MD [--steps K --warmup W --reads R --read-len L]
 """
@@ -73,6 +78,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--reads", type=int, default=10_000_000)
     ap.add_argument("--read-len", type=int, default=150)
+    ap.add_argument("--inflight", type=int, default=2, help="bench.py --inflight of the kernel-trace pass")
+    ap.add_argument("--iso", type=int, default=3, help="isolated calls bench.py times after the timed region")
     a = ap.parse_args()
     import ntcomp_amd as nt
 
@@ -84,17 +91,22 @@ def main():
     seq = defaultdict(list)
     for r in kt:
         seq[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
-    n_enc, n_dec = 1 + a.warmup + a.steps, a.warmup + a.steps
+    I, WK = a.inflight, a.warmup + a.steps
+    N = a.iso if I > 1 else 0
+    c_total = I + WK + N + I
     dur = {"C91": {}, "D91": {}, "S91": {}, "SD91": {}}
+    inflight = {"C91": {}, "D91": {}}
     for kname in ("k_ms4", "k_parse4", "k_pack", "k_emit4"):
         xs = seq.get(kname, [])
-        dur["C91"][kname] = mean(xs[:n_enc])
-        # the D91 phase re-runs nothing of encode; S91's encode launches follow
-        dur["S91"][kname] = mean(xs[n_enc:n_enc * 2]) if len(xs) >= 2 * n_enc else None
+        timed = xs[I:I + WK]
+        dur["C91"][kname] = mean(xs[I + WK:I + WK + N]) if N else mean(timed)
+        inflight["C91"][kname] = mean(timed)
+        dur["S91"][kname] = mean(xs[c_total + 1:c_total + 1 + WK]) if len(xs) >= c_total + 1 + WK else None
     for kname in ("k_dec_rec", "k_dec_tiles"):
         xs = seq.get(kname, [])
-        dur["D91"][kname] = mean(xs[:n_dec])
-        dur["SD91"][kname] = mean(xs[n_dec:2 * n_dec]) if len(xs) >= 2 * n_dec else None
+        dur["D91"][kname] = mean(xs[WK:WK + N]) if N else mean(xs[:WK])
+        inflight["D91"][kname] = mean(xs[:WK])
+        dur["SD91"][kname] = mean(xs[WK + N:WK + N + WK]) if len(xs) >= WK + N + WK else None
 
     units = {"C91": (a.reads, "read"), "S91": (a.reads, "read"),
              "D91": (a.reads * a.read_len, "base"), "SD91": (a.reads * a.read_len, "base")}
@@ -106,7 +118,7 @@ def main():
            "source": f"scripts/profile_bench.sh -> {os.path.relpath(a.prof_dir, REPO)}", "workloads": {}}
     md = ["# rocprofv3 summary (bench.py, one MI355X)", "",
           f"device source hash `{out['device_source_hash']}`; kernel-trace pass = `bench.py --steps {a.steps} "
-          f"--warmup {a.warmup}` (all configs); counter passes = `bench.py --configs <w> --no-cpu --steps 3 "
+          f"--warmup {a.warmup}` (all configs, --inflight {a.inflight}); counter passes = `bench.py --configs <w> --no-cpu --steps 3 "
           f"--warmup 0`, one pass per counter group.", "",
           "| workload | kernel | avg ms (trace) | read B/launch | write B/launch | B/unit | RDREQ/unit | 32/64/128 B req | "
           "DRAM rd B | L2 hit | GB/s | frac of 8 TB/s |", "|---|---|---|---|---|---|---|---|---|---|---|---|"]
@@ -140,6 +152,8 @@ def main():
                           "GRBM_GUI_ACTIVE"):
                     e[c] = m(M, c)
             ns = dur[wl].get(kname)
+            if inflight.get(wl, {}).get(kname):
+                e["avg_ns_inflight"] = inflight[wl][kname]
             if ns:
                 e["avg_ns"] = ns
                 if e.get("GRBM_GUI_ACTIVE"):
@@ -159,7 +173,10 @@ def main():
         md.append(f"| {short(r['Name'])} | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.2f} | "
                   f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['MinNs']) / 1e3:.1f} | {float(r['MaxNs']) / 1e3:.1f} | "
                   f"{float(r['Percentage']):.1f} |")
-    md += ["", "Per-workload trace averages (dispatch order split):", "", "```json", json.dumps(dur, indent=1), "```"]
+    md += ["", "Per-workload trace averages (dispatch order split; C91/D91: isolated launches, the roofline's "
+           "denominator):", "", "```json", json.dumps(dur, indent=1), "```", "",
+           "C91/D91 timed launches with calls in flight (each shares the GPU with the other context's kernels):",
+           "", "```json", json.dumps(inflight, indent=1), "```"]
     if not all(out["workloads"].get(w, {}).get("kernels") for w in ("C91", "D91")):
         sys.exit("counter passes missing for C91/D91: nothing written")
     json.dump(out, open(a.out_json, "w"), indent=1)
