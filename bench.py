@@ -127,11 +127,19 @@ def load_pmc(path, want_hash):
     return pj.get("workloads", {}), "ok"
 
 
-def random_line_roof():
+def random_line_roof(working_set=None):
+    """Random 128 B line requests per second past L2 (scripts/randbw.hip): the best rate over
+    buffers >= 32 MB, or, for a kernel whose random loads go to one structure of working_set
+    bytes (k_dec_rec: the walk table), the rate measured on the largest buffer not larger
+    than it (the rate falls with the buffer: 66 G/s at 32 MB, 55 at 512 MB, 51 at 4 GB)."""
     try:
-        roofs = [json.loads(l) for l in open(RANDBW_JSONL)]
-        return max(r["g_lines_per_s"] for r in roofs
-                   if r.get("test") == "random_8B_loads" and r["buffer_bytes"] >= (32 << 20))
+        roofs = [r for r in (json.loads(l) for l in open(RANDBW_JSONL))
+                 if r.get("test") == "random_8B_loads" and r["buffer_bytes"] >= (32 << 20)]
+        if working_set:
+            fit = [r for r in roofs if r["buffer_bytes"] <= working_set]
+            if fit:
+                return max(fit, key=lambda r: r["buffer_bytes"])["g_lines_per_s"]
+        return max(r["g_lines_per_s"] for r in roofs)
     except (OSError, ValueError, KeyError):
         return None
 
@@ -143,7 +151,7 @@ def launch_ms(kms, units, ref):
     return sum(kms) / sum(units * (len(kms) // len(units))) * ref, min(per) * ref
 
 
-def roofline(kname, kernel_ms, kernel_ms_min, units, unit_name, pmc, pmc_note, wl_key, extra=None):
+def roofline(kname, kernel_ms, kernel_ms_min, units, unit_name, pmc, pmc_note, wl_key, extra=None, working_set=None):
     """Roofline of one dominant kernel: PMC bytes past L2 per unit (read or base) x units per
     launch / live kernel time."""
     r = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": None, "traffic": None,
@@ -161,7 +169,7 @@ def roofline(kname, kernel_ms, kernel_ms_min, units, unit_name, pmc, pmc_note, w
         r["bytes_per_" + unit_name] = round(traffic / units, 2)
         if kd.get("dram_read_bytes") is not None:
             r["dram_read_bytes"] = int(kd["dram_read_bytes"] * scale)
-        roof = random_line_roof()
+        roof = random_line_roof(working_set)
         rq, wq = kd.get("rdreq", 0) * scale, (kd.get("wrreq") or 0) * scale
         req = rq + wq  # every request past L2 occupies the fabric, reads and writes alike
         if roof and req:
@@ -581,7 +589,8 @@ def main():
                  "config": {"workload": f"D{k}: decode of the C{k} records ({n_recs} records, {n} reads per GPU) "
                                         f"-> bases via the inverse-SBWT walk, k={k}"},
                  "roofline": roofline("k_dec_rec", kavg, kmin, b0["bases"], "base", pmc, pmc_note, f"D{k}",
-                                      {"kernel_ms_inflight": round(kin, 4), "isolated_launches": len(iso["decode"])}),
+                                      {"kernel_ms_inflight": round(kin, 4), "isolated_launches": len(iso["decode"])},
+                                      working_set=index.n * 32),
                  "cpu_baseline": dcpu,
                  "parity": {"round_trip_exact_all_ranks": all(v["check"]["decode_ok"] for v in verdicts)
                             if chk else None, "bases_checked_per_rank": n * L if chk else None},
@@ -639,7 +648,7 @@ def main():
             s["decode"] = {"value": round(sh.bases * world * args.steps / el / 1e6, 2), "unit": "Mbases/s",
                            "ms_per_step": round(el / args.steps * 1e3, 3),
                            "roofline": roofline("k_dec_rec", kavg, kmin, b0["bases"], "base", pmc, pmc_note,
-                                                f"SD{k}")}
+                                                f"SD{k}", working_set=index.n * 32)}
         secs = 0 if args.no_cpu else 3.0
         chk = check_shard(ctx, orc, sh, secs, not args.dry_run, False, args.dry_run) if secs > 0 else None
         vs = gather(chk)

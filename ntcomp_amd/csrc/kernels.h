@@ -64,9 +64,11 @@ struct DebugArgs {
 };
 
 // decode tiles: k_dec_rec's block of 256 threads owns kDecTileRecs consecutive records, kDecR
-// per thread (two independent walk chains per lane: twice the loads in flight per wave)
+// per thread (independent walk chains per lane).  4: 126 VGPRs, 4 waves/SIMD = 16 chains per
+// SIMD (2: 84 VGPRs, 5 waves = 10 chains); D91 k_dec_rec 0.935 -> 0.900 ms, SD91 1.117 ->
+// 1.103 ms (A/B on one box, round 3)
 #ifndef NTC_DEC_R
-#define NTC_DEC_R 2
+#define NTC_DEC_R 4
 #endif
 constexpr uint32_t kDecR = NTC_DEC_R;
 constexpr uint32_t kDecTileRecs = 256 * kDecR;
