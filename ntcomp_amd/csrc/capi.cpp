@@ -66,6 +66,7 @@ struct ntc_ctx {
     int filter_opt = -1;     // SCAN pre-filter at the next upload: -1 auto (off when saturated), 0 off, 1 on
     int64_t filter_density_ppm = -1;  // presence density of the filter level at the last upload
     int joint_opt = -1;      // joint path runs at the next upload: -1 auto (fragmented path cover), 0 off, 1 on
+    int win_opt = -1;        // SCAN window words at the next upload: -1 auto (joint-run builds), 0 off, 1 on
     int ext2_opt = 0;        // build the two-character rank chunks at the next upload (A/B option: 1 measured
                              // slower -- 8 B/node from HBM against 1 B/node of Infinity-Cache-resident rank words)
     uint64_t n_paths = 0, path_text_len = 0;
@@ -681,6 +682,15 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
         const bool on = ctx->filter_opt == 1 || (ctx->filter_opt < 0 && ctx->filter_density_ppm <= kFiltMaxDensityPpm);
         if (!on) d.filt_f = 0;
     }
+    d.win_w = nullptr;
+    // SCAN window words for the joint-run build (genome collections: the filter is off and
+    // every position after an error is a pair-word test); needs the level-U presence bitmap
+    if (U >= 4 && ((ctx->win_opt < 0 && d.joint) || ctx->win_opt == 1)) {
+        void *d_win;
+        if ((rc = dalloc(win_words_count(U) * 32, &d_win))) return rc;
+        launch_win_words((const uint32_t *)d_bits, U, (uint32_t *)d_win, ctx->stream);
+        d.win_w = (const uint32_t *)d_win;
+    }
     d.pair_w = nullptr;
     if (ctx->pair_bytes_opt) {
         void *d_pair;
@@ -720,6 +730,11 @@ int ntc_ctx_set_option(ntc_ctx *ctx, const char *key, int64_t value) {
         ctx->joint_opt = (int)value;
         return NTC_OK;
     }
+    if (std::strcmp(key, "win") == 0) {  // applies to the next ntc_index_upload
+        if (value < -1 || value > 1) return set_err(ctx, NTC_ERR_INVALID_ARG, "win must be -1 (auto), 0 or 1");
+        ctx->win_opt = (int)value;
+        return NTC_OK;
+    }
     if (std::strcmp(key, "ext2") == 0) {  // applies to the next ntc_index_upload
         if (value != 0 && value != 1) return set_err(ctx, NTC_ERR_INVALID_ARG, "ext2 must be 0 or 1");
         ctx->ext2_opt = (int)value;
@@ -747,6 +762,7 @@ int ntc_ctx_get_option(const ntc_ctx *ctx, const char *key, int64_t *value) {
     else if (std::strcmp(key, "ext2") == 0) *value = ctx->has_index ? (ctx->dix.rank2 != nullptr) : ctx->ext2_opt;
     else if (std::strcmp(key, "filter") == 0) *value = ctx->has_index ? (ctx->dix.filt_f != 0) : ctx->filter_opt;
     else if (std::strcmp(key, "joint") == 0) *value = ctx->has_index ? (int64_t)ctx->dix.joint : ctx->joint_opt;
+    else if (std::strcmp(key, "win") == 0) *value = ctx->has_index ? (ctx->dix.win_w != nullptr) : ctx->win_opt;
     else if (std::strcmp(key, "filter_density_ppm") == 0) *value = ctx->filter_density_ppm;
     else if (std::strcmp(key, "n_paths") == 0) *value = (int64_t)ctx->n_paths;
     else if (std::strcmp(key, "path_text_len") == 0) *value = (int64_t)ctx->path_text_len;

@@ -126,6 +126,7 @@ struct DevIndex {
     uint32_t absent;              // bit c: no node ends with character c
     const Rank2Chunk *rank2;      // [4][rank2_blocks(n)] two-character rank chunks, or null
     uint32_t joint;               // 1: encode with joint path runs (k_ms4<true>, MsLaneT)
+    const uint32_t *win_w;        // window words of each (U-3)-mer (see win_word), or null
 };
 
 // per-read status codes (values of ntc_status)
@@ -497,6 +498,28 @@ NTC_HD uint32_t pair_word(const uint2 *top, uint32_t U, uint64_t M) {
     return w;
 }
 
+// Window word of the (U-3)-mer K, 8 x 32 bits: bit 64 j + ctx (j = 0..3) says whether the
+// U-mer  (3 - j characters) . K . (j characters)  is present, ctx = the 3 - j characters
+// before K in the low bits, the j after K above them (2 bits each, first character lowest,
+// as key_at packs them).  For K ending at e in a read, one 32-byte entry answers "is the
+// U-mer ending at e + j present" for j = 0..3 -- four SCAN positions per cache line, where a
+// pair word answers two.  4^(U-3) x 32 bytes (134 MB at U = 14), built from the level-U
+// presence bitmap.
+NTC_HD uint64_t win_words_count(uint32_t U) { return 1ULL << (2 * (U - 3)); }
+NTC_HD uint32_t win_ctx(uint64_t ukey, uint32_t U, uint32_t j) {  // context of the U-mer ending at e + j
+    return (uint32_t)(ukey & ((1ULL << (2 * (3 - j))) - 1)) | (uint32_t)((ukey >> (2 * (U - j))) << (2 * (3 - j)));
+}
+NTC_HD uint32_t win_word(const uint32_t *bits, uint32_t U, uint64_t K, uint32_t i) {  // 32-bit word i of K's entry
+    uint32_t w = 0;
+    for (uint32_t b = 0; b < 32; b++) {
+        const uint32_t j = (32 * i + b) >> 6, ctx = (32 * i + b) & 63u;
+        const uint32_t lo = 2 * (3 - j);
+        const uint64_t key = (uint64_t)(ctx & ((1u << lo) - 1u)) | (K << lo) | ((uint64_t)(ctx >> lo) << (2 * (U - j)));
+        w |= ((bits[key >> 5] >> (key & 31)) & 1u) << b;
+    }
+    return w;
+}
+
 // presence bits of one level: bit key of word key / 32
 NTC_HD uint32_t tab_bits_word(const uint2 *top, uint64_t w) {
     uint32_t b = 0;
@@ -585,6 +608,9 @@ constexpr uint32_t kScanExact = 4;   // filter candidates tested exactly per SCA
 #endif
 #ifndef NTC_PAIR_TESTS
 #define NTC_PAIR_TESTS 4  // pair words loaded per SCAN
+#endif
+#ifndef NTC_WIN_ENTRIES
+#define NTC_WIN_ENTRIES 2  // window-word entries per SCAN (4 positions each, one 32-bit load per position)
 #endif
 #ifndef NTC_PAIR_STRIDE
 #define NTC_PAIR_STRIDE 1  // SCAN pair words at non-overlapping positions: 1 in the joint-run build, 2 always, 0 never
@@ -1330,6 +1356,36 @@ struct MsLaneT {
                 uint32_t slot[NTC_PAIR_TESTS], pbv[NTC_PAIR_TESTS];
                 uint32_t hit = 0, single = 0, open = 0, keep = cand;
                 if constexpr (kStride) {
+                  if (ix.win_w) {
+                    // window words: entry t (key: the (U-3)-mer ending at p + 4t) answers the
+                    // four positions p + 4t .. p + 4t + 3; two entries, eight positions, two
+                    // lines (stride pair words: four).  One 32-bit load per position, all
+                    // issued before the first use (the loads of one entry share its line).
+                    constexpr uint32_t kWin = NTC_WIN_ENTRIES;
+                    uint32_t wv[4 * kWin];
+#pragma unroll
+                    for (uint32_t i = 0; i < 4 * kWin; i++) {
+                        const uint32_t t = i >> 2, jj = i & 3u;
+                        const uint64_t K = key_at(4 * t < W ? p + 4 * t : p, U - 3);  // past W: entry 0's line again
+                        const uint32_t bi = i < W ? 64 * jj + win_ctx(key_at(p + i, U), U, jj) : 0u;
+                        if (i < W && jj == 0) NTC_TOUCH(kTrBits, ix.win_w + K * 8);
+                        wv[i] = ld_hint<32>(ix.win_w + K * 8 + (bi >> 5));
+                    }
+                    uint32_t longm = 0;
+#pragma unroll
+                    for (uint32_t i = 0; i < 4 * kWin; i++) {
+                        const uint32_t jj = i & 3u;
+                        const uint32_t bi = i < W ? 64 * jj + win_ctx(key_at(p + i, U), U, jj) : 0u;
+                        longm |= ((wv[i] >> (bi & 31u)) & 1u) << i;
+                    }
+                    const uint32_t lim = W < 4 * kWin ? W : 4 * kWin;
+                    const uint32_t known = (1u << lim) - 1u;
+                    longm &= cand & known;  // a position failing the filter is short
+                    const uint32_t kshort = (known & ~longm) | (~cand & ((1u << W) - 1u));
+                    hit = longm & (longm >> 1);
+                    open = cp & ~kshort & ~(kshort >> 1) & ~(known & (known >> 1));
+                    keep = cand & ~kshort;
+                  } else {
                     uint32_t todo = cp | (cp << 1), starts = 0;
                     const uint32_t first = cp ? (uint32_t)__builtin_ctz(cp) : 0u;
 #pragma unroll
@@ -1364,6 +1420,7 @@ struct MsLaneT {
                     const uint32_t kshort = known & ~longm;
                     open = cp & ~kshort & ~(kshort >> 1) & ~(known & (known >> 1));
                     keep = cand & ~kshort;
+                  }
                 } else {
                     uint32_t untested = cp;
 #pragma unroll

@@ -112,6 +112,7 @@ void launch_emit4(const Enc4Args &a, uint64_t *wave_off, uint64_t *tmp, uint64_t
 int ms4_blocks_per_cu();
 void launch_debug_gather4(const Enc4Args &a, uint32_t *d_out, uint32_t *s_out, hipStream_t s);
 void launch_pair_words(const uint2 *top, uint32_t U, uint16_t *out, hipStream_t s);
+void launch_win_words(const uint32_t *bits, uint32_t U, uint32_t *out, hipStream_t s);
 void launch_tab_build(const DevIndex &ix, uint32_t U, uint2 *tab, uint32_t *bits, uint32_t F, uint32_t *fbits,
                       hipStream_t s);
 void launch_tile_rows(const uint64_t *offs, uint64_t n_reads, uint32_t *tile_rows, hipStream_t s);

@@ -951,6 +951,18 @@ void launch_pair_words(const uint2 *top, uint32_t U, uint16_t *out, hipStream_t 
                        (uint32_t *)out);
 }
 
+// window words (encode_core.h win_word): one 32-bit word per thread, from the level-U
+// presence bitmap (32 MB at U = 14, L2 / Infinity-Cache resident while this runs)
+__global__ __launch_bounds__(256) void k_win_words(const uint32_t *bits, uint32_t U, uint32_t *out) {
+    const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (w >= win_words_count(U) * 8) return;
+    out[w] = win_word(bits, U, w >> 3, (uint32_t)(w & 7));
+}
+
+void launch_win_words(const uint32_t *bits, uint32_t U, uint32_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_win_words, grid_for(win_words_count(U) * 8), dim3(256), 0, s, bits, U, out);
+}
+
 void launch_tab_build(const DevIndex &ix, uint32_t U, uint2 *tab, uint32_t *bits, uint32_t F, uint32_t *fbits,
                       hipStream_t s) {
     for (uint32_t u = 1; u <= U; u++) {

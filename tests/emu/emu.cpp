@@ -107,6 +107,16 @@ bool load(const ntc_index_view *v, HostIndex &hx, Derived &dv, std::vector<WalkE
         d.filt_bits = nullptr;
     }
     d.tab_u = U;
+    {  // window words (SCAN, joint builds): NTC_EMU_WIN=0 off, else on whenever U >= 4
+        static std::vector<uint32_t> winb;
+        const char *ew = getenv("NTC_EMU_WIN");
+        d.win_w = nullptr;
+        if (U >= 4 && !(ew && atoi(ew) == 0)) {
+            winb.resize(win_words_count(U) * 8);
+            for (uint64_t w = 0; w < winb.size(); w++) winb[w] = win_word(bits.data(), U, w >> 3, (uint32_t)(w & 7));
+            d.win_w = winb.data();
+        }
+    }
     d.pair_w = nullptr;
     const char *pe = getenv("NTC_EMU_PAIR_BYTES");
     if (!pe || atoi(pe) != 0) {
