@@ -79,6 +79,10 @@ int ntc_deflate_block(const ntc_block_meta *meta, const uint8_t *payload, int en
  * decode loop, src/main.rs:202).                                                      */
 int ntc_read_block(const uint8_t *data, uint64_t len, uint64_t *consumed, uint64_t **recs,
                    uint64_t *n_recs, uint64_t *num_records);
+/* The same into a caller buffer of capacity records (NTC_ERR_CAPACITY, with *n_recs the
+ * block's count, when it does not fit).  Inflate through libdeflate when present.       */
+int ntc_read_block_into(const uint8_t *data, uint64_t len, uint64_t *consumed, uint64_t *recs, uint64_t capacity,
+                        uint64_t *n_recs, uint64_t *num_records);
 void ntc_buffer_free(void *p);
 
 /* ---- GPU packer ---------------------------------------------------------------------- */

@@ -154,6 +154,15 @@ int ntc_decode_batch_device(ntc_ctx *ctx, const uint64_t *d_recs, uint64_t n_rec
                             uint8_t *d_bases_out, uint64_t bases_capacity,
                             uint64_t *d_read_offsets_out, uint64_t offsets_capacity);
 int ntc_decode_status(ntc_ctx *ctx, uint64_t *n_reads, uint64_t *n_bases);
+/* decode_sequence and the decode command's output lines (src/lib.rs:254-318,
+ * src/main.rs:203-209) in one device pass: the records of whole reads (host buffer) in,
+ * ">seq.{first_id + r}\n{read r}\n" for every read out (host buffer), the FASTA text
+ * formatted on the GPU.  n_reads / n_bases: what the records hold (first flags; record
+ * lengths) -- they size the device buffers and are checked against the decode
+ * (NTC_ERR_FORMAT if they differ).  *out_len = the text's bytes (the size needed on
+ * NTC_ERR_CAPACITY).  Synchronous.                                                      */
+int ntc_decode_fasta(ntc_ctx *ctx, const uint64_t *recs, uint64_t n_recs, uint64_t n_reads, uint64_t n_bases,
+                     uint64_t first_id, uint8_t *out, uint64_t out_capacity, uint64_t *out_len);
 
 /* Timings of the last encode/decode call (synchronises). */
 int ntc_last_timing(ntc_ctx *ctx, ntc_timing *out);

@@ -4,6 +4,9 @@
  *   ntc_encode_file   src/main.rs:141-181 (`ntcomp encode -i P reads > encoded.dat`):
  *                     FASTX batches -> GPU encode + block packer on every context ->
  *                     deflate on the host pool -> file header + blocks, in file order.
+ *   ntc_decode_file   src/main.rs:183-211 (`ntcomp decode -i P encoded.dat > out.fasta`):
+ *                     blocks inflated + stream-decoded on the host pool -> GPU walk and
+ *                     FASTA formatting on every context -> ">seq.N" records in file order.
  *
  * Behaviour kept from the reference: blocks of 65,536 reads (main.rs:152), the last block's
  * header carries num_records % 65,536 (main.rs:176), a block with no long or no short
@@ -44,6 +47,18 @@ typedef struct ntc_pipeline_stats {
 /* ctxs: n_ctx contexts with the index uploaded (one per GPU; two on one device are allowed).
  * Writes encoded.dat to out_fd (not closed).                                              */
 int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int out_fd, const ntc_pipeline_opts *opts,
+                    ntc_pipeline_stats *stats);
+
+/* Reads encoded.dat at in_path (mapped), writes FASTA to out_fd (not closed): ">seq.i\n"
+ * + bases + "\n" per read, i from 1 across the file (main.rs:204).  opts->threads sizes the
+ * inflate pool, opts->blocks_per_batch the GPU call (batch_bases and deflate_engine are
+ * unused).  A truncated block ends the input like read_exact (main.rs:199); a damaged block
+ * (bad gzip member or stream sizes) ends the output after the blocks before it and still
+ * returns NTC_OK, as decode_block's Err just ends the reference's loop (main.rs:202): the
+ * caller sees it in stats->dropped_blocks (> 0) and stats->error.  stats: reads, bases,
+ * blocks decoded, dropped_blocks = whole blocks not decoded, bytes_out = FASTA bytes,
+ * parse_s = inflate CPU time summed over threads, gpu_s, write_s, wall_s.            */
+int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int out_fd, const ntc_pipeline_opts *opts,
                     ntc_pipeline_stats *stats);
 
 #ifdef __cplusplus

@@ -40,9 +40,10 @@ EXPORTED = [
     "ntc_memcpy_d2h", "ntc_debug_matching_statistics", "ntc_build_index", "ntc_index_free",
     "ntc_index_view_of", "ntc_index_save", "ntc_index_save_as", "ntc_index_load", "ntc_synth_genome", "ntc_synth_strains", "ntc_synth_reads", "ntc_minimizer_keys",
     "ntc_file_header", "ntc_write_block", "ntc_read_block", "ntc_buffer_free", "ntc_pack_block",
-    "ntc_deflate_block", "ntc_pack_blocks_device", "ntc_encode_pack_batch",
+    "ntc_deflate_block", "ntc_pack_blocks_device", "ntc_encode_pack_batch", "ntc_read_block_into",
     "ntc_fastx_open", "ntc_fastx_next_batch", "ntc_fastx_close", "ntc_fasta_format", "ntc_fastx_next_batch_into",
-    "ntc_fastx_set_threads", "ntc_host_threads", "ntc_encode_file",
+    "ntc_fastx_set_threads", "ntc_host_threads", "ntc_encode_file", "ntc_decode_fasta",
+    "ntc_decode_file",
 ]
 
 
@@ -159,6 +160,7 @@ def lib():
         "ntc_read_block": (I, [P, u64, ctypes.POINTER(u64), ctypes.POINTER(P), ctypes.POINTER(u64),
                                ctypes.POINTER(u64)]),
         "ntc_buffer_free": (None, [P]),
+        "ntc_read_block_into": (I, [P, u64, ctypes.POINTER(u64), P, u64, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "ntc_pack_block": (I, [P, u64, u64, ctypes.POINTER(BlockMeta), ctypes.POINTER(P), ctypes.POINTER(u64)]),
         "ntc_deflate_block": (I, [ctypes.POINTER(BlockMeta), P, I, ctypes.POINTER(P), ctypes.POINTER(u64)]),
         "ntc_pack_blocks_device": (I, [P, P, P, u64, u32, P, u64, P, ctypes.POINTER(u64)]),
@@ -172,6 +174,8 @@ def lib():
         "ntc_host_threads": (I, []),
         "ntc_encode_file": (I, [P, I, ctypes.c_char_p, I, ctypes.POINTER(PipelineOpts), ctypes.POINTER(PipelineStats)]),
         "ntc_fasta_format": (I, [P, P, u64, u64, ctypes.POINTER(P), ctypes.POINTER(u64)]),
+        "ntc_decode_fasta": (I, [P, P, u64, u64, u64, u64, P, u64, ctypes.POINTER(u64)]),
+        "ntc_decode_file": (I, [P, I, ctypes.c_char_p, I, ctypes.POINTER(PipelineOpts), ctypes.POINTER(PipelineStats)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -571,10 +575,23 @@ def encode_file(ctxs, in_path, out_fd, threads=0, blocks_per_batch=16, batch_bas
     """`ntcomp encode` file to file (ntc_encode_file, include/ntcomp_pipeline.h): FASTX ->
     GPU encode + block packer on every context -> deflate pool -> encoded.dat on out_fd.
     Returns the per-stage stats as a dict; raises NtcError (with .bad_read)."""
+    return _run_pipeline("ntc_encode_file", ctxs, in_path, out_fd,
+                         PipelineOpts(threads, blocks_per_batch, batch_bases, DEFLATE_ENGINES[deflate], 0))
+
+
+def decode_file(ctxs, in_path, out_fd, threads=0, blocks_per_batch=16):
+    """`ntcomp decode` file to file (ntc_decode_file, include/ntcomp_pipeline.h): encoded.dat
+    -> inflate + stream decode pool -> GPU inverse-SBWT walk + FASTA formatting on every
+    context -> FASTA on out_fd.  Stats as a dict; a damaged block ends the output after the
+    blocks before it without an error, like decode_block's Err ends the reference's loop
+    (src/main.rs:202): stats["dropped_blocks"] > 0 and stats["error"] say so."""
+    return _run_pipeline("ntc_decode_file", ctxs, in_path, out_fd, PipelineOpts(threads, blocks_per_batch, 0, 0, 0))
+
+
+def _run_pipeline(fn, ctxs, in_path, out_fd, o):
     arr = (ctypes.c_void_p * len(ctxs))(*[c.h.value for c in ctxs])
-    o = PipelineOpts(threads, blocks_per_batch, batch_bases, DEFLATE_ENGINES[deflate], 0)
     st = PipelineStats()
-    rc = lib().ntc_encode_file(arr, len(ctxs), os.fsencode(in_path), out_fd, ctypes.byref(o), ctypes.byref(st))
+    rc = getattr(lib(), fn)(arr, len(ctxs), os.fsencode(in_path), out_fd, ctypes.byref(o), ctypes.byref(st))
     d = {k: (getattr(st, k).decode(errors="replace") if k == "error" else getattr(st, k))
          for k, _ in PipelineStats._fields_ if k != "reserved"}
     if rc:

@@ -14,11 +14,8 @@ Index files: <prefix>.sbwt / <prefix>.lcs in this library's own layout (the sbwt
 byte layout is unavailable offline -- DESIGN.md section 8).
 """
 import argparse
-import concurrent.futures as cf
-import os
 import sys
 
-import numpy as np
 
 BLOCK_READS = 65536  # main.rs:152
 
@@ -151,88 +148,33 @@ def cmd_encode(args):
               dropped_blocks=res["dropped_blocks"], pipeline_wall_s=round(res["wall_s"], 3), deflate=args.deflate)
 
 
-def _block_extents(data, pos):
-    """Byte ranges of the blocks after the file header: each block is four
-    (32-byte BlockHeader, gzip payload) streams, payload length = the header's first u32
-    (lib.rs:37-50, 232-252).  A truncated tail ends the list, as it ends the reference's
-    read loop (main.rs:202)."""
-    out, n = [], len(data)
-    while pos < n:
-        p = pos
-        for _ in range(4):
-            if p + 32 > n:
-                return out
-            p += 32 + int(np.frombuffer(data[p:p + 4], dtype="<u4")[0])
-        if p > n:
-            return out
-        out.append((pos, p))
-        pos = p
-    return out
-
-
 def cmd_decode(args):
+    """main.rs:183-211 through the native pipeline (ntc_decode_file): blocks inflated and
+    stream-decoded on the host pool, inverse-SBWT walk + FASTA formatting per context on the
+    GPU, ">seq.N" text written in file order."""
     import ntcomp_amd as nt
     st = _Stats(args.stats)
     index = st.wrap("index_load", nt.Index.load)(args.index_prefix)
     ctxs = _open_gpus(index, _devices(args), st)
-    read_block = st.wrap("unzip", nt.read_block)
-    fasta_format = st.wrap("format", nt.fasta_format)
-    gpu_decode = st.wrap("gpu_decode", lambda ctx, r: ctx.decode(r))
-    data = np.memmap(args.input_path, dtype=np.uint8, mode="r") if os.path.getsize(args.input_path) else \
-        np.zeros(0, dtype=np.uint8)
-    out = sys.stdout.buffer
     log("Decoding encoded data...")
-    # blocks unzip in parallel on the CPU pool, batches decode on the GPUs (round-robin),
-    # FASTA formatting runs on the pool, and everything is written in file order
-    extents = _block_extents(data, 32)  # after the file header (main.rs:196-198)
-    pool = cf.ThreadPoolExecutor(max_workers=args.threads)
-    gpu_pools = [cf.ThreadPoolExecutor(max_workers=1) for _ in ctxs]  # one driver thread per context
-    bpb = args.blocks_per_batch
-    unzip = [pool.submit(read_block, data[a:b]) for a, b in extents[:2 * bpb]]
-    submitted = len(unzip)
-    decodes = []  # (future of (bases, offs)) in file order
-    formats = []  # (future of bytes) in file order
-    seq_id = 1
-    stop = False
-
-    def finish_decodes(keep):
-        nonlocal seq_id
-        while len(decodes) > keep:
-            bases, offs = decodes.pop(0).result()
-            formats.append(pool.submit(fasta_format, bases, offs, seq_id))
-            seq_id += len(offs) - 1
-            while formats and (formats[0].done() or len(formats) > 2):
-                out.write(formats.pop(0).result())
-
-    b0, gi = 0, 0
-    while b0 < len(extents) and not stop:
-        recs = []
-        for i in range(b0, min(b0 + bpb, len(extents))):
-            try:
-                recs.append(unzip[i].result()[0])
-            except nt.NtcError:
-                stop = True  # a damaged block ends the reference's loop (main.rs:202)
-                break
-        # keep about two batches of blocks unzipping ahead
-        while submitted < min(len(extents), b0 + 3 * bpb):
-            a, b = extents[submitted]
-            unzip.append(pool.submit(read_block, data[a:b]))
-            submitted += 1
-        for i in range(b0, min(b0 + bpb, len(extents))):
-            unzip[i] = None
-        b0 += bpb
-        if recs:
-            allr = np.concatenate(recs) if len(recs) > 1 else recs[0]
-            decodes.append(gpu_pools[gi % len(ctxs)].submit(gpu_decode, ctxs[gi % len(ctxs)], allr))
-            gi += 1
-        finish_decodes(len(ctxs))
-    finish_decodes(0)
-    for f in formats:
-        out.write(f.result())
+    out = sys.stdout.buffer
     out.flush()
-    for c in ctxs:
-        c.close()
-    st.report(command="decode", gpus=len(ctxs), blocks=len(extents))
+    try:
+        res = st.wrap("pipeline", nt.decode_file)(ctxs, args.input_path, out.fileno(), threads=args.threads,
+                                                  blocks_per_batch=args.blocks_per_batch)
+    except nt.NtcError as e:
+        raise SystemExit(f"ntcomp decode: {e}")
+    finally:
+        for c in ctxs:
+            c.close()
+    if res["dropped_blocks"]:
+        # the reference's `while let Ok(..) = decode_block` just ends here (main.rs:202)
+        log(f"warning: {res['error']}; {res['dropped_blocks']} block(s) not decoded")
+    if st.on:
+        for k, name in (("parse_s", "unzip"), ("gpu_s", "gpu"), ("write_s", "write")):
+            st.acc[name] = res[k]
+    st.report(command="decode", gpus=len(ctxs), threads=res["threads"], reads=res["reads"], blocks=res["blocks"],
+              pipeline_wall_s=round(res["wall_s"], 3))
 
 
 def main(argv=None):

@@ -242,6 +242,36 @@ bool gzip_append(const uint8_t *data, size_t n, int engine, std::vector<uint8_t>
     return true;
 }
 
+// libdeflate gzip inflate (one decompressor per thread) into a buffer of the expected size
+struct LibInflate {
+    void *(*alloc_d)() = nullptr;
+    void (*free_d)(void *) = nullptr;
+    int (*gz_d)(void *, const void *, size_t, void *, size_t, size_t *) = nullptr;
+    bool ok = false;
+    LibInflate() {
+        void *h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        alloc_d = (void *(*)())dlsym(h, "libdeflate_alloc_decompressor");
+        free_d = (void (*)(void *))dlsym(h, "libdeflate_free_decompressor");
+        gz_d = (int (*)(void *, const void *, size_t, void *, size_t, size_t *))dlsym(h, "libdeflate_gzip_decompress");
+        ok = alloc_d && free_d && gz_d;
+    }
+};
+LibInflate &libinflate() {
+    static LibInflate L;
+    return L;
+}
+struct ThreadDecompressor {
+    void *d = nullptr;
+    ~ThreadDecompressor() {
+        if (d) libinflate().free_d(d);
+    }
+};
+thread_local ThreadDecompressor tl_decompressor;
+
+// exactly `want` bytes out of one gzip member, or false (libdeflate when present, else zlib)
+bool gunzip_exact(const uint8_t *data, size_t n, size_t want, std::vector<uint8_t> &out);
+
 bool gunzip_bytes(const uint8_t *data, size_t n, std::vector<uint8_t> &out) {
     z_stream zs;
     std::memset(&zs, 0, sizeof(zs));
@@ -307,17 +337,24 @@ BlockHeader read_header(const uint8_t *p) {
     return h;
 }
 
-uint64_t as_2bit(const uint8_t *codes, size_t n) {
-    uint64_t v = 0;
-    for (size_t j = 0; j < n; j++) v |= (uint64_t)codes[j] << (2 * j);
-    return v;
-}
-
 inline uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
+
+bool gunzip_exact(const uint8_t *data, size_t n, size_t want, std::vector<uint8_t> &out) {
+    LibInflate &L = libinflate();
+    if (L.ok && (tl_decompressor.d || (tl_decompressor.d = L.alloc_d()))) {
+        out.resize(want);
+        size_t got = 0;
+        // libdeflate needs the whole member; a longer (corrupt) one fails with short output
+        if (L.gz_d(tl_decompressor.d, data, n, out.data(), want, &got) == 0) return got == want;
+        return false;
+    }
+    if (!gunzip_bytes(data, n, out)) return false;
+    return out.size() == want;
+}
 
 bool decompress_block(const uint8_t *payload, const BlockHeader &h, bool rice, std::vector<uint64_t> &out) {
     std::vector<uint8_t> bytes;
-    if (!gunzip_bytes(payload, h.block_size, bytes)) return false;
+    if (!gunzip_exact(payload, h.block_size, (size_t)h.encoded_size * 8, bytes)) return false;
     std::vector<uint64_t> words(bytes.size() / 8);
     for (size_t i = 0; i < words.size(); i++) {  // big-endian words (see pack_block)
         uint64_t w;
@@ -513,10 +550,14 @@ int ntc_write_block(const uint64_t *recs, uint64_t n_recs, uint64_t num_records,
     return rc;
 }
 
-int ntc_read_block(const uint8_t *data, uint64_t len, uint64_t *consumed, uint64_t **recs, uint64_t *n_recs,
-                   uint64_t *num_records) {
-    if (!data || !consumed || !recs || !n_recs) return NTC_ERR_INVALID_ARG;
-    *recs = nullptr;
+}  // extern "C"
+
+namespace {
+// decode_block's container half (lib.rs:320-363): the block's four streams, decompressed and
+// zipped back into u64 records (zip_block_contents, decode.rs:102-149), into vec (resized)
+// or out (cap records; NTC_ERR_CAPACITY if more).  *n_recs = the block's record count.
+int read_block_impl(const uint8_t *data, uint64_t len, uint64_t *consumed, std::vector<uint64_t> *vec, uint64_t *out,
+                    uint64_t cap, uint64_t *n_recs, uint64_t *num_records) {
     *n_recs = 0;
     *consumed = 0;
     uint64_t pos = 0;
@@ -530,21 +571,25 @@ int ntc_read_block(const uint8_t *data, uint64_t len, uint64_t *consumed, uint64
         if (!decompress_block(data + pos, hs[s], s == 1 || s == 2, parts[s])) return NTC_ERR_FORMAT;
         pos += hs[s].block_size;
     }
-    // zip_block_contents (decode.rs:102-149)
     const auto &c1 = parts[0], &c2 = parts[1], &fl = parts[2], &bn = parts[3];
     if (c1.size() != c2.size()) return NTC_ERR_FORMAT;
     uint64_t T = 0;
     for (uint64_t f : fl) T += (f & 0xFC) >> 2;
-    std::vector<uint8_t> vals;
-    vals.reserve(T);
-    for (size_t i = 0; i < bn.size(); i++) {
-        // decode.rs:114-118 uses T % 31 for the last chunk, which panics whenever T is a
-        // positive multiple of 31 (Appendix B.4); ((T-1) % 31) + 1 agrees everywhere else
-        uint64_t l = (i + 1 == bn.size()) ? ((T - 1) % 31) + 1 : 31;
-        for (uint64_t j = 0; j < l; j++) vals.push_back((uint8_t)((bn[i] >> (2 * j)) & 3));
+    // short-record bases: chunk i holds 31 bases, the last one the rest.  decode.rs:114-118
+    // uses T % 31 for the last chunk, which panics whenever T is a positive multiple of 31
+    // (Appendix B.4); ((T-1) % 31) + 1 agrees everywhere else
+    if (T ? bn.size() != (T + 30) / 31 : false) return NTC_ERR_FORMAT;
+    *n_recs = fl.size();
+    if (num_records) *num_records = hs[0].num_records;
+    *consumed = pos;
+    if (vec) {
+        vec->resize(fl.size());
+        out = vec->data();
+    } else if (fl.size() > cap) {
+        return NTC_ERR_CAPACITY;
     }
-    std::vector<uint64_t> out(fl.size());
-    size_t i = 0, j = 0;
+    size_t i = 0;
+    uint64_t j = 0;  // next short base
     for (size_t r = 0; r < fl.size(); r++) {
         const uint8_t flag = (uint8_t)fl[r];
         uint64_t w;
@@ -554,20 +599,48 @@ int ntc_read_block(const uint8_t *data, uint64_t len, uint64_t *consumed, uint64
             i++;
         } else {
             const uint32_t l = flag >> 2;
-            if (j + l > vals.size()) return NTC_ERR_FORMAT;
-            w = as_2bit(vals.data() + j, l) & 0x00FFFFFFFFFFFFFFULL;
+            if (j + l > T) return NTC_ERR_FORMAT;
+            // bases j .. j + l - 1 of the concatenation: from chunk j / 31 (and the next)
+            w = 0;
+            for (uint32_t t = 0; t < l; t++) {
+                const uint64_t q = j + t;
+                w |= ((bn[q / 31] >> (2 * (q % 31))) & 3ULL) << (2 * t);
+            }
+            w &= 0x00FFFFFFFFFFFFFFULL;
             j += l;
         }
         out[r] = w | ((uint64_t)flag << 56);
     }
-    uint64_t *buf = (uint64_t *)std::malloc((out.size() ? out.size() : 1) * 8);
-    if (!buf) return NTC_ERR_CAPACITY;
-    std::memcpy(buf, out.data(), out.size() * 8);
-    *recs = buf;
-    *n_recs = out.size();
-    *consumed = pos;
-    if (num_records) *num_records = hs[0].num_records;
     return NTC_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int ntc_read_block(const uint8_t *data, uint64_t len, uint64_t *consumed, uint64_t **recs, uint64_t *n_recs,
+                   uint64_t *num_records) {
+    if (!data || !consumed || !recs || !n_recs) return NTC_ERR_INVALID_ARG;
+    *recs = nullptr;
+    std::vector<uint64_t> v;
+    uint64_t used = 0;
+    const int rc = read_block_impl(data, len, &used, &v, nullptr, 0, n_recs, num_records);
+    if (rc) {
+        *n_recs = 0;
+        *consumed = 0;
+        return rc;
+    }
+    uint64_t *buf = (uint64_t *)std::malloc((v.size() ? v.size() : 1) * 8);
+    if (!buf) return NTC_ERR_CAPACITY;
+    std::memcpy(buf, v.data(), v.size() * 8);
+    *recs = buf;
+    *consumed = used;
+    return NTC_OK;
+}
+
+int ntc_read_block_into(const uint8_t *data, uint64_t len, uint64_t *consumed, uint64_t *recs, uint64_t capacity,
+                        uint64_t *n_recs, uint64_t *num_records) {
+    if (!data || !consumed || !n_recs || (capacity && !recs)) return NTC_ERR_INVALID_ARG;
+    return read_block_impl(data, len, consumed, nullptr, recs, capacity, n_recs, num_records);
 }
 
 void ntc_buffer_free(void *p) { std::free(p); }

@@ -33,6 +33,14 @@ enum CallKind { kNone = 0, kEncode = 1, kDecode = 2 };
 
 }  // namespace
 
+// device workspace slots of a context (grown by ensure, freed with the context)
+enum WsSlot {
+    WS_D = 0, WS_S, WS_F, WS_R, WS_RECCOUNT, WS_SCANTMP, WS_TILEBASE, WS_TILEROWS,
+    WS_STAGE_BASES, WS_STAGE_OFFS, WS_STAGE_RECS, WS_E, WS_DEC_A, WS_DEC_B, WS_DEC_C,
+    WS_DEC_D, WS_Q, WS_E3, WS_NE, WS_COUNTER, WS_R2, WS_ED, WS_WAVECNT, WS_PACK_CHUNKS, WS_PACK_META,
+    WS_PACK_PAYLOAD, WS_FA_BASES, WS_FA_OFFS, WS_FA_SCAN, WS_COUNT
+};
+
 struct ntc_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -44,7 +52,7 @@ struct ntc_ctx {
     std::vector<void *> index_mem;
     uint64_t index_bytes = 0;
     // workspace buffers (grown, never shrunk)
-    DevBuf ws[28];
+    DevBuf ws[WS_COUNT];
     unsigned long long *d_status = nullptr;
     // status mailbox in pinned host memory: {status, count a, count b}, written by k_status_box
     // at the end of a device call, so *_status() is one stream sync instead of D2H copies
@@ -80,12 +88,6 @@ namespace {
 
 constexpr uint64_t kCounterBytes = 8 * 64;  // work queue heads (kernels.hip WaveQueue: 8, 64 B apart)
 
-enum WsSlot {
-    WS_D = 0, WS_S, WS_F, WS_R, WS_RECCOUNT, WS_SCANTMP, WS_TILEBASE, WS_TILEROWS,
-    WS_STAGE_BASES, WS_STAGE_OFFS, WS_STAGE_RECS, WS_E, WS_DEC_A, WS_DEC_B, WS_DEC_C,
-    WS_DEC_D, WS_Q, WS_E3, WS_NE, WS_COUNTER, WS_R2, WS_ED, WS_WAVECNT, WS_PACK_CHUNKS, WS_PACK_META,
-    WS_PACK_PAYLOAD
-};
 
 #define HIP_TRY(ctx, expr)                                                                   \
     do {                                                                                     \
@@ -1158,6 +1160,46 @@ int ntc_encode_pack_batch(ntc_ctx *ctx, const uint8_t *bases, const uint64_t *re
     }
     *payload = h;
     *payload_bytes = used;
+    return NTC_OK;
+}
+
+int ntc_decode_fasta(ntc_ctx *ctx, const uint64_t *recs, uint64_t n_recs, uint64_t n_reads, uint64_t n_bases,
+                     uint64_t first_id, uint8_t *out, uint64_t out_capacity, uint64_t *out_len) {
+    if (!ctx || !out_len || (n_recs && !recs) || (n_reads && !out)) return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    *out_len = 0;
+    if (!ctx->has_index) return set_err(ctx, NTC_ERR_NO_INDEX, "no index uploaded");
+    // bytes of ">seq.{id}\n" + read + "\n" for ids first_id .. first_id + n_reads - 1
+    uint64_t need = n_bases + 7 * n_reads;  // 5 + 2 per read, plus the digits
+    for (uint64_t lo = 1, d = 1; lo <= first_id + n_reads - 1 && n_reads; lo *= 10, d++) {
+        const uint64_t hi = lo > UINT64_MAX / 10 ? UINT64_MAX : lo * 10 - 1;  // ids with d digits: [lo, hi]
+        const uint64_t a = std::max(lo, first_id), b = std::min(hi, first_id + n_reads - 1);
+        if (a <= b) need += d * (b - a + 1);
+        if (hi == UINT64_MAX) break;
+    }
+    *out_len = need;
+    if (need > out_capacity) return set_err(ctx, NTC_ERR_CAPACITY, "out_capacity smaller than the FASTA text");
+    if (n_recs == 0) return n_reads ? set_err(ctx, NTC_ERR_FORMAT, "reads without records") : NTC_OK;
+    void *d_recs, *d_bases, *d_offs, *d_scan, *d_out;
+    int rc;
+    if ((rc = ensure(ctx, WS_STAGE_RECS, n_recs * 8, &d_recs))) return rc;
+    if ((rc = ensure(ctx, WS_FA_BASES, n_bases + 64, &d_bases))) return rc;
+    if ((rc = ensure(ctx, WS_FA_OFFS, (n_reads + 2) * 8, &d_offs))) return rc;
+    if ((rc = ensure(ctx, WS_FA_SCAN, (2 * (n_reads + 1) + scan_tmp_words(n_reads + 1)) * 8, &d_scan))) return rc;
+    if ((rc = ensure(ctx, WS_STAGE_BASES, need + 64, &d_out))) return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(d_recs, recs, n_recs * 8, hipMemcpyHostToDevice, ctx->stream));
+    if ((rc = ntc_decode_batch_device(ctx, (const uint64_t *)d_recs, n_recs, (uint8_t *)d_bases, n_bases + 64,
+                                      (uint64_t *)d_offs, n_reads + 2)))
+        return rc;
+    uint64_t *sizes = (uint64_t *)d_scan, *out_offs = sizes + (n_reads + 1), *tmp = out_offs + (n_reads + 1);
+    launch_fasta((const uint8_t *)d_bases, (const uint64_t *)d_offs, n_reads, first_id, ctx->d_status, sizes, out_offs,
+                 tmp, (uint8_t *)d_out, need, ctx->stream);
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipMemcpyAsync(out, d_out, need, hipMemcpyDeviceToHost, ctx->stream));
+    uint64_t nr = 0, nb = 0;
+    if ((rc = ntc_decode_status(ctx, &nr, &nb))) return rc;  // synchronises
+    if (nr != n_reads || nb != n_bases)
+        return set_err(ctx, NTC_ERR_FORMAT, "records hold other read / base counts than given");
     return NTC_OK;
 }
 

@@ -103,6 +103,13 @@ void launch_pack_write(const uint64_t *recs, const uint64_t *chunks, const PackS
                        const PackParams *params, uint64_t n_blocks, uint64_t *payload, uint64_t *bits_out,
                        hipStream_t s);
 
+// decode output as FASTA text on the GPU (fasta.hip): ">seq.{first_id + r}\n{read r}\n";
+// sizes / out_offs: n + 1 words, tmp: scan_tmp_words(n) words; out_offs[n] = total bytes.
+// Nothing is written unless the decode status is clear (~0) and the text fits out_cap.
+void launch_fasta(const uint8_t *d_bases, const uint64_t *d_offs, uint64_t n, uint64_t first_id,
+                  const unsigned long long *d_status, uint64_t *sizes, uint64_t *out_offs, uint64_t *tmp, uint8_t *out,
+                  uint64_t out_cap, hipStream_t s);
+
 void launch_encode(const EncodeArgs &a, hipStream_t s);
 void launch_encode4(const Enc4Args &a, uint64_t total, uint32_t ms_blocks, hipStream_t s,
                     hipEvent_t ev_ms_begin, hipEvent_t ev_ms_end);

@@ -397,3 +397,376 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------------------
+// Native decode pipeline of the CLI: `ntcomp decode -i P encoded.dat > out.fasta`
+// (src/main.rs:183-211), every stage overlapped:
+//
+//   extents  the file is mapped; the blocks' extents and record counts come from their
+//            32-byte headers alone (block_size of each stream; the flag stream's num_u64 =
+//            records).  A truncated block ends the input, as read_exact ends decode_block.
+//   unzip    the host pool turns each block into u64 records (ntc_read_block_into:
+//            inflate, Rice / minimal-binary decode, zip_block_contents) straight into the
+//            batch's pinned buffer, counting its reads (first flags) and bases.
+//   GPU      one driver thread per context, batches dealt round-robin: ntc_decode_fasta =
+//            H2D of the records, the inverse-SBWT walk, the FASTA text formatted on the GPU
+//            (">seq.N" numbering from the reads of the batches before), D2H of the text.
+//   writer   the calling thread writes the batches' text in file order (a regular file:
+//            pwrite from the host pool at the batch's offset; otherwise write).
+// A damaged block ends the output after the blocks before it (decode_block's Err ends the
+// reference's loop, main.rs:202).
+// ---------------------------------------------------------------------------------------
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+
+namespace {
+
+struct DBlock {
+    uint64_t a, len;   // byte range of the block
+    uint64_t n_recs;   // records (the flag stream's num_u64)
+};
+
+struct DSlot {  // one batch in flight
+    uint64_t *recs = nullptr;
+    uint64_t cap_recs = 0;
+    uint8_t *text = nullptr;
+    uint64_t cap_text = 0;
+    uint64_t batch = ~0ULL;  // batch held, ~0 = free
+    uint64_t first_block = 0, n_blocks = 0;
+    uint64_t n_recs = 0, n_reads = 0, n_bases = 0, text_len = 0;
+    uint64_t first_id = 0;
+    uint64_t finished = 0;   // blocks of this batch unzipped or found damaged
+    int bad_block = -1;      // first damaged block (index in the batch)
+    bool buffer = false;     // recs sized for the batch
+    bool ready = false;      // complete + first_id known: the GPU may take it
+    bool decoded = false;
+};
+
+void count_reads(const uint64_t *r, uint64_t n, uint64_t *reads, uint64_t *bases) {
+    uint64_t rd = 0, bs = 0;  // first flags and bases of records (flag byte = bits 56..63)
+    for (uint64_t i = 0; i < n; i++) {
+        const uint64_t w = r[i];
+        const uint32_t flag = (uint32_t)(w >> 56);
+        rd += flag & 1;
+        bs += (flag & 2) ? (flag >> 2) : ((w >> 32) & 0xFFFFFFu);
+    }
+    *reads += rd;
+    *bases += bs;
+}
+
+uint64_t digits_total(uint64_t first, uint64_t n) {  // decimal digits of first .. first + n - 1
+    uint64_t tot = 0;
+    for (uint64_t lo = 1, d = 1; n && lo <= first + n - 1; lo *= 10, d++) {
+        const uint64_t hi = lo > UINT64_MAX / 10 ? UINT64_MAX : lo * 10 - 1;
+        const uint64_t a = std::max(lo, first), b = std::min(hi, first + n - 1);
+        if (a <= b) tot += d * (b - a + 1);
+        if (hi == UINT64_MAX) break;
+    }
+    return tot;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int out_fd, const ntc_pipeline_opts *opts,
+                    ntc_pipeline_stats *stats) {
+    if (!ctxs || n_ctx <= 0 || !in_path || out_fd < 0) return NTC_ERR_INVALID_ARG;
+    for (int i = 0; i < n_ctx; i++)
+        if (!ctxs[i]) return NTC_ERR_INVALID_ARG;
+    ntc_pipeline_opts o{};
+    if (opts) o = *opts;
+    const int T = o.threads > 0 ? o.threads : ntc_host_threads();
+    const uint64_t bpb = (uint64_t)(o.blocks_per_batch > 0 ? o.blocks_per_batch : 16);
+    ntc_pipeline_stats S{};
+    const auto t0 = Clock::now();
+
+    // ---- map + extents ------------------------------------------------------------------
+    const int fd = ::open(in_path, O_RDONLY);
+    if (fd < 0) return NTC_ERR_IO;
+    struct stat st;
+    if (fstat(fd, &st) != 0) {
+        ::close(fd);
+        return NTC_ERR_IO;
+    }
+    const uint64_t fsize = (uint64_t)st.st_size;
+    const uint8_t *data = nullptr;
+    if (fsize) {
+        data = (const uint8_t *)mmap(nullptr, fsize, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (data == MAP_FAILED) {
+            ::close(fd);
+            return NTC_ERR_IO;
+        }
+        madvise((void *)data, fsize, MADV_SEQUENTIAL);
+    }
+    ::close(fd);
+    auto le32 = [&](uint64_t p) { return (uint64_t)data[p] | (uint64_t)data[p + 1] << 8 | (uint64_t)data[p + 2] << 16 |
+                                         (uint64_t)data[p + 3] << 24; };
+    std::vector<DBlock> blocks;
+    for (uint64_t pos = 32; pos < fsize;) {  // after the 32-byte file header (main.rs:196-198)
+        uint64_t p = pos, nrec = 0;
+        bool whole = true;
+        for (int s = 0; s < 4 && whole; s++) {
+            if (p + 32 > fsize) {
+                whole = false;
+                break;
+            }
+            if (s == 2) nrec = le32(p + 8);
+            p += 32 + le32(p);
+            if (p > fsize) whole = false;
+        }
+        if (!whole) break;
+        blocks.push_back(DBlock{pos, p - pos, nrec});
+        pos = p;
+    }
+    const uint64_t n_batches = (blocks.size() + bpb - 1) / bpb;
+    S.alloc_s = secs(t0, Clock::now());
+
+    const int NB = n_ctx + 2;
+    std::vector<DSlot> slots((size_t)NB);
+    Shared sh;
+    uint64_t next_task = 0;       // next block to unzip
+    uint64_t next_id = 1;         // main.rs:204: seq.{i+1}
+    int64_t stop_batch = -1;      // batch holding the first damaged block (output ends in it)
+    std::atomic<double> t_unzip{0}, t_gpu{0}, t_write{0};
+    auto add_time = [](std::atomic<double> &a, double d) {
+        double cur = a.load();
+        while (!a.compare_exchange_weak(cur, cur + d)) {
+        }
+    };
+    auto slot_of = [&](uint64_t b) -> DSlot & { return slots[(size_t)(b % (uint64_t)NB)]; };
+    // pinned buffers are sized per batch (grown in the claiming thread, outside the lock)
+    auto ensure_pinned = [&](void **p, uint64_t *cap, uint64_t need) -> bool {
+        if (need <= *cap) return true;
+        if (*p) (void)hipHostFree(*p);
+        *p = nullptr;
+        *cap = 0;
+        const uint64_t want = need + need / 8 + 4096;
+        if (hipHostMalloc(p, want, hipHostMallocDefault) != hipSuccess) return false;
+        *cap = want;
+        return true;
+    };
+
+    // ---- unzip pool ------------------------------------------------------------------------
+    // Blocks are taken in file order; the first block of a batch claims the batch's slot
+    // (free once the writer is done with batch b - NB) and sizes its record buffer.  Past a
+    // damaged block no later batch is started; the rest of its own batch is still unzipped
+    // so that the batch completes (only the blocks before the damaged one are decoded).
+    std::vector<std::thread> pool;
+    for (int t = 0; t < T; t++)
+        pool.emplace_back([&] {
+            for (;;) {
+                uint64_t blk, b;
+                bool first;
+                {
+                    std::unique_lock<std::mutex> g(sh.mu);
+                    auto exhausted = [&] {
+                        return sh.error != NTC_OK || next_task >= blocks.size() ||
+                               (stop_batch >= 0 && (int64_t)(next_task / bpb) > stop_batch);
+                    };
+                    sh.cv.wait(g, [&] {
+                        if (exhausted()) return true;
+                        const uint64_t nb = next_task / bpb;
+                        const DSlot &sl = slot_of(nb);
+                        return sl.batch == nb || sl.batch == ~0ULL;
+                    });
+                    if (exhausted()) return;
+                    blk = next_task++;
+                    b = blk / bpb;
+                    DSlot &sl = slot_of(b);
+                    first = sl.batch != b;
+                    if (first) {
+                        sl = DSlot{sl.recs, sl.cap_recs, sl.text, sl.cap_text};
+                        sl.batch = b;
+                        sl.first_block = b * bpb;
+                        sl.n_blocks = std::min<uint64_t>(bpb, blocks.size() - sl.first_block);
+                        for (uint64_t i = 0; i < sl.n_blocks; i++) sl.n_recs += blocks[sl.first_block + i].n_recs;
+                    }
+                }
+                DSlot &sl = slot_of(b);
+                if (first) {  // size the batch's pinned record buffer outside the lock
+                    const bool okp = ensure_pinned((void **)&sl.recs, &sl.cap_recs, sl.n_recs * 8 + 8);
+                    if (!okp) {
+                        sh.fail(NTC_ERR_HIP, "pinned host allocation failed");
+                        return;
+                    }
+                    std::lock_guard<std::mutex> g(sh.mu);
+                    sl.buffer = true;
+                    sh.cv.notify_all();
+                } else {
+                    std::unique_lock<std::mutex> g(sh.mu);
+                    sh.cv.wait(g, [&] { return sh.error != NTC_OK || sl.buffer; });
+                    if (sh.error != NTC_OK) return;
+                }
+                uint64_t off = 0;
+                for (uint64_t i = sl.first_block; i < blk; i++) off += blocks[i].n_recs;
+                const auto tu = Clock::now();
+                uint64_t used = 0, nr = 0, numr = 0, reads = 0, bases = 0;
+                const DBlock &db = blocks[blk];
+                int rc = ntc_read_block_into(data + db.a, db.len, &used, sl.recs + off, db.n_recs, &nr, &numr);
+                if (rc == NTC_OK && (nr != db.n_recs || used != db.len)) rc = NTC_ERR_FORMAT;
+                if (rc == NTC_OK) count_reads(sl.recs + off, nr, &reads, &bases);
+                add_time(t_unzip, secs(tu, Clock::now()));
+                std::lock_guard<std::mutex> g(sh.mu);
+                const int bi = (int)(blk - sl.first_block);
+                if (rc != NTC_OK) {
+                    if (sl.bad_block < 0 || bi < sl.bad_block) sl.bad_block = bi;
+                    if (stop_batch < 0 || (int64_t)b < stop_batch) stop_batch = (int64_t)b;
+                } else {
+                    sl.n_reads += reads;  // recounted below when the batch holds a damaged block
+                    sl.n_bases += bases;
+                }
+                sl.finished++;
+                sh.cv.notify_all();
+            }
+        });
+
+    // ---- GPU drivers ---------------------------------------------------------------------------
+    // A batch is complete when all of its blocks are in (or every block before its first
+    // damaged one, once no task of it is still running).  The assigner (below, in the
+    // writer's loop) fixes first_id in batch order.
+    std::vector<std::thread> gpus;
+    for (int c = 0; c < n_ctx; c++)
+        gpus.emplace_back([&, c] {
+            for (uint64_t b = (uint64_t)c;; b += (uint64_t)n_ctx) {
+                DSlot *slp;
+                {
+                    std::unique_lock<std::mutex> g(sh.mu);
+                    sh.cv.wait(g, [&] {
+                        return sh.error != NTC_OK || b >= n_batches || (stop_batch >= 0 && (int64_t)b > stop_batch) ||
+                               (slot_of(b).batch == b && slot_of(b).ready);
+                    });
+                    if (sh.error != NTC_OK || b >= n_batches || (stop_batch >= 0 && (int64_t)b > stop_batch)) return;
+                    slp = &slot_of(b);
+                }
+                DSlot &sl = *slp;
+                const uint64_t nrec = sl.n_recs;
+                const uint64_t need = sl.n_bases + 7 * sl.n_reads + digits_total(sl.first_id, sl.n_reads) + 64;
+                const auto tg = Clock::now();
+                if (!ensure_pinned((void **)&sl.text, &sl.cap_text, need)) {
+                    sh.fail(NTC_ERR_HIP, "pinned host allocation failed");
+                    return;
+                }
+                uint64_t len = 0;
+                const int rc = ntc_decode_fasta(ctxs[c], sl.recs, nrec, sl.n_reads, sl.n_bases, sl.first_id, sl.text,
+                                                sl.cap_text, &len);
+                add_time(t_gpu, secs(tg, Clock::now()));
+                if (rc) {
+                    sh.fail(rc, std::string("decode: ") + ntc_last_error(ctxs[c]));
+                    return;
+                }
+                std::lock_guard<std::mutex> g(sh.mu);
+                sl.text_len = len;
+                sl.decoded = true;
+                S.gpu_done_s = secs(t0, Clock::now());
+                sh.cv.notify_all();
+            }
+        });
+
+    // ---- assigner + writer (this thread) ------------------------------------------------------------
+    struct stat ost;
+    const bool seekable = fstat(out_fd, &ost) == 0 && S_ISREG(ost.st_mode);
+    off_t out_pos = seekable ? lseek(out_fd, 0, SEEK_CUR) : 0;
+    auto write_text = [&](const uint8_t *p, uint64_t n) -> bool {
+        if (seekable && n > (8u << 20) && T > 1) {  // parallel pwrite into the page cache
+            const int W = std::min<int>(T, 8);
+            std::vector<std::thread> ws;
+            std::atomic<bool> ok{true};
+            for (int w = 0; w < W; w++)
+                ws.emplace_back([&, w] {
+                    const uint64_t a = n * (uint64_t)w / (uint64_t)W, e = n * (uint64_t)(w + 1) / (uint64_t)W;
+                    uint64_t q = a;
+                    while (q < e) {
+                        const ssize_t r = ::pwrite(out_fd, p + q, e - q, out_pos + (off_t)q);
+                        if (r <= 0) {
+                            ok = false;
+                            return;
+                        }
+                        q += (uint64_t)r;
+                    }
+                });
+            for (auto &x : ws) x.join();
+            out_pos += (off_t)n;
+            return ok.load();
+        }
+        while (n) {
+            const ssize_t w = seekable ? ::pwrite(out_fd, p, n, out_pos) : ::write(out_fd, p, n);
+            if (w <= 0) return false;
+            p += w;
+            n -= (uint64_t)w;
+            out_pos += w;
+        }
+        return true;
+    };
+    for (uint64_t b = 0; b < n_batches; b++) {
+        DSlot *slp;
+        {
+            std::unique_lock<std::mutex> g(sh.mu);
+            // the batch is complete once every block of it is unzipped or found damaged
+            sh.cv.wait(g, [&] {
+                if (sh.error != NTC_OK) return true;
+                if (stop_batch >= 0 && (int64_t)b > stop_batch) return true;
+                const DSlot &sl = slot_of(b);
+                return sl.batch == b && sl.finished == sl.n_blocks;
+            });
+            if (sh.error != NTC_OK || (stop_batch >= 0 && (int64_t)b > stop_batch)) break;
+            DSlot &sl = slot_of(b);
+            if (sl.bad_block >= 0) {  // only the blocks before the damaged one
+                uint64_t n = 0;
+                for (int i = 0; i < sl.bad_block; i++) n += blocks[sl.first_block + (uint64_t)i].n_recs;
+                sl.n_recs = n;
+                sl.n_reads = sl.n_bases = 0;
+                count_reads(sl.recs, n, &sl.n_reads, &sl.n_bases);
+            }
+            sl.first_id = next_id;
+            next_id += sl.n_reads;
+            sl.ready = true;
+            sh.cv.notify_all();
+            sh.cv.wait(g, [&] { return sh.error != NTC_OK || sl.decoded; });
+            if (sh.error != NTC_OK) break;
+            slp = &sl;
+        }
+        const auto tw = Clock::now();
+        if (!write_text(slp->text, slp->text_len)) sh.fail(NTC_ERR_IO, "write failed");
+        add_time(t_write, secs(tw, Clock::now()));
+        std::lock_guard<std::mutex> g(sh.mu);
+        S.reads += slp->n_reads;
+        S.bases += slp->n_bases;
+        S.bytes_out += slp->text_len;
+        S.blocks += slp->bad_block >= 0 ? (uint64_t)slp->bad_block : slp->n_blocks;
+        const bool last = stop_batch >= 0 && (int64_t)b == stop_batch;
+        slp->batch = ~0ULL;  // free the slot
+        sh.cv.notify_all();
+        if (last) break;
+    }
+    {
+        std::lock_guard<std::mutex> g(sh.mu);
+        if (sh.error == NTC_OK) sh.error = -1;  // stop the workers
+        sh.cv.notify_all();
+    }
+    for (auto &t : pool) t.join();
+    for (auto &t : gpus) t.join();
+    for (auto &sl : slots) {
+        if (sl.recs) (void)hipHostFree(sl.recs);
+        if (sl.text) (void)hipHostFree(sl.text);
+    }
+    if (data) munmap((void *)data, fsize);
+    const int result = sh.error == -1 ? NTC_OK : sh.error;
+    S.dropped_blocks = blocks.size() - S.blocks;  // after a damaged block (or none)
+    S.parse_s = t_unzip.load();
+    S.gpu_s = t_gpu.load();
+    S.write_s = t_write.load();
+    S.wall_s = secs(t0, Clock::now());
+    S.threads = T;
+    S.bad_read = -1;
+    if (result != NTC_OK)
+        std::snprintf(S.error, sizeof(S.error), "%s", sh.msg.c_str());
+    else if (stop_batch >= 0)  // not an error for the reference either: its loop just ends
+        std::snprintf(S.error, sizeof(S.error), "damaged block %llu: output ends before it",
+                      (unsigned long long)S.blocks);
+    if (stats) *stats = S;
+    return result;
+}
+
+}  // extern "C"

@@ -257,29 +257,6 @@ def test_fasta_format():
     assert nt.fasta_format(b, np.array([0, 4, 4, 6], dtype=np.uint64), 9) == b">seq.9\nACGT\n>seq.10\n\n>seq.11\nTT\n"
 
 
-def test_block_extents_follow_the_stream_headers():
-    """The decode CLI splits encoded.dat into blocks from the four BlockHeaders alone
-    (lib.rs:37-50) so the blocks can unzip in parallel; a truncated tail ends the list."""
-    from ntcomp_amd.cli import _block_extents
-    rng = np.random.default_rng(3)
-    blocks = []
-    for b in range(3):
-        n = 50 + 20 * b
-        recs = rng.integers(0, 1 << 20, n).astype(np.uint64) | (np.uint64(40) << np.uint64(32))
-        recs[::2] = rng.integers(0, 1 << 10, (n + 1) // 2).astype(np.uint64) | (np.uint64(2 | (5 << 2)) << np.uint64(56))
-        recs[0] |= np.uint64(1) << np.uint64(56)
-        blocks.append(nt.write_block(recs, n))
-    data = nt.file_header() + b"".join(blocks)
-    arr = np.frombuffer(data, dtype=np.uint8)
-    ext = _block_extents(arr, 32)
-    ends = np.cumsum([32] + [len(b) for b in blocks])
-    assert ext == [(int(ends[i]), int(ends[i + 1])) for i in range(3)]
-    for (a, b), blk in zip(ext, blocks):
-        assert nt.read_block(arr[a:b])[1] == len(blk)
-    assert _block_extents(arr[:-5], 32) == ext[:2]
-    assert _block_extents(arr[:32], 32) == []
-
-
 def test_cli_build_writes_a_loadable_index(tmp_path):
     g = nt.synth_genome(3, 20_000).tobytes().decode()
     fa = tmp_path / "g.fa"

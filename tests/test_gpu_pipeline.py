@@ -121,3 +121,92 @@ def test_cli_two_contexts_on_one_gpu_and_deflate_engines(setup, tmp_path):
     assert fa["one"] == fa["two"]
     lines = fa["one"].split(b"\n")
     assert b"".join(lines[1::2]) == reads.tobytes()
+
+
+# ---- native decode pipeline (ntc_decode_file) ---------------------------------------------
+def fasta_of(reads, offs, first=1):
+    return b"".join(b">seq.%d\n" % (first + i) + reads[int(offs[i]):int(offs[i + 1])].tobytes() + b"\n"
+                    for i in range(len(offs) - 1))
+
+
+def encoded_file(ctx, tmp_path, reads, offs, name="e.dat"):
+    """encoded.dat of ragged reads through the host codec, block by block (main.rs:162-177)."""
+    n = len(offs) - 1
+    recs, roff = ctx.encode(reads, offs)
+    out, ends = nt.file_header(), []
+    for b0 in range(0, n, 65536):
+        b1 = min(n, b0 + 65536)
+        out += nt.write_block(recs[int(roff[b0]):int(roff[b1])], b1 - b0)
+        ends.append((len(out), b1))
+    (tmp_path / name).write_bytes(out)
+    return tmp_path / name, ends
+
+
+def ragged(genome, n, seed, lo=1, hi=400):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(lo, hi, n)
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens)
+    starts = rng.integers(0, len(genome) - hi, n)
+    reads = np.concatenate([genome[s:s + l] for s, l in zip(starts, lens)]).copy()
+    flip = rng.random(len(reads)) < 0.01
+    reads[flip] = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, int(flip.sum()))]
+    return reads, offs
+
+
+@pytest.mark.parametrize("bpb,threads,nctx", [(1, 1, 1), (2, 4, 1), (16, 8, 1), (1, 3, 2)])
+def test_decode_file_equals_reads(setup, tmp_path, bpb, threads, nctx):
+    d, genome, ix = setup
+    ctxs = [nt.GpuContext(0) for _ in range(nctx)]
+    for c in ctxs:
+        c.upload(ix)
+    reads, offs = ragged(genome, 5 * 65536 + 321, 31)
+    path, ends = encoded_file(ctxs[0], tmp_path, reads, offs)
+    with open(tmp_path / "o.fa", "wb") as f:
+        st = nt.decode_file(ctxs, str(path), f.fileno(), threads=threads, blocks_per_batch=bpb)
+    exp = fasta_of(reads, offs)
+    assert (tmp_path / "o.fa").read_bytes() == exp
+    assert (st["reads"], st["bases"], st["blocks"], st["dropped_blocks"]) == (len(offs) - 1, len(reads), 6, 0)
+    assert st["bytes_out"] == len(exp)
+    for c in ctxs:
+        c.close()
+
+
+def test_decode_file_truncated_and_damaged_blocks(setup, tmp_path):
+    """A truncated tail ends the input (read_exact, main.rs:199); a damaged gzip member ends
+    the output after the blocks before it, without an error (main.rs:202)."""
+    d, genome, ix = setup
+    ctx = nt.GpuContext(0)
+    ctx.upload(ix)
+    reads, offs = ragged(genome, 4 * 65536 + 99, 32)
+    path, ends = encoded_file(ctx, tmp_path, reads, offs)
+    data = path.read_bytes()
+    cases = {"trunc": (data[:-7], 4), "header_only": (data[:32], 0), "empty": (b"", 0)}
+    bad = bytearray(data)
+    a = ends[1][0]  # block 2 starts here: corrupt its first stream's deflate data
+    bad[a + 32 + 12:a + 32 + 40] = b"\xff" * 28
+    cases["damaged"] = (bytes(bad), 2)
+    for name, (blob, keep) in cases.items():
+        for bpb in (1, 3):
+            p = tmp_path / f"{name}.dat"
+            p.write_bytes(blob)
+            with open(tmp_path / "o.fa", "wb") as f:
+                st = nt.decode_file([ctx], str(p), f.fileno(), threads=4, blocks_per_batch=bpb)
+            nr = ends[keep - 1][1] if keep else 0
+            assert (tmp_path / "o.fa").read_bytes() == fasta_of(reads, offs[:nr + 1]), (name, bpb)
+            assert st["blocks"] == keep and st["reads"] == nr, (name, bpb)
+            if name == "damaged":
+                assert st["dropped_blocks"] == 3 and "damaged" in st["error"]
+    ctx.close()
+
+
+def test_cli_decode_to_a_pipe(setup, tmp_path):
+    """stdout a pipe (not seekable): the writer falls back to write(2) in order."""
+    d, genome, ix = setup
+    ctx = nt.GpuContext(0)
+    ctx.upload(ix)
+    reads, offs = ragged(genome, 70_000, 33, 50, 3000)
+    path, _ = encoded_file(ctx, tmp_path, reads, offs)
+    ctx.close()
+    r = _cli("decode", "-i", str(d / "idx"), str(path), "--blocks-per-batch", "1", stdout=subprocess.PIPE)
+    assert r.stdout == fasta_of(reads, offs)
