@@ -51,13 +51,15 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
 
 /* Reads encoded.dat at in_path (mapped), writes FASTA to out_fd (not closed): ">seq.i\n"
  * + bases + "\n" per read, i from 1 across the file (main.rs:204).  opts->threads sizes the
- * inflate pool, opts->blocks_per_batch the GPU call (batch_bases and deflate_engine are
- * unused).  A truncated block ends the input like read_exact (main.rs:199); a damaged block
+ * inflate pool, opts->blocks_per_batch the GPU call (<= 0: 2; batch_bases and
+ * deflate_engine are unused).  A truncated block ends the input like read_exact (main.rs:199); a damaged block
  * (bad gzip member or stream sizes) ends the output after the blocks before it and still
  * returns NTC_OK, as decode_block's Err just ends the reference's loop (main.rs:202): the
  * caller sees it in stats->dropped_blocks (> 0) and stats->error.  stats: reads, bases,
  * blocks decoded, dropped_blocks = whole blocks not decoded, bytes_out = FASTA bytes,
- * parse_s = inflate CPU time summed over threads, gpu_s, write_s, wall_s.            */
+ * parse_s = inflate CPU time summed over threads, gpu_s, write_s, wall_s, alloc_s = block
+ * scan + pinned allocation seconds, first_batch_s / reader_done_s / gpu_done_s = when the
+ * first batch was written / the last block inflated / the last GPU call returned.            */
 int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int out_fd, const ntc_pipeline_opts *opts,
                     ntc_pipeline_stats *stats);
 

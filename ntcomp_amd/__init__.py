@@ -579,7 +579,7 @@ def encode_file(ctxs, in_path, out_fd, threads=0, blocks_per_batch=16, batch_bas
                          PipelineOpts(threads, blocks_per_batch, batch_bases, DEFLATE_ENGINES[deflate], 0))
 
 
-def decode_file(ctxs, in_path, out_fd, threads=0, blocks_per_batch=16):
+def decode_file(ctxs, in_path, out_fd, threads=0, blocks_per_batch=2):
     """`ntcomp decode` file to file (ntc_decode_file, include/ntcomp_pipeline.h): encoded.dat
     -> inflate + stream decode pool -> GPU inverse-SBWT walk + FASTA formatting on every
     context -> FASTA on out_fd.  Stats as a dict; a damaged block ends the output after the

@@ -216,7 +216,7 @@ def main(argv=None):
     d.add_argument("--gpus", type=int, default=1, help="GPUs to decode on (batches dealt round-robin).")
     d.add_argument("--devices", help="comma-separated device list, one context each; overrides --gpus")
     d.add_argument("--threads", type=int, default=0, help="block unzip / format threads (0: CPUs available)")
-    d.add_argument("--blocks-per-batch", type=int, default=16, help="blocks per GPU call")
+    d.add_argument("--blocks-per-batch", type=int, default=2, help="blocks per GPU call")
     d.add_argument("--stats", action="store_true", help="print per-stage seconds to stderr")
     args = ap.parse_args(argv)
     if getattr(args, "threads", None) == 0:

@@ -478,7 +478,9 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
     ntc_pipeline_opts o{};
     if (opts) o = *opts;
     const int T = o.threads > 0 ? o.threads : ntc_host_threads();
-    const uint64_t bpb = (uint64_t)(o.blocks_per_batch > 0 ? o.blocks_per_batch : 16);
+    // two blocks per GPU call: ~21 MB of text per batch keeps the pinned ring small and the
+    // writer (the bound: ~8 GB/s into one file's page cache) busy from the first 20 ms
+    const uint64_t bpb = (uint64_t)(o.blocks_per_batch > 0 ? o.blocks_per_batch : 2);
     ntc_pipeline_stats S{};
     const auto t0 = Clock::now();
 
@@ -529,7 +531,7 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
     uint64_t next_task = 0;       // next block to unzip
     uint64_t next_id = 1;         // main.rs:204: seq.{i+1}
     int64_t stop_batch = -1;      // batch holding the first damaged block (output ends in it)
-    std::atomic<double> t_unzip{0}, t_gpu{0}, t_write{0};
+    std::atomic<double> t_unzip{0}, t_gpu{0}, t_write{0}, t_pin{0};
     auto add_time = [](std::atomic<double> &a, double d) {
         double cur = a.load();
         while (!a.compare_exchange_weak(cur, cur + d)) {
@@ -539,6 +541,16 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
     // pinned buffers are sized per batch (grown in the claiming thread, outside the lock)
     auto ensure_pinned = [&](void **p, uint64_t *cap, uint64_t need) -> bool {
         if (need <= *cap) return true;
+        const auto tp = Clock::now();
+        struct Acc {
+            std::atomic<double> &a;
+            Clock::time_point t;
+            ~Acc() {
+                double cur = a.load(), d = secs(t, Clock::now());
+                while (!a.compare_exchange_weak(cur, cur + d)) {
+                }
+            }
+        } acc{t_pin, tp};
         if (*p) (void)hipHostFree(*p);
         *p = nullptr;
         *cap = 0;
@@ -618,6 +630,8 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
                     sl.n_bases += bases;
                 }
                 sl.finished++;
+                if (blk + 1 == blocks.size() || (stop_batch >= 0 && sl.finished == sl.n_blocks))
+                    S.reader_done_s = secs(t0, Clock::now());
                 sh.cv.notify_all();
             }
         });
@@ -731,6 +745,7 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
         if (!write_text(slp->text, slp->text_len)) sh.fail(NTC_ERR_IO, "write failed");
         add_time(t_write, secs(tw, Clock::now()));
         std::lock_guard<std::mutex> g(sh.mu);
+        if (b == 0) S.first_batch_s = secs(t0, Clock::now());
         S.reads += slp->n_reads;
         S.bases += slp->n_bases;
         S.bytes_out += slp->text_len;
@@ -754,6 +769,7 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
     if (data) munmap((void *)data, fsize);
     const int result = sh.error == -1 ? NTC_OK : sh.error;
     S.dropped_blocks = blocks.size() - S.blocks;  // after a damaged block (or none)
+    S.alloc_s += t_pin.load();
     S.parse_s = t_unzip.load();
     S.gpu_s = t_gpu.load();
     S.write_s = t_write.load();

@@ -116,8 +116,9 @@ def main():
                       "encoded_bytes": os.path.getsize(enc), "bits_per_base": round(8 * os.path.getsize(enc) / bases, 4),
                       "decode_s": round(td, 3), "decode_mbases_s": round(bases / td / 1e6, 1),
                       "gpus": a.gpus, "reps": a.reps,
-                      "pipeline_mbases_s": {"encode": round(bases / enc_stats["pipeline_wall_s"] / 1e6, 1)
-                                            if enc_stats and enc_stats.get("pipeline_wall_s") else None},
+                      "pipeline_mbases_s": {s: round(bases / st["pipeline_wall_s"] / 1e6, 1)
+                                            if st and st.get("pipeline_wall_s") else None
+                                            for s, st in (("encode", enc_stats), ("decode", dec_stats))},
                       "fixed_s": {"encode": round(t_fixed_enc, 3), "decode": round(t_fixed_dec, 3)},
                       "streaming_mbases_s": {"encode": round(bases / max(te - t_fixed_enc, 1e-9) / 1e6, 1),
                                              "decode": round(bases / max(td - t_fixed_dec, 1e-9) / 1e6, 1)},

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""ntc_encode_file timeline on a FASTQ (no CLI process around it): per-stage thread-seconds
-and when the reader / GPU finished, for sizing the host pipeline."""
+"""ntc_encode_file / ntc_decode_file timeline on the e2e_bench.py files (no CLI process
+around it): per-stage thread-seconds and when the reader / GPU finished, for sizing the host
+pipeline."""
 import argparse
 import json
 import os
@@ -18,6 +19,7 @@ def main():
     ap.add_argument("--bpb", type=int, nargs="+", default=[16])
     ap.add_argument("--threads", type=int, nargs="+", default=[0])
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--mode", default="encode", choices=["encode", "decode"])
     a = ap.parse_args()
     import ntcomp_amd as nt
     ix = nt.Index.load(os.path.join(a.dir, "idx"))
@@ -28,11 +30,17 @@ def main():
         for th in a.threads:
             for rep in range(a.reps):
                 t0 = time.time()
-                with open(os.path.join(a.dir, "pipe.dat"), "wb") as f:
-                    st = nt.encode_file([ctx], fq, f.fileno(), threads=th, blocks_per_batch=bpb, deflate=a.deflate)
+                if a.mode == "encode":
+                    with open(os.path.join(a.dir, "pipe.dat"), "wb") as f:
+                        st = nt.encode_file([ctx], fq, f.fileno(), threads=th, blocks_per_batch=bpb,
+                                            deflate=a.deflate)
+                else:
+                    with open(os.path.join(a.dir, "pipe.fa"), "wb") as f:
+                        st = nt.decode_file([ctx], os.path.join(a.dir, "enc.dat"), f.fileno(), threads=th,
+                                            blocks_per_batch=bpb)
                 w = time.time() - t0
                 st.pop("error")
-                print(json.dumps({"bpb": bpb, "threads": th, "rep": rep, "wall": round(w, 3),
+                print(json.dumps({"mode": a.mode, "bpb": bpb, "threads": th, "rep": rep, "wall": round(w, 3),
                                   "gbases_s": round(st["bases"] / w / 1e9, 3),
                                   **{k: (round(v, 3) if isinstance(v, float) else v) for k, v in st.items()}}),
                       flush=True)
