@@ -70,7 +70,9 @@ def parse_args(argv=None):
     ap.add_argument("--mode", choices=["encode", "decode"], default=None, help="(legacy) = --configs <mode>")
     ap.add_argument("--k", type=int, default=91)
     ap.add_argument("--reads-per-gpu", type=int, default=None, help="default 10M at N=1, 25M at N>1 (C91x8)")
-    ap.add_argument("--batch-reads", type=int, default=10_000_000, help="reads per device call")
+    ap.add_argument("--batch-reads", type=int, default=0,
+                    help="reads per device call (0: the rank's whole shard in one call; the library sizes "
+                         "its workspace by need)")
     ap.add_argument("--inflight", type=int, default=2,
                     help="device calls in flight per GPU: contexts on the rank's GPU (each with its own index "
                          "copy, stream and output buffers) take the calls in turn; a context is reused only after "
@@ -187,6 +189,18 @@ def roofline(kname, kernel_ms, kernel_ms_min, units, unit_name, pmc, pmc_note, w
     return r
 
 
+def _opt(ctx, key):
+    """a context option, None when the library predates it (A/B runs against older builds)"""
+    try:
+        return ctx.get_option(key)
+    except Exception:
+        return None
+
+
+def _gb(v):
+    return None if v is None else round(v / 1e9, 2)
+
+
 # ---- workload ----------------------------------------------------------------------
 def minimizer_order(nt, reads, n, L, threads):
     """(experiment) read order grouped by minimizer: smallest hashed 20-mer, strand as read"""
@@ -201,6 +215,7 @@ class Shard:
         import numpy as np
         self.L, self.n, self.first = L, n, first
         self.batches = []
+        batch = batch or n
         off = 0
         while off < n:
             nb = min(batch, n - off)
@@ -493,7 +508,7 @@ def main():
 
     genome = nt.synth_genome(1, args.genome_bp)
     base_cfg = {"k": k, "read_len": L, "genome_bp": args.genome_bp, "err_ppm": args.err_ppm,
-                "reads_per_gpu": n, "batch_reads": min(args.batch_reads, n)}
+                "reads_per_gpu": n, "batch_reads": min(args.batch_reads or n, n)}
 
     # ---- C91 encode / D91 decode -------------------------------------------------
     if "encode" in configs or "decode" in configs:
@@ -548,6 +563,8 @@ def main():
                 + (f"; {world} GPUs x {n} = {world * n} reads" if world > 1 else ""))
         cfg = dict(base_cfg, workload=wl_c, index_nodes=index.n, records_per_gpu=n_recs,
                    suffix_table_u=None if args.dry_run else ctx.get_option("tab_u"),
+                   workspace_gb_per_context=None if args.dry_run else _gb(_opt(ctx, "workspace_bytes")),
+                   spill_reruns=None if args.dry_run else _opt(ctx, "spill_reruns"),
                    parallelism=f"reads sharded over {world} GPU(s), index replicated, no collective",
                    inflight=len(ctxs) or None)
         if enc is not None:
@@ -637,7 +654,10 @@ def main():
             s["config"]["n_paths"] = ctx.get_option("n_paths")
             s["config"]["scan_filter"] = bool(ctx.get_option("filter"))
             s["config"]["joint_runs"] = bool(ctx.get_option("joint"))
+            s["config"]["entry_slots_per_read"] = 4 + (_opt(ctx, "ent_slots") or 0)
             el, kms = timed(Pipe(sctx, "encode"), sh, args.steps, args.warmup, barrier, sync, dist)
+            s["config"]["workspace_gb_per_context"] = _gb(_opt(ctx, "workspace_bytes"))
+            s["config"]["spill_reruns"] = _opt(ctx, "spill_reruns")
             b0 = sh.batches[0]
             kavg, kmin = launch_ms(kms, [b["n"] for b in sh.batches], b0["n"])
             s.update(value=round(sh.bases * world * args.steps / el / 1e6, 2), unit="Mbases/s",

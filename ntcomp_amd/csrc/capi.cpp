@@ -38,7 +38,7 @@ enum WsSlot {
     WS_D = 0, WS_S, WS_F, WS_R, WS_RECCOUNT, WS_SCANTMP, WS_TILEBASE, WS_TILEROWS,
     WS_STAGE_BASES, WS_STAGE_OFFS, WS_STAGE_RECS, WS_E, WS_DEC_A, WS_DEC_B, WS_DEC_C,
     WS_DEC_D, WS_Q, WS_E3, WS_NE, WS_COUNTER, WS_R2, WS_ED, WS_WAVECNT, WS_PACK_CHUNKS, WS_PACK_META,
-    WS_PACK_PAYLOAD, WS_FA_BASES, WS_FA_OFFS, WS_FA_SCAN, WS_COUNT
+    WS_PACK_PAYLOAD, WS_FA_BASES, WS_FA_OFFS, WS_FA_SCAN, WS_ES, WS_OBASE, WS_COUNT
 };
 
 struct ntc_ctx {
@@ -68,6 +68,18 @@ struct ntc_ctx {
     int last_variant = 0;
     int num_cus = 0;
     Enc4Args last4{};
+    // the last v4 encode's arguments: a call that ran out of an overflow pool is re-run
+    // with grown pools when its status is read (read_status)
+    struct {
+        const uint8_t *bases;
+        const uint64_t *offs;
+        uint64_t n_reads, total_bases, cap;
+        uint64_t *rec_out, *rec_offs;
+    } call4{};
+    uint32_t ent_slots_opt = 0;     // secondary entry slots per read (0: auto, 24 with joint runs, else 4)
+    double epool_per_read = 4.0;    // overflow pool sizes per read, raised to what calls needed
+    double rpool_per_read = 1.0;
+    uint64_t spill_reruns = 0;      // calls re-run with grown pools
     uint32_t tab_u_opt = 0;  // suffix-table depth for the next upload (0 = default_tab_u)
     int tab_u_fallback = 0;  // last upload: the default depth did not fit, U = 14 was used
     int pair_bytes_opt = 1;  // build the SCAN pair bytes at the next upload (0: bitmap tests, A/B)
@@ -86,7 +98,9 @@ struct ntc_ctx {
 
 namespace {
 
-constexpr uint64_t kCounterBytes = 8 * 64;  // work queue heads (kernels.hip WaveQueue: 8, 64 B apart)
+// work queue heads (kernels.hip WaveQueue: 8, 64 B apart), then the two pool counters
+// (kPoolCntE, kPoolCntR: words 64 and 72)
+constexpr uint64_t kCounterBytes = 8 * 64 + 2 * 64;
 
 
 #define HIP_TRY(ctx, expr)                                                                   \
@@ -158,6 +172,17 @@ int alloc_scratch(ntc_ctx *ctx, uint64_t n_reads, uint64_t total_rows, EncodeArg
     return NTC_OK;
 }
 
+// overflow pool indices are 32-bit (MsLaneT::ob, rbase)
+constexpr uint64_t kPoolMax = 0xFFFFFFF0ull;
+
+uint32_t ent_slots(const ntc_ctx *ctx) {
+    if (ctx->ent_slots_opt) return ctx->ent_slots_opt;
+    // entries per read past the dense 4 (tests/emu NTC_EMU_SPILL, 1 % errors): random genome
+    // k = 91 reads rarely spill (6 %, 0.07 % past 8); a strain collection with joint runs
+    // spills on 98 % of reads, 1 % past 28
+    return ctx->has_index && ctx->dix.joint ? 24u : 4u;
+}
+
 // v4: pack -> persistent MS -> parse -> scan -> emit, all in position space.
 // total_bases = offs[n] - offs[0] (known to the caller).
 int encode4_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, uint64_t n_reads,
@@ -170,16 +195,31 @@ int encode4_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, u
     a.status = ctx->d_status;
     void *p;
     int rc;
+    ctx->call4 = {d_bases, d_offs, n_reads, total_bases, cap, d_rec_out, d_rec_offs};
+    // Workspace by need: per read, 4 dense + S secondary entry slots, 8 dense record slots;
+    // the rest of a read's entries / records go to overflow pools sized from what earlier
+    // calls reserved (a call that runs out is re-run with the pools grown, read_status).
+    const uint32_t S = ent_slots(ctx);
+    const uint64_t pcap = std::min<uint64_t>((uint64_t)(ctx->epool_per_read * (double)n_reads) + 4096, kPoolMax);
+    const uint64_t rcap = std::min<uint64_t>((uint64_t)(ctx->rpool_per_read * (double)n_reads) + 4096, kPoolMax);
     if ((rc = ensure(ctx, WS_Q, (total_bases / 32 + 4) * 8, &p))) return rc;
     a.Q = (uint64_t *)p;
-    if ((rc = ensure(ctx, WS_E3, (total_bases + 1) * sizeof(Entry), &p))) return rc;
-    a.E = (Entry *)p;
+    if ((rc = ensure(ctx, WS_ES, (n_reads + 1) * S * sizeof(Entry), &p))) return rc;
+    a.Es = (Entry *)p;
+    a.S = S;
+    if ((rc = ensure(ctx, WS_E3, pcap * sizeof(Entry), &p))) return rc;
+    a.Ep = (Entry *)p;
+    a.pcap = pcap;
+    if ((rc = ensure(ctx, WS_OBASE, (n_reads + 1) * 8, &p))) return rc;
+    a.obase = (uint32_t *)p;
+    a.rbase = a.obase + (n_reads + 1);
     if ((rc = ensure(ctx, WS_ED, (n_reads + 1) * kEntSlot * sizeof(Entry), &p))) return rc;
     a.Ed = (Entry *)p;
     if ((rc = ensure(ctx, WS_NE, (n_reads + 1) * 4, &p))) return rc;
     a.ne = (uint32_t *)p;
-    if ((rc = ensure(ctx, WS_R, (total_bases + 1) * 8, &p))) return rc;
+    if ((rc = ensure(ctx, WS_R, rcap * 8, &p))) return rc;
     a.R = (uint64_t *)p;
+    a.rcap = rcap;
     if ((rc = ensure(ctx, WS_R2, (n_reads + 1) * kRecSlot * 8, &p))) return rc;
     a.R2 = (uint64_t *)p;
     if ((rc = ensure(ctx, WS_RECCOUNT, (n_reads + 1) * 4, &p))) return rc;
@@ -270,26 +310,54 @@ int encode_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, ui
     return NTC_OK;
 }
 
+// A v4 encode that ran out of an overflow pool (status kStatusRegrow): the pool counters
+// hold what every read reserved, so the pools grow to that (plus a quarter, remembered per
+// read for later calls) and the call runs again on the same inputs.
+int regrow_and_rerun(ntc_ctx *ctx) {
+    uint64_t cnt[2] = {0, 0};
+    HIP_TRY(ctx, hipMemcpy(&cnt[0], ctx->last4.counter + kPoolCntE, 8, hipMemcpyDeviceToHost));
+    HIP_TRY(ctx, hipMemcpy(&cnt[1], ctx->last4.counter + kPoolCntR, 8, hipMemcpyDeviceToHost));
+    const double n = (double)(ctx->call4.n_reads ? ctx->call4.n_reads : 1);
+    if (cnt[0] > ctx->last4.pcap) ctx->epool_per_read = std::max(ctx->epool_per_read, 1.25 * (double)cnt[0] / n);
+    if (cnt[1] > ctx->last4.rcap) ctx->rpool_per_read = std::max(ctx->rpool_per_read, 1.25 * (double)cnt[1] / n);
+    if ((cnt[0] > kPoolMax || cnt[1] > kPoolMax))
+        return set_err(ctx, NTC_ERR_CAPACITY, "entry / record overflow past 2^32 slots: split the batch");
+    ctx->spill_reruns++;
+    const auto &c = ctx->call4;
+    return encode4_impl(ctx, c.bases, c.offs, c.n_reads, c.total_bases, c.rec_out, c.cap, c.rec_offs);
+}
+
 int read_status(ntc_ctx *ctx, int64_t *bad_index) {
-    unsigned long long st = 0;
-    if (ctx->box_valid) {  // the call's mailbox (k_status_box): one stream sync
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-        st = ((volatile uint64_t *)ctx->h_box)[0];
-    } else {
-        HIP_TRY(ctx, hipMemcpyAsync(&st, ctx->d_status, 8, hipMemcpyDeviceToHost, ctx->stream));
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    for (int attempt = 0;; attempt++) {
+        unsigned long long st = 0;
+        if (ctx->box_valid) {  // the call's mailbox (k_status_box): one stream sync
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            st = ((volatile uint64_t *)ctx->h_box)[0];
+        } else {
+            HIP_TRY(ctx, hipMemcpyAsync(&st, ctx->d_status, 8, hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        }
+        if (st == ~0ULL) {
+            if (bad_index) *bad_index = -1;
+            return NTC_OK;
+        }
+        if (st == kStatusRegrow) {
+            if (ctx->last == kEncode && ctx->last_variant == 4 && attempt < 2) {
+                const int rc = regrow_and_rerun(ctx);
+                if (rc) return rc;
+                continue;
+            }
+            if (bad_index) *bad_index = -1;
+            return set_err(ctx, NTC_ERR_CAPACITY, "entry / record overflow pool exhausted after re-runs");
+        }
+        int code = (int)(st & 0xFF);
+        int64_t idx = (int64_t)(st >> 8);
+        if (bad_index) *bad_index = idx;
+        char buf[160];
+        std::snprintf(buf, sizeof(buf), "%s at index %lld", status_name(code), (long long)idx);
+        ctx->err = buf;
+        return code;
     }
-    if (st == ~0ULL) {
-        if (bad_index) *bad_index = -1;
-        return NTC_OK;
-    }
-    int code = (int)(st & 0xFF);
-    int64_t idx = (int64_t)(st >> 8);
-    if (bad_index) *bad_index = idx;
-    char buf[160];
-    std::snprintf(buf, sizeof(buf), "%s at index %lld", status_name(code), (long long)idx);
-    ctx->err = buf;
-    return code;
 }
 
 
@@ -747,6 +815,17 @@ int ntc_ctx_set_option(ntc_ctx *ctx, const char *key, int64_t value) {
         ctx->max_pass_bases = (uint64_t)value;
         return NTC_OK;
     }
+    if (std::strcmp(key, "ent_slots") == 0) {  // secondary entry slots per read (0: auto)
+        if (value < 0 || value > 1024 || (value & 3))
+            return set_err(ctx, NTC_ERR_INVALID_ARG, "ent_slots must be 0 (auto) or a multiple of 4 up to 1024");
+        ctx->ent_slots_opt = (uint32_t)value;
+        return NTC_OK;
+    }
+    if (std::strcmp(key, "pool_per_read") == 0) {  // test hook: overflow pools per read (entries, records)
+        if (value < 0) return set_err(ctx, NTC_ERR_INVALID_ARG, "pool_per_read must be >= 0");
+        ctx->epool_per_read = ctx->rpool_per_read = (double)value;
+        return NTC_OK;
+    }
     if (std::strcmp(key, "encode_variant") == 0) {
         if (value != 1 && value != 4)
             return set_err(ctx, NTC_ERR_INVALID_ARG, "encode_variant must be 4 (default) or 1 (A/B baseline)");
@@ -787,6 +866,13 @@ int ntc_ctx_get_option(const ntc_ctx *ctx, const char *key, int64_t *value) {
     else if (std::strcmp(key, "upload_total_us") == 0) *value = ctx->upload_total_us;
     else if (std::strcmp(key, "tab_u_fallback") == 0) *value = ctx->tab_u_fallback;
     else if (std::strcmp(key, "pack_us") == 0) *value = (int64_t)(ctx->last_pack_ms * 1000.0);
+    else if (std::strcmp(key, "ent_slots") == 0) *value = ent_slots(ctx);
+    else if (std::strcmp(key, "spill_reruns") == 0) *value = (int64_t)ctx->spill_reruns;
+    else if (std::strcmp(key, "workspace_bytes") == 0) {  // device workspace held now (all slots)
+        uint64_t t = 0;
+        for (const auto &b : ctx->ws) t += b.bytes;
+        *value = (int64_t)t;
+    }
     else return NTC_ERR_INVALID_ARG;
     return NTC_OK;
 }

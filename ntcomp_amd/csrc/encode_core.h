@@ -741,17 +741,24 @@ NTC_HD Entry load_entry(const Entry *E, int32_t i) {
 // Entry j of a read: j < kEntSlot in the dense slots Ed[j * es] (the kernels keep each read's
 // first entries together, Ed = base + read id * kEntSlot, es = 1: k_ms4 writes them as one
 // 64-byte group when the read ends, MsLane::finish, and the parse finds a read's first
-// entries in one line), later ones at E[j] (position space).  Ed = E is the plain
-// contiguous layout.
+// entries in one line); the next S in the read's secondary slots, E[j] (E = the read's
+// S-entry slot - kEntSlot); any later ones in the overflow pool, E2[j] (E2 = the read's
+// reservation - kEntSlot - S, MsLaneT::reserve).  Ed = E with S = kNoLimit is the plain
+// contiguous layout.  Every slot is sized by need: S per read from the index kind, the pool
+// from what earlier calls used (grown and re-run when a call runs out, capi.cpp).
 constexpr uint32_t kEntSlot = 4;
-NTC_HD const Entry *ent_ptr(const Entry *E, const Entry *Ed, uint64_t es, uint32_t j) {
-    return j < kEntSlot ? Ed + (uint64_t)j * es : E + j;
+constexpr uint32_t kNoLimit = 0xFFFFFFFFu;
+NTC_HD const Entry *ent_ptr(const Entry *E, const Entry *Ed, uint64_t es, uint32_t j, const Entry *E2 = nullptr,
+                            uint32_t S = kNoLimit) {
+    return j < kEntSlot ? Ed + (uint64_t)j * es : (j - kEntSlot < S ? E + j : E2 + j);
 }
 
 // Right-to-left reader of one read's entries (+ suffix table for uncovered positions).
 struct EntryView {
     const Entry *E;
     const Entry *Ed;  // dense slots (see ent_ptr)
+    const Entry *E2;  // overflow reservation (see ent_ptr)
+    uint32_t S;
     uint64_t es;
     const DevIndex *ix;
     const uint64_t *Q;
@@ -764,8 +771,10 @@ struct EntryView {
     Entry c0{0, 0, 0, 0}, c1{0, 0, 0, 0}, c2{0, 0, 0, 0}, c3{0, 0, 0, 0};
     bool dc = false;
     NTC_HD EntryView(const Entry *E_, const DevIndex *ix_, const uint64_t *Q_, uint64_t qo_, uint32_t k_, int32_t e_,
-                     const Entry *Ed_ = nullptr, uint64_t es_ = 1, const Entry *pre = nullptr)
-        : E(E_), Ed(Ed_ ? Ed_ : E_), es(Ed_ ? es_ : 1), ix(ix_), Q(Q_), qo(qo_), k(k_), e(e_), cur{0, 0, 0, 0} {
+                     const Entry *Ed_ = nullptr, uint64_t es_ = 1, const Entry *pre = nullptr,
+                     const Entry *E2_ = nullptr, uint32_t S_ = kNoLimit)
+        : E(E_), Ed(Ed_ ? Ed_ : E_), E2(E2_), S(S_), es(Ed_ ? es_ : 1), ix(ix_), Q(Q_), qo(qo_), k(k_), e(e_),
+          cur{0, 0, 0, 0} {
         if (pre) {
             c0 = pre[0];
             c1 = pre[1];
@@ -783,7 +792,7 @@ struct EntryView {
             p = i == 3 ? c3.p : p; v = i == 3 ? c3.v : v; m = i == 3 ? c3.m : m; dk = i == 3 ? c3.dk : dk;
             return Entry{p, v, m, dk};
         }
-        return load_entry(ent_ptr(E, Ed, es, (uint32_t)i), 0);
+        return load_entry(ent_ptr(E, Ed, es, (uint32_t)i, E2, S), 0);
     }
     NTC_HD void seek(uint32_t x) {  // last entry with p <= x, or entry 0
         if (e <= 0 || cur.p <= x) return;
@@ -933,16 +942,25 @@ NTC_HD void store_entry(Entry *E, uint64_t i, uint32_t p, uint32_t v, uint32_t m
 #endif
 }
 
-// The batch's packed query stream and position-space entry array: the same for every lane,
-// so they are passed to each call (scalar registers) rather than held per lane.
+// The batch's packed query stream and entry slots: the same for every lane, so they are
+// passed to each call (scalar registers) rather than held per lane.
 struct MsBufs {
     const uint64_t *Q;
-    Entry *E;
+    Entry *Es;    // secondary slots: spilled entry s < S of read rid at Es[rid * S + s] (S % 4 == 0)
     Entry *Ed;    // dense entry slots (ent_ptr): entry j < kEntSlot of read rid at Ed[rid * ds + j * es]
     uint64_t es;
     uint4 *stage = nullptr;  // k_ms4: the block's LDS write-combining slots (MsLane::put_entry)
     uint64_t ds = 1;
+    uint32_t S = kNoLimit;   // secondary slots per read (kNoLimit: Es holds all of a read's spill)
+    Entry *Ep = nullptr;     // overflow pool: reservations of 4-entry groups (MsLaneT::reserve)
+    uint64_t pcap = 0;       // pool entries
+    unsigned long long *pcnt = nullptr;  // pool entries reserved (zeroed per call)
+    uint32_t *obase = nullptr;           // each overflowing read's reservation start
+    unsigned long long *status = nullptr;
 };
+// The call ran out of an overflow pool: status 0 (below every read's (read << 8 | code)), the
+// parse and emit skip, and the host grows the pool to the reserved total and runs it again.
+constexpr unsigned long long kStatusRegrow = 0;
 #ifndef NTC_ECOMB
 #define NTC_ECOMB 1  // combine a read's spilled entries into 64-byte groups in LDS before storing
 #endif
@@ -964,6 +982,7 @@ struct MsLaneT {
     uint32_t qb;
     uint32_t len, p, d, l, r, j, ne, mode, hi, lo, l1, r1, bl, bR;
     uint32_t gj, ge;    // last run break: at position ge, node before it at path position gj (ge = 0: none)
+    uint32_t ob;        // overflow reservation of this read (kNoLimit: none, or the pool ran out)
     uint32_t vfy;       // the next run first verifies the vfy characters ending at node j
     // Joint run (note_single): path position of the interval's last node, else 0xFFFFFFFF.
     // It lives in l1, which only the binary-search probes use (written before read in
@@ -981,6 +1000,7 @@ struct MsLaneT {
         mode = kModeFirst; lo = r1 = bl = bR = 0;
         hi = kScanW;  // SCAN width cap (hi is free while scanning)
         gj = ge = vfy = 0;
+        ob = kNoLimit;
         jy() = 0xFFFFFFFFu;
         try_run = false;
     }
@@ -995,13 +1015,43 @@ struct MsLaneT {
     NTC_HD uint64_t key_at(uint32_t x, uint32_t U) const {  // U-mer ending at x (cached window)
         return (qw >> (2 * (x + 1 - U - qb))) & ((1ULL << (2 * U)) - 1);
     }
+    // Spilled entry s (entry kEntSlot + s): secondary slot s < S, else the overflow
+    // reservation (null when the pool ran out: the call is re-run, nothing is read back).
+    NTC_HD Entry *spill_at(const MsBufs &b, uint32_t s) const {
+        if (s < b.S) return b.Es + rid * (uint64_t)b.S + s;
+        return ob == kNoLimit ? nullptr : b.Ep + ob + (s - b.S);
+    }
+    // First overflow entry, at position p_: the read has at most len - p_ entries from here
+    // (each starts at its own position), reserved in 4-entry groups so that the 64-byte
+    // write groups stay aligned.
+    NTC_HD void reserve(const MsBufs &b, uint32_t p_) {
+        const uint64_t need = (uint64_t)((len - p_ + 3u) & ~3u);
+#ifdef __HIP_DEVICE_COMPILE__
+        const uint64_t at = atomicAdd(b.pcnt, (unsigned long long)need);
+#else
+        const uint64_t at = *b.pcnt;
+        *b.pcnt += need;
+#endif
+        if (at + need <= b.pcap) {
+            ob = (uint32_t)at;
+            b.obase[rid] = ob;
+        } else {
+            ob = kNoLimit;
+#ifdef __HIP_DEVICE_COMPILE__
+            atomicMin(b.status, kStatusRegrow);
+#else
+            *b.status = kStatusRegrow;
+#endif
+        }
+    }
     NTC_HD void put_entry(const MsBufs &b, uint32_t p_, uint32_t v, uint32_t m, uint32_t dk) {
+        if (ne >= kEntSlot && ne - kEntSlot == b.S) reserve(b, p_);
 #if defined(__HIP_DEVICE_COMPILE__) && NTC_ECOMB
-        // Spilled entries of one read are consecutive 16 B slots E[qo + ne], written one per
-        // lane iteration; stored one by one, each became its own 32 B partial write request
-        // past L2 (S91: 60 per read, 38 % of k_ms4's requests).  They are collected per
-        // aligned 64-byte group in LDS and stored together, so L2 sends one 64 B request.
-        // The dense slots of a read are one 64-byte group too (k_ms4 lays them out read-major,
+        // Spilled entries of one read are consecutive 16 B slots, written one per lane
+        // iteration; stored one by one, each became its own 32 B partial write request past
+        // L2 (S91: 60 per read, 38 % of k_ms4's requests).  They are collected per aligned
+        // 64-byte group in LDS and stored together, so L2 sends one 64 B request.  The dense
+        // slots of a read are one 64-byte group too (k_ms4 lays them out read-major,
         // Ed[rid * kEntSlot + j]): staged until the read ends, or until its first spilled
         // entry, when entries 1..3 go out and entry 0 moves to slot kStageSlots to wait for
         // the count (finish).
@@ -1021,28 +1071,30 @@ struct MsLaneT {
             }
             b.stage[kStageSlots * 256 + t] = b.stage[t];
         }
-        const uint64_t at = qo + ne;
-        b.stage[(uint32_t)(at & (kStageSlots - 1)) * 256 + t] = make_uint4(p_, v, m, dk);
+        const uint32_t s = ne - kEntSlot;
+        b.stage[(s & (kStageSlots - 1)) * 256 + t] = make_uint4(p_, v, m, dk);
         ne++;
-        if ((at & (kStageSlots - 1)) == kStageSlots - 1) flush_stage(b);
+        if ((s & (kStageSlots - 1)) == kStageSlots - 1) flush_stage(b);
         return;
 #endif
-        store_entry(ne < kEntSlot ? b.Ed + rid * b.ds : b.E + qo, ne < kEntSlot ? (uint64_t)ne * b.es : ne, p_, v, m, dk);
+        Entry *dst = ne < kEntSlot ? b.Ed + rid * b.ds : spill_at(b, ne - kEntSlot);
+        if (dst) store_entry(dst, ne < kEntSlot ? (uint64_t)ne * b.es : 0, p_, v, m, dk);
         ne++;
     }
-    // the staged entries of the group holding entry ne - 1 (at the end of a group or of the read)
+    // the staged entries of the group holding entry ne - 1 (at the end of a group or of the
+    // read); groups start at spilled entry 0, S and the reservation start, all multiples of 4
     NTC_HD void flush_stage(const MsBufs &b) {
 #if defined(__HIP_DEVICE_COMPILE__) && NTC_ECOMB
         if (ne <= kEntSlot) return;
-        const uint64_t last = qo + ne - 1, first = qo + kEntSlot;
-        const uint64_t g = last & ~(uint64_t)(kStageSlots - 1);
+        const uint32_t last = ne - 1 - kEntSlot, g = last & ~(kStageSlots - 1);
+        Entry *dst = spill_at(b, g);
+        if (!dst) return;
         const uint32_t t = threadIdx.x;
 #pragma unroll
         for (uint32_t i = 0; i < kStageSlots; i++) {
-            const uint64_t at = g + i;
-            if (at >= first && at <= last) {
+            if (g + i <= last) {
                 const uint4 x = b.stage[i * 256 + t];
-                store_entry(b.E, at, x.x, x.y, x.z, x.w);
+                store_entry(dst, i, x.x, x.y, x.z, x.w);
             }
         }
 #else
@@ -1699,8 +1751,9 @@ using MsLane = MsLaneT<true>;
 
 // (d, S) of every position of one read (diagnostics: ntc_debug_matching_statistics)
 NTC_HD void read_ms(const DevIndex &ix, const uint64_t *Q, uint64_t qo, const Entry *E, uint32_t ne,
-                    uint32_t len, uint32_t *d_out, uint32_t *s_out, const Entry *Ed = nullptr, uint64_t es = 1) {
-    EntryView ev(E, &ix, Q, qo, ix.k, -1, Ed, es);
+                    uint32_t len, uint32_t *d_out, uint32_t *s_out, const Entry *Ed = nullptr, uint64_t es = 1,
+                    const Entry *E2 = nullptr, uint32_t S = kNoLimit) {
+    EntryView ev(E, &ix, Q, qo, ix.k, -1, Ed, es, nullptr, E2, S);
     uint32_t x = 0;
     for (uint32_t i = 0; i <= ne && x < len; i++) {
         const Entry en = i < ne ? ev.at((int32_t)i) : Entry{0, 0, 0, 0};
@@ -1716,15 +1769,28 @@ NTC_HD void read_ms(const DevIndex &ix, const uint64_t *Q, uint64_t qo, const En
 
 constexpr uint32_t kRecSlot = 8;  // records per read in the dense slot; more spill
 
+// Records past kRecSlot (k_parse4): a reservation in a pool sized by need, like the entries'
+// (MsLaneT::reserve); the host re-runs a call that ran out of it.
+struct RecPool {
+    uint64_t *pool;
+    uint64_t cap;
+    unsigned long long *cnt;
+    uint32_t *rbase;  // each overflowing read's reservation start
+    unsigned long long *status;
+    uint64_t rid;
+};
+
 // greedy right-to-left parse over the entries, lib.rs:175-218 (+ encode.rs:144-158).
-// Record j goes to slot[j * sstride] (j < kRecSlot) or spill[j].  The kernel interleaves
-// the reads' slots (sstride = reads in the batch): the loop runs in lock step over a
-// wave's lanes, so the lanes' j-th records are one coalesced store.
+// Record j goes to slot[j * sstride] (j < kRecSlot) or spill[j] (rp: spill is reserved at
+// record kRecSlot, null when the pool ran out).  The kernel interleaves the reads' slots
+// (sstride = reads in the batch): the loop runs in lock step over a wave's lanes, so the
+// lanes' j-th records are one coalesced store.
 NTC_HD int parse_read(const DevIndex &ix, const uint64_t *Q, uint64_t qo, const Entry *E, uint32_t ne,
                       uint32_t len, uint64_t *slot, uint64_t *spill, uint64_t sstride = 1,
-                      const Entry *Ed = nullptr, uint64_t es = 1, const Entry *pre = nullptr) {
+                      const Entry *Ed = nullptr, uint64_t es = 1, const Entry *pre = nullptr,
+                      const Entry *E2 = nullptr, uint32_t S = kNoLimit, const RecPool *rp = nullptr) {
     const uint32_t k = ix.k;
-    EntryView ev(E, &ix, Q, qo, k, (int32_t)ne - 1, Ed, es, pre);
+    EntryView ev(E, &ix, Q, qo, k, (int32_t)ne - 1, Ed, es, pre, E2, S);
     uint32_t i = len;
     int nrec = 0;
     while (i > 0) {
@@ -1766,8 +1832,32 @@ NTC_HD int parse_read(const DevIndex &ix, const uint64_t *Q, uint64_t qo, const 
             const uint64_t bits = window2(Q, qo + segend - seglen);
             w = (bits & ((1ULL << (2 * seglen)) - 1)) | ((uint64_t)((first + 2) | (seglen << 2)) << 56);
         }
-        if (nrec < (int)kRecSlot) slot[(uint64_t)nrec * sstride] = w;
-        else spill[nrec] = w;
+        if (nrec < (int)kRecSlot) {
+            slot[(uint64_t)nrec * sstride] = w;
+        } else {
+            if (rp && nrec == (int)kRecSlot) {
+                // this record and at most one per position left of i (each starts one further left)
+                const uint64_t need = 1 + (uint64_t)i;
+#ifdef __HIP_DEVICE_COMPILE__
+                const uint64_t at = atomicAdd(rp->cnt, (unsigned long long)need);
+#else
+                const uint64_t at = *rp->cnt;
+                *rp->cnt += need;
+#endif
+                if (at + need <= rp->cap) {
+                    rp->rbase[rp->rid] = (uint32_t)at;
+                    spill = rp->pool + at - kRecSlot;
+                } else {
+                    spill = nullptr;
+#ifdef __HIP_DEVICE_COMPILE__
+                    atomicMin(rp->status, kStatusRegrow);
+#else
+                    *rp->status = kStatusRegrow;
+#endif
+                }
+            }
+            if (spill) spill[nrec] = w;
+        }
         nrec++;
         if (i > 0) i -= 1;
         else break;

@@ -29,16 +29,26 @@ struct Enc4Args {
     const uint64_t *offs;        // [n_reads+1], absolute into bases
     uint64_t n_reads;
     uint64_t *Q;                 // packed bases, position space (2 bits, 32 per word)
-    Entry *E;                    // entries past kEntSlot, position space
+    Entry *Es;                   // the next S entries of each read (secondary slots, ent_ptr)
+    uint32_t S;                  // secondary slots per read (multiple of 4)
+    Entry *Ep;                   // overflow pool of entries (reservations, MsLaneT::reserve)
+    uint64_t pcap;               // its entries (< 2^32)
+    uint32_t *obase;             // each overflowing read's entry reservation
     Entry *Ed;                   // first kEntSlot entries of each read (dense slots, ent_ptr)
     uint32_t *ne;                // entries per read
-    uint64_t *R;                 // records past kRecSlot, position space
+    uint64_t *R;                 // records past kRecSlot: reservations (parse_read's RecPool)
+    uint64_t rcap;               // its records (< 2^32)
+    uint32_t *rbase;             // each overflowing read's record reservation
     uint64_t *R2;                // first kRecSlot records of each read (dense slots)
     uint32_t *rec_count;
     uint32_t *wave_cnt;          // records of each wave's 64 reads (k_parse4 -> scan -> k_emit4)
     unsigned long long *status;
-    unsigned long long *counter; // work queue heads of k_ms4 (WaveQueue, zeroed per call)
+    unsigned long long *counter; // work queue heads of k_ms4 (WaveQueue, zeroed per call), then
+                                 // the entry and record pool counters (kPoolCounters)
 };
+// the pools' reservation counters: words 64 and 72 of the counter area (past the 8 queue
+// heads, 64 B apart), zeroed with them per call
+constexpr uint32_t kPoolCntE = 64, kPoolCntR = 72;
 
 struct EmitArgs {
     const uint64_t *R;           // [tile][j][lane]

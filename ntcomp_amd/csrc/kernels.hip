@@ -267,12 +267,15 @@ __device__ __forceinline__ uint32_t parse_one(const Enc4Args &a, uint64_t r) {
     for (uint32_t j = 0; j < kEntSlot; j++) pre[j] = load_entry(a.Ed + r * kEntSlot, (int32_t)j);
     const uint32_t c0 = entry0_count(pre[0]);
     const uint32_t ne = c0 == kNeInE0 ? a.ne[r] : c0;
-    const int rc = parse_read(a.ix, a.Q, P, a.E + P, ne, (uint32_t)(e - b), a.R2 + r, a.R + P, a.n_reads,
-                              a.Ed + r * kEntSlot, 1, pre);
 #else
-    const int rc = parse_read(a.ix, a.Q, P, a.E + P, read_entry_count(a, r), (uint32_t)(e - b), a.R2 + r, a.R + P, a.n_reads,
-                              a.Ed + r * kEntSlot, 1);
+    const uint32_t ne = read_entry_count(a, r);
+    const Entry *pre = nullptr;
 #endif
+    const RecPool rp{a.R, a.rcap, a.counter + kPoolCntR, a.rbase, a.status, r};
+    const Entry *E1 = a.Es + r * a.S - kEntSlot;
+    const Entry *E2 = ne > kEntSlot + a.S ? a.Ep + a.obase[r] - kEntSlot - a.S : nullptr;
+    const int rc = parse_read(a.ix, a.Q, P, E1, ne, (uint32_t)(e - b), a.R2 + r, nullptr, a.n_reads,
+                              a.Ed + r * kEntSlot, 1, pre, E2, a.S, &rp);
     if (rc < 0) {
         atomicMin(a.status, (unsigned long long)((r << 8) | (uint64_t)(-rc)));
         a.rec_count[r] = 0;
@@ -295,7 +298,8 @@ __global__ __launch_bounds__(256, NTC_MS_WAVES) void k_ms4(Enc4Args a) {
     uint64_t rd = 0;
     const WaveQueue wq(a.counter, a.n_reads);
     __shared__ uint4 s_stage[(kStageSlots + 1) * 256];  // MsLane::put_entry write combining, entry 0
-    const MsBufs bufs{a.Q, a.E, a.Ed, 1, s_stage, kEntSlot};  // dense slots read-major
+    // dense slots read-major, secondary slots and the overflow pool sized by need
+    const MsBufs bufs{a.Q, a.Es, a.Ed, 1, s_stage, kEntSlot, a.S, a.Ep, a.pcap, a.counter + kPoolCntE, a.obase, a.status};
     MsLaneT<kJoint> st;
     for (;;) {
         // ---- hand idle lanes the next reads (wave-uniform control flow) ----------------
@@ -401,7 +405,7 @@ __global__ __launch_bounds__(256) void k_emit4(Enc4Args a, const uint64_t *wave_
             if (j < ns) dst[j] = early[j];
         for (uint32_t j = kEmitEarly; j < ns; j++) dst[j] = slot[(uint64_t)j * a.n_reads];
         if (cnt > kRecSlot) {
-            const uint64_t *spill = a.R + (a.offs[r] - a.offs[0]);
+            const uint64_t *spill = a.R + a.rbase[r] - kRecSlot;
             for (uint32_t j = kRecSlot; j < cnt; j++) dst[j] = spill[j];
         }
     }
@@ -422,7 +426,7 @@ __global__ __launch_bounds__(256) void k_emit4(Enc4Args a, const uint64_t *wave_
         if (j < ns) out[off + j] = early[j];
     for (uint32_t j = kEmitEarly; j < ns; j++) out[off + j] = slot[(uint64_t)j * a.n_reads];
     if (cnt > kRecSlot) {
-        const uint64_t *spill = a.R + (a.offs[r] - a.offs[0]);
+        const uint64_t *spill = a.R + a.rbase[r] - kRecSlot;
         for (uint32_t j = kRecSlot; j < cnt; j++) out[off + j] = spill[j];
     }
 }
@@ -904,7 +908,10 @@ __global__ __launch_bounds__(256) void k_debug_gather4(Enc4Args a, uint32_t *d_o
     if (r >= a.n_reads) return;
     const uint64_t o0 = a.offs[0], b = a.offs[r], e = a.offs[r + 1];
     const uint64_t P = b - o0;
-    read_ms(a.ix, a.Q, P, a.E + P, read_entry_count(a, r), (uint32_t)(e - b), d_out + P, s_out + P, a.Ed + r * kEntSlot, 1);
+    const uint32_t ne = read_entry_count(a, r);
+    const Entry *E2 = ne > kEntSlot + a.S ? a.Ep + a.obase[r] - kEntSlot - a.S : nullptr;
+    read_ms(a.ix, a.Q, P, a.Es + r * a.S - kEntSlot, ne, (uint32_t)(e - b), d_out + P, s_out + P, a.Ed + r * kEntSlot,
+            1, E2, a.S);
 }
 
 // two-character rank lines (encode_core.h Rank2Chunk): one thread per (block, c1) chunk

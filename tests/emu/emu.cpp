@@ -164,6 +164,11 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
     *bad = -1;
     uint64_t tiles = (n_reads + 63) / 64, total = 0;
     rec_offsets[0] = 0;
+    // NTC_EMU_SPILL=1: spill footprint of the v4 layout (entries past kEntSlot, records past
+    // kRecSlot) -> stderr, for sizing the spill pools
+    const bool spill_stats = getenv("NTC_EMU_SPILL") && atoi(getenv("NTC_EMU_SPILL"));
+    uint64_t sp_reads_e = 0, sp_ent = 0, sp_reads_r = 0, sp_rec = 0, sp_len_e = 0, sp_len_r = 0, sp_rem_e = 0;
+    uint64_t ne_hist[9] = {0};  // reads with ne > 4 + 4 * i
     for (uint64_t t = 0; t < tiles; t++) {
         uint64_t mx = 0;
         for (uint64_t r = t * 64; r < n_reads && r < t * 64 + 64; r++) mx = std::max(mx, offs[r + 1] - offs[r]);
@@ -184,7 +189,7 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
                 auto run = [&](auto &ms) {
                     trace_phase(0);
                     ms.start(d, 0, len);
-                    const MsBufs bufs{Q.data(), E4.data(), E4.data(), 1};
+                    const MsBufs bufs{Q.data(), E4.data() + kEntSlot, E4.data(), 1};  // contiguous: entry j at E4[j]
                     for (;;) {
                         int st = ms.step(d, bufs);
                         if (st < 0) { rc = st; break; }
@@ -203,6 +208,20 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
                 }
                 trace_phase(1);
                 if (rc == 0) rc = parse_read(d, Q.data(), 0, E4.data(), ne, len, R4.data(), R4.data());
+                if (spill_stats && rc >= 0) {
+                    for (int h = 0; h < 9; h++) ne_hist[h] += ne > kEntSlot + 4u * (uint32_t)h;
+                    if (ne > kEntSlot) {
+                        sp_reads_e++;
+                        sp_ent += ne - kEntSlot;
+                        sp_len_e += len;
+                        sp_rem_e += len - E4[kEntSlot].p;  // positions from the first spilled entry on
+                    }
+                    if ((uint32_t)rc > kRecSlot) {
+                        sp_reads_r++;
+                        sp_rec += (uint64_t)rc - kRecSlot;
+                        sp_len_r += len;
+                    }
+                }
                 trace_read_done();
                 if (d_out && rc >= 0)
                     read_ms(d, Q.data(), 0, E4.data(), ne, len, d_out + (offs[r] - offs[0]), s_out + (offs[r] - offs[0]));
@@ -233,6 +252,20 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
             rec_offsets[r + 1] = total;
         }
     }
+    if (spill_stats) {
+        fprintf(stderr, "ne > 4 + 4i, i = 0..8:");
+        for (int h = 0; h < 9; h++) fprintf(stderr, " %llu", (unsigned long long)ne_hist[h]);
+        fprintf(stderr, "\n");
+    }
+    if (spill_stats)
+        fprintf(stderr,
+                "{\"reads\": %llu, \"bases\": %llu, \"records\": %llu, \"spill_e_reads\": %llu, \"spill_entries\": %llu, "
+                "\"spill_e_len\": %llu, \"spill_e_rem\": %llu, \"spill_r_reads\": %llu, \"spill_records\": %llu, "
+                "\"spill_r_len\": %llu}\n",
+                (unsigned long long)n_reads, (unsigned long long)(offs[n_reads] - offs[0]), (unsigned long long)total,
+                (unsigned long long)sp_reads_e, (unsigned long long)sp_ent, (unsigned long long)sp_len_e,
+                (unsigned long long)sp_rem_e, (unsigned long long)sp_reads_r, (unsigned long long)sp_rec,
+                (unsigned long long)sp_len_r);
     return NTC_OK;
 }
 
@@ -350,7 +383,7 @@ extern "C" int emu_wave_modes(const ntc_index_view *v, const uint8_t *bases, con
             modes |= 1u << m;
             out[3 + m]++;
             out[2]++;
-            const MsBufs bufs{l.Q.data(), l.E.data(), l.E.data(), 1};
+            const MsBufs bufs{l.Q.data(), l.E.data() + kEntSlot, l.E.data(), 1};
             const int st = l.ms.step(d, bufs);
             if (st != 0) l.busy = false;
         }
