@@ -485,20 +485,26 @@ def main():
 
     ctxs = []
 
+    build_info = {}
+
     def setup_index(texts, label, n_ctx):
         nonlocal ctx
+        if not args.dry_run and ctx is None:
+            for _ in range(max(1, args.inflight)):
+                c = nt.GpuContext(device)
+                for kv in args.opt:
+                    key, val = kv.split("=")
+                    c.set_option(key, int(val))
+                ctxs.append(c)
+            ctx = ctxs[0]
         t0 = time.time()
-        index = nt.Index.build([t.tobytes() for t in texts], k, threads=nthreads)
-        log(f"[rank {rank}] {label} index k={k} n={index.n} built in {time.time() - t0:.1f}s")
+        seqs = [t.tobytes() for t in texts]
+        # the GPU builder (build.hip; equal to the host builder, tests/test_gpu_build.py), the
+        # host one for --dry-run
+        index = nt.Index.build(seqs, k, threads=nthreads) if args.dry_run else nt.Index.build_gpu(ctx, seqs, k)
+        build_info[label] = {"builder": "host" if args.dry_run else "gpu", "seconds": round(time.time() - t0, 3)}
+        log(f"[rank {rank}] {label} index k={k} n={index.n} built in {time.time() - t0:.1f}s ({build_info[label]['builder']})")
         if not args.dry_run:
-            if ctx is None:
-                for _ in range(max(1, args.inflight)):
-                    c = nt.GpuContext(device)
-                    for kv in args.opt:
-                        key, val = kv.split("=")
-                        c.set_option(key, int(val))
-                    ctxs.append(c)
-                ctx = ctxs[0]
             t0 = time.time()
             for c in ctxs[:n_ctx]:
                 c.upload(index)
@@ -565,6 +571,7 @@ def main():
                    suffix_table_u=None if args.dry_run else ctx.get_option("tab_u"),
                    workspace_gb_per_context=None if args.dry_run else _gb(_opt(ctx, "workspace_bytes")),
                    spill_reruns=None if args.dry_run else _opt(ctx, "spill_reruns"),
+                   index_build=build_info.get("C"),
                    parallelism=f"reads sharded over {world} GPU(s), index replicated, no collective",
                    inflight=len(ctxs) or None)
         if enc is not None:
@@ -655,6 +662,7 @@ def main():
             s["config"]["scan_filter"] = bool(ctx.get_option("filter"))
             s["config"]["joint_runs"] = bool(ctx.get_option("joint"))
             s["config"]["entry_slots_per_read"] = 4 + (_opt(ctx, "ent_slots") or 0)
+            s["config"]["index_build"] = build_info.get("S")
             el, kms = timed(Pipe(sctx, "encode"), sh, args.steps, args.warmup, barrier, sync, dist)
             s["config"]["workspace_gb_per_context"] = _gb(_opt(ctx, "workspace_bytes"))
             s["config"]["spill_reruns"] = _opt(ctx, "spill_reruns")

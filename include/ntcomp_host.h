@@ -30,6 +30,13 @@ typedef struct ntc_index_host ntc_index_host;
  * n_threads <= 0 picks the hardware concurrency.                                     */
 int ntc_build_index(const uint8_t *seqs, const uint64_t *seq_offsets, uint64_t n_seqs,
                     uint32_t k, int add_revcomp, int n_threads, ntc_index_host **out);
+/* The same index built on ctx's GPU (build.hip; also kbo::build's stand-in, main.rs:111-134):
+ * k-mers, radix sort, dummies, LCS and labels in HBM, then rows + LCS to the host.  Equal
+ * to ntc_build_index's output for every input.  Synchronous on ctx's stream; no index
+ * needs to be uploaded.  NTC_ERR_HIP when device memory runs out (~2 x 8 x W B per k-mer
+ * occurrence, W = ceil(2k / 64)).                                                     */
+int ntc_build_index_device(ntc_ctx *ctx, const uint8_t *seqs, const uint64_t *seq_offsets, uint64_t n_seqs,
+                           uint32_t k, int add_revcomp, ntc_index_host **out);
 void ntc_index_free(ntc_index_host *ix);
 /* Borrowed view (valid until ntc_index_free) for ntc_index_upload or inspection. */
 int ntc_index_view_of(const ntc_index_host *ix, ntc_index_view *view);

@@ -43,7 +43,7 @@ EXPORTED = [
     "ntc_deflate_block", "ntc_pack_blocks_device", "ntc_encode_pack_batch", "ntc_read_block_into",
     "ntc_fastx_open", "ntc_fastx_next_batch", "ntc_fastx_close", "ntc_fasta_format", "ntc_fastx_next_batch_into",
     "ntc_fastx_set_threads", "ntc_host_threads", "ntc_encode_file", "ntc_decode_fasta",
-    "ntc_decode_file",
+    "ntc_decode_file", "ntc_build_index_device",
 ]
 
 
@@ -146,6 +146,7 @@ def lib():
         "ntc_memcpy_d2h": (I, [P, P, P, u64]),
         "ntc_debug_matching_statistics": (I, [P, P, P, u64, P, P]),
         "ntc_build_index": (I, [P, P, u64, u32, I, I, ctypes.POINTER(P)]),
+        "ntc_build_index_device": (I, [P, P, P, u64, u32, I, ctypes.POINTER(P)]),
         "ntc_index_free": (None, [P]),
         "ntc_index_view_of": (I, [P, ctypes.POINTER(IndexView)]),
         "ntc_index_save": (I, [P, ctypes.c_char_p]),
@@ -216,6 +217,17 @@ class Index:
                                    ctypes.byref(h))
         if rc:
             raise NtcError(rc, "ntc_build_index")
+        return cls(h)
+
+    @classmethod
+    def build_gpu(cls, ctx, seqs, k, add_revcomp=True):
+        """The same index built on ctx's GPU (ntc_build_index_device, build.hip)."""
+        bases, offs = pack_reads(seqs)
+        h = ctypes.c_void_p()
+        rc = lib().ntc_build_index_device(ctx.h, _p(bases), _p(offs), len(offs) - 1, k, int(add_revcomp),
+                                          ctypes.byref(h))
+        if rc:
+            raise NtcError(rc, lib().ntc_last_error(ctx.h).decode(errors="replace"))
         return cls(h)
 
     @classmethod

@@ -88,7 +88,15 @@ def cmd_build(args):
             for i in range(len(offs) - 1):
                 seqs.append(bases[int(offs[i]):int(offs[i + 1])].tobytes())
         rd.close()
-    ix = nt.Index.build(seqs, args.kmer_size, add_revcomp=True, threads=args.num_threads)
+    if args.builder == "gpu":
+        # the same index built on the GPU (build.hip; tests/test_gpu_build.py: equal to the host build)
+        ctx = nt.GpuContext(args.device)
+        try:
+            ix = nt.Index.build_gpu(ctx, seqs, args.kmer_size, add_revcomp=True)
+        finally:
+            ctx.close()
+    else:
+        ix = nt.Index.build(seqs, args.kmer_size, add_revcomp=True, threads=args.num_threads)
     log(f"Serializing SBWT index to {args.output_prefix}.sbwt ...")
     log(f"Serializing LCS array to {args.output_prefix}.lcs ...")
     ix.save(args.output_prefix, layout=args.index_format)
@@ -192,6 +200,10 @@ def main(argv=None):
     b.add_argument("-m", "--mem-gb", type=int, default=4, help="Accepted for compatibility (unused).")
     b.add_argument("--temp-dir", help="Accepted for compatibility (unused; builds in memory).")
     b.add_argument("--verbose", action="store_true")
+    b.add_argument("--builder", choices=["host", "gpu"], default="host",
+                   help="host: threaded C++ builder; gpu: k-mer sort, dummies, LCS and labels on the GPU "
+                        "(same index)")
+    b.add_argument("--device", type=int, default=0, help="GPU for --builder gpu")
     b.add_argument("--index-format", choices=["own", "sbwt-rs"], default="own",
                    help="own layout (default) or a restatement of sbwt 0.3.11/kbo 0.5.1 files (parity unpinned); "
                         "encode/decode read either")

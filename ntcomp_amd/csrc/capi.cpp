@@ -1405,6 +1405,26 @@ int ntc_build_index(const uint8_t *seqs, const uint64_t *seq_offsets, uint64_t n
     return NTC_OK;
 }
 
+int ntc_build_index_device(ntc_ctx *ctx, const uint8_t *seqs, const uint64_t *seq_offsets, uint64_t n_seqs,
+                           uint32_t k, int add_revcomp, ntc_index_host **out) {
+    if (!ctx || !out || !seq_offsets || (n_seqs && !seqs)) return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument");
+    if (k < 1 || k > 255) return set_err(ctx, NTC_ERR_UNSUPPORTED, "k must be in [1, 255]");
+    *out = nullptr;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    for (uint64_t i = 0; i < n_seqs; i++)
+        if (seq_offsets[i + 1] < seq_offsets[i]) return set_err(ctx, NTC_ERR_INVALID_ARG, "sequence offsets decrease");
+    auto *h = new ntc_index_host();
+    std::string err;
+    if (!build_index_device(ctx->stream, seqs, seq_offsets, n_seqs, k, add_revcomp != 0, h->ix, err)) {
+        delete h;
+        return set_err(ctx, err.rfind("hip", 0) == 0 || err.find("allocation") != std::string::npos ? NTC_ERR_HIP
+                                                                                                      : NTC_ERR_FORMAT,
+                       "ntc_build_index_device: " + err);
+    }
+    *out = h;
+    return NTC_OK;
+}
+
 void ntc_index_free(ntc_index_host *ix) { delete ix; }
 
 int ntc_index_view_of(const ntc_index_host *ix, ntc_index_view *v) {

@@ -3,10 +3,16 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <string>
 
 #include "encode_core.h"
 
 namespace ntc {
+
+struct HostIndex;
+// GPU index build (build.hip): the host builder's index (sbwt_build.cpp), built on stream s
+bool build_index_device(hipStream_t s, const uint8_t *seqs, const uint64_t *offs, uint64_t n_seqs, uint32_t k,
+                        bool revcomp, HostIndex &out, std::string &err);
 
 struct EncodeArgs {
     DevIndex ix;

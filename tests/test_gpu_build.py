@@ -1,0 +1,80 @@
+"""GPU index build (ntc_build_index_device, build.hip) against the host builder
+(sbwt_build.cpp, the stand-in for kbo::build, src/main.rs:111-134): identical n, C, rows and
+LCS for every k-word width W = ceil(2k / 64) from 1 to 8, with non-ACGT bytes, lower case,
+sequences shorter than k, empty sequences, many short sequences and without reverse
+complements; an index built on the GPU encodes and decodes like the host-built one."""
+import numpy as np
+import pytest
+
+import ntcomp_amd as nt
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = nt.GpuContext(0)
+    yield c
+    c.close()
+
+
+def same(a, b):
+    assert (a.n, a.k) == (b.n, b.k)
+    assert list(a.C) == list(b.C)
+    assert np.array_equal(a.lcs, b.lcs)
+    for c in range(4):
+        assert np.array_equal(a.rows[c], b.rows[c]), c
+
+
+def messy_seqs(seed, n, lo, hi):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        L = int(rng.integers(lo, hi))
+        s = bytearray(rng.choice(list(b"ACGT"), L).astype(np.uint8).tobytes())
+        if L > 10 and i % 3 == 0:
+            s[int(rng.integers(0, L))] = ord("N")
+        if i % 5 == 0:
+            s = s.lower()
+        out.append(bytes(s))
+    return out + [b"", b"ACG", b"NNNNNNNN"]
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 5, 11, 31, 32, 33, 63, 64, 65, 91, 96, 97, 160, 255])
+def test_gpu_build_equals_host_build(ctx, k):
+    seqs = messy_seqs(k, 40, 1, 600)
+    same(nt.Index.build_gpu(ctx, seqs, k), nt.Index.build(seqs, k))
+    same(nt.Index.build_gpu(ctx, seqs, k, add_revcomp=False), nt.Index.build(seqs, k, add_revcomp=False))
+
+
+def test_gpu_build_genome_collection_and_reads(ctx):
+    genome = nt.synth_genome(5, 1_000_000)
+    strains = nt.synth_strains(genome, 3, 3, 10_000)
+    texts = [genome.tobytes()] + [strains[i].tobytes() for i in range(3)]
+    for k in (31, 91):
+        same(nt.Index.build_gpu(ctx, texts, k), nt.Index.build(texts, k))
+    reads = nt.synth_reads(genome, 3, 0, 20_000, 150, 10_000)
+    many = [reads[i * 150:(i + 1) * 150].tobytes() for i in range(20_000)]
+    same(nt.Index.build_gpu(ctx, many, 31), nt.Index.build(many, 31))
+
+
+def test_gpu_built_index_encodes_like_host_built(ctx):
+    genome = nt.synth_genome(6, 500_000)
+    ix = nt.Index.build_gpu(ctx, [genome.tobytes()], 91)
+    ref = nt.Index.build([genome.tobytes()], 91)
+    same(ix, ref)
+    ctx.upload(ix)
+    n, L = 20_000, 150
+    reads = nt.synth_reads(genome, 7, 0, n, L, 10_000)
+    offs = np.arange(0, n * L + 1, L, dtype=np.uint64)
+    recs, roff = ctx.encode(reads, offs)
+    out, o2 = ctx.decode(recs)
+    assert np.array_equal(out, reads)
+    from oracle_lib import OracleIndex
+    exp, _ = OracleIndex(ref.n, 91, ref.rows, ref.C, ref.lcs).encode(reads[:500 * L], offs[:501])
+    assert np.array_equal(recs[:len(exp)], exp)
+
+
+def test_gpu_build_empty_inputs(ctx):
+    for seqs in ([], [b""], [b"AC"], [b"NNNN"]):
+        same(nt.Index.build_gpu(ctx, seqs, 5), nt.Index.build(seqs, 5))
