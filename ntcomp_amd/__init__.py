@@ -95,14 +95,27 @@ _lib = None
 
 
 def device_source_hash():
-    """sha256 (16 hex) of the device code (kernels + lane functions): profiles/pmc_traffic.json
-    records it, and bench.py uses counter data only when it matches the build it times."""
+    """sha256 (16 hex) of the hot path's device code object -- the offload bundle of
+    kernels.hip (k_pack, k_ms4, k_parse4, k_emit4, k_dec_rec, ...) inside the library's
+    .hip_fatbin section: profiles/pmc_traffic.json records it, and bench.py uses counter data
+    only when it matches the build it times.  Host-only or comment edits leave it unchanged."""
     import hashlib
-    h = hashlib.sha256()
-    for name in ("kernels.hip", "kernels.h", "encode_core.h"):
-        with open(os.path.join(_HERE, "csrc", name), "rb") as f:
-            h.update(name.encode() + b"\0" + f.read())
-    return h.hexdigest()[:16]
+    import struct
+    with open(LIB_PATH, "rb") as f:
+        b = f.read()
+    shoff = struct.unpack_from("<Q", b, 0x28)[0]
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", b, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", b, shoff + i * shentsize) for i in range(shnum)]
+    stro = secs[shstrndx][4]
+    for sec in secs:
+        name = b[stro + sec[0]:b.index(b"\0", stro + sec[0])]
+        if name == b".hip_fatbin":
+            fat = b[sec[4]:sec[4] + sec[5]]
+            magic = b"__CLANG_OFFLOAD_BUNDLE__"
+            parts = [magic + x for x in fat.split(magic)[1:]]
+            hot = [x for x in parts if b"_ZN3ntc5k_ms4" in x]
+            return hashlib.sha256(b"".join(hot or parts)).hexdigest()[:16]
+    raise RuntimeError(f"{LIB_PATH}: no .hip_fatbin section")
 
 
 def build_library(force=False):

@@ -961,6 +961,15 @@ struct MsBufs {
 // The call ran out of an overflow pool: status 0 (below every read's (read << 8 | code)), the
 // parse and emit skip, and the host grows the pool to the reserved total and runs it again.
 constexpr unsigned long long kStatusRegrow = 0;
+// the host emulator's lane (tests/emu): its slot of the staging array, as threadIdx.x in k_ms4
+inline uint32_t ntc_host_lane = 0;
+NTC_HD uint32_t stage_lane() {
+#ifdef __HIP_DEVICE_COMPILE__
+    return threadIdx.x;
+#else
+    return ntc_host_lane;
+#endif
+}
 #ifndef NTC_ECOMB
 #define NTC_ECOMB 1  // combine a read's spilled entries into 64-byte groups in LDS before storing
 #endif
@@ -1046,7 +1055,7 @@ struct MsLaneT {
     }
     NTC_HD void put_entry(const MsBufs &b, uint32_t p_, uint32_t v, uint32_t m, uint32_t dk) {
         if (ne >= kEntSlot && ne - kEntSlot == b.S) reserve(b, p_);
-#if defined(__HIP_DEVICE_COMPILE__) && NTC_ECOMB
+#if NTC_ECOMB
         // Spilled entries of one read are consecutive 16 B slots, written one per lane
         // iteration; stored one by one, each became its own 32 B partial write request past
         // L2 (S91: 60 per read, 38 % of k_ms4's requests).  They are collected per aligned
@@ -1056,7 +1065,7 @@ struct MsLaneT {
         // entry, when entries 1..3 go out and entry 0 moves to slot kStageSlots to wait for
         // the count (finish).
         static_assert(kEntSlot == kStageSlots, "dense slots and staging groups share the LDS slots");
-        const uint32_t t = threadIdx.x;
+        const uint32_t t = stage_lane();
         if (ne < kEntSlot) {
             b.stage[ne * 256 + t] = make_uint4(p_, v, m, dk);
             ne++;
@@ -1084,12 +1093,12 @@ struct MsLaneT {
     // the staged entries of the group holding entry ne - 1 (at the end of a group or of the
     // read); groups start at spilled entry 0, S and the reservation start, all multiples of 4
     NTC_HD void flush_stage(const MsBufs &b) {
-#if defined(__HIP_DEVICE_COMPILE__) && NTC_ECOMB
+#if NTC_ECOMB
         if (ne <= kEntSlot) return;
         const uint32_t last = ne - 1 - kEntSlot, g = last & ~(kStageSlots - 1);
         Entry *dst = spill_at(b, g);
         if (!dst) return;
-        const uint32_t t = threadIdx.x;
+        const uint32_t t = stage_lane();
 #pragma unroll
         for (uint32_t i = 0; i < kStageSlots; i++) {
             if (g + i <= last) {
@@ -1104,8 +1113,8 @@ struct MsLaneT {
     // the read is done: staged entries out, entry 0 with the count; true when the count does
     // not fit entry 0 and goes to the count array instead
     NTC_HD bool finish(const MsBufs &b) {
-#if defined(__HIP_DEVICE_COMPILE__) && NTC_ECOMB
-        const uint32_t t = threadIdx.x;
+#if NTC_ECOMB
+        const uint32_t t = stage_lane();
         const uint32_t c = ne < kNeInE0 ? ne : kNeInE0;
         Entry *dst = b.Ed + rid * b.ds;
         if (ne > kEntSlot) {

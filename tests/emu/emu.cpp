@@ -167,6 +167,9 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
     // NTC_EMU_SPILL=1: spill footprint of the v4 layout (entries past kEntSlot, records past
     // kRecSlot) -> stderr, for sizing the spill pools
     const bool spill_stats = getenv("NTC_EMU_SPILL") && atoi(getenv("NTC_EMU_SPILL"));
+    // secondary entry slots (capi.cpp ent_slots: 24 with joint runs, else 4; NTC_EMU_SLOTS overrides)
+    const char *es_env = getenv("NTC_EMU_SLOTS");
+    const uint32_t emu_S = es_env ? (uint32_t)atoi(es_env) : (d.joint ? 24u : 4u);
     uint64_t sp_reads_e = 0, sp_ent = 0, sp_reads_r = 0, sp_rec = 0, sp_len_e = 0, sp_len_r = 0, sp_rem_e = 0;
     uint64_t ne_hist[9] = {0};  // reads with ne > 4 + 4 * i
     for (uint64_t t = 0; t < tiles; t++) {
@@ -181,20 +184,29 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
             uint32_t len = (uint32_t)(offs[r + 1] - offs[r]);
             int rc;
             if (variant == 4) {
+                // the kernels' layout (k_ms4 / k_parse4 with one read per call): dense group Ed
+                // staged through the ECOMB slots with entry 0 carrying the count, S secondary
+                // slots, an overflow pool reserved at the first entry past them; 8 record slots
+                // then the record pool (capi.cpp encode4_impl)
                 std::vector<uint64_t> Q(len / 32 + 3, 0);
-                std::vector<Entry> E4(len + 1);
-                std::vector<uint64_t> R4(len + 1);
+                std::vector<Entry> Ed(kEntSlot), Es(emu_S), Ep(len + 8);
+                std::vector<uint4> stage((kStageSlots + 1) * 256);
+                std::vector<uint64_t> R2(kRecSlot), Rp(len + 8);
+                unsigned long long pcnt = 0, rcnt = 0, status = ~0ull;
+                uint32_t obase = 0, rbase = 0;
                 rc = pack_read(bases + offs[r], len, Q.data(), d.absent);
                 uint32_t ne = 0;
+                const MsBufs bufs{Q.data(), Es.data(), Ed.data(), 1, stage.data(), kEntSlot, emu_S, Ep.data(),
+                                  Ep.size(), &pcnt, &obase, &status};
                 auto run = [&](auto &ms) {
                     trace_phase(0);
                     ms.start(d, 0, len);
-                    const MsBufs bufs{Q.data(), E4.data() + kEntSlot, E4.data(), 1};  // contiguous: entry j at E4[j]
                     for (;;) {
                         int st = ms.step(d, bufs);
                         if (st < 0) { rc = st; break; }
                         if (st == 1) break;
                     }
+                    if (rc == 0) ms.finish(bufs);
                     ne = ms.ne;
                 };
                 if (rc == 0) {
@@ -206,28 +218,29 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
                         run(ms);
                     }
                 }
+                if (rc == 0 && status != ~0ull) return NTC_ERR_CAPACITY;  // the pool fits every read by construction
                 trace_phase(1);
-                if (rc == 0) rc = parse_read(d, Q.data(), 0, E4.data(), ne, len, R4.data(), R4.data());
-                if (spill_stats && rc >= 0) {
-                    for (int h = 0; h < 9; h++) ne_hist[h] += ne > kEntSlot + 4u * (uint32_t)h;
-                    if (ne > kEntSlot) {
-                        sp_reads_e++;
-                        sp_ent += ne - kEntSlot;
-                        sp_len_e += len;
-                        sp_rem_e += len - E4[kEntSlot].p;  // positions from the first spilled entry on
-                    }
-                    if ((uint32_t)rc > kRecSlot) {
-                        sp_reads_r++;
-                        sp_rec += (uint64_t)rc - kRecSlot;
-                        sp_len_r += len;
-                    }
-                }
+                // k_parse4: the dense group in one load, the count from entry 0
+                Entry pre[kEntSlot];
+                for (uint32_t j = 0; j < kEntSlot; j++) pre[j] = Ed[j];
+                const uint32_t c0 = entry0_count(pre[0]);
+                const uint32_t ne2 = c0 == kNeInE0 ? ne : c0;
+                if (rc == 0 && ne2 != ne) return NTC_ERR_FORMAT;
+                const Entry *E1 = Es.data() - kEntSlot;
+                const Entry *E2 = ne2 > kEntSlot + emu_S ? Ep.data() + obase - kEntSlot - emu_S : nullptr;
+                const RecPool rp{Rp.data(), Rp.size(), &rcnt, &rbase, &status, 0};
+                if (rc == 0)
+                    rc = parse_read(d, Q.data(), 0, E1, ne2, len, R2.data(), nullptr, 1, Ed.data(), 1, pre, E2, emu_S,
+                                    &rp);
                 trace_read_done();
                 if (d_out && rc >= 0)
-                    read_ms(d, Q.data(), 0, E4.data(), ne, len, d_out + (offs[r] - offs[0]), s_out + (offs[r] - offs[0]));
+                    read_ms(d, Q.data(), 0, E1, ne2, len, d_out + (offs[r] - offs[0]), s_out + (offs[r] - offs[0]),
+                            Ed.data(), 1, E2, emu_S);
                 if (rc >= 0) {
+                    if (status != ~0ull) return NTC_ERR_CAPACITY;
                     if (total + (uint64_t)rc > cap) return NTC_ERR_CAPACITY;
-                    for (int jj = 0; jj < rc; jj++) rec_out[total + jj] = R4[jj];
+                    for (int jj = 0; jj < rc; jj++)
+                        rec_out[total + jj] = jj < (int)kRecSlot ? R2[jj] : Rp[rbase + jj - kRecSlot];
                     total += (uint64_t)rc;
                     rec_offsets[r + 1] = total;
                     continue;
@@ -358,9 +371,12 @@ extern "C" int emu_wave_modes(const ntc_index_view *v, const uint8_t *bases, con
     struct Lane {
         MsLane ms;
         std::vector<uint64_t> Q;
-        std::vector<Entry> E;
+        std::vector<Entry> Ed, Es, Ep;
+        unsigned long long pcnt = 0, status = ~0ull;
+        uint32_t obase = 0;
         bool busy = false;
     };
+    std::vector<uint4> stage((kStageSlots + 1) * 256);  // lane i stages in slot i (ntc_host_lane)
     std::vector<Lane> L(64);
     uint64_t next = 0;
     for (;;) {
@@ -369,21 +385,27 @@ extern "C" int emu_wave_modes(const ntc_index_view *v, const uint8_t *bases, con
             const uint64_t r = next++;
             const uint32_t len = (uint32_t)(offs[r + 1] - offs[r]);
             l.Q.assign(len / 32 + 3, 0);
-            l.E.assign(len + 1, Entry{0, 0, 0, 0});
+            l.Ed.assign(kEntSlot, Entry{0, 0, 0, 0});
+            l.Es.assign(4, Entry{0, 0, 0, 0});
+            l.Ep.assign(len + 8, Entry{0, 0, 0, 0});
+            l.pcnt = 0;
             if (len == 0 || pack_read(bases + offs[r], len, l.Q.data(), d.absent) != 0) continue;
             l.ms.start(d, 0, len);
             l.busy = true;
         }
         uint32_t modes = 0;
         bool any = false;
-        for (auto &l : L) {
+        for (uint32_t li = 0; li < L.size(); li++) {
+            Lane &l = L[li];
             if (!l.busy) continue;
+            ntc_host_lane = li;
             any = true;
             const uint32_t m = l.ms.try_run ? 9u : l.ms.mode;
             modes |= 1u << m;
             out[3 + m]++;
             out[2]++;
-            const MsBufs bufs{l.Q.data(), l.E.data() + kEntSlot, l.E.data(), 1};
+            const MsBufs bufs{l.Q.data(), l.Es.data(), l.Ed.data(), 1, stage.data(), kEntSlot, 4, l.Ep.data(),
+                              l.Ep.size(), &l.pcnt, &l.obase, &l.status};
             const int st = l.ms.step(d, bufs);
             if (st != 0) l.busy = false;
         }
