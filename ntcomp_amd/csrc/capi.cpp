@@ -178,9 +178,9 @@ constexpr uint64_t kPoolMax = 0xFFFFFFF0ull;
 uint32_t ent_slots(const ntc_ctx *ctx) {
     if (ctx->ent_slots_opt) return ctx->ent_slots_opt;
     // entries per read past the dense 4 (tests/emu NTC_EMU_SPILL, 1 % errors): random genome
-    // k = 91 reads rarely spill (6 %, 0.07 % past 8); a strain collection with joint runs
-    // spills on 98 % of reads, 1 % past 28
-    return ctx->has_index && ctx->dix.joint ? 24u : 4u;
+    // k = 91 reads rarely spill (6 %, 0.07 % past 8); a strain collection with joint runs and
+    // fork hops spills on 98 % of reads, 2.6 % past 20, 0.17 % past 24
+    return ctx->has_index && ctx->dix.joint ? 20u : 4u;
 }
 
 // v4: pack -> persistent MS -> parse -> scan -> emit, all in position space.
@@ -663,6 +663,9 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
             HIP_TRY(ctx, hipMemsetAsync(d_pos, 0xFF, n * 4, ctx->stream));
             launch_path_place(pa, st, prv, (const uint64_t *)d_base, (uint32_t *)d_colex_at, (uint32_t *)d_pos,
                               (uint4 *)d_pstream, (uint64_t *)d_puniq, ctx->stream);
+            if (hx.k >= 4)
+                launch_path_forks(pa, st, (const uint32_t *)d_len, (const uint64_t *)d_base, (const uint32_t *)d_pos,
+                                  (uint32_t *)d_colex_at, ctx->stream);
             HIP_TRY(ctx, hipGetLastError());
             has_paths = true;
         }
@@ -689,6 +692,7 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     d.colex_at = (const uint32_t *)d_colex_at;
     d.pos_of_node = (const uint32_t *)d_pos;
     d.puniq = (const uint64_t *)d_puniq;
+    d.forks = has_paths && hx.k >= 4 ? 1u : 0u;
     d.absent = dv.absent;
     // Joint path runs pay off when MS intervals above U hold several nodes for long stretches:
     // genome collections, whose shared regions split the path cover into short unitigs (S91:

@@ -205,6 +205,20 @@ uint32_t path_succ(const HostIndex &ix, const Derived &dv, const std::vector<uin
     return dummy[y] ? kNoNode : y;
 }
 
+// w[c] = path position of the node v[1..k]c, or kNoNode: the labels sit on the first node
+// of v's (k-1)-suffix group (the SBWT's extension of v by c at depth k goes through it)
+void fork_words(const HostIndex &ix, const Derived &dv, const std::vector<uint8_t> &dummy, uint32_t v, uint32_t *w) {
+    uint64_t h = v;
+    while (h > 0 && ix.lcs[h] >= ix.k - 1) h--;
+    const uint32_t m = labels_of(dv, h);
+    for (int c = 0; c < 4; c++) {
+        w[c] = kNoNode;
+        if (!((m >> c) & 1u)) continue;
+        const uint32_t y = dv.C[c] + host_rank(dv, c, h);
+        if (!dummy[y]) w[c] = dv.pos_of_node[y];
+    }
+}
+
 // Path cover = the unitigs of the de Bruijn graph on real k-mers: edge z -> y when z is
 // alone in its (k-1)-suffix group, has exactly one successor y, and neither is a dummy
 // (y then has z as its only predecessor).  Paths start at real nodes without an in-edge;
@@ -285,6 +299,20 @@ void build_paths(const HostIndex &ix, Derived &dv) {
         }
         b += (e - a) + k;  // last node at b+(e-a)-1; positions up to b+(e-a)+k-1 hold no node
     }
+    // Fork words (k >= 4): the k free positions after a path's last node v hold, at
+    // v's position + 1 + c, the path position of the node v[1..k]c (from the labels of v's
+    // (k-1)-suffix group head), or kNoNode.  k_ms4's joint-run build follows a run across
+    // the path end with them (MsLaneT::fork_hop) instead of colex_at + extension + pos_of_node.
+    if (k >= 4) {
+        b = 0;
+        for (uint64_t p = 0; p < np; p++) {
+            const uint64_t a = path_start[p], e = path_start[p + 1];
+            const uint32_t v = order[e - 1];
+            const uint64_t pos = b + (e - a) - 1;
+            fork_words(ix, dv, dummy, v, dv.colex_at.data() + pos + 1);
+            b += (e - a) + k;
+        }
+    }
     dv.tlen = tlen;
     dv.n_paths = np;
     dv.has_paths = true;
@@ -343,6 +371,7 @@ DevIndex host_dev_index(const HostIndex &ix, const Derived &dv, const std::vecto
     d.colex_at = dv.colex_at.empty() ? nullptr : dv.colex_at.data();
     d.pos_of_node = dv.pos_of_node.empty() ? nullptr : dv.pos_of_node.data();
     d.puniq = dv.puniq.empty() ? nullptr : dv.puniq.data();
+    d.forks = dv.has_paths && ix.k >= 4 ? 1u : 0u;
     d.absent = dv.absent;
     d.tab = nullptr;  // see build_tab_host
     d.tab_u = 0;

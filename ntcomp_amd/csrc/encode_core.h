@@ -127,6 +127,7 @@ struct DevIndex {
     const Rank2Chunk *rank2;      // [4][rank2_blocks(n)] two-character rank chunks, or null
     uint32_t joint;               // 1: encode with joint path runs (k_ms4<true>, MsLaneT)
     const uint32_t *win_w;        // window words of each (U-3)-mer (see win_word), or null
+    uint32_t forks;               // 1: colex_at holds fork words after each path end (derived.cpp)
 };
 
 // per-read status codes (values of ntc_status)
@@ -1137,6 +1138,52 @@ struct MsLaneT {
         return true;
 #endif
     }
+    // Path position of the node at the next query position on the side whose last covered
+    // node is at path position t - 1, the read's character there being c: the path's next
+    // node when the path goes on with c (a mid-path node's only successor), the fork word
+    // colex_at[t + c] when the path ended at t - 1 (k-mer end bit clear), else none.
+    NTC_HD uint32_t fork_next(const DevIndex &ix, uint32_t t, uint32_t c) const {
+        const uint64_t te = (uint64_t)t + ix.k - 1;  // the k-mer end of path position t
+        NTC_TOUCH(kTrPst, ix.pstream + (te >> 5));
+        const uint4 g = ld4<4>(ix.pstream + (te >> 5));  // the group the run just read (L1/L2)
+        const uint32_t o = (uint32_t)(te & 31);
+        const uint32_t pc = (o < 16 ? g.x >> (2 * o) : g.y >> (2 * (o - 16))) & 3u;
+        if ((g.z >> o) & 1u) return pc == c ? t : 0xFFFFFFFFu;
+        NTC_TOUCH(kTrColex, ix.colex_at + t + c);
+        return ix.colex_at[t + c];
+    }
+    // (joint-run build) A run over m >= 1 positions stopped at p + m < len.  If every side of
+    // the interval goes on with the read's character c there, the extension is the interval
+    // of those next nodes (the first and last node of an interval with edge c extend to the
+    // first and last node of the extension, see note_path) at depth d + m + 1 (capped at k):
+    // a single node (or both sides at one node) or, below k - 1, a joint interval.  The run
+    // then goes on from there as a new run entry (the same (d, S) per position as the SBWT
+    // entry + run of the path through colex_at, EXT and pos_of_node it replaces).
+    NTC_HD bool fork_hop(const DevIndex &ix, const MsBufs &b, uint32_t &m) {
+        const uint32_t k = ix.k;
+        const uint64_t qq = qo + p + m;
+        const uint32_t c = (uint32_t)(b.Q[qq >> 5] >> (2 * (qq & 31))) & 3u;
+        const bool joint = jy() != 0xFFFFFFFFu;
+        // (a next node at path position 0 would make j = nx - 1 the "none" value: left to EXT)
+        const uint32_t nx = fork_next(ix, j + m + 1, c);
+        if (nx == 0xFFFFFFFFu || nx == 0) return false;
+        uint32_t ny = nx;
+        if (joint) {
+            ny = fork_next(ix, jy() + m + 1, c);
+            if (ny == 0xFFFFFFFFu || ny == 0) return false;
+        }
+        const uint32_t d1 = d + m + 1 < k ? d + m + 1 : k;
+        const bool single = ny == nx;
+
+        if (d1 < ix.t_jump || (!single && d1 + 1 >= k)) return false;  // as note_single would decide
+        put_entry(b, p, j + 1, m, (d + 1 < k ? d + 1 : k) | kRunTag);
+        p += m;
+        d = d + m < k ? d + m : k;
+        j = nx - 1;
+        jy() = single ? 0xFFFFFFFFu : ny - 1;
+        m = 0;
+        return true;
+    }
     // after a commit: look for the path position of a single-node interval.  A multi-node
     // interval [l, r) (d < k: strains sharing the read's suffix) starts a JOINT run when both
     // its first and its last node lie on paths: while both paths go on with the query's next
@@ -1269,7 +1316,20 @@ struct MsLaneT {
                 }
                 m += lim - pre;
                 pre = 0;
-                if (lim < 64) break;
+                if (lim < 64) {
+                    if constexpr (kJoint) {
+                        // the run stopped inside its window with the read going on: across a
+                        // path end (or both sides' next nodes), the run going on in the next
+                        // call.  Hops chained in one call hold the whole wave on this lane's
+                        // dependent loads (A/B, S91 k_ms4: 12.3 ms before, 16.3 ms with every
+                        // hop chained, 12.4 with one, 12.0 with none)
+                        if (ix.forks && m > 0 && p + m < len && fork_hop(ix, b, m)) {
+                            try_run = true;
+                            return 0;
+                        }
+                    }
+                    break;
+                }
             }
             if (kJoint && jy() != 0xFFFFFFFFu) {
                 // joint run over a multi-node interval [l, r) (its first and last nodes followed

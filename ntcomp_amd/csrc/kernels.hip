@@ -1165,6 +1165,35 @@ __global__ __launch_bounds__(256) void k_path_place(PathArgs a, const uint4 *st,
     }
 }
 
+// fork words after each path end (derived.cpp fork_words): run after k_path_place, so that
+// every real node's path position is known
+__global__ __launch_bounds__(256) void k_path_forks(PathArgs a, const uint4 *st, const uint32_t *len,
+                                                    const uint64_t *base, const uint32_t *pos_of_node,
+                                                    uint32_t *colex_at) {
+    const uint32_t z = blockIdx.x * 256u + threadIdx.x;
+    if (z == 0 || z >= a.n || path_dummy(a.dummy, z)) return;
+    const uint4 e = st[z];
+    if (e.y + 1 != len[e.x]) return;  // not its path's last node
+    const uint64_t pos = base[e.x] + e.y;
+    uint32_t h = z;
+    while (h > 0 && a.lcs[h] >= a.k - 1) h--;  // the (k-1)-suffix group's first node holds the labels
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const uint2 w = a.rank[(uint64_t)c * a.rwords + (h >> 5)];
+        uint32_t v = 0xFFFFFFFFu;
+        if ((w.y >> (h & 31)) & 1u) {
+            const uint32_t y = rank_word(w, h);
+            if (!path_dummy(a.dummy, y)) v = pos_of_node[y];
+        }
+        colex_at[pos + 1 + c] = v;
+    }
+}
+
+void launch_path_forks(const PathArgs &a, const uint4 *st, const uint32_t *len, const uint64_t *base,
+                       const uint32_t *pos_of_node, uint32_t *colex_at, hipStream_t s) {
+    hipLaunchKernelGGL(k_path_forks, grid_for(a.n), dim3(256), 0, s, a, st, len, base, pos_of_node, colex_at);
+}
+
 void launch_path_edges(const PathArgs &a, uint32_t *prv, hipStream_t s) {
     hipLaunchKernelGGL(k_path_edges, grid_for(a.n), dim3(256), 0, s, a, prv);
 }

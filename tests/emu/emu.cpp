@@ -93,6 +93,8 @@ bool load(const ntc_index_view *v, HostIndex &hx, Derived &dv, std::vector<WalkE
        // fragmented path covers, the emulation checks them on every index
         const char *ej = getenv("NTC_EMU_JOINT");
         d.joint = (ej && atoi(ej) == 0) ? 0u : 1u;
+        const char *ef = getenv("NTC_EMU_FORKS");  // fork words (joint build): NTC_EMU_FORKS=0 off
+        if (ef && atoi(ef) == 0) d.forks = 0;
     }
     const uint32_t U = tab_u ? std::min<uint32_t>(tab_u, std::min<uint32_t>(hx.k, kTabMaxU)) : default_tab_u(hx.n, hx.k, hx.lcs.data());
     d.tab_u = U;
@@ -167,9 +169,9 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
     // NTC_EMU_SPILL=1: spill footprint of the v4 layout (entries past kEntSlot, records past
     // kRecSlot) -> stderr, for sizing the spill pools
     const bool spill_stats = getenv("NTC_EMU_SPILL") && atoi(getenv("NTC_EMU_SPILL"));
-    // secondary entry slots (capi.cpp ent_slots: 24 with joint runs, else 4; NTC_EMU_SLOTS overrides)
+    // secondary entry slots (capi.cpp ent_slots: 20 with joint runs, else 4; NTC_EMU_SLOTS overrides)
     const char *es_env = getenv("NTC_EMU_SLOTS");
-    const uint32_t emu_S = es_env ? (uint32_t)atoi(es_env) : (d.joint ? 24u : 4u);
+    const uint32_t emu_S = es_env ? (uint32_t)atoi(es_env) : (d.joint ? 20u : 4u);
     uint64_t sp_reads_e = 0, sp_ent = 0, sp_reads_r = 0, sp_rec = 0, sp_len_e = 0, sp_len_r = 0, sp_rem_e = 0;
     uint64_t ne_hist[9] = {0};  // reads with ne > 4 + 4 * i
     for (uint64_t t = 0; t < tiles; t++) {
@@ -233,6 +235,20 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
                     rc = parse_read(d, Q.data(), 0, E1, ne2, len, R2.data(), nullptr, 1, Ed.data(), 1, pre, E2, emu_S,
                                     &rp);
                 trace_read_done();
+                if (spill_stats && rc >= 0) {
+                    for (int h = 0; h < 9; h++) ne_hist[h] += ne2 > kEntSlot + 4u * (uint32_t)h;
+                    if (ne2 > kEntSlot) {
+                        sp_reads_e++;
+                        sp_ent += ne2 - kEntSlot;
+                        sp_len_e += len;
+                        sp_rem_e += len - (emu_S ? Es[0].p : Ep[obase].p);  // positions from the first spilled entry on
+                    }
+                    if ((uint32_t)rc > kRecSlot) {
+                        sp_reads_r++;
+                        sp_rec += (uint64_t)rc - kRecSlot;
+                        sp_len_r += len;
+                    }
+                }
                 if (d_out && rc >= 0)
                     read_ms(d, Q.data(), 0, E1, ne2, len, d_out + (offs[r] - offs[0]), s_out + (offs[r] - offs[0]),
                             Ed.data(), 1, E2, emu_S);
