@@ -78,3 +78,20 @@ def test_gpu_built_index_encodes_like_host_built(ctx):
 def test_gpu_build_empty_inputs(ctx):
     for seqs in ([], [b""], [b"AC"], [b"NNNN"]):
         same(nt.Index.build_gpu(ctx, seqs, 5), nt.Index.build(seqs, 5))
+
+
+def test_cli_build_gpu_writes_the_host_index(tmp_path):
+    """`build --builder gpu` (main.rs:111-140 stand-in on the GPU) saves the same files as the
+    host builder."""
+    import subprocess
+    import sys
+    import os
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    g = nt.synth_genome(4, 50_000).tobytes().decode()
+    fa = tmp_path / "g.fa"
+    fa.write_text(">g\n" + "\n".join(g[i:i + 60] for i in range(0, len(g), 60)) + "\nACGTNNNNACGT\n")
+    for b in ("host", "gpu"):
+        subprocess.run([sys.executable, "-m", "ntcomp_amd", "build", "-o", str(tmp_path / b), "-k", "31",
+                        "--builder", b, str(fa)], cwd=repo, check=True, stderr=subprocess.PIPE)
+    for ext in (".sbwt", ".lcs"):
+        assert (tmp_path / ("gpu" + ext)).read_bytes() == (tmp_path / ("host" + ext)).read_bytes()
