@@ -135,7 +135,11 @@ int ntc_encode_batch(ntc_ctx *ctx, const uint8_t *bases, const uint64_t *read_of
  * upper bound on every read's length, e.g. 150); with max_read_len = 0 the library
  * first sizes its scratch from the offsets (one small device->host read).  Call
  * ntc_encode_status() (which synchronises) for the verdict.  rec_capacity must be >=
- * the total number of records (total bases is always enough).                       */
+ * the total number of records (total bases is always enough).  The workspace is sized
+ * by need: when a call runs out of an overflow pool (reads with many entries or
+ * records), ntc_encode_status grows the pools and runs the call again on the same
+ * buffers, so d_bases, d_read_offsets and the outputs must stay valid and unchanged until
+ * ntc_encode_status returns (option "spill_reruns" counts such re-runs).              */
 int ntc_encode_batch_device(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_read_offsets,
                             uint64_t n_reads, uint32_t max_read_len, uint64_t *d_rec_out,
                             uint64_t rec_capacity, uint64_t *d_rec_offsets_out);

@@ -37,7 +37,8 @@ typedef struct ntc_pipeline_stats {
     uint64_t reads, bases, blocks, dropped_blocks, bytes_out;
     double parse_s, gpu_s, deflate_s, write_s; /* thread-seconds per stage                  */
     double wall_s;
-    double alloc_s, first_batch_s, reader_done_s, gpu_done_s; /* timeline from the call's start */
+    double alloc_s;                            /* seconds spent pinning host buffers        */
+    double first_batch_s, reader_done_s, gpu_done_s; /* timeline from the call's start       */
     int32_t threads;
     int32_t reserved;
     int64_t bad_read;                          /* file index of the failing read, or -1     */

@@ -100,23 +100,23 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
     if (rc) return rc;
     ntc_fastx_set_threads(fx, T);
 
-    // pinned ring: the GPU threads hold at most n_ctx buffers, the reader fills one more
+    // pinned ring: the GPU threads hold at most n_ctx buffers, the reader fills one more.
+    // A slot's base buffer (the large part, ~320 MB) is pinned by the reader when it first
+    // fills the slot, so only the first one delays the first batch (pinning runs at a few
+    // GB/s); the offsets are pinned here.
     const int NB = n_ctx + 2;
     std::vector<Batch> ring((size_t)NB);
     for (auto &b : ring) {
         b.cap_bases = cap_bases + BR * 1024ull;  // a carry of < 65,536 reads sits in front
         b.cap_reads = per_batch + BR + 1;
-        if (hipHostMalloc((void **)&b.bases, b.cap_bases, hipHostMallocDefault) != hipSuccess ||
-            hipHostMalloc((void **)&b.offs, b.cap_reads * 8, hipHostMallocDefault) != hipSuccess) {
-            for (auto &x : ring) {
-                if (x.bases) (void)hipHostFree(x.bases);
+        if (hipHostMalloc((void **)&b.offs, b.cap_reads * 8, hipHostMallocDefault) != hipSuccess) {
+            for (auto &x : ring)
                 if (x.offs) (void)hipHostFree(x.offs);
-            }
             ntc_fastx_close(fx);
             return NTC_ERR_HIP;
         }
     }
-
+    std::atomic<double> t_pin{0};
     S.alloc_s = secs(t0, Clock::now());
     Shared sh;
     std::vector<std::deque<int>> gpu_q((size_t)n_ctx);  // per context: ring indices in batch order
@@ -168,6 +168,15 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
                 if (sh.error != NTC_OK) break;
             }
             Batch &b = ring[(size_t)bi];
+            if (!b.bases) {
+                const auto ta = Clock::now();
+                if (hipHostMalloc((void **)&b.bases, b.cap_bases, hipHostMallocDefault) != hipSuccess) {
+                    b.bases = nullptr;
+                    sh.fail(NTC_ERR_HIP, "pinned host allocation failed");
+                    break;
+                }
+                t_pin = t_pin.load() + secs(ta, Clock::now());  // the reader alone writes it
+            }
             uint64_t used = 0;  // bases in b
             b.offs[0] = 0;
             if (carry) {  // the previous buffer's unprocessed reads go first
@@ -379,11 +388,12 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
     for (auto &t : pool) t.join();
     for (auto &kv : done) ntc_buffer_free(kv.second.data);
     for (auto &b : ring) {
-        (void)hipHostFree(b.bases);
+        if (b.bases) (void)hipHostFree(b.bases);
         (void)hipHostFree(b.offs);
     }
     ntc_fastx_close(fx);
     const int result = sh.error == -1 ? NTC_OK : sh.error;
+    S.alloc_s += t_pin.load();
     S.parse_s = t_parse.load();
     S.gpu_s = t_gpu.load();
     S.deflate_s = t_deflate.load();
