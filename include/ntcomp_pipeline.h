@@ -27,8 +27,8 @@ extern "C" {
 
 typedef struct ntc_pipeline_opts {
     int32_t threads;          /* host pool (parse, deflate); <= 0: ntc_host_threads()        */
-    int32_t blocks_per_batch; /* 65,536-read blocks per GPU call; <= 0: 16                    */
-    uint64_t batch_bases;     /* bases per pinned batch buffer; 0: 256 Mi (grows for long reads) */
+    int32_t blocks_per_batch; /* 65,536-read blocks per GPU call; <= 0: 4 (encode), 2 (decode) */
+    uint64_t batch_bases;     /* encode: bases per pinned batch buffer; 0: 64 Mi (grows for long reads) */
     int32_t deflate_engine;   /* NTC_DEFLATE_ZLIB (0) or NTC_DEFLATE_LIBDEFLATE (1)           */
     int32_t reserved;
 } ntc_pipeline_opts;

@@ -596,7 +596,7 @@ def read_block(data):
 
 
 # ---- FASTX ingest ---------------------------------------------------------------------
-def encode_file(ctxs, in_path, out_fd, threads=0, blocks_per_batch=16, batch_bases=0, deflate="zlib"):
+def encode_file(ctxs, in_path, out_fd, threads=0, blocks_per_batch=4, batch_bases=0, deflate="zlib"):
     """`ntcomp encode` file to file (ntc_encode_file, include/ntcomp_pipeline.h): FASTX ->
     GPU encode + block packer on every context -> deflate pool -> encoded.dat on out_fd.
     Returns the per-stage stats as a dict; raises NtcError (with .bad_read)."""

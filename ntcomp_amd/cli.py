@@ -215,7 +215,7 @@ def main(argv=None):
                                      "overrides --gpus")
     e.add_argument("--threads", type=int, default=0,
                    help="host pool for FASTQ parse and deflate (0: CPUs available to the process)")
-    e.add_argument("--blocks-per-batch", type=int, default=16, help="65,536-read blocks per GPU call")
+    e.add_argument("--blocks-per-batch", type=int, default=4, help="65,536-read blocks per GPU call")
     e.add_argument("--deflate", choices=["auto", "zlib", "libdeflate"], default="auto",
                    help="gzip engine for the block streams, level 6 either way (the reference's "
                         "Compression::default()): libdeflate (auto, when libdeflate.so.0 loads; ~3x faster) or "

@@ -89,8 +89,11 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
     if (opts) o = *opts;
     const int T = o.threads > 0 ? o.threads : ntc_host_threads();
     const uint32_t BR = 65536;  // main.rs:152
-    const uint64_t per_batch = (uint64_t)(o.blocks_per_batch > 0 ? o.blocks_per_batch : 16) * BR;
-    const uint64_t cap_bases = o.batch_bases > 0 ? o.batch_bases : (256ull << 20);
+    // 4 blocks per GPU call and 64 Mi-base buffers: the first batch is on the GPU after
+    // ~30 ms and the pinned ring stays small (10 M x 150 bp: pipeline 0.59 -> 0.32 s against
+    // 16 blocks and 256 Mi bases, scripts/pipe_bench.py on one MI355X box)
+    const uint64_t per_batch = (uint64_t)(o.blocks_per_batch > 0 ? o.blocks_per_batch : 4) * BR;
+    const uint64_t cap_bases = o.batch_bases > 0 ? o.batch_bases : (64ull << 20);
     const int engine = o.deflate_engine;
     ntc_pipeline_stats S{};
     const auto t0 = Clock::now();
