@@ -600,6 +600,13 @@ constexpr uint32_t kScanExact = 4;   // filter candidates tested exactly per SCA
 #ifndef NTC_GUESS_SLACK
 #define NTC_GUESS_SLACK 2  // guess only for x - ge in [U, U + slack] (a lone substitution: x = ge + U)
 #endif
+#ifndef NTC_FIRST_PAIR
+// 1: the read start also loads the pair word of position U (is it long?) beside U - 1's
+// table entry.  0: a long U - 1 enters the walk directly and the extension at U decides
+// (U is short after a long U - 1 only for an error at U or a chance U-mer, ~1 % of reads,
+// which then pay the EXT and its failure's table entry instead of one pair-word line per read)
+#define NTC_FIRST_PAIR 0
+#endif
 #ifndef NTC_CHAIN
 // A wave runs the blocks of MsLane::step in program order for all its lanes (a wave
 // iteration holds ~7.6 distinct modes on C91, so nearly every block runs anyway): a lane
@@ -1372,8 +1379,10 @@ struct MsLaneT {
                 window(b, 0);
                 NTC_TOUCH(kTrTabU, ix.tab + tab_base(U) + key_at(U - 1, U));
                 const uint2 te = load2_stream(ix.tab + tab_base(U) + key_at(U - 1, U));
-                uint32_t b2;
-                if (ix.pair_w) {
+                uint32_t b2 = 1u;
+                if (!NTC_FIRST_PAIR) {
+                    // U decided by the extension at U (a failure loads U's entry then)
+                } else if (ix.pair_w) {
                     // U is long iff bit 4 + q[U] of the pair word of the (U-1)-mer ending at U - 1
                     // (the 32 MB level-U bitmap then stays out of the Infinity Cache entirely)
                     const uint64_t M = key_at(U - 1, U - 1);
