@@ -600,6 +600,12 @@ constexpr uint32_t kScanExact = 4;   // filter candidates tested exactly per SCA
 #ifndef NTC_GUESS_SLACK
 #define NTC_GUESS_SLACK 2  // guess only for x - ge in [U, U + slack] (a lone substitution: x = ge + U)
 #endif
+#ifndef NTC_BRK_LATE
+// 1 (k_ms4 without joint runs): a run break's pair word goes out with the SCAN's pair words,
+// only when the break position passes the filter (55 % of breaks at C91 do not: the F-mer
+// ending there holds the sequencing error); 0: with the SCAN's filter loads, always
+#define NTC_BRK_LATE 1
+#endif
 #ifndef NTC_FIRST_PAIR
 // 1: the read start also loads the pair word of position U (is it long?) beside U - 1's
 // table entry.  0: a long U - 1 enters the walk directly and the extension at U decides
@@ -1411,12 +1417,15 @@ struct MsLaneT {
         // SCAN of p + 1, ...; a long p abandons that SCAN for EXT at p.  One round trip.
         uint32_t bpw = 0, bc = 0;
         bool brk = false;
+        constexpr bool kBrkLate = NTC_BRK_LATE && !kJoint;
         if (mode == kModeBrk && ix.pair_w && p + 2 < len) {
             if (!covers(p + 1 - U, p + 2)) window(b, p + 1 - U);
-            const uint64_t M = key_at(p - 1, U - 1);
             bc = (uint32_t)(qw >> (2 * (p - qb))) & 3u;
-            NTC_TOUCH(kTrBits, ix.pair_w + M);
-            bpw = ld_hint<32>(ix.pair_w + M);
+            if (!kBrkLate) {
+                const uint64_t M = key_at(p - 1, U - 1);
+                NTC_TOUCH(kTrBits, ix.pair_w + M);
+                bpw = ld_hint<32>(ix.pair_w + M);
+            }
             brk = true;
             p += 1;  // a short p: m <= U - 1 skips nothing beyond p itself
             mode = kModeScan;
@@ -1437,6 +1446,7 @@ struct MsLaneT {
             // test them in the small level-F bitmap first; the F-mer ending at y is shared
             // by the U-mers ending at y, y + 1 and y + 2, so W + 2 filter bits cover W positions
             uint32_t cand = (1u << W) - 1u;
+            uint32_t bpass = 1u;  // (late break word) the break position p - 1 passes the filter
             if (ix.filt_f) {
                 const uint32_t F = ix.filt_f;
                 uint32_t fm = 0;  // bit i: F-mer ending at p - 2 + i is present
@@ -1459,9 +1469,10 @@ struct MsLaneT {
                     fm |= ((fw[i] >> ((uint32_t)(v >> (2 * i)) & 31u)) & 1u) << i;
                 fm &= (1u << (W + kFiltGap)) - 1u;
                 cand &= fm & (fm >> 1) & (fm >> kFiltGap);  // all three F-mers of the U-mer
+                bpass = (fm & 3u) == 3u;  // the F-mers ending at p - 2 and p - 1
             }
 #if NTC_BRK_MERGE
-            if (brk && ((bpw >> (4 + bc)) & 1u)) {  // the break position is long: EXT there
+            if (!kBrkLate && brk && ((bpw >> (4 + bc)) & 1u)) {  // the break position is long: EXT there
                 p -= 1;
                 mode = kModeBrkLong;
                 return 0;
@@ -1567,6 +1578,17 @@ struct MsLaneT {
                         if ((tested >> slot[t]) & 1u) NTC_TOUCH(kTrBits, ix.pair_w + M);
                         pbv[t] = ld_hint<32>(ix.pair_w + M);
                     }
+#if NTC_BRK_MERGE
+                    if (kBrkLate && brk) {
+                        // the break position p - 1 can be long only if it passes the filter: its
+                        // pair word (of the (U-1)-mer ending at p - 2, inside the window the break
+                        // set) goes out with the SCAN's pair words, in their round trip, and only
+                        // then (else slot 0's line again, no further request)
+                        const uint64_t Mb = bpass ? key_at(p - 2, U - 1) : M0;
+                        if (bpass) NTC_TOUCH(kTrBits, ix.pair_w + Mb);
+                        bpw = ld_hint<32>(ix.pair_w + Mb);
+                    }
+#endif
 #pragma unroll
                     for (uint32_t t = 0; t < NTC_PAIR_TESTS; t++) {
                         const uint32_t y = p + slot[t];
@@ -1578,6 +1600,13 @@ struct MsLaneT {
                     hit &= tested;
                     open = untested;  // resume at the first untested candidate pair
                 }
+#if NTC_BRK_MERGE
+                if (kBrkLate && brk && bpass && ((bpw >> (4 + bc)) & 1u)) {  // the break position is long: EXT there
+                    p -= 1;
+                    mode = kModeBrkLong;
+                    return 0;
+                }
+#endif
                 if (hit) {
                     const uint32_t xi = (uint32_t)__builtin_ctz(hit);
                     const uint32_t x = p + xi;  // x, x + 1 long, x - 1 short

@@ -235,6 +235,32 @@ def test_emulated_strain_collection(k, ext2, joint, monkeypatch):
     assert np.array_equal(out, reads)
 
 
+@pytest.mark.parametrize("k", [31, 91])
+def test_emulated_run_breaks_with_filter_without_joint_runs(k, monkeypatch):
+    """k_ms4 as built for C91 (no joint runs) with the SCAN filter on (U = 12 and 14): a run
+    break's pair word is loaded only when the break position passes the filter, with the
+    SCAN's pair words (NTC_BRK_LATE).  Two strains make break positions long now and then
+    (the mismatch is another copy's base), 3 % errors make breaks frequent; records and the
+    (d, S) of a read sample equal the oracle's."""
+    monkeypatch.setenv("NTC_EMU_JOINT", "0")
+    g = nt.synth_genome(41, 120_000)
+    st = nt.synth_strains(g, 5, 2, 30_000)
+    texts = [g] + [st[i] for i in range(2)]
+    ix = nt.Index.build([t.tobytes() for t in texts], k)
+    n, L = 1200, 150
+    reads = nt.synth_reads(np.concatenate(texts), 6, 0, n, L, 30_000)
+    offs = np.arange(0, n * L + 1, L, dtype=np.uint64)
+    orc = OracleIndex(ix.n, k, ix.rows, ix.C, ix.lcs)
+    exp, eoff = orc.encode(reads, offs)
+    for u in (12, 14):
+        got, goff, d, s = emu_encode(ix.n, k, ix.rows, ix.C, ix.lcs, reads, offs, want_ms=True, tab_u=u)
+        assert np.array_equal(goff, eoff) and np.array_equal(got, exp), u
+        for r in range(0, n, 13):
+            od, olo = orc.ms(reads[r * L:(r + 1) * L].tobytes())
+            assert np.array_equal(d[r * L:(r + 1) * L], od), (u, r)
+            assert np.array_equal(s[r * L:(r + 1) * L].astype(np.uint64), olo), (u, r)
+
+
 def test_default_suffix_table_depth_follows_umer_density():
     """The upload's default depth (derived.cpp default_tab_u): U = min(k, 14, ceil(log4 n) + 2),
     one level deeper when the distinct 14-mers (nodes whose LCS with their colex predecessor is
