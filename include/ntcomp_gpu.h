@@ -102,9 +102,10 @@ int ntc_ctx_synchronize(ntc_ctx *ctx);
  * "joint" for the NEXT upload: -1 (default, auto: on when the path cover averages fewer
  * than 4096 nodes per path, i.e. a genome collection), 0 or 1: joint path runs over
  * multi-node matching-statistics intervals (results never depend on it; after an upload
- * get_option returns the setting in use).  "win" (-1 auto = joint-run builds / 0 / 1): SCAN
- * window words, 4^(U-3) x 32 B, four positions per line.  Also "filter" (-1 auto / 0 / 1: SCAN
- * pre-filter), "ext2" (0 / 1: two-character rank chunks), "pair_bytes" (0 / 1), same rules.
+ * get_option returns the setting in use).  "win" (-1 auto = on for U >= 4 / 0 / 1): SCAN
+ * window words, 4^(U-3) x 32 B, four positions per line.  Also "filter" (-1 auto = on only
+ * without window words and below 60 % density / 0 / 1: SCAN pre-filter), "ext2" (0 / 1:
+ * two-character rank chunks), "pair_bytes" (0 / 1), same rules.
  * Read-only: "n_paths", "path_text_len" (the path cover built on the device at upload),
  * "path_hash" (test hook: FNV-1a of the cover arrays, derived.h path_cover_hash),
  * "tab_u" (after an upload: the depth in use), "tab_u_fallback" (1: the default depth 15

@@ -86,7 +86,7 @@ struct ntc_ctx {
     int filter_opt = -1;     // SCAN pre-filter at the next upload: -1 auto (off when saturated), 0 off, 1 on
     int64_t filter_density_ppm = -1;  // presence density of the filter level at the last upload
     int joint_opt = -1;      // joint path runs at the next upload: -1 auto (fragmented path cover), 0 off, 1 on
-    int win_opt = -1;        // SCAN window words at the next upload: -1 auto (joint-run builds), 0 off, 1 on
+    int win_opt = -1;        // SCAN window words at the next upload: -1 auto (U >= 4), 0 off, 1 on
     int ext2_opt = 0;        // build the two-character rank chunks at the next upload (A/B option: 1 measured
                              // slower -- 8 B/node from HBM against 1 B/node of Infinity-Cache-resident rank words)
     uint64_t n_paths = 0, path_text_len = 0;
@@ -742,6 +742,19 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     d.tab_u = U;
     d.tab_pos = (has_paths && U >= dv.t_jump && n < (1ULL << 31)) ? 1u : 0u;
     launch_tab_build(d, U, (uint2 *)d_tab, (uint32_t *)d_bits, F, (uint32_t *)d_fbits, ctx->stream);
+    d.win_w = nullptr;
+    // SCAN window words (a (U-3)-mer keyed 32-byte entry answers four positions): two lines
+    // answer the eight positions of a SCAN unit.  k_ms4 is bound by its lane loads in the
+    // CU's vector memory path (TA/TD 93-96 % busy at C91, TCP stalled on pending L2 data), and
+    // the L2-resident filter took 18 of them per SCAN: C91 k_ms4 3.70 -> 2.40 ms with window
+    // words and no filter.  Auto: on for every U >= 4, both builds.
+    const bool win_on = U >= 4 && ctx->win_opt != 0;
+    if (win_on) {
+        void *d_win;
+        if ((rc = dalloc(win_words_count(U) * 32, &d_win))) return rc;
+        launch_win_words((const uint32_t *)d_bits, U, (uint32_t *)d_win, ctx->stream);
+        d.win_w = (const uint32_t *)d_win;
+    }
     ctx->filter_density_ppm = -1;
     if (F) {
         // A filter over a large index is mostly ones (S91's 70 M nodes: 72 % of all 12-mers)
@@ -753,17 +766,10 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
         uint64_t ones = 0;
         for (uint32_t x : fb) ones += (uint64_t)__builtin_popcount(x);
         ctx->filter_density_ppm = (int64_t)(ones * 1000000 / ((uint64_t)fb.size() * 32));
-        const bool on = ctx->filter_opt == 1 || (ctx->filter_opt < 0 && ctx->filter_density_ppm <= kFiltMaxDensityPpm);
+        // (auto: off with window words, whose loads do not depend on it)
+        const bool on = ctx->filter_opt == 1 ||
+                        (ctx->filter_opt < 0 && !win_on && ctx->filter_density_ppm <= kFiltMaxDensityPpm);
         if (!on) d.filt_f = 0;
-    }
-    d.win_w = nullptr;
-    // SCAN window words for the joint-run build (genome collections: the filter is off and
-    // every position after an error is a pair-word test); needs the level-U presence bitmap
-    if (U >= 4 && ((ctx->win_opt < 0 && d.joint) || ctx->win_opt == 1)) {
-        void *d_win;
-        if ((rc = dalloc(win_words_count(U) * 32, &d_win))) return rc;
-        launch_win_words((const uint32_t *)d_bits, U, (uint32_t *)d_win, ctx->stream);
-        d.win_w = (const uint32_t *)d_win;
     }
     d.pair_w = nullptr;
     if (ctx->pair_bytes_opt) {

@@ -606,6 +606,9 @@ constexpr uint32_t kScanExact = 4;   // filter candidates tested exactly per SCA
 // ending there holds the sequencing error); 0: with the SCAN's filter loads, always
 #define NTC_BRK_LATE 1
 #endif
+#ifndef NTC_START_WINDOW
+#define NTC_START_WINDOW 1  // MsLaneT::start loads the read-start query window (see start)
+#endif
 #ifndef NTC_FIRST_PAIR
 // 1: the read start also loads the pair word of position U (is it long?) beside U - 1's
 // table entry.  0: a long U - 1 enters the walk directly and the extension at U decides
@@ -627,7 +630,7 @@ constexpr uint32_t kScanExact = 4;   // filter candidates tested exactly per SCA
 #define NTC_WIN_ENTRIES 2  // window-word entries per SCAN (4 positions each, one 32-bit load per position)
 #endif
 #ifndef NTC_PAIR_STRIDE
-#define NTC_PAIR_STRIDE 1  // SCAN pair words at non-overlapping positions: 1 in the joint-run build, 2 always, 0 never
+#define NTC_PAIR_STRIDE 2  // SCAN pair words at non-overlapping positions (or window words): 1 in the joint-run build, 2 always, 0 never
 #endif
 #ifndef NTC_SEEK_BS
 #define NTC_SEEK_BS 1  // EntryView::seek: binary search instead of a forward scan
@@ -1013,12 +1016,20 @@ struct MsLaneT {
     NTC_HD uint32_t &jy() { return l1; }
     bool try_run;
 
-    NTC_HD void start(const DevIndex &ix, uint64_t qo_, uint32_t len_, uint64_t rid_ = 0) {
+    // Q (NTC_START_WINDOW): the read-start window is loaded here, so that its round trip
+    // overlaps the other lanes' run loads instead of adding one to the read-start block
+    NTC_HD void start(const DevIndex &ix, uint64_t qo_, uint32_t len_, uint64_t rid_ = 0, const uint64_t *Q = nullptr) {
         qo = qo_;
         rid = rid_;
         len = len_;
         qw = 0;
         qb = 0xFFFFFFFFu;
+        if (NTC_START_WINDOW && Q && len_ >= ix.tab_u + 1) {
+            qb = 0;
+            NTC_TOUCH(kTrQ, Q + (qo_ >> 5));
+            NTC_TOUCH(kTrQ, Q + (qo_ >> 5) + 1);
+            qw = window2(Q, qo_);
+        }
         p = 0; d = 0; l = 0; r = ix.n; j = 0xFFFFFFFFu; ne = 0;
         mode = kModeFirst; lo = r1 = bl = bR = 0;
         hi = kScanW;  // SCAN width cap (hi is free while scanning)
@@ -1382,7 +1393,7 @@ struct MsLaneT {
             // pair (U - 1, U), so test it directly with U - 1's full entry
             mode = kModeScan;
             if (len >= U + 1) {
-                window(b, 0);
+                if (!covers(0, U)) window(b, 0);
                 NTC_TOUCH(kTrTabU, ix.tab + tab_base(U) + key_at(U - 1, U));
                 const uint2 te = load2_stream(ix.tab + tab_base(U) + key_at(U - 1, U));
                 uint32_t b2 = 1u;
@@ -1411,13 +1422,16 @@ struct MsLaneT {
                 // (NTC_CHAIN) on into the SCAN block below, in this same call
             }
         }
+        // SCAN pair words at non-overlapping positions / window words (see the SCAN block)
+        constexpr bool kStrideScan = NTC_PAIR_STRIDE == 2 || (NTC_PAIR_STRIDE == 1 && kJoint);
 #if NTC_BRK_MERGE
         // The run broke at p.  p is short after almost every break, so p's long/short test
         // (its pair word, and the node before p for a long p) is issued together with the
         // SCAN of p + 1, ...; a long p abandons that SCAN for EXT at p.  One round trip.
+        // (The stride SCAN keeps the break word with its first loads.)
         uint32_t bpw = 0, bc = 0;
         bool brk = false;
-        constexpr bool kBrkLate = NTC_BRK_LATE && !kJoint;
+        constexpr bool kBrkLate = NTC_BRK_LATE && !kStrideScan;
         if (mode == kModeBrk && ix.pair_w && p + 2 < len) {
             if (!covers(p + 1 - U, p + 2)) window(b, p + 1 - U);
             bc = (uint32_t)(qw >> (2 * (p - qb))) & 3u;
@@ -1472,7 +1486,8 @@ struct MsLaneT {
                 bpass = (fm & 3u) == 3u;  // the F-mers ending at p - 2 and p - 1
             }
 #if NTC_BRK_MERGE
-            if (!kBrkLate && brk && ((bpw >> (4 + bc)) & 1u)) {  // the break position is long: EXT there
+            // (the stride SCAN tests the break word after issuing its own loads, below: one round trip)
+            if (!kBrkLate && !kStrideScan && brk && ((bpw >> (4 + bc)) & 1u)) {  // the break position is long: EXT there
                 p -= 1;
                 mode = kModeBrkLong;
                 return 0;
@@ -1492,7 +1507,7 @@ struct MsLaneT {
                 // Every load is issued before the first use.  A slot without a word repeats the
                 // first one's (the same line, no further request past L2); with no candidate at
                 // all every slot reads word 0, one line all lanes share.
-                constexpr bool kStride = NTC_PAIR_STRIDE == 2 || (NTC_PAIR_STRIDE == 1 && kJoint);
+                constexpr bool kStride = kStrideScan;
                 const uint32_t cp = cand & (cand >> 1);  // candidate pair starts (<= W - 2)
                 uint32_t slot[NTC_PAIR_TESTS], pbv[NTC_PAIR_TESTS];
                 uint32_t hit = 0, single = 0, open = 0, keep = cand;
@@ -1601,7 +1616,7 @@ struct MsLaneT {
                     open = untested;  // resume at the first untested candidate pair
                 }
 #if NTC_BRK_MERGE
-                if (kBrkLate && brk && bpass && ((bpw >> (4 + bc)) & 1u)) {  // the break position is long: EXT there
+                if ((kStrideScan || (kBrkLate && bpass)) && brk && ((bpw >> (4 + bc)) & 1u)) {  // the break position is long: EXT there
                     p -= 1;
                     mode = kModeBrkLong;
                     return 0;

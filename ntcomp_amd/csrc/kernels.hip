@@ -313,7 +313,7 @@ __global__ __launch_bounds__(256, NTC_MS_WAVES) void k_ms4(Enc4Args a) {
                 idle = false;
                 const uint64_t b = a.offs[rd], e = a.offs[rd + 1];
                 const uint64_t P = b - o0;
-                st.start(a.ix, P, (uint32_t)(e - b), rd);
+                st.start(a.ix, P, (uint32_t)(e - b), rd, e > b ? a.Q : nullptr);
                 if (e <= b) {  // empty read (EncodeError, encode.rs:133-135) or bad offsets
                     atomicMin(a.status, (unsigned long long)((rd << 8) | (uint64_t)(e == b ? kErrEmptyRead : kErrFormat)));
                     a.ne[rd] = 0;

@@ -104,12 +104,16 @@ bool load(const ntc_index_view *v, HostIndex &hx, Derived &dv, std::vector<WalkE
     d.tab_bits = bits.data();
     d.filt_f = fbits.empty() ? 0u : filter_level(U);
     d.filt_bits = fbits.empty() ? nullptr : fbits.data();
-    if (const char *ef = getenv("NTC_EMU_FILTER"); ef && atoi(ef) == 0) {  // as the upload's filter=0 (S91 auto)
-        d.filt_f = 0;
-        d.filt_bits = nullptr;
+    {  // as the upload's auto filter: off with window words; NTC_EMU_FILTER=0/1 forces it
+        const char *ef = getenv("NTC_EMU_FILTER"), *ew = getenv("NTC_EMU_WIN");
+        const bool win_on = U >= 4 && !(ew && atoi(ew) == 0);
+        if (ef ? atoi(ef) == 0 : win_on) {
+            d.filt_f = 0;
+            d.filt_bits = nullptr;
+        }
     }
     d.tab_u = U;
-    {  // window words (SCAN, joint builds): NTC_EMU_WIN=0 off, else on whenever U >= 4
+    {  // window words (SCAN): NTC_EMU_WIN=0 off, else on whenever U >= 4 (the upload's auto)
         static std::vector<uint32_t> winb;
         const char *ew = getenv("NTC_EMU_WIN");
         d.win_w = nullptr;
@@ -202,7 +206,7 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
                                   Ep.size(), &pcnt, &obase, &status};
                 auto run = [&](auto &ms) {
                     trace_phase(0);
-                    ms.start(d, 0, len);
+                    ms.start(d, 0, len, 0, Q.data());
                     for (;;) {
                         int st = ms.step(d, bufs);
                         if (st < 0) { rc = st; break; }
@@ -406,7 +410,7 @@ extern "C" int emu_wave_modes(const ntc_index_view *v, const uint8_t *bases, con
             l.Ep.assign(len + 8, Entry{0, 0, 0, 0});
             l.pcnt = 0;
             if (len == 0 || pack_read(bases + offs[r], len, l.Q.data(), d.absent) != 0) continue;
-            l.ms.start(d, 0, len);
+            l.ms.start(d, 0, len, 0, l.Q.data());
             l.busy = true;
         }
         uint32_t modes = 0;

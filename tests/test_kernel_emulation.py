@@ -235,14 +235,15 @@ def test_emulated_strain_collection(k, ext2, joint, monkeypatch):
     assert np.array_equal(out, reads)
 
 
+@pytest.mark.parametrize("win", ["1", "0"])
 @pytest.mark.parametrize("k", [31, 91])
-def test_emulated_run_breaks_with_filter_without_joint_runs(k, monkeypatch):
-    """k_ms4 as built for C91 (no joint runs) with the SCAN filter on (U = 12 and 14): a run
-    break's pair word is loaded only when the break position passes the filter, with the
-    SCAN's pair words (NTC_BRK_LATE).  Two strains make break positions long now and then
-    (the mismatch is another copy's base), 3 % errors make breaks frequent; records and the
-    (d, S) of a read sample equal the oracle's."""
+def test_emulated_run_breaks_without_joint_runs(k, win, monkeypatch):
+    """k_ms4 as built for C91 (no joint runs) at U = 12 and 14, its SCAN on window words (the
+    default) or on stride pair words behind the filter (win = 0).  Two strains make break
+    positions long now and then (the mismatch is another copy's base), 3 % errors make breaks
+    frequent; records and the (d, S) of a read sample equal the oracle's."""
     monkeypatch.setenv("NTC_EMU_JOINT", "0")
+    monkeypatch.setenv("NTC_EMU_WIN", win)
     g = nt.synth_genome(41, 120_000)
     st = nt.synth_strains(g, 5, 2, 30_000)
     texts = [g] + [st[i] for i in range(2)]
