@@ -600,6 +600,9 @@ constexpr uint32_t kScanExact = 4;   // filter candidates tested exactly per SCA
 #ifndef NTC_GUESS_SLACK
 #define NTC_GUESS_SLACK 2  // guess only for x - ge in [U, U + slack] (a lone substitution: x = ge + U)
 #endif
+#ifndef NTC_BRK_IN_WIN
+#define NTC_BRK_IN_WIN 1  // the SCAN after a run break starts at the break position (window words test it)
+#endif
 #ifndef NTC_BRK_LATE
 // 1 (k_ms4 without joint runs): a run break's pair word goes out with the SCAN's pair words,
 // only when the break position passes the filter (55 % of breaks at C91 do not: the F-mer
@@ -1424,26 +1427,31 @@ struct MsLaneT {
         }
         // SCAN pair words at non-overlapping positions / window words (see the SCAN block)
         constexpr bool kStrideScan = NTC_PAIR_STRIDE == 2 || (NTC_PAIR_STRIDE == 1 && kJoint);
+        bool brk0 = false;  // the SCAN starts at a run break position p, whose long/short it tests
 #if NTC_BRK_MERGE
         // The run broke at p.  p is short after almost every break, so p's long/short test
         // (its pair word, and the node before p for a long p) is issued together with the
         // SCAN of p + 1, ...; a long p abandons that SCAN for EXT at p.  One round trip.
         // (The stride SCAN keeps the break word with its first loads.)
         uint32_t bpw = 0, bc = 0;
-        bool brk = false;
+        bool brk = false;  // (brk0: see below)
         constexpr bool kBrkLate = NTC_BRK_LATE && !kStrideScan;
         if (mode == kModeBrk && ix.pair_w && p + 2 < len) {
             if (!covers(p + 1 - U, p + 2)) window(b, p + 1 - U);
             bc = (uint32_t)(qw >> (2 * (p - qb))) & 3u;
-            if (!kBrkLate) {
+            // Window words answer p itself: the SCAN starts AT p (its first position tells
+            // whether p is long) and no break word is loaded -- one random line less per break.
+            const bool in_win = NTC_BRK_IN_WIN && kStrideScan && ix.win_w != nullptr;
+            if (!kBrkLate && !in_win) {
                 const uint64_t M = key_at(p - 1, U - 1);
                 NTC_TOUCH(kTrBits, ix.pair_w + M);
                 bpw = ld_hint<32>(ix.pair_w + M);
             }
-            brk = true;
-            p += 1;  // a short p: m <= U - 1 skips nothing beyond p itself
+            brk = !in_win;
+            brk0 = in_win;
+            if (!in_win) p += 1;  // a short p: m <= U - 1 skips nothing beyond p itself
             mode = kModeScan;
-            hi = U + 1 < kScanW ? U + 1 : kScanW;
+            hi = U + 1 + in_win < kScanW ? U + 1 + in_win : kScanW;
         }
 #endif
         if (mode == kModeScan) {
@@ -1537,6 +1545,10 @@ struct MsLaneT {
                     const uint32_t lim = W < 4 * kWin ? W : 4 * kWin;
                     const uint32_t known = (1u << lim) - 1u;
                     longm &= cand & known;  // a position failing the filter is short
+                    if (brk0 && (longm & 1u)) {  // the break position p is long: EXT there
+                        mode = kModeBrkLong;
+                        return 0;
+                    }
                     const uint32_t kshort = (known & ~longm) | (~cand & ((1u << W) - 1u));
                     hit = longm & (longm >> 1);
                     open = cp & ~kshort & ~(kshort >> 1) & ~(known & (known >> 1));
