@@ -434,17 +434,20 @@ def test_gpu_host_api_splits_large_batches_into_passes(ctx):
 
 @pytest.mark.parametrize("pair_bytes", [1, 0])
 @pytest.mark.parametrize("k,tab_u", [(91, 0), (31, 12), (21, 5)])
-def test_gpu_scan_exact_test_paths(ctx, k, tab_u, pair_bytes):
-    """SCAN's exact test through the pair bytes (default) and through the level-U bitmap
-    (pair_bytes = 0): identical records, bit-exact vs the oracle, for filtered (U >= 12)
-    and unfiltered table depths."""
+@pytest.mark.parametrize("win", [-1, 0])
+def test_gpu_scan_exact_test_paths(ctx, k, tab_u, pair_bytes, win):
+    """SCAN on window words (win = -1, the default) or, with win = 0, through the filter and
+    the pair bytes or the level-U bitmap (pair_bytes = 0): identical records, bit-exact vs the
+    oracle, for filtered (U >= 12) and unfiltered table depths."""
     genome = nt.synth_genome(500 + k, 1_000_000)
     ix = nt.Index.build([genome.tobytes()], k, threads=8)
     ctx.set_option("pair_bytes", pair_bytes)
     ctx.set_option("tab_u", tab_u)
+    ctx.set_option("win", win)
     try:
         ctx.upload(ix)
         assert ctx.get_option("pair_bytes") == pair_bytes
+        assert ctx.get_option("win") == (0 if win == 0 else int(ctx.get_option("tab_u") >= 4))
         n, L = 20_000, 150
         reads = nt.synth_reads(genome, 9, 0, n, L, 15_000, threads=8)
         offs = np.arange(0, n * L + 1, L, dtype=np.uint64)
@@ -454,6 +457,7 @@ def test_gpu_scan_exact_test_paths(ctx, k, tab_u, pair_bytes):
     finally:
         ctx.set_option("pair_bytes", 1)
         ctx.set_option("tab_u", 0)
+        ctx.set_option("win", -1)
 
 
 def test_gpu_decode_direct_path_for_long_records(ctx):
