@@ -33,10 +33,42 @@ int ntc_build_index(const uint8_t *seqs, const uint64_t *seq_offsets, uint64_t n
 /* The same index built on ctx's GPU (build.hip; also kbo::build's stand-in, main.rs:111-134):
  * k-mers, radix sort, dummies, LCS and labels in HBM, then rows + LCS to the host.  Equal
  * to ntc_build_index's output for every input.  Synchronous on ctx's stream; no index
- * needs to be uploaded.  NTC_ERR_HIP when device memory runs out (~2 x 8 x W B per k-mer
- * occurrence, W = ceil(2k / 64)).                                                     */
+ * needs to be uploaded.  = ntc_build_index_device_ex with default options.            */
 int ntc_build_index_device(ntc_ctx *ctx, const uint8_t *seqs, const uint64_t *seq_offsets, uint64_t n_seqs,
                            uint32_t k, int add_revcomp, ntc_index_host **out);
+/* Memory bounds of the GPU build: kbo's BuildOpts { mem_gb, temp_dir } (src/cli.rs:56-61,
+ * src/main.rs:111-134).  The k-mers are processed in contiguous colex ranges (their last
+ * 7 characters) small enough that every pass fits device_budget_bytes; sorted ranges wait in
+ * host memory up to host_budget_bytes, past it in unlinked files under temp_dir.  Any input
+ * size works (passes never sort 2^32 keys); the index itself must have < 2^32 nodes.   */
+typedef struct ntc_build_opts {
+    uint64_t device_budget_bytes;  /* 0: 85 % of the device's free memory                          */
+    uint64_t host_budget_bytes;    /* 0: no limit (nothing spills)                                  */
+    const char *temp_dir;          /* NULL: $TMPDIR, else /tmp                                     */
+    uint64_t max_partition_keys;   /* test hook: k-mer occurrences per pass (0: from the budget)    */
+} ntc_build_opts;
+typedef struct ntc_build_stats {
+    uint64_t occurrences;          /* k-mer windows (x2 with reverse complements)                   */
+    uint64_t kmers;                /* distinct k-mers                                               */
+    uint64_t sources;              /* k-mers without an in-neighbour (each brings k-1 dummies)      */
+    uint64_t nodes;                /* index nodes                                                   */
+    uint64_t spilled_bytes;        /* partition bytes written under temp_dir                        */
+    uint64_t device_budget_bytes;  /* the budget used                                               */
+    uint64_t pass_keys;            /* keys per pass                                                 */
+    uint64_t peak_device_bytes;    /* the build's largest device allocation total                   */
+    uint32_t kmer_partitions, node_partitions, compactions, seq_uploads;
+    double seconds, seconds_kmers, seconds_sources, seconds_nodes, seconds_labels;
+} ntc_build_stats;
+int ntc_build_index_device_ex(ntc_ctx *ctx, const uint8_t *seqs, const uint64_t *seq_offsets, uint64_t n_seqs,
+                              uint32_t k, int add_revcomp, const ntc_build_opts *opts, ntc_build_stats *stats,
+                              ntc_index_host **out);
+/* -p/--prefix-precalc (src/cli.rs:46): the colex interval of every p-mer (4^p ranges, first
+ * character most significant, [0, 0) when absent), kept with the index and written by the
+ * NTC_INDEX_SBWT_RS layout as sbwt's PrefixLookupTable [ext, recalled].  p in [0, min(k, 12)];
+ * 0 drops the table.                                                                 */
+int ntc_index_set_prefix_precalc(ntc_index_host *ix, uint32_t p);
+/* the table's p and range count; ranges (2 x 4^p words: start, end) may be NULL          */
+int ntc_index_prefix_table(const ntc_index_host *ix, uint32_t *p, uint64_t *ranges);
 void ntc_index_free(ntc_index_host *ix);
 /* Borrowed view (valid until ntc_index_free) for ntc_index_upload or inspection. */
 int ntc_index_view_of(const ntc_index_host *ix, ntc_index_view *view);

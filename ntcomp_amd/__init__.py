@@ -43,7 +43,8 @@ EXPORTED = [
     "ntc_deflate_block", "ntc_pack_blocks_device", "ntc_encode_pack_batch", "ntc_read_block_into",
     "ntc_fastx_open", "ntc_fastx_next_batch", "ntc_fastx_close", "ntc_fasta_format", "ntc_fastx_next_batch_into",
     "ntc_fastx_set_threads", "ntc_host_threads", "ntc_encode_file", "ntc_decode_fasta",
-    "ntc_decode_file", "ntc_build_index_device",
+    "ntc_decode_file", "ntc_build_index_device", "ntc_build_index_device_ex", "ntc_index_set_prefix_precalc",
+    "ntc_index_prefix_table",
 ]
 
 
@@ -84,6 +85,23 @@ class PipelineStats(ctypes.Structure):
                 ("wall_s", ctypes.c_double), ("alloc_s", ctypes.c_double), ("first_batch_s", ctypes.c_double),
                 ("reader_done_s", ctypes.c_double), ("gpu_done_s", ctypes.c_double), ("threads", ctypes.c_int32), ("reserved", ctypes.c_int32),
                 ("bad_read", ctypes.c_int64), ("error", ctypes.c_char * 256)]
+
+
+class BuildOpts(ctypes.Structure):
+    """ntc_build_opts (include/ntcomp_host.h): memory bounds of the GPU index build."""
+    _fields_ = [("device_budget_bytes", ctypes.c_uint64), ("host_budget_bytes", ctypes.c_uint64),
+                ("temp_dir", ctypes.c_char_p), ("max_partition_keys", ctypes.c_uint64)]
+
+
+class BuildStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in ("occurrences", "kmers", "sources", "nodes", "spilled_bytes",
+                                               "device_budget_bytes", "pass_keys", "peak_device_bytes")] + \
+               [(n, ctypes.c_uint32) for n in ("kmer_partitions", "node_partitions", "compactions", "seq_uploads")] + \
+               [(n, ctypes.c_double) for n in ("seconds", "seconds_kmers", "seconds_sources", "seconds_nodes",
+                                               "seconds_labels")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
 
 
 class Timing(ctypes.Structure):
@@ -160,6 +178,10 @@ def lib():
         "ntc_debug_matching_statistics": (I, [P, P, P, u64, P, P]),
         "ntc_build_index": (I, [P, P, u64, u32, I, I, ctypes.POINTER(P)]),
         "ntc_build_index_device": (I, [P, P, P, u64, u32, I, ctypes.POINTER(P)]),
+        "ntc_build_index_device_ex": (I, [P, P, P, u64, u32, I, ctypes.POINTER(BuildOpts),
+                                          ctypes.POINTER(BuildStats), ctypes.POINTER(P)]),
+        "ntc_index_set_prefix_precalc": (I, [P, u32]),
+        "ntc_index_prefix_table": (I, [P, ctypes.POINTER(u32), P]),
         "ntc_index_free": (None, [P]),
         "ntc_index_view_of": (I, [P, ctypes.POINTER(IndexView)]),
         "ntc_index_save": (I, [P, ctypes.c_char_p]),
@@ -233,15 +255,44 @@ class Index:
         return cls(h)
 
     @classmethod
-    def build_gpu(cls, ctx, seqs, k, add_revcomp=True):
-        """The same index built on ctx's GPU (ntc_build_index_device, build.hip)."""
-        bases, offs = pack_reads(seqs)
+    def build_gpu(cls, ctx, seqs, k, add_revcomp=True, device_budget=0, host_budget=0, temp_dir=None,
+                  max_partition_keys=0, stats=None):
+        """The same index built on ctx's GPU (ntc_build_index_device_ex, build.hip), in
+        passes that fit device_budget bytes (0: 85 % of free HBM), sorted partitions held on
+        the host up to host_budget bytes (0: no limit), past it in files under temp_dir.
+        seqs: list of bytes/str, or a (bases uint8, offsets uint64[n+1]) pair.  stats: a dict
+        filled with ntc_build_stats."""
+        if isinstance(seqs, tuple) and len(seqs) == 2 and isinstance(seqs[0], np.ndarray):
+            bases, offs = np.ascontiguousarray(seqs[0], np.uint8), np.ascontiguousarray(seqs[1], np.uint64)
+        else:
+            bases, offs = pack_reads(seqs)
         h = ctypes.c_void_p()
-        rc = lib().ntc_build_index_device(ctx.h, _p(bases), _p(offs), len(offs) - 1, k, int(add_revcomp),
-                                          ctypes.byref(h))
+        o = BuildOpts(device_budget, host_budget, str(temp_dir).encode() if temp_dir else None, max_partition_keys)
+        st = BuildStats()
+        rc = lib().ntc_build_index_device_ex(ctx.h, _p(bases), _p(offs), len(offs) - 1, k, int(add_revcomp),
+                                             ctypes.byref(o), ctypes.byref(st), ctypes.byref(h))
+        if stats is not None:
+            stats.update(st.as_dict())
         if rc:
             raise NtcError(rc, lib().ntc_last_error(ctx.h).decode(errors="replace"))
         return cls(h)
+
+    def set_prefix_precalc(self, p):
+        """-p/--prefix-precalc: the colex interval of every p-mer (sbwt's PrefixLookupTable),
+        written with the sbwt-rs layout."""
+        rc = lib().ntc_index_set_prefix_precalc(self.h, p)
+        if rc:
+            raise NtcError(rc, f"ntc_index_set_prefix_precalc({p})")
+
+    def prefix_table(self):
+        """(p, ranges uint64[4^p, 2]) or (0, None)."""
+        p = ctypes.c_uint32()
+        lib().ntc_index_prefix_table(self.h, ctypes.byref(p), None)
+        if not p.value:
+            return 0, None
+        r = np.zeros((4 ** p.value, 2), dtype=np.uint64)
+        lib().ntc_index_prefix_table(self.h, ctypes.byref(p), _p(r))
+        return p.value, r
 
     @classmethod
     def load(cls, prefix):

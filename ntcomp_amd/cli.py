@@ -10,8 +10,9 @@ per context, deflate on the host pool, blocks in file order.  Decode: blocks unz
 thread pool (ctypes releases the GIL), batches decode on the GPU contexts, FASTA
 formatting on the pool, output in file order.
 
-Index files: <prefix>.sbwt / <prefix>.lcs in this library's own layout (the sbwt 0.3.11
-byte layout is unavailable offline -- DESIGN.md section 8).
+Index files: <prefix>.sbwt / <prefix>.lcs in this library's own layout, or (--index-format
+sbwt-rs) a recalled restatement of the sbwt 0.3.11 layout with the -p prefix lookup table
+(unpinned offline -- DESIGN.md section 8).
 """
 import argparse
 import sys
@@ -88,15 +89,34 @@ def cmd_build(args):
             for i in range(len(offs) - 1):
                 seqs.append(bases[int(offs[i]):int(offs[i + 1])].tobytes())
         rd.close()
-    if args.builder == "gpu":
-        # the same index built on the GPU (build.hip; tests/test_gpu_build.py: equal to the host build)
-        ctx = nt.GpuContext(args.device)
+    builder = args.builder
+    ctx = None
+    if builder in ("auto", "gpu"):
         try:
-            ix = nt.Index.build_gpu(ctx, seqs, args.kmer_size, add_revcomp=True)
+            ctx = nt.GpuContext(args.device)
+            builder = "gpu"
+        except Exception as e:  # auto without a usable GPU: the host builder
+            if builder == "gpu":
+                raise SystemExit(f"build: --builder gpu: {e}")
+            builder = "host"
+    if builder == "gpu":
+        # the same index built on the GPU (build.hip; tests/test_gpu_build.py: equal to the host
+        # build) in passes that fit -m/--mem-gb of device memory, sorted partitions past the same
+        # amount of host memory spilled to --temp-dir (kbo's BuildOpts, main.rs:111-134)
+        budget = int(args.mem_gb * (1 << 30))
+        stats = {}
+        try:
+            ix = nt.Index.build_gpu(ctx, seqs, args.kmer_size, add_revcomp=True, device_budget=budget,
+                                    host_budget=budget, temp_dir=args.temp_dir, stats=stats)
         finally:
             ctx.close()
+        if args.verbose:
+            log("build: " + ", ".join(f"{k}={v:.3f}" if isinstance(v, float) else f"{k}={v}"
+                                      for k, v in stats.items()))
     else:
         ix = nt.Index.build(seqs, args.kmer_size, add_revcomp=True, threads=args.num_threads)
+    if args.index_format == "sbwt-rs" and args.prefix_precalc:
+        ix.set_prefix_precalc(min(args.prefix_precalc, args.kmer_size, 12))
     log(f"Serializing SBWT index to {args.output_prefix}.sbwt ...")
     log(f"Serializing LCS array to {args.output_prefix}.lcs ...")
     ix.save(args.output_prefix, layout=args.index_format)
@@ -194,15 +214,20 @@ def main(argv=None):
     b.add_argument("-l", "--input-list", help="File with paths or tab separated name and path on each line.")
     b.add_argument("-o", "--output-prefix", required=True, help="Prefix for output files <prefix>.sbwt and <prefix>.lcs.")
     b.add_argument("-k", dest="kmer_size", type=int, default=31, help="k-mer size.")
-    b.add_argument("-p", "--prefix-precalc", type=int, default=8, help="Accepted for compatibility (unused).")
-    b.add_argument("-d", "--dedup-batches", action="store_true", help="Accepted for compatibility (unused).")
+    b.add_argument("-p", "--prefix-precalc", type=int, default=8,
+                   help="Prefix lookup table length (written with --index-format sbwt-rs).")
+    b.add_argument("-d", "--dedup-batches", action="store_true",
+                   help="Deduplicate k-mers per batch (the GPU build always deduplicates a full pass in place).")
     b.add_argument("-t", "--threads", dest="num_threads", type=int, default=1)
-    b.add_argument("-m", "--mem-gb", type=int, default=4, help="Accepted for compatibility (unused).")
-    b.add_argument("--temp-dir", help="Accepted for compatibility (unused; builds in memory).")
+    b.add_argument("-m", "--mem-gb", type=float, default=4,
+                   help="Memory budget in GB: device memory per GPU build pass, and host memory for sorted "
+                        "partitions (past it they spill to --temp-dir).")
+    b.add_argument("--temp-dir", help="Directory for partitions past the memory budget (default $TMPDIR or /tmp).")
     b.add_argument("--verbose", action="store_true")
-    b.add_argument("--builder", choices=["host", "gpu"], default="host",
-                   help="host: threaded C++ builder; gpu: k-mer sort, dummies, LCS and labels on the GPU "
-                        "(same index)")
+    b.add_argument("--builder", choices=["auto", "host", "gpu"], default="auto",
+                   help="auto (default): the GPU when one is usable, else the host; host: threaded C++ builder "
+                        "(in memory); gpu: k-mer sort, dummies, LCS and labels on the GPU in memory-bounded "
+                        "passes (same index)")
     b.add_argument("--device", type=int, default=0, help="GPU for --builder gpu")
     b.add_argument("--index-format", choices=["own", "sbwt-rs"], default="own",
                    help="own layout (default) or a restatement of sbwt 0.3.11/kbo 0.5.1 files (parity unpinned); "

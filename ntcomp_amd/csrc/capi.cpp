@@ -77,8 +77,10 @@ struct ntc_ctx {
         uint64_t *rec_out, *rec_offs;
     } call4{};
     uint32_t ent_slots_opt = 0;     // secondary entry slots per read (0: auto, 24 with joint runs, else 4)
-    double epool_per_read = 4.0;    // overflow pool sizes per read, raised to what calls needed
+    double epool_per_read = 4.0;    // overflow pools: a floor per read (the test hook pool_per_read sets it)
     double rpool_per_read = 1.0;
+    double epool_per_base = 0.0;    // and what the last call's reads reserved per base (learn_pool_rates)
+    double rpool_per_base = 0.0;
     uint64_t spill_reruns = 0;      // calls re-run with grown pools
     uint32_t tab_u_opt = 0;  // suffix-table depth for the next upload (0 = default_tab_u)
     int tab_u_fallback = 0;  // last upload: the default depth did not fit, U = 14 was used
@@ -128,7 +130,20 @@ int ensure(ntc_ctx *ctx, int slot, uint64_t bytes, void **out) {
             b.bytes = 0;
         }
         uint64_t want = bytes + bytes / 8;  // headroom for slightly larger next calls
-        HIP_TRY(ctx, hipMalloc(&b.p, want));
+        if (hipMalloc(&b.p, want) != hipSuccess) {
+            (void)hipGetLastError();
+            b.p = nullptr;
+            want = bytes;  // no headroom when memory is short
+            if (hipMalloc(&b.p, want) != hipSuccess) {
+                (void)hipGetLastError();
+                b.p = nullptr;
+                size_t fr = 0, tot = 0;
+                (void)hipMemGetInfo(&fr, &tot);
+                return set_err(ctx, NTC_ERR_CAPACITY,
+                               "device workspace of " + std::to_string(bytes) + " bytes does not fit (" +
+                                   std::to_string(fr) + " bytes free): split the batch");
+            }
+        }
         b.bytes = want;
     }
     *out = b.p;
@@ -200,8 +215,15 @@ int encode4_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, u
     // the rest of a read's entries / records go to overflow pools sized from what earlier
     // calls reserved (a call that runs out is re-run with the pools grown, read_status).
     const uint32_t S = ent_slots(ctx);
-    const uint64_t pcap = std::min<uint64_t>((uint64_t)(ctx->epool_per_read * (double)n_reads) + 4096, kPoolMax);
-    const uint64_t rcap = std::min<uint64_t>((uint64_t)(ctx->rpool_per_read * (double)n_reads) + 4096, kPoolMax);
+    // A read never holds more entries or records than it has positions, so this call's bases
+    // bound both pools whatever rate an earlier call (e.g. one of long reads) left behind.
+    const uint64_t pos_cap = total_bases + 4 * n_reads + 4096;  // + reservations rounded to 4-entry groups
+    auto pool_size = [&](double per_read, double per_base) {
+        const double want = std::max(per_read * (double)n_reads, per_base * (double)total_bases);
+        return std::min<uint64_t>(std::min<uint64_t>((uint64_t)want + 4096, pos_cap), kPoolMax);
+    };
+    const uint64_t pcap = pool_size(ctx->epool_per_read, ctx->epool_per_base);
+    const uint64_t rcap = pool_size(ctx->rpool_per_read, ctx->rpool_per_base);
     if ((rc = ensure(ctx, WS_Q, (total_bases / 32 + 4) * 8, &p))) return rc;
     a.Q = (uint64_t *)p;
     if ((rc = ensure(ctx, WS_ES, (n_reads + 1) * S * sizeof(Entry), &p))) return rc;
@@ -254,10 +276,20 @@ int encode4_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, u
     launch_emit4(a, wave_off, (uint64_t *)tmp, d_rec_offs, d_rec_out, cap, ctx->stream);
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
-    launch_status_box(ctx->d_status, d_rec_offs + n_reads, nullptr, ctx->h_box, ctx->stream);
+    launch_status_box(ctx->d_status, d_rec_offs + n_reads, (const uint64_t *)(a.counter + kPoolCntE),
+                      (const uint64_t *)(a.counter + kPoolCntR), ctx->h_box, ctx->stream);
     HIP_TRY(ctx, hipGetLastError());
     ctx->box_valid = true;
     return NTC_OK;
+}
+
+// Pool rates for the next call: what this call's reads reserved (plus a quarter) per input
+// base.  Taken from the latest call alone and per base, not per read, so a batch of long
+// reads does not inflate the pools of later batches of short ones.
+void learn_pool_rates(ntc_ctx *ctx, uint64_t cnt_e, uint64_t cnt_r) {
+    const double b = (double)(ctx->call4.total_bases ? ctx->call4.total_bases : 1);
+    ctx->epool_per_base = 1.25 * (double)cnt_e / b;
+    ctx->rpool_per_base = 1.25 * (double)cnt_r / b;
 }
 
 int encode_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, uint64_t n_reads,
@@ -317,9 +349,7 @@ int regrow_and_rerun(ntc_ctx *ctx) {
     uint64_t cnt[2] = {0, 0};
     HIP_TRY(ctx, hipMemcpy(&cnt[0], ctx->last4.counter + kPoolCntE, 8, hipMemcpyDeviceToHost));
     HIP_TRY(ctx, hipMemcpy(&cnt[1], ctx->last4.counter + kPoolCntR, 8, hipMemcpyDeviceToHost));
-    const double n = (double)(ctx->call4.n_reads ? ctx->call4.n_reads : 1);
-    if (cnt[0] > ctx->last4.pcap) ctx->epool_per_read = std::max(ctx->epool_per_read, 1.25 * (double)cnt[0] / n);
-    if (cnt[1] > ctx->last4.rcap) ctx->rpool_per_read = std::max(ctx->rpool_per_read, 1.25 * (double)cnt[1] / n);
+    learn_pool_rates(ctx, cnt[0], cnt[1]);
     if ((cnt[0] > kPoolMax || cnt[1] > kPoolMax))
         return set_err(ctx, NTC_ERR_CAPACITY, "entry / record overflow past 2^32 slots: split the batch");
     ctx->spill_reruns++;
@@ -339,6 +369,8 @@ int read_status(ntc_ctx *ctx, int64_t *bad_index) {
         }
         if (st == ~0ULL) {
             if (bad_index) *bad_index = -1;
+            if (ctx->box_valid && ctx->last == kEncode && ctx->last_variant == 4)
+                learn_pool_rates(ctx, ((volatile uint64_t *)ctx->h_box)[2], ((volatile uint64_t *)ctx->h_box)[3]);
             return NTC_OK;
         }
         if (st == kStatusRegrow) {
@@ -379,8 +411,9 @@ int pack_blocks_impl(ntc_ctx *ctx, const uint64_t *d_recs, const uint64_t *d_rof
     if (ends[1] < ends[0]) return set_err(ctx, NTC_ERR_INVALID_ARG, "record offsets decrease");
     void *d_chunks, *d_meta;
     int rc;
-    // chunks of block b at rec_begin + b (at most n_recs + 1 chunks per block)
-    if ((rc = ensure(ctx, WS_PACK_CHUNKS, (ends[1] + n_blocks + 1) * 8, &d_chunks))) return rc;
+    // chunks of block b at rec_begin + rec_begin / 31 + 2 b (pack.hip chunk_base: room for
+    // 32 bases in every short record)
+    if ((rc = ensure(ctx, WS_PACK_CHUNKS, (ends[1] + ends[1] / 31 + 2 * n_blocks + 2) * 8, &d_chunks))) return rc;
     const uint64_t meta_bytes = n_blocks * (sizeof(PackStats) + sizeof(PackParams) + 32);
     if ((rc = ensure(ctx, WS_PACK_META, meta_bytes, &d_meta))) return rc;
     PackStats *d_stats = (PackStats *)d_meta;
@@ -834,6 +867,7 @@ int ntc_ctx_set_option(ntc_ctx *ctx, const char *key, int64_t value) {
     if (std::strcmp(key, "pool_per_read") == 0) {  // test hook: overflow pools per read (entries, records)
         if (value < 0) return set_err(ctx, NTC_ERR_INVALID_ARG, "pool_per_read must be >= 0");
         ctx->epool_per_read = ctx->rpool_per_read = (double)value;
+        ctx->epool_per_base = ctx->rpool_per_base = 0.0;
         return NTC_OK;
     }
     if (std::strcmp(key, "encode_variant") == 0) {
@@ -878,6 +912,8 @@ int ntc_ctx_get_option(const ntc_ctx *ctx, const char *key, int64_t *value) {
     else if (std::strcmp(key, "pack_us") == 0) *value = (int64_t)(ctx->last_pack_ms * 1000.0);
     else if (std::strcmp(key, "ent_slots") == 0) *value = ent_slots(ctx);
     else if (std::strcmp(key, "spill_reruns") == 0) *value = (int64_t)ctx->spill_reruns;
+    else if (std::strcmp(key, "pool_entries") == 0) *value = (int64_t)ctx->last4.pcap;  // last call's pools
+    else if (std::strcmp(key, "pool_records") == 0) *value = (int64_t)ctx->last4.rcap;
     else if (std::strcmp(key, "workspace_bytes") == 0) {  // device workspace held now (all slots)
         uint64_t t = 0;
         for (const auto &b : ctx->ws) t += b.bytes;
@@ -1103,7 +1139,7 @@ int ntc_decode_batch_device(ntc_ctx *ctx, const uint64_t *d_recs, uint64_t n_rec
     HIP_TRY(ctx, hipEventRecord(ctx->ev[3], ctx->stream));  // k_dec_rec alone: ev[1] -> ev[3]
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
-    launch_status_box(ctx->d_status, pfs + tiles, pls + tiles, ctx->h_box, ctx->stream);
+    launch_status_box(ctx->d_status, pfs + tiles, pls + tiles, nullptr, ctx->h_box, ctx->stream);
     HIP_TRY(ctx, hipGetLastError());
     ctx->box_valid = true;
     return NTC_OK;
@@ -1417,21 +1453,79 @@ int ntc_build_index(const uint8_t *seqs, const uint64_t *seq_offsets, uint64_t n
 
 int ntc_build_index_device(ntc_ctx *ctx, const uint8_t *seqs, const uint64_t *seq_offsets, uint64_t n_seqs,
                            uint32_t k, int add_revcomp, ntc_index_host **out) {
+    return ntc_build_index_device_ex(ctx, seqs, seq_offsets, n_seqs, k, add_revcomp, nullptr, nullptr, out);
+}
+
+int ntc_build_index_device_ex(ntc_ctx *ctx, const uint8_t *seqs, const uint64_t *seq_offsets, uint64_t n_seqs,
+                              uint32_t k, int add_revcomp, const ntc_build_opts *opts, ntc_build_stats *stats,
+                              ntc_index_host **out) {
     if (!ctx || !out || !seq_offsets || (n_seqs && !seqs)) return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument");
     if (k < 1 || k > 255) return set_err(ctx, NTC_ERR_UNSUPPORTED, "k must be in [1, 255]");
     *out = nullptr;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     for (uint64_t i = 0; i < n_seqs; i++)
         if (seq_offsets[i + 1] < seq_offsets[i]) return set_err(ctx, NTC_ERR_INVALID_ARG, "sequence offsets decrease");
+    BuildOpts o;
+    if (opts) {
+        o.device_budget = opts->device_budget_bytes;
+        o.host_budget = opts->host_budget_bytes;
+        o.max_partition_keys = opts->max_partition_keys;
+        if (opts->temp_dir && *opts->temp_dir) o.temp_dir = opts->temp_dir;
+    }
+    if (o.temp_dir.empty()) {
+        const char *t = std::getenv("TMPDIR");
+        o.temp_dir = t && *t ? t : "/tmp";
+    }
     auto *h = new ntc_index_host();
     std::string err;
-    if (!build_index_device(ctx->stream, seqs, seq_offsets, n_seqs, k, add_revcomp != 0, h->ix, err)) {
+    BuildStats st;
+    const bool ok = build_index_device(ctx->stream, seqs, seq_offsets, n_seqs, k, add_revcomp != 0, o, h->ix, st, err);
+    if (stats) {
+        stats->occurrences = st.occurrences;
+        stats->kmers = st.kmers;
+        stats->sources = st.sources;
+        stats->nodes = st.nodes;
+        stats->spilled_bytes = st.spilled_bytes;
+        stats->device_budget_bytes = st.device_budget;
+        stats->pass_keys = st.pass_keys;
+        stats->peak_device_bytes = st.peak_device_bytes;
+        stats->kmer_partitions = st.kmer_partitions;
+        stats->node_partitions = st.node_partitions;
+        stats->compactions = st.compactions;
+        stats->seq_uploads = st.seq_uploads;
+        stats->seconds = st.seconds;
+        stats->seconds_kmers = st.seconds_kmers;
+        stats->seconds_sources = st.seconds_sources;
+        stats->seconds_nodes = st.seconds_nodes;
+        stats->seconds_labels = st.seconds_labels;
+    }
+    if (!ok) {
         delete h;
-        return set_err(ctx, err.rfind("hip", 0) == 0 || err.find("allocation") != std::string::npos ? NTC_ERR_HIP
-                                                                                                      : NTC_ERR_FORMAT,
-                       "ntc_build_index_device: " + err);
+        const int code = err.rfind("hip", 0) == 0 ? NTC_ERR_HIP
+                         : err.find("allocation") != std::string::npos || err.find("budget") != std::string::npos
+                             ? NTC_ERR_CAPACITY
+                         : err.find("temp-dir") != std::string::npos || err.find("partition file") != std::string::npos
+                             ? NTC_ERR_IO
+                             : NTC_ERR_FORMAT;
+        return set_err(ctx, code, "ntc_build_index_device: " + err);
     }
     *out = h;
+    return NTC_OK;
+}
+
+int ntc_index_set_prefix_precalc(ntc_index_host *ix, uint32_t p) {
+    if (!ix || p > 12 || p > ix->ix.k) return NTC_ERR_INVALID_ARG;
+    ix->ix.prefix_len = p;
+    ix->ix.prefix_ranges.clear();
+    if (p) prefix_table(ix->ix, p, ix->ix.prefix_ranges);
+    return NTC_OK;
+}
+
+int ntc_index_prefix_table(const ntc_index_host *ix, uint32_t *p, uint64_t *ranges) {
+    if (!ix || !p) return NTC_ERR_INVALID_ARG;
+    *p = ix->ix.prefix_len;
+    if (ranges && !ix->ix.prefix_ranges.empty())
+        std::memcpy(ranges, ix->ix.prefix_ranges.data(), ix->ix.prefix_ranges.size() * 8);
     return NTC_OK;
 }
 

@@ -16,7 +16,10 @@
 //   BitVector  = u64 ones, RawVector, Option<rank>, Option<select>, Option<select_zero>
 //   .sbwt = u64 L, "plain-matrix" (the variant id, L bytes), then SbwtIndex<SubsetMatrix>:
 //           4 BitVectors (rows A, C, G, T; n bits each), Vec<u64> C (4 entries),
-//           u64 n_sets (= n), u64 k, prefix lookup table (u64 prefix_len = 0, Vec<u64> empty)
+//           u64 n_sets (= n), u64 k, prefix lookup table (sbwt's PrefixLookupTable, -p /
+//           --prefix-precalc, src/cli.rs:46): u64 prefix_len p, u64 4^p, then per p-mer
+//           (first character most significant) its colex interval as u64 start, u64 end
+//           ([0, 0) when absent; p = 0: the single range [0, n))
 //   .lcs  = IntVector of n entries, width = bits of k
 // Written with every Option None; read tolerantly (Options are skipped by their size).
 // load_index detects the layout from the first 8 bytes.
@@ -97,7 +100,13 @@ bool save_sbwt_rs(const HostIndex &ix, const std::string &prefix, std::string &e
         }
         ok = ok && wr64(f.f, 4);
         for (int c = 0; c < 4 && ok; c++) ok = wr64(f.f, ix.C[c]);
-        ok = ok && wr64(f.f, ix.n) && wr64(f.f, ix.k) && wr64(f.f, 0) && wr64(f.f, 0);
+        ok = ok && wr64(f.f, ix.n) && wr64(f.f, ix.k);
+        if (ix.prefix_len && ix.prefix_ranges.size() == 2 * (1ULL << (2 * ix.prefix_len))) {
+            ok = ok && wr64(f.f, ix.prefix_len) && wr64(f.f, ix.prefix_ranges.size() / 2) &&
+                 wr(f.f, ix.prefix_ranges.data(), ix.prefix_ranges.size() * 8);
+        } else {
+            ok = ok && wr64(f.f, 0) && wr64(f.f, 1) && wr64(f.f, 0) && wr64(f.f, ix.n);
+        }
         if (!ok) { err = "write failed: " + prefix + ".sbwt"; return false; }
     }
     {
@@ -153,6 +162,18 @@ bool load_sbwt_rs(const std::string &prefix, HostIndex &ix, std::string &err) {
         }
         ix.n = n;
         ix.k = (uint32_t)k;
+        // the prefix lookup table (absent in files written before round 4)
+        uint64_t p = 0, nr = 0;
+        ix.prefix_len = 0;
+        ix.prefix_ranges.clear();
+        if (rd64(f.f, p) && rd64(f.f, nr) && p >= 1 && p <= 12 && nr == (1ULL << (2 * p))) {
+            ix.prefix_ranges.resize(2 * nr);
+            if (!rd(f.f, ix.prefix_ranges.data(), 16 * nr)) {
+                err = prefix + ".sbwt: truncated prefix lookup table";
+                return false;
+            }
+            ix.prefix_len = (uint32_t)p;
+        }
     }
     {
         File f(prefix + ".lcs", "rb");
@@ -176,6 +197,49 @@ bool load_sbwt_rs(const std::string &prefix, HostIndex &ix, std::string &err) {
     return true;
 }
 }  // namespace
+
+// sbwt's search from [0, n) per character (extend_right: [C[c] + rank_c(l), C[c] + rank_c(r))),
+// level by level: the p-mer X.c has index 4 idx(X) + c
+void prefix_table(const HostIndex &ix, uint32_t p, std::vector<uint64_t> &ranges) {
+    const uint64_t nw = (ix.n + 63) / 64;
+    std::vector<uint64_t> cum[4];  // ones before every 8th word
+    for (int c = 0; c < 4; c++) {
+        cum[c].assign(nw / 8 + 2, 0);
+        uint64_t acc = 0;
+        for (uint64_t w = 0; w < nw; w++) {
+            if (w % 8 == 0) cum[c][w / 8] = acc;
+            acc += (uint64_t)__builtin_popcountll(ix.rows[c][w]);
+        }
+        cum[c][nw / 8 + 1] = acc;
+        if (nw % 8 == 0) cum[c][nw / 8] = acc;
+    }
+    auto rank = [&](int c, uint64_t i) {  // ones of row c in [0, i)
+        const uint64_t w = i / 64;
+        uint64_t r = cum[c][w / 8];
+        for (uint64_t x = w / 8 * 8; x < w; x++) r += (uint64_t)__builtin_popcountll(ix.rows[c][x]);
+        if (i % 64) r += (uint64_t)__builtin_popcountll(ix.rows[c][w] & ((1ULL << (i % 64)) - 1));
+        return r;
+    };
+    std::vector<uint64_t> cur = {0, ix.n}, nxt;
+    for (uint32_t d = 1; d <= p; d++) {
+        nxt.assign(cur.size() * 4, 0);
+        for (uint64_t x = 0; x < cur.size() / 2; x++) {
+            const uint64_t l = cur[2 * x], r = cur[2 * x + 1];
+            for (int c = 0; c < 4; c++) {
+                uint64_t a = 0, b = 0;
+                if (l < r) {
+                    a = ix.C[c] + rank(c, l);
+                    b = ix.C[c] + rank(c, r);
+                }
+                if (a >= b) a = b = 0;
+                nxt[2 * (4 * x + c)] = a;
+                nxt[2 * (4 * x + c) + 1] = b;
+            }
+        }
+        cur.swap(nxt);
+    }
+    ranges.swap(cur);
+}
 
 bool save_index_as(const HostIndex &ix, const std::string &prefix, int layout, std::string &err) {
     if (layout == kIndexSbwtRs) return save_sbwt_rs(ix, prefix, err);

@@ -11,8 +11,21 @@ namespace ntc {
 
 struct HostIndex;
 // GPU index build (build.hip): the host builder's index (sbwt_build.cpp), built on stream s
+// in bucket-range partitions whose passes fit device_budget (0: 85 % of the free HBM);
+// sorted partitions wait in host memory up to host_budget (0: no limit), past it in files
+// under temp_dir.  max_partition_keys caps a pass (test hook, 0: from the budget).
+struct BuildOpts {
+    uint64_t device_budget = 0, host_budget = 0, max_partition_keys = 0;
+    std::string temp_dir;
+};
+struct BuildStats {
+    uint64_t occurrences = 0, kmers = 0, sources = 0, nodes = 0;
+    uint64_t spilled_bytes = 0, device_budget = 0, pass_keys = 0, peak_device_bytes = 0;
+    uint32_t kmer_partitions = 0, node_partitions = 0, compactions = 0, seq_uploads = 0;
+    double seconds = 0, seconds_kmers = 0, seconds_sources = 0, seconds_nodes = 0, seconds_labels = 0;
+};
 bool build_index_device(hipStream_t s, const uint8_t *seqs, const uint64_t *offs, uint64_t n_seqs, uint32_t k,
-                        bool revcomp, HostIndex &out, std::string &err);
+                        bool revcomp, const BuildOpts &o, HostIndex &out, BuildStats &st, std::string &err);
 
 struct EncodeArgs {
     DevIndex ix;
@@ -148,8 +161,8 @@ void launch_dec_tiles(const uint64_t *recs, uint64_t n, uint64_t *pf, uint64_t *
                       uint64_t *tmp, hipStream_t s);
 void launch_dec_walk(const DecWalkArgs &a, hipStream_t s);
 void launch_rank2(const DevIndex &ix, Rank2Chunk *out, hipStream_t s);
-void launch_status_box(const unsigned long long *status, const uint64_t *a, const uint64_t *b, uint64_t *box,
-                       hipStream_t s);
+void launch_status_box(const unsigned long long *status, const uint64_t *a, const uint64_t *b, const uint64_t *c,
+                       uint64_t *box, hipStream_t s);
 void launch_walk_build(const uint32_t *pred, const uint8_t *code, uint64_t n, WalkStep *a, WalkStep *b,
                        WalkEntry *out, hipStream_t s);
 uint64_t scan_tmp_words(uint64_t n);

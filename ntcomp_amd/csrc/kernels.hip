@@ -434,15 +434,16 @@ __global__ __launch_bounds__(256) void k_emit4(Enc4Args a, const uint64_t *wave_
 // the call's status and up to two counts into the host mailbox (pinned memory): thread t
 // writes word t with a vector store; the host reads it after one stream sync
 __global__ __launch_bounds__(64) void k_status_box(const unsigned long long *status, const uint64_t *a,
-                                                   const uint64_t *b, uint64_t *box) {
+                                                   const uint64_t *b, const uint64_t *c, uint64_t *box) {
     const uint32_t t = threadIdx.x;
-    if (t >= 3) return;
-    const uint64_t v = t == 0 ? (uint64_t)*status : t == 1 ? (a ? *a : 0) : (b ? *b : 0);
+    if (t >= 4) return;
+    const uint64_t *src = t == 1 ? a : t == 2 ? b : c;
+    const uint64_t v = t == 0 ? (uint64_t)*status : (src ? *src : 0);
     box[t] = v;  // per-lane address: a vector store
 }
-void launch_status_box(const unsigned long long *status, const uint64_t *a, const uint64_t *b, uint64_t *box,
-                       hipStream_t s) {
-    hipLaunchKernelGGL(k_status_box, dim3(1), dim3(64), 0, s, status, a, b, box);
+void launch_status_box(const unsigned long long *status, const uint64_t *a, const uint64_t *b, const uint64_t *c,
+                       uint64_t *box, hipStream_t s) {
+    hipLaunchKernelGGL(k_status_box, dim3(1), dim3(64), 0, s, status, a, b, c, box);
 }
 
 // rows of scratch a tile of 64 reads needs = longest read, rounded up to 32

@@ -13,7 +13,12 @@ struct HostIndex {
     std::vector<uint64_t> rows[4];  // ceil(n/64) words each, LSB-first
     uint64_t C[4] = {0, 0, 0, 0};
     std::vector<uint8_t> lcs;       // n bytes
+    // -p/--prefix-precalc lookup table (sbwt PrefixLookupTable): [start, end) per p-mer
+    uint32_t prefix_len = 0;
+    std::vector<uint64_t> prefix_ranges;  // 2 * 4^prefix_len words
 };
+// colex interval of every p-mer, first character most significant (index_io.cpp)
+void prefix_table(const HostIndex &ix, uint32_t p, std::vector<uint64_t> &ranges);
 
 void build_index(const uint8_t *seqs, const uint64_t *offs, uint64_t nseqs, uint32_t k,
                  bool revcomp, int threads, HostIndex &out);

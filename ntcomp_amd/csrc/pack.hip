@@ -51,6 +51,12 @@ static_assert(kS4Tile * 63 / 64 + 4 <= kBuf1, "s4 tile must fit the s1 buffer");
 
 __device__ __forceinline__ uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
 
+// First s4 chunk slot of block b whose records start at beg.  A block of n records holds at
+// most 32 n short bases (from_2bit's limit; longer ones are flagged bad), i.e. ceil(32 n / 31)
+// <= n + floor(n / 31) + 1 chunks, and chunk_base(end, b + 1) - chunk_base(beg, b) >=
+// n + floor(n / 31) + 2, so neighbouring blocks never overlap (pack_chunk_words sizes it).
+__device__ __forceinline__ uint64_t chunk_base(uint64_t beg, uint64_t b) { return beg + beg / 31 + 2 * b; }
+
 // 3-way exclusive block scan of u64 values (kPackThreads threads); sh: 3 * 16 words
 __device__ __forceinline__ void block_scan3(const uint64_t v[3], uint64_t ex[3], uint64_t tot[3], uint64_t *sh) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -161,7 +167,7 @@ __global__ void __launch_bounds__(kPackThreads) k_pack_stats(const uint64_t *rec
     const uint64_t b = blockIdx.x;
     const uint64_t r0 = b * block_reads, r1 = r0 + block_reads < n_reads ? r0 + block_reads : n_reads;
     const uint64_t beg = roffs[r0], end = roffs[r1];
-    uint64_t *ch = chunks + beg + b;  // block b's chunks (at most n_recs + 1)
+    uint64_t *ch = chunks + chunk_base(beg, b);  // block b's chunks (up to 32 bases per short record)
     uint64_t n_long = 0, max1 = 0, sum2 = 0, sum3 = 0, max4 = 0, bad = 0;
     uint64_t T = 0;  // short bases so far
     for (uint64_t i = threadIdx.x; i < kChunkBufWords; i += kPackThreads) cbuf[i] = 0;
@@ -352,7 +358,7 @@ __global__ void __launch_bounds__(kPackThreads) k_pack_write(const uint64_t *rec
         }
     }
     // s4: minimal binary over the block's chunks, 2 chunks per thread per tile, in buf1
-    const uint64_t *ch = chunks + beg + b;
+    const uint64_t *ch = chunks + chunk_base(beg, b);
     const uint64_t nch = (S.T + 30) / 31;
     uint64_t p4 = 0;
     for (uint64_t t0 = 0; t0 < nch; t0 += kS4Tile) {

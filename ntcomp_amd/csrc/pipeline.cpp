@@ -693,7 +693,12 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
 
     // ---- assigner + writer (this thread) ------------------------------------------------------------
     struct stat ost;
-    const bool seekable = fstat(out_fd, &ost) == 0 && S_ISREG(ost.st_mode);
+    // pwrite only into a regular file opened without O_APPEND (Linux pwrite ignores the
+    // offset under O_APPEND); the shared file offset is moved past the text at the end, so
+    // `{ decode a; decode b; } > out` keeps both outputs as the reference's stdout does
+    const int fl = fcntl(out_fd, F_GETFL);
+    const bool seekable = fstat(out_fd, &ost) == 0 && S_ISREG(ost.st_mode) && fl >= 0 && !(fl & O_APPEND) &&
+                          lseek(out_fd, 0, SEEK_CUR) >= 0;
     off_t out_pos = seekable ? lseek(out_fd, 0, SEEK_CUR) : 0;
     auto write_text = [&](const uint8_t *p, uint64_t n) -> bool {
         if (seekable && n > (8u << 20) && T > 1) {  // parallel pwrite into the page cache
@@ -780,6 +785,7 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
         if (sl.text) (void)hipHostFree(sl.text);
     }
     if (data) munmap((void *)data, fsize);
+    if (seekable) (void)lseek(out_fd, out_pos, SEEK_SET);
     const int result = sh.error == -1 ? NTC_OK : sh.error;
     S.dropped_blocks = blocks.size() - S.blocks;  // after a damaged block (or none)
     S.alloc_s += t_pin.load();

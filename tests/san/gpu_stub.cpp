@@ -1,0 +1,106 @@
+// Test stub (tests/san only): the GPU stage of the native pipelines on the CPU, so that
+// ntc_encode_file / ntc_decode_file (pipeline.cpp) run their host threads under the
+// sanitizers.  ntc_encode_pack_batch = the C oracle's encode (oracle/ntcomp_oracle.c, the
+// test checker) + the host packer (ntc_pack_block); ntc_decode_fasta = the oracle's decode
+// + ">seq.N" lines.  Nothing here ships: the product path is capi.cpp + the HIP kernels.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/ntcomp_codec.h"
+#include "../../include/ntcomp_gpu.h"
+#include "../../ntcomp_amd/csrc/ntc_internal.h"
+
+extern "C" {
+struct orc_index;
+orc_index *orc_index_new(uint64_t n, uint32_t k, const uint64_t *rowA, const uint64_t *rowC, const uint64_t *rowG,
+                         const uint64_t *rowT, const uint64_t *Carr, const uint8_t *lcs, uint32_t precalc);
+void orc_index_free(orc_index *ix);
+int64_t orc_encode_batch(const orc_index *ix, const uint8_t *bases, const uint64_t *offsets, uint64_t n_reads,
+                         uint64_t *rec_out, uint64_t cap, uint64_t *rec_offsets, int64_t *bad_read);
+int64_t orc_decode(const orc_index *ix, const uint64_t *recs, uint64_t n_recs, uint8_t *out, uint64_t cap,
+                   uint64_t *read_offsets, uint64_t off_cap, uint64_t *n_reads_out);
+}
+
+struct ntc_ctx {
+    const orc_index *ix = nullptr;
+    std::string err;
+};
+
+ntc_ctx *stub_ctx_new(const orc_index *ix) {
+    auto *c = new ntc_ctx();
+    c->ix = ix;
+    return c;
+}
+void stub_ctx_free(ntc_ctx *c) { delete c; }
+
+extern "C" {
+
+const char *ntc_last_error(const ntc_ctx *ctx) { return ctx ? ctx->err.c_str() : "no context"; }
+
+int ntc_encode_pack_batch(ntc_ctx *ctx, const uint8_t *bases, const uint64_t *offs, uint64_t n_reads,
+                          uint32_t block_reads, ntc_block_meta *meta, uint8_t **payload, uint64_t *payload_bytes,
+                          int64_t *bad_read) {
+    *payload = nullptr;
+    *payload_bytes = 0;
+    if (bad_read) *bad_read = -1;
+    const uint64_t total = n_reads ? offs[n_reads] - offs[0] : 0;
+    std::vector<uint64_t> recs(total + 1), roff(n_reads + 1);
+    std::vector<uint64_t> rel(n_reads + 1);
+    for (uint64_t r = 0; r <= n_reads; r++) rel[r] = offs[r] - offs[0];
+    int64_t bad = -1;
+    const int64_t nr = orc_encode_batch(ctx->ix, bases + offs[0], rel.data(), n_reads, recs.data(), recs.size(),
+                                        roff.data(), &bad);
+    if (nr < 0) {
+        if (bad_read) *bad_read = bad;
+        ctx->err = "oracle encode failed";
+        return NTC_ERR_INVALID_BASE;
+    }
+    const uint64_t nb = (n_reads + block_reads - 1) / block_reads;
+    std::vector<uint8_t> all;
+    for (uint64_t b = 0; b < nb; b++) {
+        const uint64_t r0 = b * block_reads, r1 = std::min<uint64_t>(n_reads, r0 + block_reads);
+        uint8_t *p = nullptr;
+        uint64_t len = 0;
+        ntc_pack_block(recs.data() + roff[r0], roff[r1] - roff[r0], r1 - r0, &meta[b], &p, &len);
+        const uint64_t base = all.size();
+        all.insert(all.end(), p, p + len);
+        ntc_buffer_free(p);
+        for (int s = 0; s < 4; s++) meta[b].stream[s].offset += base;
+    }
+    *payload = (uint8_t *)std::malloc(all.size() ? all.size() : 1);
+    if (!all.empty()) std::memcpy(*payload, all.data(), all.size());
+    *payload_bytes = all.size();
+    return NTC_OK;
+}
+
+int ntc_decode_fasta(ntc_ctx *ctx, const uint64_t *recs, uint64_t n_recs, uint64_t n_reads, uint64_t n_bases,
+                     uint64_t first_id, uint8_t *out, uint64_t out_capacity, uint64_t *out_len) {
+    std::vector<uint8_t> b(n_bases + 1);
+    std::vector<uint64_t> ro(n_reads + 2);
+    uint64_t got_reads = 0;
+    const int64_t nb = orc_decode(ctx->ix, recs, n_recs, b.data(), b.size(), ro.data(), ro.size(), &got_reads);
+    if (nb < 0 || (uint64_t)nb != n_bases || got_reads != n_reads) {
+        ctx->err = "oracle decode failed or sizes differ";
+        return NTC_ERR_FORMAT;
+    }
+    std::string text;
+    char hdr[40];
+    for (uint64_t r = 0; r < n_reads; r++) {
+        const int h = std::snprintf(hdr, sizeof(hdr), ">seq.%llu\n", (unsigned long long)(first_id + r));
+        text.append(hdr, (size_t)h);
+        text.append((const char *)b.data() + ro[r], ro[r + 1] - ro[r]);
+        text.push_back('\n');
+    }
+    *out_len = text.size();
+    if (text.size() > out_capacity) {
+        ctx->err = "text capacity";
+        return NTC_ERR_CAPACITY;
+    }
+    std::memcpy(out, text.data(), text.size());
+    return NTC_OK;
+}
+
+}  // extern "C"

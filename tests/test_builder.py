@@ -71,3 +71,43 @@ def test_index_sbwt_rs_layout_round_trip(tmp_path, k):
         assert (x.n, x.k, x.C) == (ix.n, ix.k, ix.C)
         assert all(np.array_equal(p, q) for p, q in zip(x.rows, ix.rows))
         assert np.array_equal(x.lcs, ix.lcs)
+
+
+@pytest.mark.parametrize("k,p", [(7, 1), (7, 3), (15, 4), (31, 5)])
+def test_prefix_table_equals_search_by_definition(k, p):
+    """-p/--prefix-precalc (src/cli.rs:46): every p-mer's colex interval (sbwt's
+    PrefixLookupTable [ext, recalled]) equals the brute-force SBWT's search of that p-mer
+    (tests/golden/make_golden.py NaiveSBWT: the nodes whose suffix is the pattern), [0, 0)
+    when absent; index = the p-mer's 2-bit codes, first character most significant."""
+    import itertools
+    import sys
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_golden import NaiveSBWT
+    rng = np.random.default_rng(k * 10 + p)
+    seqs = ["".join(rng.choice(list("ACGT"), int(n))) for n in (300, 41, 120)]
+    sb = NaiveSBWT(seqs, k)
+    ix = nt.Index.build([s.encode() for s in seqs], k)
+    assert ix.n == sb.n
+    ix.set_prefix_precalc(p)
+    got_p, ranges = ix.prefix_table()
+    assert got_p == p and ranges.shape == (4 ** p, 2)
+    for idx, t in enumerate(itertools.product("ACGT", repeat=p)):
+        r = sb.search("".join(t))
+        assert tuple(int(x) for x in ranges[idx]) == (r if r else (0, 0)), "".join(t)
+
+
+def test_prefix_table_in_sbwt_rs_files(tmp_path):
+    ix = nt.Index.build([nt.synth_genome(3, 20_000).tobytes()], 31)
+    ix.set_prefix_precalc(6)
+    _, exp = ix.prefix_table()
+    ix.save(tmp_path / "rs", layout="sbwt-rs")
+    jx = nt.Index.load(tmp_path / "rs")
+    p, got = jx.prefix_table()
+    assert p == 6 and np.array_equal(got, exp)
+    # no table: the single range [0, n), read back as none
+    ix.set_prefix_precalc(0)
+    ix.save(tmp_path / "rs0", layout="sbwt-rs")
+    assert nt.Index.load(tmp_path / "rs0").prefix_table() == (0, None)
+    with pytest.raises(nt.NtcError):
+        ix.set_prefix_precalc(13)

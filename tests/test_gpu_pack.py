@@ -123,3 +123,22 @@ def test_gpu_pack_empty_and_errors(ctx):
     bad = np.array([5 | (40 << 32) | (1 << 56), (2 | (40 << 2)) << 56], dtype=np.uint64)
     metas, _ = device_pack(ctx, [good, bad, good])
     assert [m.status for m in metas] == [0, 8, 0]
+
+
+def test_gpu_pack_short_records_of_32_bases(ctx):
+    """Short records at from_2bit's 32-base limit: a block of n of them fills ceil(32 n / 31)
+    s4 chunks, more than n + 1, so neighbouring blocks' chunk regions must not overlap
+    (pack.hip chunk_base).  Several such blocks side by side equal the host packer."""
+    rng = np.random.default_rng(5)
+    blocks = []
+    for b in range(5):
+        n = 64 + 37 * b
+        short = rng.integers(0, 1 << 56, n, dtype=np.uint64) | (np.uint64(2 | (32 << 2)) << np.uint64(56))
+        long_ = np.array([7 + b | (40 << 32) | (1 << 56)], dtype=np.uint64)
+        blocks.append(np.concatenate([long_, short]))
+    metas, payload = device_pack(ctx, blocks)
+    for b, m in enumerate(metas):
+        hm, hp = nt.pack_block(blocks[b], 1)
+        assert m.status == hm.status == 0, b
+        assert m.stream[3].num_u64 == hm.stream[3].num_u64 == -(-32 * (len(blocks[b]) - 1) // 31), b
+        assert nt.stream_payloads(m, payload) == nt.stream_payloads(hm, hp), b

@@ -210,3 +210,28 @@ def test_cli_decode_to_a_pipe(setup, tmp_path):
     ctx.close()
     r = _cli("decode", "-i", str(d / "idx"), str(path), "--blocks-per-batch", "1", stdout=subprocess.PIPE)
     assert r.stdout == fasta_of(reads, offs)
+
+
+def test_cli_decode_appends_and_shares_a_redirect(setup, tmp_path):
+    """`decode >> out` (O_APPEND: pwrite would ignore its offset) and `{ decode a; decode b; }
+    > out` (one open file shared by two processes: the writer leaves the file offset past
+    its text) keep every byte in order, as the reference's stdout does (main.rs:203-209).
+    The batches hold > 8 MiB of text, so the parallel pwrite path is the one exercised."""
+    d, genome, ix = setup
+    ctx = nt.GpuContext(0)
+    ctx.upload(ix)
+    reads, offs = ragged(genome, 2 * 65536 + 7, 34, 100, 200)
+    path, _ = encoded_file(ctx, tmp_path, reads, offs)
+    ctx.close()
+    exp = fasta_of(reads, offs)
+    assert len(exp) > (8 << 20)
+    out = tmp_path / "app.fa"
+    out.write_bytes(b"head\n")
+    with open(out, "ab") as f:
+        _cli("decode", "-i", str(d / "idx"), str(path), "--blocks-per-batch", "2", stdout=f)
+    assert out.read_bytes() == b"head\n" + exp
+    shared = tmp_path / "shared.fa"
+    with open(shared, "wb") as f:
+        for _ in range(2):
+            _cli("decode", "-i", str(d / "idx"), str(path), "--blocks-per-batch", "2", stdout=f)
+    assert shared.read_bytes() == exp + exp

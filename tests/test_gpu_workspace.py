@@ -94,6 +94,16 @@ def test_record_pool_rerun_on_long_reads():
     assert np.array_equal(goff, eoff) and np.array_equal(got, exp)
     out, o2 = ctx.decode(got)
     assert np.array_equal(out, bases)
+    # the pools a later batch of short reads gets follow its own bases, not the long reads'
+    # per-read need (rates are learned per base from the latest call)
+    n, L = 20_000, 150
+    short = nt.synth_reads(genome, 6, 0, n, L, 10_000)
+    soffs = np.arange(0, n * L + 1, L, dtype=np.uint64)
+    sexp, _ = OracleIndex(ix.n, 31, ix.rows, ix.C, ix.lcs).encode(short[:2000 * L], soffs[:2001])
+    sgot, _ = ctx.encode(short, soffs)
+    assert np.array_equal(sgot[:len(sexp)], sexp)
+    assert ctx.get_option("pool_entries") <= n * L + 4 * n + 4096
+    assert ctx.get_option("pool_records") <= n * L + 4 * n + 4096
     ctx.close()
 
 
