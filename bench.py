@@ -66,7 +66,7 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--configs", default=None,
-                    help="comma list of encode,decode,strains (default: all three at N=1, encode,decode at N>1)")
+                    help="comma list of encode,decode,strains,c31 (default: all four at N=1, encode,decode at N>1)")
     ap.add_argument("--mode", choices=["encode", "decode"], default=None, help="(legacy) = --configs <mode>")
     ap.add_argument("--k", type=int, default=91)
     ap.add_argument("--reads-per-gpu", type=int, default=None, help="default 10M at N=1, 25M at N>1 (C91x8)")
@@ -173,13 +173,16 @@ def roofline(kname, kernel_ms, kernel_ms_min, units, unit_name, pmc, pmc_note, w
             r["dram_read_bytes"] = int(kd["dram_read_bytes"] * scale)
         roof = random_line_roof(working_set)
         rq, wq = kd.get("rdreq", 0) * scale, (kd.get("wrreq") or 0) * scale
-        req = rq + wq  # every request past L2 occupies the fabric, reads and writes alike
-        if roof and req:
-            rate = req / (kernel_ms / 1e3) / 1e9
-            r["line_rate"] = {"requests_per_launch": int(req), "read_requests_per_launch": int(rq),
-                              "write_requests_per_launch": int(wq), "requests_per_" + unit_name: round(req / units, 3),
-                              "g_requests_per_s": round(rate, 2), "roof_g_requests_per_s": roof,
-                              "frac": round(rate / roof, 4)}
+        if roof and rq:
+            # the random READ lines against the random-read roof (scripts/randbw.hip) of the
+            # kernel's random working set; the writes are streamed (coalesced output), not
+            # random lines, so they are reported beside it, not counted against it
+            rate = rq / (kernel_ms / 1e3) / 1e9
+            r["line_rate"] = {"read_requests_per_launch": int(rq), "write_requests_per_launch": int(wq),
+                              "read_requests_per_" + unit_name: round(rq / units, 3),
+                              "write_requests_per_" + unit_name: round(wq / units, 3),
+                              "g_read_requests_per_s": round(rate, 2), "roof_g_requests_per_s": roof,
+                              "roof_working_set_bytes": working_set, "frac": round(rate / roof, 4)}
         r["pmc_profile_kernel_ms"] = round(kd.get("avg_ns", 0) / 1e6 * scale, 4)
     r["note"] = ("achieved = bytes past L2 per launch (rocprofv3 PMC of this device build, each request at its "
                  "own 32/64/128 B size, plus writes; " + pmc_note + ") / live HIP-event kernel time of isolated "
@@ -187,6 +190,31 @@ def roofline(kname, kernel_ms, kernel_ms_min, units, unit_name, pmc, pmc_note, w
     if extra:
         r.update(extra)
     return r
+
+
+def io_floor(in_bytes, out_bytes, call_ms):
+    """The path's own I/O -- its input read once and its output written once (encode: 1 B
+    of ASCII per base in, 8 B per record out; decode: 8 B per record in, 1 B per base out)
+    -- over the whole call's device time (every kernel), against 8 TB/s: the efficiency a
+    perfect kernel would reach 1.0 on, beside the counter-based frac."""
+    b = in_bytes + out_bytes
+    gbs = b / (call_ms / 1e3) / 1e9
+    return {"bytes_per_call": int(b), "in_bytes": int(in_bytes), "out_bytes": int(out_bytes),
+            "call_ms": round(call_ms, 4), "achieved": round(gbs, 1), "peak": HBM_PEAK_GBPS,
+            "frac": round(gbs / HBM_PEAK_GBPS, 4)}
+
+
+def aggregate_roofline(per_rank, world):
+    """N > 1: every rank's dominant-kernel bytes past L2 summed, over the slowest rank's
+    kernel time, against N x 8 TB/s (BASELINE's 1/2/4/8-GPU fractions)."""
+    rs = [x for x in per_rank if x and x.get("traffic")]
+    if len(rs) != world:
+        return None
+    tot = sum(x["traffic"] for x in rs)
+    tmax = max(x["kernel_ms"] for x in rs)
+    gbs = tot / (tmax / 1e3) / 1e9
+    return {"ranks": world, "traffic": int(tot), "kernel_ms_max": round(tmax, 4), "achieved": round(gbs, 1),
+            "peak": HBM_PEAK_GBPS * world, "unit": "GB/s", "frac": round(gbs / (HBM_PEAK_GBPS * world), 4)}
 
 
 def _opt(ctx, key):
@@ -254,7 +282,8 @@ class Pipe:
         self.ctxs, self.kind = ctxs, kind
         self.pending = [None] * len(ctxs)
         self.i = 0
-        self.kms = []
+        self.kms = []  # the dominant kernel's ms per call
+        self.tms = []  # the whole call's device ms (every kernel of it)
 
     def issue(self, sh, b, check=False):
         c = self.i % len(self.ctxs)
@@ -283,7 +312,9 @@ class Pipe:
                 raise RuntimeError(f"record count changed between passes: {got} vs {b['n_recs']}")
         elif ctx.decode_status() != (b["n"], b["bases"]):
             raise RuntimeError(f"decode status {ctx.decode_status()} != {(b['n'], b['bases'])}")
-        self.kms.append(ctx.timing()["main_ms"])
+        t = ctx.timing()
+        self.kms.append(t["main_ms"])
+        self.tms.append(t["total_ms"])
 
     def drain(self):
         for k in range(len(self.ctxs)):
@@ -304,7 +335,8 @@ def encode_all_outputs(ctxs, sh):
 
 def timed(pipe, sh, steps, warmup, barrier, sync, dist):
     """W untimed steps, then K steps between barrier + sync; a step = one call per batch of
-    the shard through the pipe.  -> (max over ranks of the elapsed time, kernel ms per call)"""
+    the shard through the pipe.  -> (max over ranks of the elapsed time, dominant-kernel ms per
+    call); the whole calls' device ms stay in pipe.tms"""
     from ntcomp_amd import shard as shard_mod
     for _ in range(warmup):
         for b in sh.batches:
@@ -312,7 +344,7 @@ def timed(pipe, sh, steps, warmup, barrier, sync, dist):
     pipe.drain()
     barrier()
     sync()
-    pipe.kms = []
+    pipe.kms, pipe.tms = [], []
     t0 = time.perf_counter()
     for _ in range(steps):
         for b in sh.batches:
@@ -423,7 +455,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    configs = (args.configs or ("encode,decode,strains" if world == 1 else "encode,decode")).split(",")
+    configs = (args.configs or ("encode,decode,strains,c31" if world == 1 else "encode,decode")).split(",")
     reads_per_gpu = args.reads_per_gpu or (10_000_000 if world == 1 else 25_000_000)
 
     import numpy as np
@@ -487,8 +519,9 @@ def main():
 
     build_info = {}
 
-    def setup_index(texts, label, n_ctx):
+    def setup_index(texts, label, n_ctx, kk=None):
         nonlocal ctx
+        kk = kk or k
         if not args.dry_run and ctx is None:
             for _ in range(max(1, args.inflight)):
                 c = nt.GpuContext(device)
@@ -501,9 +534,14 @@ def main():
         seqs = [t.tobytes() for t in texts]
         # the GPU builder (build.hip; equal to the host builder, tests/test_gpu_build.py), the
         # host one for --dry-run
-        index = nt.Index.build(seqs, k, threads=nthreads) if args.dry_run else nt.Index.build_gpu(ctx, seqs, k)
+        bst = {}
+        index = nt.Index.build(seqs, kk, threads=nthreads) if args.dry_run else \
+            nt.Index.build_gpu(ctx, seqs, kk, stats=bst)
         build_info[label] = {"builder": "host" if args.dry_run else "gpu", "seconds": round(time.time() - t0, 3)}
-        log(f"[rank {rank}] {label} index k={k} n={index.n} built in {time.time() - t0:.1f}s ({build_info[label]['builder']})")
+        if bst:
+            build_info[label].update({x: bst[x] for x in ("kmer_partitions", "node_partitions", "occurrences",
+                                                          "peak_device_bytes")})
+        log(f"[rank {rank}] {label} index k={kk} n={index.n} built in {time.time() - t0:.1f}s ({build_info[label]['builder']})")
         if not args.dry_run:
             t0 = time.time()
             for c in ctxs[:n_ctx]:
@@ -516,33 +554,34 @@ def main():
     base_cfg = {"k": k, "read_len": L, "genome_bp": args.genome_bp, "err_ppm": args.err_ppm,
                 "reads_per_gpu": n, "batch_reads": min(args.batch_reads or n, n)}
 
-    # ---- C91 encode / D91 decode -------------------------------------------------
-    if "encode" in configs or "decode" in configs:
-        index = setup_index([genome], "C", len(ctxs) or max(1, args.inflight))
+    def c_block(kk, want_enc, want_dec, label, cpu_secs):
+        """C{kk} encode (+ D{kk} decode) of this rank's shard: the timed lines, rooflines
+        (dominant kernel per launch; at N > 1 also summed over ranks), I/O floor, parity on an
+        oracle sample (every rank) and, on rank 0, the oracle on one pinned core."""
+        index = setup_index([genome], label, len(ctxs) or max(1, args.inflight), kk)
         sh = Shard(nt, ctx, genome, first, n, L, args.err_ppm, args.batch_reads, nthreads, args.dry_run,
                    args.presort, n_out=len(ctxs))
-        log(f"[rank {rank}] reads {first}..{first + n} in {len(sh.batches)} batch(es)")
-        orc = OracleIndex(index.n, k, index.rows, index.C, index.lcs)
+        log(f"[rank {rank}] {label}{kk}: reads {first}..{first + n} in {len(sh.batches)} batch(es)")
+        orc = OracleIndex(index.n, kk, index.rows, index.C, index.lcs)
         n_recs = None
         if not args.dry_run:
             encode_all_outputs(ctxs, sh)
             n_recs = sum(b["n_recs"] for b in sh.batches)
         enc = dec = None
-        iso = {}  # kernel ms of isolated launches (one context, one call at a time): the roofline's
-        # denominator -- with calls in flight, a launch shares the GPU with the other context's
-        # kernels and its event time measures both
+        iso = {}  # isolated launches (one context, one call at a time): the roofline's denominator --
+        # with calls in flight, a launch shares the GPU with the other context's kernels
         n_iso = max(3, len(sh.batches))
-        if "encode" in configs and not args.dry_run:
+        if want_enc and not args.dry_run:
             enc = timed(Pipe(ctxs, "encode"), sh, args.steps, args.warmup, barrier, sync, dist)
-            iso["encode"] = timed(Pipe(ctxs[:1], "encode"), sh, n_iso, 0, barrier, sync, dist)[1] \
-                if len(ctxs) > 1 else enc[1]
+            ip = Pipe(ctxs[:1], "encode")
+            iso["encode"] = (timed(ip, sh, n_iso, 0, barrier, sync, dist)[1], list(ip.tms))
             encode_all_outputs(ctxs, sh)  # the timed calls alternate contexts: refresh every output
-        if "decode" in configs and not args.dry_run:
+        if want_dec and not args.dry_run:
             dec = timed(Pipe(ctxs, "decode"), sh, args.steps, args.warmup, barrier, sync, dist)
-            iso["decode"] = timed(Pipe(ctxs[:1], "decode"), sh, n_iso, 0, barrier, sync, dist)[1] \
-                if len(ctxs) > 1 else dec[1]
-        pin = world == 1
-        secs = args.cpu_seconds if (world == 1 and not args.no_cpu) else (0 if args.no_cpu else 2.0)
+            ip = Pipe(ctxs[:1], "decode")
+            iso["decode"] = (timed(ip, sh, n_iso, 0, barrier, sync, dist)[1], list(ip.tms))
+        pin = rank == 0
+        secs = 0 if args.no_cpu else (cpu_secs if rank == 0 else 2.0)
         chk = check_shard(ctx, orc, sh, secs, dec is not None, pin, args.dry_run) if secs > 0 else None
         verdicts = gather({"rank": rank, "first": first, "n": n, "check": chk})
         units_all = sh.bases * world * args.steps
@@ -551,91 +590,119 @@ def main():
                "reads_checked_per_rank": [v["check"]["reads_checked"] for v in verdicts] if chk else None,
                "shards": [[v["first"], v["n"]] for v in verdicts]}
         cpu = None
-        if chk and world == 1 and not args.no_cpu:
+        if chk and rank == 0 and not args.no_cpu:
             cv = chk["reads_checked"] * L / chk["cpu_encode_s"] / 1e6
             avail = nt.host_threads()
             cpu = {"value": round(cv, 3), "unit": "Mbases/s", "cores": 1, "kind": "port",
                    "sample": f"{chk['reads_checked']} reads ({chk['reads_checked'] * L} bases) from the start of "
                              f"each batch, faithful C oracle (oracle/ntcomp_oracle.c) on one pinned core "
-                             f"({chk['core']}) of {os.cpu_count()}",
+                             f"({chk['core']}) of {os.cpu_count()}" +
+                             (f"; rank 0 of {world}, while the other ranks check their own samples" if world > 1
+                              else ""),
                    "cpu_model": cpu_model(), "logical_cpus": os.cpu_count(), "cpus_available": avail,
                    "cpus_available_note": "min(affinity mask, cgroup v2 CPU quota): the CPUs this process may use"}
-            av, an = cpu_all_cores(orc, sh, chk["spans"], avail)
-            cpu["all_cores"] = {"value": round(av, 3), "unit": "Mbases/s", "cores": avail, "kind": "port",
-                                "sample": f"the same {an} reads, read-sharded over {avail} threads of the "
-                                          f"reentrant C oracle (wall clock)"}
-        wl_c = (f"C{k}: {n} x {L}bp synthetic reads per GPU ({args.err_ppm / 1e4:g}% subst, 50% revcomp) vs SBWT "
-                f"of a {args.genome_bp / 1e6:g} Mbp synthetic genome (+revcomp), k={k}"
+            if world == 1:
+                av, an = cpu_all_cores(orc, sh, chk["spans"], avail)
+                cpu["all_cores"] = {"value": round(av, 3), "unit": "Mbases/s", "cores": avail, "kind": "port",
+                                    "sample": f"the same {an} reads, read-sharded over {avail} threads of the "
+                                              f"reentrant C oracle (wall clock)"}
+        wl_c = (f"C{kk}: {n} x {L}bp synthetic reads per GPU ({args.err_ppm / 1e4:g}% subst, 50% revcomp) vs SBWT "
+                f"of a {args.genome_bp / 1e6:g} Mbp synthetic genome (+revcomp), k={kk}"
                 + (f"; {world} GPUs x {n} = {world * n} reads" if world > 1 else ""))
-        cfg = dict(base_cfg, workload=wl_c, index_nodes=index.n, records_per_gpu=n_recs,
+        cfg = dict(base_cfg, k=kk, workload=wl_c, index_nodes=index.n, records_per_gpu=n_recs,
                    suffix_table_u=None if args.dry_run else ctx.get_option("tab_u"),
                    workspace_gb_per_context=None if args.dry_run else _gb(_opt(ctx, "workspace_bytes")),
                    spill_reruns=None if args.dry_run else _opt(ctx, "spill_reruns"),
-                   index_build=build_info.get("C"),
+                   index_build=build_info.get(label),
                    parallelism=f"reads sharded over {world} GPU(s), index replicated, no collective",
                    inflight=len(ctxs) or None)
+        out = {}
         if enc is not None:
             el, kms = enc
             b0 = sh.batches[0]
-            kavg, kmin = launch_ms(iso["encode"], [b["n"] for b in sh.batches], b0["n"])
-            kin = launch_ms(kms, [b["n"] for b in sh.batches], b0["n"])[0]
-            rl = roofline("k_ms4", kavg, kmin, b0["n"], "read", pmc, pmc_note, f"C{k}",
-                          {"kernel_ms_inflight": round(kin, 4), "isolated_launches": len(iso["encode"]),
+            units = [b["n"] for b in sh.batches]
+            kavg, kmin = launch_ms(iso["encode"][0], units, b0["n"])
+            call_ms = launch_ms(iso["encode"][1], units, b0["n"])[0]
+            kin = launch_ms(kms, units, b0["n"])[0]
+            rl = roofline("k_ms4", kavg, kmin, b0["n"], "read", pmc, pmc_note, f"C{kk}",
+                          {"kernel_ms_inflight": round(kin, 4), "isolated_launches": len(iso["encode"][0]),
                            "reference_work_avoided": round(
                               b0["bases"] * (1 + 2 * 64) / (kavg / 1e3) / 1e9 / HBM_PEAK_GBPS, 3),
                            "reference_work_note": "SURVEY 8(d) B_enc (1 B + two 64 B rank lines per base) / "
                                                   "kernel time / peak: the reference algorithm's bytes this "
                                                   "kernel's suffix table and path runs avoid; not a roofline"})
-            metric = METRIC if k == 91 else METRIC.replace("k=91", f"k={k}")
-            line.update({"metric": metric, "value": round(units_all / el / 1e6, 2), "unit": "Mbases/s",
-                         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-                         "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
-                         "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-                         "data": "synthetic (seeded; reads regenerate per shard)", "config": cfg,
-                         "roofline": rl, "cpu_baseline": cpu, "parity": par,
-                         "kernel_ms_per_step": round(sum(kms) / args.steps, 3)})
+            rl["io_floor"] = io_floor(b0["bases"], 8 * n_recs * b0["n"] / n, call_ms)
+            if world > 1:
+                rl["aggregate"] = aggregate_roofline(gather({"traffic": rl.get("traffic"), "kernel_ms": kavg}), world)
+            metric = METRIC if kk == 91 else METRIC.replace("k=91", f"k={kk}")
+            out.update({"metric": metric, "value": round(units_all / el / 1e6, 2), "unit": "Mbases/s",
+                        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                        "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+                        "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+                        "data": "synthetic (seeded; reads regenerate per shard)", "config": cfg,
+                        "roofline": rl, "cpu_baseline": cpu, "parity": par,
+                        "kernel_ms_per_step": round(sum(kms) / args.steps, 3)})
             if cpu:
-                cpu["speedup_gpu_vs_cpu"] = round(line["value"] / cpu["value"], 1)
-                cpu["all_cores"]["speedup_gpu_vs_cpu"] = round(line["value"] / cpu["all_cores"]["value"], 1)
+                cpu["speedup_gpu_vs_cpu"] = round(out["value"] / cpu["value"], 1)
+                if "all_cores" in cpu:
+                    cpu["all_cores"]["speedup_gpu_vs_cpu"] = round(out["value"] / cpu["all_cores"]["value"], 1)
         if dec is not None:
             el, kms = dec
             b0 = sh.batches[0]
-            kavg, kmin = launch_ms(iso["decode"], [b["bases"] for b in sh.batches], b0["bases"])
-            kin = launch_ms(kms, [b["bases"] for b in sh.batches], b0["bases"])[0]
+            units = [b["bases"] for b in sh.batches]
+            kavg, kmin = launch_ms(iso["decode"][0], units, b0["bases"])
+            call_ms = launch_ms(iso["decode"][1], units, b0["bases"])[0]
+            kin = launch_ms(kms, units, b0["bases"])[0]
             dcpu = None
-            if chk and chk["cpu_decode_s"] > 0 and world == 1:
+            if chk and chk["cpu_decode_s"] > 0 and rank == 0:
                 dcpu = {"value": round(chk["cpu_decode_bases"] / chk["cpu_decode_s"] / 1e6, 3), "unit": "Mbases/s",
                         "cores": 1, "kind": "port",
                         "sample": f"oracle decode of {chk['cpu_decode_bases']} bases of oracle records, one pinned core"}
-            d = {"metric": f"decode Mbases/sec at k={k}, 150bp reads (output bases), MI355X; bit-exact vs CPU",
+            drl = roofline("k_dec_rec", kavg, kmin, b0["bases"], "base", pmc, pmc_note, f"D{kk}",
+                           {"kernel_ms_inflight": round(kin, 4), "isolated_launches": len(iso["decode"][0])},
+                           working_set=index.n * 32)
+            drl["io_floor"] = io_floor(8 * n_recs * b0["n"] / n, b0["bases"], call_ms)
+            if world > 1:
+                drl["aggregate"] = aggregate_roofline(gather({"traffic": drl.get("traffic"), "kernel_ms": kavg}),
+                                                      world)
+            d = {"metric": f"decode Mbases/sec at k={kk}, 150bp reads (output bases), MI355X; bit-exact vs CPU",
                  "value": round(units_all / el / 1e6, 2), "unit": "Mbases/s",
                  "ms_per_step": round(el / args.steps * 1e3, 3),
-                 "config": {"workload": f"D{k}: decode of the C{k} records ({n_recs} records, {n} reads per GPU) "
-                                        f"-> bases via the inverse-SBWT walk, k={k}"},
-                 "roofline": roofline("k_dec_rec", kavg, kmin, b0["bases"], "base", pmc, pmc_note, f"D{k}",
-                                      {"kernel_ms_inflight": round(kin, 4), "isolated_launches": len(iso["decode"])},
-                                      working_set=index.n * 32),
-                 "cpu_baseline": dcpu,
+                 "config": {"workload": f"D{kk}: decode of the C{kk} records ({n_recs} records, {n} reads per GPU) "
+                                        f"-> bases via the inverse-SBWT walk, k={kk}"},
+                 "roofline": drl, "cpu_baseline": dcpu,
                  "parity": {"round_trip_exact_all_ranks": all(v["check"]["decode_ok"] for v in verdicts)
                             if chk else None, "bases_checked_per_rank": n * L if chk else None},
                  "kernel_ms_per_step": round(sum(kms) / args.steps, 3)}
             if dcpu:
                 d["cpu_baseline"]["speedup_gpu_vs_cpu"] = round(d["value"] / dcpu["value"], 1)
-            if line:
-                line["decode"] = d
+            if out:
+                out["decode"] = d
             else:
-                line.update({"metric": d["metric"], "value": d["value"], "unit": "Mbases/s", "n_gpus": world,
-                             "steps": args.steps, "warmup": args.warmup, "ms_per_step": d["ms_per_step"],
-                             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-                             "data": "synthetic (seeded; reads regenerate per shard)",
-                             "config": dict(cfg, workload=d["config"]["workload"]), "roofline": d["roofline"],
-                             "cpu_baseline": d["cpu_baseline"], "parity": dict(par, **d["parity"])})
+                out.update({"metric": d["metric"], "value": d["value"], "unit": "Mbases/s", "n_gpus": world,
+                            "steps": args.steps, "warmup": args.warmup, "ms_per_step": d["ms_per_step"],
+                            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+                            "data": "synthetic (seeded; reads regenerate per shard)",
+                            "config": dict(cfg, workload=d["config"]["workload"]), "roofline": d["roofline"],
+                            "cpu_baseline": d["cpu_baseline"], "parity": dict(par, **d["parity"])})
         if args.dry_run:
-            line.update({"metric": METRIC, "value": None, "unit": "Mbases/s", "n_gpus": world, "dry_run": True,
-                         "config": cfg, "parity": par})
+            out.update({"metric": METRIC, "value": None, "unit": "Mbases/s", "n_gpus": world, "dry_run": True,
+                        "config": cfg, "parity": par})
         if not args.dry_run:
             sh.free(ctx)
-        del sh
+        return out
+
+    # ---- C91 encode / D91 decode -------------------------------------------------
+    if "encode" in configs or "decode" in configs:
+        line.update(c_block(k, "encode" in configs, "decode" in configs, "C",
+                            args.cpu_seconds if world == 1 else args.cpu_seconds / 2))
+    # ---- C31: BASELINE configs[1], the same reads at k = 31 -----------------------------
+    if "c31" in configs:
+        c31 = c_block(31, True, False, "C31_", 4.0)
+        if line:
+            line["c31"] = c31
+        else:
+            line.update(c31)
 
     # ---- S91: strain collection ------------------------------------------------------
     if "strains" in configs:
@@ -663,20 +730,27 @@ def main():
             s["config"]["joint_runs"] = bool(ctx.get_option("joint"))
             s["config"]["entry_slots_per_read"] = 4 + (_opt(ctx, "ent_slots") or 0)
             s["config"]["index_build"] = build_info.get("S")
-            el, kms = timed(Pipe(sctx, "encode"), sh, args.steps, args.warmup, barrier, sync, dist)
+            pe = Pipe(sctx, "encode")
+            el, kms = timed(pe, sh, args.steps, args.warmup, barrier, sync, dist)
             s["config"]["workspace_gb_per_context"] = _gb(_opt(ctx, "workspace_bytes"))
             s["config"]["spill_reruns"] = _opt(ctx, "spill_reruns")
             b0 = sh.batches[0]
-            kavg, kmin = launch_ms(kms, [b["n"] for b in sh.batches], b0["n"])
+            units = [b["n"] for b in sh.batches]
+            kavg, kmin = launch_ms(kms, units, b0["n"])
+            srecs = s["config"]["records_per_gpu"]
+            srl = roofline("k_ms4", kavg, kmin, b0["n"], "read", pmc, pmc_note, f"S{k}")
+            srl["io_floor"] = io_floor(b0["bases"], 8 * srecs * b0["n"] / ns, launch_ms(pe.tms, units, b0["n"])[0])
             s.update(value=round(sh.bases * world * args.steps / el / 1e6, 2), unit="Mbases/s",
-                     ms_per_step=round(el / args.steps * 1e3, 3),
-                     roofline=roofline("k_ms4", kavg, kmin, b0["n"], "read", pmc, pmc_note, f"S{k}"))
-            el, kms = timed(Pipe(sctx, "decode"), sh, args.steps, args.warmup, barrier, sync, dist)
-            kavg, kmin = launch_ms(kms, [b["bases"] for b in sh.batches], b0["bases"])
+                     ms_per_step=round(el / args.steps * 1e3, 3), roofline=srl)
+            pd = Pipe(sctx, "decode")
+            el, kms = timed(pd, sh, args.steps, args.warmup, barrier, sync, dist)
+            units = [b["bases"] for b in sh.batches]
+            kavg, kmin = launch_ms(kms, units, b0["bases"])
+            sdrl = roofline("k_dec_rec", kavg, kmin, b0["bases"], "base", pmc, pmc_note, f"SD{k}",
+                            working_set=index.n * 32)
+            sdrl["io_floor"] = io_floor(8 * srecs * b0["n"] / ns, b0["bases"], launch_ms(pd.tms, units, b0["bases"])[0])
             s["decode"] = {"value": round(sh.bases * world * args.steps / el / 1e6, 2), "unit": "Mbases/s",
-                           "ms_per_step": round(el / args.steps * 1e3, 3),
-                           "roofline": roofline("k_dec_rec", kavg, kmin, b0["bases"], "base", pmc, pmc_note,
-                                                f"SD{k}", working_set=index.n * 32)}
+                           "ms_per_step": round(el / args.steps * 1e3, 3), "roofline": sdrl}
         secs = 0 if args.no_cpu else 3.0
         chk = check_shard(ctx, orc, sh, secs, not args.dry_run, False, args.dry_run) if secs > 0 else None
         vs = gather(chk)

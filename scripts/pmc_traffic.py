@@ -14,6 +14,7 @@ its workloads by dispatch order (bench.py with --inflight I contexts):
   C91 encode calls: I (every context's outputs) + W + K (timed, I in flight) + N isolated
       (one at a time, I > 1 only: the roofline's denominator) + I (outputs refreshed)
   D91 decode calls: W + K (timed) + N isolated (I > 1 only)
+  C31 encode calls (when the trace has them): as C91, after D91
   S91: 1 + W + K encode calls, SD91: W + K decode calls (one context)
 avg_ns is the isolated launches' mean (the timed ones where I = 1); avg_ns_inflight the
 timed launches' mean.
@@ -80,6 +81,8 @@ def main():
     ap.add_argument("--read-len", type=int, default=150)
     ap.add_argument("--inflight", type=int, default=2, help="bench.py --inflight of the kernel-trace pass")
     ap.add_argument("--iso", type=int, default=3, help="isolated calls bench.py times after the timed region")
+    ap.add_argument("--no-c31", dest="with_c31", action="store_false",
+                    help="the kernel-trace pass ran without the C31 block (bench.py --configs without c31)")
     a = ap.parse_args()
     import ntcomp_amd as nt
 
@@ -94,24 +97,31 @@ def main():
     I, WK = a.inflight, a.warmup + a.steps
     N = a.iso if I > 1 else 0
     c_total = I + WK + N + I
-    dur = {"C91": {}, "D91": {}, "S91": {}, "SD91": {}}
-    inflight = {"C91": {}, "D91": {}}
+    dur = {"C91": {}, "D91": {}, "C31": {}, "S91": {}, "SD91": {}}
+    inflight = {"C91": {}, "D91": {}, "C31": {}}
+    n_c = 2 if a.with_c31 else 1  # C blocks before S91
     for kname in ("k_ms4", "k_parse4", "k_pack", "k_emit4"):
         xs = seq.get(kname, [])
         timed = xs[I:I + WK]
         dur["C91"][kname] = mean(xs[I + WK:I + WK + N]) if N else mean(timed)
         inflight["C91"][kname] = mean(timed)
-        dur["S91"][kname] = mean(xs[c_total + 1:c_total + 1 + WK]) if len(xs) >= c_total + 1 + WK else None
+        if a.with_c31:
+            c = c_total
+            dur["C31"][kname] = mean(xs[c + I + WK:c + I + WK + N]) if N else mean(xs[c + I:c + I + WK])
+            inflight["C31"][kname] = mean(xs[c + I:c + I + WK])
+        s0 = n_c * c_total + 1
+        dur["S91"][kname] = mean(xs[s0:s0 + WK]) if len(xs) >= s0 + WK else None
     for kname in ("k_dec_rec", "k_dec_tiles"):
         xs = seq.get(kname, [])
         dur["D91"][kname] = mean(xs[WK:WK + N]) if N else mean(xs[:WK])
         inflight["D91"][kname] = mean(xs[:WK])
         dur["SD91"][kname] = mean(xs[WK + N:WK + N + WK]) if len(xs) >= WK + N + WK else None
 
-    units = {"C91": (a.reads, "read"), "S91": (a.reads, "read"),
+    units = {"C91": (a.reads, "read"), "S91": (a.reads, "read"), "C31": (a.reads, "read"),
              "D91": (a.reads * a.read_len, "base"), "SD91": (a.reads * a.read_len, "base")}
     src = {"C91": ("encode", ("k_ms4", "k_parse4", "k_pack", "k_emit4")),
            "D91": ("decode", ("k_dec_rec", "k_dec_tiles")),
+           "C31": ("c31", ("k_ms4", "k_parse4", "k_pack", "k_emit4")),
            "S91": ("strains", ("k_ms4", "k_parse4", "k_pack", "k_emit4")),
            "SD91": ("strains", ("k_dec_rec", "k_dec_tiles"))}
     out = {"device_source_hash": nt.device_source_hash(), "collected": time.strftime("%Y-%m-%d %H:%M"),

@@ -10,7 +10,7 @@ OUT=${OUT:-gpurun_out/prof}
 TAG=${TAG:-r02}
 KRE=${KRE:-'k_ms4|k_parse4|k_pack|k_emit4|k_dec_rec|k_dec_tiles'}
 BENCH_KT=${BENCH_KT:-"--steps 20 --warmup 5"}
-WORKLOADS=${WORKLOADS:-"encode decode strains"}
+WORKLOADS=${WORKLOADS:-"encode decode c31 strains"}
 PASSES=${PASSES:-"kt rd wr misc"}
 mkdir -p "$OUT"
 export TMPDIR=/tmp

@@ -30,7 +30,7 @@ def test_bench_spawns_ranks_without_torchrun():
     assert par["ranks"] == 2 and par["shards"] == [[0, 4000], [4000, 4000]]
     assert par["encode_bit_exact_all_ranks"] is True
     assert all(c > 0 for c in par["reads_checked_per_rank"])
-    assert "[rank 1] reads 4000..8000 in 3 batch(es)" in err
+    assert "[rank 1] C91: reads 4000..8000 in 3 batch(es)" in err
 
 
 def test_bench_default_sizing_is_c91x8_per_gpu_at_n_gt_1():
