@@ -58,6 +58,8 @@ typedef struct ntc_build_stats {
     uint64_t peak_device_bytes;    /* the build's largest device allocation total                   */
     uint32_t kmer_partitions, node_partitions, compactions, seq_uploads;
     double seconds, seconds_kmers, seconds_sources, seconds_nodes, seconds_labels;
+    double seconds_plan;           /* of seconds_kmers: sequence upload + occurrence histogram      */
+    double seconds_sort;           /* every radix sort of the build                                 */
 } ntc_build_stats;
 int ntc_build_index_device_ex(ntc_ctx *ctx, const uint8_t *seqs, const uint64_t *seq_offsets, uint64_t n_seqs,
                               uint32_t k, int add_revcomp, const ntc_build_opts *opts, ntc_build_stats *stats,

@@ -98,7 +98,7 @@ class BuildStats(ctypes.Structure):
                                                "device_budget_bytes", "pass_keys", "peak_device_bytes")] + \
                [(n, ctypes.c_uint32) for n in ("kmer_partitions", "node_partitions", "compactions", "seq_uploads")] + \
                [(n, ctypes.c_double) for n in ("seconds", "seconds_kmers", "seconds_sources", "seconds_nodes",
-                                               "seconds_labels")]
+                                               "seconds_labels", "seconds_plan", "seconds_sort")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

@@ -176,48 +176,94 @@ __device__ __forceinline__ uint64_t wave_append(uint32_t n_mine, unsigned long l
     return base + incl - n_mine;
 }
 
+// Block-level append: kEmitPer positions per thread (strided by the block, coalesced), the
+// block's in-range keys counted first (a 2-bit mask per position kept in a register), one
+// atomic per block of 4096 positions, then the keys built and stored.  (A wave-level atomic
+// on the one counter serialised at ~170 M/s and bounded the pass.)
+constexpr uint32_t kEmitPer = 16;
+constexpr uint32_t kEmitTile = 256 * kEmitPer;
+
+// exclusive block scan of one u32 per thread (256 threads); *total for the block
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t *sh, uint32_t &total) {
+    const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
+    uint32_t incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_up(incl, d, 64);
+        if ((int)lane >= d) incl += t;
+    }
+    if (lane == 63) sh[wid] = incl;
+    __syncthreads();
+    uint32_t base = 0;
+    total = 0;
+    for (uint32_t w = 0; w < 4; w++) {
+        base += w < wid ? sh[w] : 0;
+        total += sh[w];
+    }
+    __syncthreads();
+    return base + incl - v;
+}
+
 template <int W>
 __global__ __launch_bounds__(256) void k_emit_kmers(const uint8_t *cb, const uint8_t *ok, uint64_t g0, uint64_t p0,
                                                     uint64_t p1, uint32_t k, uint32_t rc, uint32_t m, uint32_t blo,
                                                     uint32_t bhi, uint64_t *acc, uint64_t stride,
                                                     unsigned long long *cnt) {
-    const uint64_t p = p0 + (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    uint32_t inf = 0, ing = 0;
-    const uint64_t i = p - g0;
-    if (p < p1 && ok[i]) {
+    __shared__ uint32_t sh[4];
+    __shared__ unsigned long long sbase;
+    const uint64_t t0 = p0 + (uint64_t)blockIdx.x * kEmitTile;
+    uint32_t mask = 0, mine = 0;  // bits 2j, 2j + 1: forward / reverse complement of position j
+#pragma unroll
+    for (uint32_t j = 0; j < kEmitPer; j++) {
+        const uint64_t p = t0 + threadIdx.x + 256 * j;
+        if (p >= p1) continue;
+        const uint64_t i = p - g0;
+        if (!ok[i]) continue;
         uint32_t bf, bg;
         kmer_buckets(cb, i, k, m, bf, bg);
-        inf = bf >= blo && bf < bhi;
-        ing = rc && bg >= blo && bg < bhi;
+        const uint32_t inf = bf >= blo && bf < bhi, ing = rc && bg >= blo && bg < bhi;
+        mask |= (inf | (ing << 1)) << (2 * j);
+        mine += inf + ing;
     }
-    const uint64_t slot = wave_append(inf + ing, cnt);
-    if (!(inf | ing)) return;
-    uint64_t f[W], g[W];
+    uint32_t total;
+    const uint32_t ex = block_excl_scan256(mine, sh, total);
+    if (threadIdx.x == 0) sbase = total ? atomicAdd(cnt, (unsigned long long)total) : 0;
+    __syncthreads();
+    uint64_t slot = sbase + ex;
+    while (mask) {
+        const uint32_t j = (uint32_t)__builtin_ctz(mask) / 2;
+        const uint32_t two = (mask >> (2 * j)) & 3u;
+        mask &= ~(3u << (2 * j));
+        const uint64_t i = t0 + threadIdx.x + 256 * j - g0;
+        uint64_t f[W], g[W];
 #pragma unroll
-    for (int j = 0; j < W; j++) f[j] = g[j] = 0;
-    for (uint32_t t = 0; t < k; t++) {
-        // forward: character t is seq[p - t]; reverse complement: t is the complement of
-        // seq[p - k + 1 + t]
-        const uint64_t c = cb[i - t] & 3;
-        const uint64_t r = 3 - (uint64_t)(cb[i - k + 1 + t] & 3);
-        const uint32_t j = t / 32, sh = 62 - 2 * (t % 32);
+        for (int q = 0; q < W; q++) f[q] = g[q] = 0;
+        for (uint32_t t = 0; t < k; t++) {
+            // forward: character t is seq[p - t]; reverse complement: t is the complement of
+            // seq[p - k + 1 + t]
+            const uint64_t c = cb[i - t] & 3;
+            const uint64_t r = 3 - (uint64_t)(cb[i - k + 1 + t] & 3);
+            const uint32_t jj = t / 32, sft = 62 - 2 * (t % 32);
 #pragma unroll
-        for (int q = 0; q < W; q++)
-            if (q == (int)j) {
-                f[q] |= c << sh;
-                g[q] |= r << sh;
-            }
+            for (int q = 0; q < W; q++)
+                if (q == (int)jj) {
+                    f[q] |= c << sft;
+                    g[q] |= r << sft;
+                }
+        }
+        if (two & 1) {
+            if (slot < stride)
+#pragma unroll
+                for (int q = 0; q < W; q++) acc[(uint64_t)q * stride + slot] = f[q];
+            slot++;
+        }
+        if (two & 2) {
+            if (slot < stride)
+#pragma unroll
+                for (int q = 0; q < W; q++) acc[(uint64_t)q * stride + slot] = g[q];
+            slot++;
+        }
     }
-    uint64_t s = slot;
-    if (inf) {
-        if (s < stride)
-#pragma unroll
-            for (int j = 0; j < W; j++) acc[(uint64_t)j * stride + s] = f[j];
-        s++;
-    }
-    if (ing && s < stride)
-#pragma unroll
-        for (int j = 0; j < W; j++) acc[(uint64_t)j * stride + s] = g[j];
 }
 
 // ---- sort / unique ----------------------------------------------------------------------
@@ -526,13 +572,113 @@ class KeyStore {
         Part p;
         p.base = total_;
         p.n = n;
+        if (!place(p, n, err)) return false;
+        if (n) {
+            BTRY(hipMemcpyAsync((void *)p.wp, d_keys, (uint64_t)W_ * n * 8, hipMemcpyDeviceToHost, s));
+            if (with_len_) BTRY(hipMemcpyAsync((void *)p.lp, d_len, n, hipMemcpyDeviceToHost, s));
+            BTRY(hipStreamSynchronize(s));
+        }
+        for (size_t b = 0; b < hist.size(); b++) bucket_cnt_[b] += hist[b];
+        total_ += n;
+        parts_.push_back(std::move(p));
+        return true;
+    }
+    // keep d_keys / d_len (allocated from the build's arena) as the partition itself: later
+    // uploads are device-to-device copies, so a build that fits one pass never round-trips
+    // its keys through the host
+    void add_device(uint64_t *d_keys, uint8_t *d_len, uint64_t n, const std::vector<uint64_t> &hist) {
+        Part p;
+        p.base = total_;
+        p.n = n;
+        p.dw = d_keys;
+        p.dl = d_len;
+        for (size_t b = 0; b < hist.size(); b++) bucket_cnt_[b] += hist[b];
+        total_ += n;
+        parts_.push_back(std::move(p));
+    }
+    uint64_t device_bytes() const {
+        uint64_t b = 0;
+        for (const Part &p : parts_)
+            if (p.dw) b += p.n * (8 * (uint64_t)W_ + (with_len_ ? 1 : 0));
+        return b;
+    }
+    // device partitions -> host memory (or files past the host budget), device buffers freed
+    template <class Ar>
+    bool evict(Ar &A, hipStream_t s, std::string &err) {
+        for (Part &p : parts_) {
+            if (!p.dw) continue;
+            Part h;
+            if (!place(h, p.n, err)) return false;
+            if (p.n) {
+                BTRY(hipMemcpyAsync((void *)h.wp, p.dw, (uint64_t)W_ * p.n * 8, hipMemcpyDeviceToHost, s));
+                if (with_len_) BTRY(hipMemcpyAsync((void *)h.lp, p.dl, p.n, hipMemcpyDeviceToHost, s));
+                BTRY(hipStreamSynchronize(s));
+            }
+            A.release(p.dw);
+            A.release(p.dl);
+            h.base = p.base;
+            h.n = p.n;
+            p = std::move(h);
+        }
+        return true;
+    }
+    template <class Ar>
+    void release_device(Ar &A) {
+        for (Part &p : parts_) {
+            A.release(p.dw);
+            A.release(p.dl);
+            p.dw = nullptr;
+            p.dl = nullptr;
+        }
+    }
+    void finalize() {
+        bucket_begin_.assign(bucket_cnt_.size() + 1, 0);
+        for (size_t b = 0; b < bucket_cnt_.size(); b++) bucket_begin_[b + 1] = bucket_begin_[b] + bucket_cnt_[b];
+    }
+    uint64_t bucket_begin(uint64_t b) const { return bucket_begin_[std::min<uint64_t>(b, bucket_cnt_.size())]; }
+    const std::vector<uint64_t> &bucket_counts() const { return bucket_cnt_; }
+    size_t n_parts() const { return parts_.size(); }
+    uint64_t part_base(size_t i) const { return parts_[i].base; }
+    uint64_t part_n(size_t i) const { return parts_[i].n; }
+
+    // global keys [a, b) into a device SoA at stride (offset off), counts into d_len + off
+    bool upload(uint64_t a, uint64_t b, uint64_t *d_keys, uint64_t stride, uint64_t off, uint8_t *d_len,
+                hipStream_t s, std::string &err) const {
+        for (const Part &p : parts_) {
+            const uint64_t lo = std::max(a, p.base), hi = std::min(b, p.base + p.n);
+            if (lo >= hi) continue;
+            const uint64_t i0 = lo - p.base, cnt = hi - lo, o = off + (lo - a);
+            const uint64_t *w = p.dw ? p.dw : p.wp;
+            const uint8_t *l = p.dw ? p.dl : p.lp;
+            const hipMemcpyKind kind = p.dw ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+            for (int j = 0; j < W_; j++)
+                BTRY(hipMemcpyAsync(d_keys + (uint64_t)j * stride + o, w + (uint64_t)j * p.n + i0, cnt * 8, kind, s));
+            if (with_len_ && d_len) BTRY(hipMemcpyAsync(d_len + o, l + i0, cnt, kind, s));
+        }
+        BTRY(hipStreamSynchronize(s));
+        return true;
+    }
+
+  private:
+    struct Part {
+        uint64_t base = 0, n = 0;
+        std::vector<uint64_t> w;
+        std::vector<uint8_t> len;
+        void *map = nullptr;
+        size_t map_bytes = 0;
+        const uint64_t *wp = nullptr;
+        const uint8_t *lp = nullptr;
+        uint64_t *dw = nullptr;  // a device-resident partition (add_device)
+        uint8_t *dl = nullptr;
+    };
+    bool place(Part &p, uint64_t n, std::string &err) {
         const uint64_t bytes = n * (8 * (uint64_t)W_ + (with_len_ ? 1 : 0));
         uint64_t *w = nullptr;
         uint8_t *l = nullptr;
         if (budget_ && host_bytes_ + bytes > budget_ && bytes) {
             // spill: a file under the temp dir, mapped (its pages are the page cache's)
             std::string path = dir_ + "/ntcomp_build_" + std::to_string(getpid()) + "_" +
-                               std::to_string((uint64_t)(uintptr_t)this) + "_" + std::to_string(parts_.size());
+                               std::to_string((uint64_t)(uintptr_t)this) + "_" + std::to_string(files_++);
             const int fd = ::open(path.c_str(), O_RDWR | O_CREAT | O_EXCL, 0600);
             if (fd < 0) {
                 err = "cannot create a partition file in " + dir_ + " (--temp-dir)";
@@ -564,55 +710,11 @@ class KeyStore {
         }
         p.wp = w;
         p.lp = l;
-        if (n) {
-            BTRY(hipMemcpyAsync(w, d_keys, (uint64_t)W_ * n * 8, hipMemcpyDeviceToHost, s));
-            if (with_len_) BTRY(hipMemcpyAsync(l, d_len, n, hipMemcpyDeviceToHost, s));
-            BTRY(hipStreamSynchronize(s));
-        }
-        for (size_t b = 0; b < hist.size(); b++) bucket_cnt_[b] += hist[b];
-        total_ += n;
-        parts_.push_back(std::move(p));
         return true;
     }
-    void finalize() {
-        bucket_begin_.assign(bucket_cnt_.size() + 1, 0);
-        for (size_t b = 0; b < bucket_cnt_.size(); b++) bucket_begin_[b + 1] = bucket_begin_[b] + bucket_cnt_[b];
-    }
-    uint64_t bucket_begin(uint64_t b) const { return bucket_begin_[std::min<uint64_t>(b, bucket_cnt_.size())]; }
-    const std::vector<uint64_t> &bucket_counts() const { return bucket_cnt_; }
-    size_t n_parts() const { return parts_.size(); }
-    uint64_t part_base(size_t i) const { return parts_[i].base; }
-    uint64_t part_n(size_t i) const { return parts_[i].n; }
-
-    // global keys [a, b) into a device SoA at stride (offset off), counts into d_len + off
-    bool upload(uint64_t a, uint64_t b, uint64_t *d_keys, uint64_t stride, uint64_t off, uint8_t *d_len,
-                hipStream_t s, std::string &err) const {
-        for (const Part &p : parts_) {
-            const uint64_t lo = std::max(a, p.base), hi = std::min(b, p.base + p.n);
-            if (lo >= hi) continue;
-            const uint64_t i0 = lo - p.base, cnt = hi - lo, o = off + (lo - a);
-            for (int j = 0; j < W_; j++)
-                BTRY(hipMemcpyAsync(d_keys + (uint64_t)j * stride + o, p.wp + (uint64_t)j * p.n + i0, cnt * 8,
-                                    hipMemcpyHostToDevice, s));
-            if (with_len_ && d_len) BTRY(hipMemcpyAsync(d_len + o, p.lp + i0, cnt, hipMemcpyHostToDevice, s));
-        }
-        BTRY(hipStreamSynchronize(s));
-        return true;
-    }
-
-  private:
-    struct Part {
-        uint64_t base = 0, n = 0;
-        std::vector<uint64_t> w;
-        std::vector<uint8_t> len;
-        void *map = nullptr;
-        size_t map_bytes = 0;
-        const uint64_t *wp = nullptr;
-        const uint8_t *lp = nullptr;
-    };
     int W_;
     bool with_len_;
-    uint64_t budget_, host_bytes_ = 0, total_ = 0;
+    uint64_t budget_, host_bytes_ = 0, total_ = 0, files_ = 0;
     std::string dir_;
     BuildStats *st_;
     std::vector<uint64_t> bucket_cnt_, bucket_begin_;
@@ -655,6 +757,19 @@ double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// NTC_BUILD_TRACE=1: per-step seconds on stderr (stream synchronised at each mark)
+struct Tracer {
+    bool on = std::getenv("NTC_BUILD_TRACE") != nullptr;
+    double t = now_s();
+    void mark(hipStream_t s, const char *what, uint64_t x = 0) {
+        if (!on) return;
+        (void)hipStreamSynchronize(s);
+        const double n = now_s();
+        std::fprintf(stderr, "[build] %-28s %8.3f s  %llu\n", what, n - t, (unsigned long long)x);
+        t = n;
+    }
+};
+
 template <int W>
 struct Builder {
     hipStream_t s;
@@ -684,6 +799,11 @@ struct Builder {
     // characters).  n < 2^32: the permutation is 32-bit (partitions guarantee it).
     bool sort(const uint64_t *keys, uint64_t stride, const uint8_t *len, uint64_t n, uint64_t *&okeys,
               uint8_t *&olen) {
+        const double t0 = now_s();
+        struct Acc {
+            double t0, &sum;
+            ~Acc() { sum += now_s() - t0; }
+        } acc_{t0, st.seconds_sort};
         if (n >= (1ULL << 32)) {
             err = "internal: a sort pass of 2^32 or more keys";
             return false;
@@ -879,7 +999,8 @@ struct Builder {
         if (p0 >= p1) return true;
         const uint64_t n_before = n;
         BTRY(hipMemcpyAsync(d_cnt, &n, 8, hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(k_emit_kmers<W>, grid(p1 - p0), dim3(256), 0, s, c.cb, c.ok, c.g0, p0, p1, k,
+        hipLaunchKernelGGL(k_emit_kmers<W>, dim3((uint32_t)((p1 - p0 + kEmitTile - 1) / kEmitTile)), dim3(256), 0, s,
+                           c.cb, c.ok, c.g0, p0, p1, k,
                            (uint32_t)rc, m, blo, bhi, acc, cap, d_cnt);
         BTRY(hipGetLastError());
         uint64_t got = 0;
@@ -903,6 +1024,7 @@ struct Builder {
 
     bool run(const uint8_t *h_seq, const uint64_t *h_offs, uint64_t n_seqs, const BuildOpts &o, HostIndex &out) {
         const double t0 = now_s();
+        Tracer tr;
         Seq q{h_seq, h_offs, n_seqs, n_seqs ? h_offs[0] : 0, n_seqs ? h_offs[n_seqs] : 0};
         const uint64_t T = q.P1 - q.P0;
         const uint64_t nb = 1ULL << (2 * m);
@@ -925,7 +1047,9 @@ struct Builder {
         }
         // >= 1024 keys: a source's k - 1 <= 254 dummies fit a quarter of a pass
         if (o.max_partition_keys) cap = std::min<uint64_t>(cap, std::max<uint64_t>(1024, o.max_partition_keys));
-        cap = std::min<uint64_t>(cap, 0xFFFFFFFFULL - 1024);
+        // and <= 2^30: rocPRIM's radix sort of 3 G pairs took 4x longer per key than of 0.7 G
+        // (3 Gbp build: 6.0 against 0.7 s of sorting), so big budgets make more passes
+        cap = std::min<uint64_t>(cap, 1ULL << 30);
         host_budget = o.host_budget;
         temp_dir = o.temp_dir;
         st.device_budget = budget;
@@ -952,6 +1076,8 @@ struct Builder {
         std::vector<uint64_t> occ(nb);
         BTRY(hipMemcpyAsync(occ.data(), d_hist, nb * 8, hipMemcpyDeviceToHost, s));
         BTRY(hipStreamSynchronize(s));
+        st.seconds_plan = now_s() - t0;
+        tr.mark(s, "plan (seq + histogram)", T);
         A.release(d_hist);
         for (uint64_t x : occ) st.occurrences += x;
         const auto kparts = plan_parts(occ, cap);
@@ -982,12 +1108,19 @@ struct Builder {
                 uint64_t *u;
                 uint8_t *ul;
                 uint64_t mu = 0;
+                tr.mark(s, "kmers: emit", n);
                 if (!sort_unique_release(acc, cap, nullptr, n, u, ul, mu)) return false;
+                tr.mark(s, "kmers: sort+unique", mu);
                 cap = save_cap;
                 if (!key_hist(u, mu, h)) return false;
-                if (!kstore.add(u, nullptr, mu, h, s, err)) return false;
-                A.release(u);
+                if (kparts.size() == 1) {
+                    kstore.add_device(u, nullptr, mu, h);  // one pass: the k-mers stay in HBM
+                } else {
+                    if (!kstore.add(u, nullptr, mu, h, s, err)) return false;
+                    A.release(u);
+                }
                 st.kmers += mu;
+                tr.mark(s, "kmers: hist+store", mu);
             }
             A.release(d_cnt);
         }
@@ -1044,6 +1177,7 @@ struct Builder {
         }
         const uint64_t nsrc = sources.size() / W;
         st.sources = nsrc;
+        tr.mark(s, "sources", nsrc);
         const double t2 = now_s();
         st.seconds_sources = t2 - t1;
 
@@ -1070,6 +1204,15 @@ struct Builder {
         std::vector<uint64_t>().swap(sources);
         const auto nparts = plan_parts(ncnt, cap);
         st.node_partitions = (uint32_t)nparts.size();
+        {
+            uint64_t most = 0;
+            for (const auto &pr : nparts) {
+                uint64_t w = 0;
+                for (uint32_t b = pr.first; b < pr.second; b++) w += ncnt[b];
+                most = std::max(most, std::min(w, cap));
+            }
+            if (kstore.device_bytes() && A.live + per_key * most > budget && !kstore.evict(A, s, err)) return false;
+        }
         KeyStore nstore(W, true, m, host_budget, temp_dir, &st);
         {
             BALLOC(d_cnt, unsigned long long, 1);
@@ -1126,17 +1269,24 @@ struct Builder {
                 uint64_t *u;
                 uint8_t *ul;
                 uint64_t mu = 0;
+                tr.mark(s, "nodes: assemble", n);
                 if (!sort_unique_release(acc, cap, alen, n, u, ul, mu)) return false;
+                tr.mark(s, "nodes: sort+unique", mu);
                 cap = save_cap;
                 std::vector<uint64_t> h;
                 if (!key_hist(u, mu, h)) return false;
-                if (!nstore.add(u, ul, mu, h, s, err)) return false;
-                A.release(u);
-                A.release(ul);
+                if (nparts.size() == 1 && A.live + (8 * (uint64_t)W + 40) * mu <= budget) {
+                    nstore.add_device(u, ul, mu, h);  // one pass: the nodes stay in HBM
+                } else {
+                    if (!nstore.add(u, ul, mu, h, s, err)) return false;
+                    A.release(u);
+                    A.release(ul);
+                }
             }
             A.release(d_cnt);
         }
         A.release(d_src);
+        kstore.release_device(A);  // the k-mers are no longer needed
         nstore.finalize();
         const uint64_t n = nstore.size();
         st.nodes = n;
@@ -1145,6 +1295,7 @@ struct Builder {
             return false;
         }
         // the k-mer store is no longer needed
+        tr.mark(s, "nodes: stored", n);
         const double t3 = now_s();
         st.seconds_nodes = t3 - t2;
 
@@ -1174,7 +1325,9 @@ struct Builder {
                 if (!scan_flags(gflag, nj, grank, G)) return false;
                 BALLOC(gfirst, uint32_t, G);
                 hipLaunchKernelGGL(k_gfirst, grid(nj), dim3(256), 0, s, gflag, grank, nj, gfirst);
+                tr.mark(s, "labels: lcs+groups", G);
                 BTRY(hipMemcpyAsync(out.lcs.data() + base, lcs, nj, hipMemcpyDeviceToHost, s));
+                tr.mark(s, "labels: lcs d2h", nj);
                 A.release(gflag);
                 A.release(grank);
                 A.release(lcs);
@@ -1194,6 +1347,7 @@ struct Builder {
                         BTRY(hipGetLastError());
                         BTRY(hipStreamSynchronize(s));
                     }
+                tr.mark(s, "labels: kernels", nj);
                 std::vector<uint64_t> hr(4 * sw);
                 BTRY(hipMemcpyAsync(hr.data(), rows, 4 * sw * 8, hipMemcpyDeviceToHost, s));
                 BTRY(hipStreamSynchronize(s));
@@ -1201,6 +1355,7 @@ struct Builder {
                     for (uint64_t w = 0; w < sw; w++) out.rows[c][w0 + w] |= hr[c * sw + w];
                 for (void *p : {(void *)uk, (void *)ul, (void *)rows, (void *)gfirst, (void *)nk, (void *)nl})
                     A.release(p);
+                tr.mark(s, "labels: rows d2h+or", sw);
             }
             unsigned int hbad = 0;
             BTRY(hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, s));

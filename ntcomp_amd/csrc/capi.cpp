@@ -1498,6 +1498,8 @@ int ntc_build_index_device_ex(ntc_ctx *ctx, const uint8_t *seqs, const uint64_t 
         stats->seconds_sources = st.seconds_sources;
         stats->seconds_nodes = st.seconds_nodes;
         stats->seconds_labels = st.seconds_labels;
+        stats->seconds_plan = st.seconds_plan;
+        stats->seconds_sort = st.seconds_sort;
     }
     if (!ok) {
         delete h;

@@ -23,6 +23,7 @@ struct BuildStats {
     uint64_t spilled_bytes = 0, device_budget = 0, pass_keys = 0, peak_device_bytes = 0;
     uint32_t kmer_partitions = 0, node_partitions = 0, compactions = 0, seq_uploads = 0;
     double seconds = 0, seconds_kmers = 0, seconds_sources = 0, seconds_nodes = 0, seconds_labels = 0;
+    double seconds_plan = 0, seconds_sort = 0;  // the occurrence histogram (sequence upload included); sorts
 };
 bool build_index_device(hipStream_t s, const uint8_t *seqs, const uint64_t *offs, uint64_t n_seqs, uint32_t k,
                         bool revcomp, const BuildOpts &o, HostIndex &out, BuildStats &st, std::string &err);

@@ -55,6 +55,13 @@ _Static_assert(offsetof(ntc_pipeline_stats, parse_s) == 40 && offsetof(ntc_pipel
                    offsetof(ntc_pipeline_stats, bad_read) == 120 && offsetof(ntc_pipeline_stats, error) == 128 &&
                    sizeof(ntc_pipeline_stats) == 384,
                "ntc_pipeline_stats");
+_Static_assert(offsetof(ntc_build_opts, host_budget_bytes) == 8 && offsetof(ntc_build_opts, temp_dir) == 16 &&
+                   offsetof(ntc_build_opts, max_partition_keys) == 24 && sizeof(ntc_build_opts) == 32,
+               "ntc_build_opts");
+_Static_assert(offsetof(ntc_build_stats, peak_device_bytes) == 56 && offsetof(ntc_build_stats, kmer_partitions) == 64 &&
+                   offsetof(ntc_build_stats, seq_uploads) == 76 && offsetof(ntc_build_stats, seconds) == 80 &&
+                   offsetof(ntc_build_stats, seconds_sort) == 128 && sizeof(ntc_build_stats) == 136,
+               "ntc_build_stats");
 /* the status enum crosses the boundary as a C int (Rust: c_int) */
 _Static_assert(sizeof(ntc_status) == sizeof(int), "ntc_status");
 
