@@ -1,0 +1,313 @@
+// ntcomp -- the command-line driver as a native binary: `ntcomp build | encode | decode`
+// with the reference's flags (src/cli.rs:27-93) and stderr messages (src/main.rs:91-211),
+// the hot path on the GPU through libntcomp_gpu.so's C ABI (include/*.h).  The Python CLI
+// (`python -m ntcomp_amd`) is the same program; this one starts without an interpreter
+// (the reference's binary is compiled code too), which is what a process-level timing sees.
+//
+//   ntcomp build -o P [-k 31] [-p 8] [-d] [-t 1] [-m 4] [--temp-dir D] [--verbose]
+//                [-l LIST] [--builder auto|host|gpu] [--device N] [--index-format own|sbwt-rs] FILES...
+//   ntcomp encode -i P [--gpus N | --devices 0,0,..] [--threads T] [--blocks-per-batch B]
+//                 [--deflate auto|zlib|libdeflate] [--stats] FILE > encoded.dat
+//   ntcomp decode -i P [--gpus N | --devices ..] [--threads T] [--blocks-per-batch B] [--stats] FILE > out.fasta
+#include <dlfcn.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <string>
+#include <vector>
+
+#include "../../include/ntcomp_codec.h"
+#include "../../include/ntcomp_gpu.h"
+#include "../../include/ntcomp_host.h"
+#include "../../include/ntcomp_pipeline.h"
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+double since(Clock::time_point t) { return std::chrono::duration<double>(Clock::now() - t).count(); }
+
+[[noreturn]] void die(const std::string &msg) {
+    std::fprintf(stderr, "ntcomp: %s\n", msg.c_str());
+    std::exit(1);
+}
+void info(const char *msg) { std::fprintf(stderr, "%s\n", msg); }
+
+struct Args {
+    std::vector<std::string> pos;
+    std::vector<std::pair<std::string, std::string>> kv;
+    bool flag(const char *a, const char *b = nullptr) const {
+        for (auto &p : kv)
+            if (p.first == a || (b && p.first == b)) return true;
+        return false;
+    }
+    std::string get(const char *a, const char *b, const std::string &def) const {
+        std::string v = def;
+        for (auto &p : kv)
+            if (p.first == a || (b && p.first == b)) v = p.second;
+        return v;
+    }
+};
+
+// options taking a value; everything else starting with '-' is a switch
+bool takes_value(const std::string &o) {
+    static const char *v[] = {"-o", "--output-prefix", "-k", "-p", "--prefix-precalc", "-t", "--threads", "-m",
+                              "--mem-gb", "--temp-dir", "-l", "--input-list", "--builder", "--device",
+                              "--index-format", "-i", "--index", "--gpus", "--devices", "--blocks-per-batch",
+                              "--deflate"};
+    for (const char *x : v)
+        if (o == x) return true;
+    return false;
+}
+
+Args parse(int argc, char **argv, int from) {
+    Args a;
+    for (int i = from; i < argc; i++) {
+        std::string s = argv[i];
+        if (s.size() > 1 && s[0] == '-') {
+            const size_t eq = s.find('=');
+            if (eq != std::string::npos && s.rfind("--", 0) == 0) {
+                a.kv.push_back({s.substr(0, eq), s.substr(eq + 1)});
+            } else if (takes_value(s)) {
+                if (i + 1 >= argc) die("option " + s + " needs a value");
+                a.kv.push_back({s, argv[++i]});
+            } else {
+                a.kv.push_back({s, "1"});
+            }
+        } else {
+            a.pos.push_back(s);
+        }
+    }
+    return a;
+}
+
+std::vector<int> devices_of(const Args &a) {
+    std::vector<int> d;
+    const std::string list = a.get("--devices", nullptr, "");
+    if (!list.empty()) {
+        size_t p = 0;
+        while (p <= list.size()) {
+            const size_t q = list.find(',', p);
+            const std::string t = list.substr(p, q == std::string::npos ? std::string::npos : q - p);
+            if (!t.empty()) d.push_back(std::atoi(t.c_str()));
+            if (q == std::string::npos) break;
+            p = q + 1;
+        }
+    } else {
+        const int n = std::atoi(a.get("--gpus", nullptr, "1").c_str());
+        for (int i = 0; i < n; i++) d.push_back(i);
+    }
+    if (d.empty()) die("no GPU given (--gpus / --devices)");
+    return d;
+}
+
+std::vector<ntc_ctx *> open_gpus(const ntc_index_host *ix, const std::vector<int> &devs) {
+    ntc_index_view v;
+    if (ntc_index_view_of(ix, &v)) die("index view");
+    std::vector<ntc_ctx *> ctxs;
+    for (int d : devs) {
+        ntc_ctx *c = nullptr;
+        if (ntc_ctx_create(d, &c)) die("no usable GPU " + std::to_string(d));
+        if (ntc_index_upload(c, &v)) die(std::string("index upload: ") + ntc_last_error(c));
+        ctxs.push_back(c);
+    }
+    return ctxs;
+}
+
+bool libdeflate_present() {
+    void *h = dlopen("libdeflate.so.0", RTLD_LAZY | RTLD_LOCAL);
+    if (h) dlclose(h);
+    return h != nullptr;
+}
+
+int cmd_encode(const Args &a) {
+    const auto t0 = Clock::now();
+    if (a.pos.size() != 1) die("encode: one query file");
+    const std::string prefix = a.get("-i", "--index", "");
+    if (prefix.empty()) die("encode: -i/--index is required");
+    info("Loading SBWT index...");
+    ntc_index_host *ix = nullptr;
+    if (ntc_index_load(prefix.c_str(), &ix)) die("cannot load index " + prefix);
+    const double t_load = since(t0);
+    auto ctxs = open_gpus(ix, devices_of(a));
+    const double t_gpu = since(t0);
+    info("Encoding fastX data...");
+    std::string engine = a.get("--deflate", nullptr, "auto");
+    if (engine == "auto") engine = libdeflate_present() ? "libdeflate" : "zlib";
+    ntc_pipeline_opts o{};
+    o.threads = std::atoi(a.get("--threads", nullptr, "0").c_str());
+    o.blocks_per_batch = std::atoi(a.get("--blocks-per-batch", nullptr, "4").c_str());
+    o.deflate_engine = engine == "libdeflate" ? NTC_DEFLATE_LIBDEFLATE : NTC_DEFLATE_ZLIB;
+    ntc_pipeline_stats st{};
+    std::fflush(stdout);
+    const int rc = ntc_encode_file(ctxs.data(), (int)ctxs.size(), a.pos[0].c_str(), 1, &o, &st);
+    for (auto *c : ctxs) ntc_ctx_destroy(c);
+    ntc_index_free(ix);
+    if (rc) {
+        std::string m = std::string("encode: ") + st.error;
+        if (st.bad_read >= 0) m += " (read " + std::to_string(st.bad_read + 1) + ")";
+        die(m);
+    }
+    if (st.dropped_blocks)
+        std::fprintf(stderr, "warning: %llu block(s) dropped (no long or no short records; main.rs:170 ignores "
+                             "write_block_to's error, SURVEY App. B.3)\n",
+                     (unsigned long long)st.dropped_blocks);
+    if (a.flag("--stats"))
+        std::fprintf(stderr,
+                     "{\"stats\": {\"index_load\": %.3f, \"gpu_init_upload\": %.3f, \"parse\": %.3f, \"gpu\": %.3f, "
+                     "\"deflate\": %.3f, \"write\": %.3f}, \"command\": \"encode\", \"native\": true, \"gpus\": %zu, "
+                     "\"threads\": %d, \"reads\": %llu, \"blocks\": %llu, \"dropped_blocks\": %llu, "
+                     "\"pipeline_wall_s\": %.3f, \"deflate\": \"%s\", \"process_s\": %.3f}\n",
+                     t_load, t_gpu - t_load, st.parse_s, st.gpu_s, st.deflate_s, st.write_s, ctxs.size(), st.threads,
+                     (unsigned long long)st.reads, (unsigned long long)st.blocks,
+                     (unsigned long long)st.dropped_blocks, st.wall_s, engine.c_str(), since(t0));
+    return 0;
+}
+
+int cmd_decode(const Args &a) {
+    const auto t0 = Clock::now();
+    if (a.pos.size() != 1) die("decode: one input file");
+    const std::string prefix = a.get("-i", "--index", "");
+    if (prefix.empty()) die("decode: -i/--index is required");
+    ntc_index_host *ix = nullptr;
+    if (ntc_index_load(prefix.c_str(), &ix)) die("cannot load index " + prefix);
+    const double t_load = since(t0);
+    auto ctxs = open_gpus(ix, devices_of(a));
+    const double t_gpu = since(t0);
+    info("Decoding encoded data...");
+    ntc_pipeline_opts o{};
+    o.threads = std::atoi(a.get("--threads", nullptr, "0").c_str());
+    o.blocks_per_batch = std::atoi(a.get("--blocks-per-batch", nullptr, "2").c_str());
+    ntc_pipeline_stats st{};
+    std::fflush(stdout);
+    const int rc = ntc_decode_file(ctxs.data(), (int)ctxs.size(), a.pos[0].c_str(), 1, &o, &st);
+    for (auto *c : ctxs) ntc_ctx_destroy(c);
+    ntc_index_free(ix);
+    if (rc) die(std::string("decode: ") + st.error);
+    if (st.dropped_blocks)  // the reference's `while let Ok(..) = decode_block` just ends here (main.rs:202)
+        std::fprintf(stderr, "warning: %s; %llu block(s) not decoded\n", st.error,
+                     (unsigned long long)st.dropped_blocks);
+    if (a.flag("--stats"))
+        std::fprintf(stderr,
+                     "{\"stats\": {\"index_load\": %.3f, \"gpu_init_upload\": %.3f, \"unzip\": %.3f, \"gpu\": %.3f, "
+                     "\"write\": %.3f}, \"command\": \"decode\", \"native\": true, \"gpus\": %zu, \"threads\": %d, "
+                     "\"reads\": %llu, \"blocks\": %llu, \"pipeline_wall_s\": %.3f, \"process_s\": %.3f}\n",
+                     t_load, t_gpu - t_load, st.parse_s, st.gpu_s, st.write_s, ctxs.size(), st.threads,
+                     (unsigned long long)st.reads, (unsigned long long)st.blocks, st.wall_s, since(t0));
+    return 0;
+}
+
+// --input-list: one path, or tab-separated name and path, per line (main.rs:64-89)
+std::vector<std::string> read_list(const std::string &path) {
+    std::vector<std::string> out;
+    std::ifstream f(path);
+    if (!f) die("cannot read " + path);
+    std::string line;
+    while (std::getline(f, line)) {
+        if (line.empty()) continue;
+        const size_t t = line.find('\t');
+        out.push_back(t == std::string::npos ? line : line.substr(t + 1));
+    }
+    return out;
+}
+
+int cmd_build(const Args &a) {
+    std::vector<std::string> files = a.pos;
+    const std::string list = a.get("-l", "--input-list", "");
+    if (!list.empty())
+        for (auto &p : read_list(list)) files.push_back(p);
+    if (files.empty()) die("build: no input files");
+    const std::string prefix = a.get("-o", "--output-prefix", "");
+    if (prefix.empty()) die("build: -o/--output-prefix is required");
+    const uint32_t k = (uint32_t)std::atoi(a.get("-k", nullptr, "31").c_str());
+    const uint32_t pre = (uint32_t)std::atoi(a.get("-p", "--prefix-precalc", "8").c_str());
+    const int threads = std::atoi(a.get("-t", "--threads", "1").c_str());
+    const double mem_gb = std::atof(a.get("-m", "--mem-gb", "4").c_str());
+    const std::string temp = a.get("--temp-dir", nullptr, "");
+    const std::string builder = a.get("--builder", nullptr, "auto");
+    const std::string layout = a.get("--index-format", nullptr, "own");
+    const int device = std::atoi(a.get("--device", nullptr, "0").c_str());
+    const bool verbose = a.flag("--verbose");
+    std::fprintf(stderr, "Building SBWT index from %zu files...\n", files.size());
+    // every sequence of every file, back to back (main.rs:37-62: read_fastx_file per file)
+    std::vector<uint8_t> seq;
+    std::vector<uint64_t> offs{0};
+    for (const auto &path : files) {
+        ntc_fastx *fx = nullptr;
+        if (ntc_fastx_open(path.c_str(), &fx)) die("cannot read " + path);
+        for (;;) {
+            const uint8_t *b;
+            const uint64_t *o;
+            uint64_t n = 0;
+            const int rc = ntc_fastx_next_batch(fx, 1u << 16, 1ull << 28, &b, &o, &n);
+            if (rc) die("malformed or unreadable input: " + path);
+            if (!n) break;
+            seq.insert(seq.end(), b + o[0], b + o[n]);
+            const uint64_t base = offs.back() - o[0];
+            for (uint64_t r = 1; r <= n; r++) offs.push_back(base + o[r]);
+        }
+        ntc_fastx_close(fx);
+    }
+    ntc_index_host *ix = nullptr;
+    ntc_ctx *ctx = nullptr;
+    if (builder != "host" && ntc_ctx_create(device, &ctx) != NTC_OK) {
+        if (builder == "gpu") die("--builder gpu: no usable GPU " + std::to_string(device));
+        ctx = nullptr;
+    }
+    if (ctx) {
+        // kbo's BuildOpts { mem_gb, temp_dir } (main.rs:111-134): -m bounds the device memory of a
+        // pass and the host memory of sorted partitions (past it: files under --temp-dir)
+        ntc_build_opts o{};
+        o.device_budget_bytes = (uint64_t)(mem_gb * (double)(1ull << 30));
+        o.host_budget_bytes = o.device_budget_bytes;
+        o.temp_dir = temp.empty() ? nullptr : temp.c_str();
+        ntc_build_stats st{};
+        const int rc = ntc_build_index_device_ex(ctx, seq.data(), offs.data(), offs.size() - 1, k, 1, &o, &st, &ix);
+        if (rc) die(std::string("build: ") + ntc_last_error(ctx));
+        ntc_ctx_destroy(ctx);
+        if (verbose)
+            std::fprintf(stderr,
+                         "build: %llu occurrences, %llu k-mers, %llu nodes, %u + %u passes, %.3f s (GPU, budget %llu "
+                         "B, peak %llu B, spilled %llu B)\n",
+                         (unsigned long long)st.occurrences, (unsigned long long)st.kmers,
+                         (unsigned long long)st.nodes, st.kmer_partitions, st.node_partitions, st.seconds,
+                         (unsigned long long)st.device_budget_bytes, (unsigned long long)st.peak_device_bytes,
+                         (unsigned long long)st.spilled_bytes);
+    } else {
+        if (ntc_build_index(seq.data(), offs.data(), offs.size() - 1, k, 1, threads, &ix)) die("build failed");
+    }
+    const int lay = layout == "sbwt-rs" ? NTC_INDEX_SBWT_RS : NTC_INDEX_OWN;
+    if (lay == NTC_INDEX_SBWT_RS && pre) ntc_index_set_prefix_precalc(ix, pre < k ? (pre < 12 ? pre : 12) : k);
+    std::fprintf(stderr, "Serializing SBWT index to %s.sbwt ...\n", prefix.c_str());
+    std::fprintf(stderr, "Serializing LCS array to %s.lcs ...\n", prefix.c_str());
+    if (ntc_index_save_as(ix, prefix.c_str(), lay)) die("cannot write " + prefix);
+    ntc_index_free(ix);
+    return 0;
+}
+
+void usage() {
+    std::fprintf(stderr,
+                 "Sequencing data compression with SBWT + k-bounded matching statistics; encode/decode hot path on "
+                 "MI355X.\n\nusage: ntcomp build -o PREFIX [-k K] [-m MEM_GB] [--temp-dir DIR] FILES...\n"
+                 "       ntcomp encode -i PREFIX FILE > encoded.dat\n"
+                 "       ntcomp decode -i PREFIX FILE > out.fasta\n");
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    if (argc < 2) {
+        usage();
+        return 2;
+    }
+    const std::string cmd = argv[1];
+    const Args a = parse(argc, argv, 2);
+    if (cmd == "build") return cmd_build(a);
+    if (cmd == "encode") return cmd_encode(a);
+    if (cmd == "decode") return cmd_decode(a);
+    usage();
+    return 2;
+}

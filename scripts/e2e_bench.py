@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--deflate", default="zlib", choices=["zlib", "libdeflate"])
     ap.add_argument("--keep", action="store_true", help="reuse an existing FASTQ + index in --dir")
     ap.add_argument("--reps", type=int, default=3, help="runs per timing (the best counts)")
+    ap.add_argument("--cli", default="native", choices=["native", "python"],
+                    help="native: the ntcomp binary (ntcomp_main.cpp); python: python -m ntcomp_amd")
     a = ap.parse_args()
     a.gpus_arg = ["--devices", a.devices] if a.devices else ["--gpus", str(a.gpus)]
     import numpy as np
@@ -72,7 +74,7 @@ def main():
             f.write(rec)
     print(f"fastq {len(rec) / 1e9:.2f} GB written in {time.time() - t0:.1f}s", file=sys.stderr)
     enc, dec = os.path.join(a.dir, "enc.dat"), os.path.join(a.dir, "dec.fa")
-    cmd = [sys.executable, "-m", "ntcomp_amd"]
+    cmd = [os.path.join(REPO, "ntcomp_amd", "ntcomp")] if a.cli == "native" else [sys.executable, "-m", "ntcomp_amd"]
 
     def stats_line(err):
         for line in reversed(err.decode(errors="replace").splitlines()):
@@ -115,7 +117,7 @@ def main():
                       "encode_s": round(te, 3), "encode_mbases_s": round(bases / te / 1e6, 1),
                       "encoded_bytes": os.path.getsize(enc), "bits_per_base": round(8 * os.path.getsize(enc) / bases, 4),
                       "decode_s": round(td, 3), "decode_mbases_s": round(bases / td / 1e6, 1),
-                      "gpus": a.gpus, "reps": a.reps,
+                      "gpus": a.gpus, "devices": a.devices, "cli": a.cli, "reps": a.reps,
                       "pipeline_mbases_s": {s: round(bases / st["pipeline_wall_s"] / 1e6, 1)
                                             if st and st.get("pipeline_wall_s") else None
                                             for s, st in (("encode", enc_stats), ("decode", dec_stats))},

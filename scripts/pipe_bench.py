@@ -21,31 +21,38 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--mode", default="encode", choices=["encode", "decode"])
     ap.add_argument("--batch-bases", type=int, nargs="+", default=[0], help="encode: pinned batch buffer (0: default)")
+    ap.add_argument("--contexts", type=int, nargs="+", default=[1], help="contexts on device 0 (calls alternate)")
     a = ap.parse_args()
     import ntcomp_amd as nt
     ix = nt.Index.load(os.path.join(a.dir, "idx"))
-    ctx = nt.GpuContext(0)
-    ctx.upload(ix)
+    pool = []
+    for _ in range(max(a.contexts)):
+        c = nt.GpuContext(0)
+        c.upload(ix)
+        pool.append(c)
     fq = os.path.join(a.dir, "reads.fq")
-    for bpb, bb in [(x, y) for x in a.bpb for y in a.batch_bases]:
+    for bpb, bb, nc in [(x, y, z) for x in a.bpb for y in a.batch_bases for z in a.contexts]:
+        ctxs = pool[:nc]
         for th in a.threads:
             for rep in range(a.reps):
                 t0 = time.time()
                 if a.mode == "encode":
                     with open(os.path.join(a.dir, "pipe.dat"), "wb") as f:
-                        st = nt.encode_file([ctx], fq, f.fileno(), threads=th, blocks_per_batch=bpb,
+                        st = nt.encode_file(ctxs, fq, f.fileno(), threads=th, blocks_per_batch=bpb,
                                             batch_bases=bb, deflate=a.deflate)
                 else:
                     with open(os.path.join(a.dir, "pipe.fa"), "wb") as f:
-                        st = nt.decode_file([ctx], os.path.join(a.dir, "enc.dat"), f.fileno(), threads=th,
+                        st = nt.decode_file(ctxs, os.path.join(a.dir, "enc.dat"), f.fileno(), threads=th,
                                             blocks_per_batch=bpb)
                 w = time.time() - t0
                 st.pop("error")
-                print(json.dumps({"mode": a.mode, "bpb": bpb, "batch_bases": bb, "threads": th, "rep": rep, "wall": round(w, 3),
+                print(json.dumps({"mode": a.mode, "bpb": bpb, "batch_bases": bb, "contexts": nc, "threads": th, "rep": rep,
+                                  "wall": round(w, 3),
                                   "gbases_s": round(st["bases"] / w / 1e9, 3),
                                   **{k: (round(v, 3) if isinstance(v, float) else v) for k, v in st.items()}}),
                       flush=True)
-    ctx.close()
+    for c in pool:
+        c.close()
 
 
 if __name__ == "__main__":

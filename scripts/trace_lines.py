@@ -56,6 +56,7 @@ def main():
     emu_lib.EMU_SO = so
     L = emu_lib.emu_lib()
     L.emu_trace_report.argtypes = [ctypes.c_void_p]
+    L.emu_trace_overlap.argtypes = [ctypes.c_void_p]
     genome = nt.synth_genome(1, args.genome_bp)
     texts = [genome]
     if args.strains:
@@ -70,7 +71,9 @@ def main():
     recs, _ = emu_lib.emu_encode(ix.n, args.k, ix.rows, ix.C, ix.lcs, reads, offs, tab_u=args.tab_u)
     K = len(KINDS)
     out = np.zeros(1 + 4 * K, dtype=np.uint64)
+    ov = np.zeros(K, dtype=np.uint64)
     L.emu_trace_report(out.ctypes.data)
+    L.emu_trace_overlap(ov.ctypes.data)
     n = int(out[0])
     req = out[1:1 + 2 * K].reshape(2, K) / n
     lines = out[1 + 2 * K:].reshape(2, K) / n
@@ -80,7 +83,8 @@ def main():
         print(f"-- {name}: loads/read {req[ph].sum():.2f}, lines/read {lines[ph].sum():.2f}")
         for i in np.argsort(-lines[ph]):
             if req[ph][i] > 0:
-                print(f"   {KINDS[i]:12s} loads {req[ph][i]:7.2f}  lines {lines[ph][i]:6.2f}")
+                extra = f"  (also touched by ms: {ov[i] / n:5.2f})" if ph == 1 else ""
+                print(f"   {KINDS[i]:12s} loads {req[ph][i]:7.2f}  lines {lines[ph][i]:6.2f}{extra}")
 
 
 if __name__ == "__main__":

@@ -22,6 +22,7 @@ namespace {
 int g_phase = -1;
 std::unordered_set<uint64_t> g_lines[2][kTrKinds];
 uint64_t g_req[2][kTrKinds], g_ltot[2][kTrKinds], g_reads;
+uint64_t g_over[kTrKinds];  // parse lines the MS phase of the same reads touched too
 void trace_phase(int ph) { g_phase = ph; }
 uint64_t g_group = 0, g_in_group = 0;  // NTC_TRACE_GROUP=G: distinct lines per G consecutive reads
 void trace_read_done() {
@@ -33,6 +34,8 @@ void trace_read_done() {
     g_phase = -1;
     if (++g_in_group < g_group) return;
     g_in_group = 0;
+    for (int b = 0; b < kTrKinds; b++)
+        for (uint64_t x : g_lines[1][b]) g_over[b] += g_lines[0][b].count(x);
     for (int a = 0; a < 2; a++)
         for (int b = 0; b < kTrKinds; b++) {
             g_ltot[a][b] += g_lines[a][b].size();
@@ -55,6 +58,10 @@ extern "C" void emu_trace_report(uint64_t *out) {  // [reads, req[2][K], lines[2
     memset(g_req, 0, sizeof g_req);
     memset(g_ltot, 0, sizeof g_ltot);
     g_reads = 0;
+}
+extern "C" void emu_trace_overlap(uint64_t *out) {  // [K]: parse lines also touched by the MS phase
+    for (int b = 0; b < kTrKinds; b++) out[b] = g_over[b];
+    memset(g_over, 0, sizeof g_over);
 }
 #else
 namespace {

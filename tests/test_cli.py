@@ -301,3 +301,53 @@ def test_cli_encode_decode_end_to_end(tmp_path):
     assert lines[-1] == b"" and len(lines) == 2 * n + 1
     assert lines[0] == b">seq.1" and lines[2 * (n - 1)] == b">seq.%d" % n
     assert b"".join(lines[1::2]) == reads.tobytes()
+
+
+NATIVE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ntcomp_amd", "ntcomp")
+
+
+def test_native_cli_build_equals_python_cli(tmp_path):
+    """`ntcomp build` as a native binary (ntcomp_main.cpp, no interpreter) writes the same
+    index files as the Python CLI, with -l lists, several files and the sbwt-rs layout + -p;
+    without a GPU `--builder auto` uses the host builder."""
+    g = nt.synth_genome(5, 30_000).tobytes().decode()
+    (tmp_path / "a.fa").write_text(">a\n" + g[:17_000] + "\n")
+    (tmp_path / "b.fq").write_text("@b\n" + g[17_000:] + "\n+\n" + "I" * (30_000 - 17_000) + "\n")
+    (tmp_path / "list.txt").write_text(f"x\t{tmp_path / 'b.fq'}\n")
+    for fmt in ("own", "sbwt-rs"):
+        subprocess.run([NATIVE, "build", "-o", str(tmp_path / "n"), "-k", "31", "--builder", "host",
+                        "--index-format", fmt, "-p", "5", "-l", str(tmp_path / "list.txt"), str(tmp_path / "a.fa")],
+                       check=True, stderr=subprocess.PIPE)
+        _cli("build", "-o", str(tmp_path / "p"), "-k", "31", "--builder", "host", "--index-format", fmt, "-p", "5",
+             "-l", str(tmp_path / "list.txt"), str(tmp_path / "a.fa"))
+        for ext in (".sbwt", ".lcs"):
+            assert (tmp_path / ("n" + ext)).read_bytes() == (tmp_path / ("p" + ext)).read_bytes(), (fmt, ext)
+    assert nt.Index.load(str(tmp_path / "n")).prefix_table()[0] == 5
+    r = subprocess.run([NATIVE], stderr=subprocess.PIPE)
+    assert r.returncode == 2 and b"usage" in r.stderr
+
+
+@pytest.mark.gpu
+def test_native_cli_encode_decode_equal_python_cli(tmp_path):
+    """`ntcomp encode|decode` (native) and `python -m ntcomp_amd encode|decode` write the same
+    bytes: the same native pipelines behind both (ntc_encode_file / ntc_decode_file)."""
+    genome = nt.synth_genome(6, 300_000)
+    (tmp_path / "g.fa").write_text(">g\n" + genome.tobytes().decode() + "\n")
+    subprocess.run([NATIVE, "build", "-o", str(tmp_path / "idx"), "-k", "31", str(tmp_path / "g.fa")], check=True,
+                   stderr=subprocess.PIPE)
+    n, L = 150_000, 100
+    reads = nt.synth_reads(genome, 9, 0, n, L, 10_000)
+    fq = tmp_path / "r.fq"
+    fq.write_bytes(b"".join(b"@r\n" + reads[i * L:(i + 1) * L].tobytes() + b"\n+\n" + b"I" * L + b"\n"
+                            for i in range(n)))
+    with open(tmp_path / "n.dat", "wb") as f:
+        subprocess.run([NATIVE, "encode", "-i", str(tmp_path / "idx"), "--deflate", "zlib", "--devices", "0,0",
+                        str(fq)], stdout=f, stderr=subprocess.PIPE, check=True)
+    with open(tmp_path / "p.dat", "wb") as f:
+        _cli("encode", "-i", str(tmp_path / "idx"), "--deflate", "zlib", str(fq), stdout=f)
+    assert (tmp_path / "n.dat").read_bytes() == (tmp_path / "p.dat").read_bytes()
+    with open(tmp_path / "n.fa", "wb") as f:
+        subprocess.run([NATIVE, "decode", "-i", str(tmp_path / "idx"), str(tmp_path / "n.dat")], stdout=f,
+                       stderr=subprocess.PIPE, check=True)
+    lines = (tmp_path / "n.fa").read_bytes().split(b"\n")
+    assert b"".join(lines[1::2]) == reads.tobytes() and lines[0] == b">seq.1"
