@@ -120,6 +120,11 @@ int ntc_ctx_get_option(const ntc_ctx *ctx, const char *key, int64_t *value);
  * bitvector, the path cover, the suffix table (+ presence bitmaps) and the inverse-walk
  * jump table in HBM (DESIGN.md "Data layout in HBM").  About 3 GB at n = 10 M, k = 91. */
 int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *ix);
+/* dst uses src's device index (both contexts on one GPU): no second upload, no second copy
+ * in HBM; the index is freed with the last context holding it.  Each context keeps its own
+ * stream and workspace, so two contexts on one GPU overlap one call's copies and host work
+ * with the other's kernels (the CLI's contexts per GPU).                                  */
+int ntc_index_share(ntc_ctx *dst, const ntc_ctx *src);
 int ntc_index_info(const ntc_ctx *ctx, uint64_t *n_nodes, uint32_t *k, uint64_t *device_bytes);
 
 /* ---- encode ---------------------------------------------------------------------- */

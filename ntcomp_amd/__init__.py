@@ -44,7 +44,7 @@ EXPORTED = [
     "ntc_fastx_open", "ntc_fastx_next_batch", "ntc_fastx_close", "ntc_fasta_format", "ntc_fastx_next_batch_into",
     "ntc_fastx_set_threads", "ntc_host_threads", "ntc_encode_file", "ntc_decode_fasta",
     "ntc_decode_file", "ntc_build_index_device", "ntc_build_index_device_ex", "ntc_index_set_prefix_precalc",
-    "ntc_index_prefix_table",
+    "ntc_index_prefix_table", "ntc_index_share",
 ]
 
 
@@ -163,6 +163,7 @@ def lib():
         "ntc_ctx_set_option": (I, [P, ctypes.c_char_p, i64]),
         "ntc_ctx_get_option": (I, [P, ctypes.c_char_p, ctypes.POINTER(i64)]),
         "ntc_index_upload": (I, [P, ctypes.POINTER(IndexView)]),
+        "ntc_index_share": (I, [P, P]),
         "ntc_index_info": (I, [P, P, P, P]),
         "ntc_encode_batch": (I, [P, P, P, u64, P, u64, P, P]),
         "ntc_encode_batch_device": (I, [P, P, P, u64, u32, P, u64, P]),
@@ -371,6 +372,11 @@ class GpuContext:
 
     def upload(self, index):
         self._check(self.L.ntc_index_upload(self.h, ctypes.byref(index.view)), "ntc_index_upload")
+        return self
+
+    def share_index(self, other):
+        """Use other's device index (same GPU, ntc_index_share): no second upload or copy."""
+        self._check(self.L.ntc_index_share(self.h, other.h), "ntc_index_share")
         return self
 
     def upload_arrays(self, n, k, rows, C, lcs):

@@ -19,6 +19,7 @@ import sys
 
 
 BLOCK_READS = 65536  # main.rs:152
+CONTEXTS_PER_GPU = 1  # encode / decode contexts per device (--contexts-per-gpu)
 
 
 def log(*a):
@@ -122,17 +123,25 @@ def cmd_build(args):
     ix.save(args.output_prefix, layout=args.index_format)
 
 
-def _open_gpus(index, devices, st=None):
-    """One context per entry of devices, each holding its own copy of the index (SURVEY.md
-    8(e)); an int n means devices 0..n-1."""
+def _open_gpus(index, devices, st=None, per_gpu=1):
+    """per_gpu contexts per entry of devices; an int n means devices
+    0..n-1.  The first context of a device uploads the index, the others on that device share
+    it (ntc_index_share): calls alternate over the contexts, so one call's copies and host
+    work overlap another's kernels."""
     import ntcomp_amd as nt
-    ctxs = []
+    ctxs, first = [], {}
     for d in (range(devices) if isinstance(devices, int) else devices):
-        c = (st.wrap("gpu_init", nt.GpuContext) if st else nt.GpuContext)(d)
-        (st.wrap("index_upload", c.upload) if st else c.upload)(index)
-        if st and st.on:
-            st.acc["upload_host_derive"] = st.acc.get("upload_host_derive", 0.0) + c.get_option("upload_host_us") / 1e6
-        ctxs.append(c)
+        for _ in range(max(1, per_gpu)):
+            c = (st.wrap("gpu_init", nt.GpuContext) if st else nt.GpuContext)(d)
+            if d in first:
+                c.share_index(first[d])
+            else:
+                (st.wrap("index_upload", c.upload) if st else c.upload)(index)
+                first[d] = c
+                if st and st.on:
+                    st.acc["upload_host_derive"] = (st.acc.get("upload_host_derive", 0.0) +
+                                                    c.get_option("upload_host_us") / 1e6)
+            ctxs.append(c)
     return ctxs
 
 
@@ -151,7 +160,7 @@ def cmd_encode(args):
     st = _Stats(args.stats)
     log("Loading SBWT index...")
     index = st.wrap("index_load", nt.Index.load)(args.index_prefix)
-    ctxs = _open_gpus(index, _devices(args), st)
+    ctxs = _open_gpus(index, _devices(args), st, args.contexts_per_gpu)
     log("Encoding fastX data...")
     if args.deflate == "auto":
         args.deflate = "libdeflate" if nt.libdeflate_available() else "zlib"
@@ -183,7 +192,7 @@ def cmd_decode(args):
     import ntcomp_amd as nt
     st = _Stats(args.stats)
     index = st.wrap("index_load", nt.Index.load)(args.index_prefix)
-    ctxs = _open_gpus(index, _devices(args), st)
+    ctxs = _open_gpus(index, _devices(args), st, args.contexts_per_gpu)
     log("Decoding encoded data...")
     out = sys.stdout.buffer
     out.flush()
@@ -240,6 +249,8 @@ def main(argv=None):
                                      "overrides --gpus")
     e.add_argument("--threads", type=int, default=0,
                    help="host pool for FASTQ parse and deflate (0: CPUs available to the process)")
+    e.add_argument("--contexts-per-gpu", type=int, default=CONTEXTS_PER_GPU,
+                   help="contexts per device sharing one index copy; calls alternate over them")
     e.add_argument("--blocks-per-batch", type=int, default=4, help="65,536-read blocks per GPU call")
     e.add_argument("--deflate", choices=["auto", "zlib", "libdeflate"], default="auto",
                    help="gzip engine for the block streams, level 6 either way (the reference's "
@@ -253,6 +264,8 @@ def main(argv=None):
     d.add_argument("--gpus", type=int, default=1, help="GPUs to decode on (batches dealt round-robin).")
     d.add_argument("--devices", help="comma-separated device list, one context each; overrides --gpus")
     d.add_argument("--threads", type=int, default=0, help="block unzip / format threads (0: CPUs available)")
+    d.add_argument("--contexts-per-gpu", type=int, default=CONTEXTS_PER_GPU,
+                   help="contexts per device sharing one index copy; calls alternate over them")
     d.add_argument("--blocks-per-batch", type=int, default=2, help="blocks per GPU call")
     d.add_argument("--stats", action="store_true", help="print per-stage seconds to stderr")
     args = ap.parse_args(argv)

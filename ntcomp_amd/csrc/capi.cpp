@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <exception>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -41,6 +42,18 @@ enum WsSlot {
     WS_PACK_PAYLOAD, WS_FA_BASES, WS_FA_OFFS, WS_FA_SCAN, WS_ES, WS_OBASE, WS_COUNT
 };
 
+// The device index of one upload: freed with the last context that holds it
+// (ntc_index_share lets several contexts on one GPU use one copy).
+struct IndexMem {
+    int device = 0;
+    std::vector<void *> ptrs;
+    explicit IndexMem(int d) : device(d) {}
+    ~IndexMem() {
+        (void)hipSetDevice(device);
+        for (void *p : ptrs) (void)hipFree(p);
+    }
+};
+
 struct ntc_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -49,7 +62,7 @@ struct ntc_ctx {
     // index
     bool has_index = false;
     DevIndex dix{};
-    std::vector<void *> index_mem;
+    std::shared_ptr<IndexMem> index_mem;
     uint64_t index_bytes = 0;
     // workspace buffers (grown, never shrunk)
     DevBuf ws[WS_COUNT];
@@ -540,7 +553,7 @@ void ntc_ctx_destroy(ntc_ctx *ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (auto &b : ctx->ws)
         if (b.p) (void)hipFree(b.p);
-    for (void *p : ctx->index_mem) (void)hipFree(p);
+    ctx->index_mem.reset();
     if (ctx->d_status) (void)hipFree(ctx->d_status);
     if (ctx->h_box) (void)hipHostFree(ctx->h_box);
     for (auto &e : ctx->ev)
@@ -575,6 +588,25 @@ int ntc_ctx_synchronize(ntc_ctx *ctx) {
     return NTC_OK;
 }
 
+int ntc_index_share(ntc_ctx *dst, const ntc_ctx *src) {
+    if (!dst || !src) return set_err(dst, NTC_ERR_INVALID_ARG, "null context");
+    if (!src->has_index) return set_err(dst, NTC_ERR_NO_INDEX, "the source context holds no index");
+    if (src->device != dst->device) return set_err(dst, NTC_ERR_INVALID_ARG, "contexts on different devices");
+    if (dst == src) return NTC_OK;
+    HIP_TRY(dst, hipSetDevice(dst->device));
+    HIP_TRY(dst, hipStreamSynchronize(dst->stream));
+    dst->index_mem = src->index_mem;
+    dst->dix = src->dix;
+    dst->index_bytes = src->index_bytes;
+    dst->n_paths = src->n_paths;
+    dst->path_text_len = src->path_text_len;
+    dst->filter_density_ppm = src->filter_density_ppm;
+    dst->tab_u_fallback = src->tab_u_fallback;
+    dst->upload_host_us = dst->upload_total_us = 0;
+    dst->has_index = true;
+    return NTC_OK;
+}
+
 int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     if (!ctx || !v || !v->lcs) return set_err(ctx, NTC_ERR_INVALID_ARG, "null index view");
     for (int c = 0; c < 4; c++)
@@ -600,14 +632,13 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     ctx->upload_host_us = us_since();
     // free a previous index
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    for (void *p : ctx->index_mem) HIP_TRY(ctx, hipFree(p));
-    ctx->index_mem.clear();
+    ctx->index_mem = std::make_shared<IndexMem>(ctx->device);  // the previous one goes with its last holder
     ctx->has_index = false;
     ctx->index_bytes = 0;
     const uint64_t n = hx.n;
     auto dalloc = [&](uint64_t bytes, void **p) -> int {
         HIP_TRY(ctx, hipMalloc(p, bytes));
-        ctx->index_mem.push_back(*p);
+        ctx->index_mem->ptrs.push_back(*p);
         ctx->index_bytes += bytes;
         return NTC_OK;
     };
@@ -762,7 +793,7 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
         ctx->tab_u_fallback = 1;
         if ((rc = dalloc(tab_base(U + 1) * sizeof(uint2), &d_tab))) return rc;
     } else {
-        ctx->index_mem.push_back(d_tab);
+        ctx->index_mem->ptrs.push_back(d_tab);
         ctx->index_bytes += tab_base(U + 1) * sizeof(uint2);
     }
     const uint32_t F = filter_level(U);

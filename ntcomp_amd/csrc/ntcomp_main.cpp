@@ -57,7 +57,7 @@ bool takes_value(const std::string &o) {
     static const char *v[] = {"-o", "--output-prefix", "-k", "-p", "--prefix-precalc", "-t", "--threads", "-m",
                               "--mem-gb", "--temp-dir", "-l", "--input-list", "--builder", "--device",
                               "--index-format", "-i", "--index", "--gpus", "--devices", "--blocks-per-batch",
-                              "--deflate"};
+                              "--deflate", "--contexts-per-gpu"};
     for (const char *x : v)
         if (o == x) return true;
     return false;
@@ -104,17 +104,33 @@ std::vector<int> devices_of(const Args &a) {
     return d;
 }
 
-std::vector<ntc_ctx *> open_gpus(const ntc_index_host *ix, const std::vector<int> &devs) {
+// per_gpu contexts per listed device: the first uploads the index, the others on that device
+// share it (ntc_index_share); batches alternate over all of them
+constexpr int kContextsPerGpu = 1;
+std::vector<ntc_ctx *> open_gpus(const ntc_index_host *ix, const std::vector<int> &devs, int per_gpu) {
     ntc_index_view v;
     if (ntc_index_view_of(ix, &v)) die("index view");
     std::vector<ntc_ctx *> ctxs;
-    for (int d : devs) {
-        ntc_ctx *c = nullptr;
-        if (ntc_ctx_create(d, &c)) die("no usable GPU " + std::to_string(d));
-        if (ntc_index_upload(c, &v)) die(std::string("index upload: ") + ntc_last_error(c));
-        ctxs.push_back(c);
-    }
+    std::vector<std::pair<int, ntc_ctx *>> first;
+    for (int d : devs)
+        for (int i = 0; i < (per_gpu > 0 ? per_gpu : 1); i++) {
+            ntc_ctx *c = nullptr;
+            if (ntc_ctx_create(d, &c)) die("no usable GPU " + std::to_string(d));
+            ntc_ctx *src = nullptr;
+            for (auto &f : first)
+                if (f.first == d) src = f.second;
+            if (src) {
+                if (ntc_index_share(c, src)) die(std::string("index share: ") + ntc_last_error(c));
+            } else {
+                if (ntc_index_upload(c, &v)) die(std::string("index upload: ") + ntc_last_error(c));
+                first.push_back({d, c});
+            }
+            ctxs.push_back(c);
+        }
     return ctxs;
+}
+int per_gpu_of(const Args &a) {
+    return std::atoi(a.get("--contexts-per-gpu", nullptr, std::to_string(kContextsPerGpu)).c_str());
 }
 
 bool libdeflate_present() {
@@ -132,7 +148,7 @@ int cmd_encode(const Args &a) {
     ntc_index_host *ix = nullptr;
     if (ntc_index_load(prefix.c_str(), &ix)) die("cannot load index " + prefix);
     const double t_load = since(t0);
-    auto ctxs = open_gpus(ix, devices_of(a));
+    auto ctxs = open_gpus(ix, devices_of(a), per_gpu_of(a));
     const double t_gpu = since(t0);
     info("Encoding fastX data...");
     std::string engine = a.get("--deflate", nullptr, "auto");
@@ -175,7 +191,7 @@ int cmd_decode(const Args &a) {
     ntc_index_host *ix = nullptr;
     if (ntc_index_load(prefix.c_str(), &ix)) die("cannot load index " + prefix);
     const double t_load = since(t0);
-    auto ctxs = open_gpus(ix, devices_of(a));
+    auto ctxs = open_gpus(ix, devices_of(a), per_gpu_of(a));
     const double t_gpu = since(t0);
     info("Decoding encoded data...");
     ntc_pipeline_opts o{};

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--bgzf", action="store_true", help="with --gzip: BGZF members (bgzip layout) instead of one member")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--devices", help="CLI --devices list (several contexts may share a GPU)")
+    ap.add_argument("--contexts-per-gpu", type=int, default=0, help="CLI --contexts-per-gpu (0: the CLI default)")
     ap.add_argument("--deflate", default="zlib", choices=["zlib", "libdeflate"])
     ap.add_argument("--keep", action="store_true", help="reuse an existing FASTQ + index in --dir")
     ap.add_argument("--reps", type=int, default=3, help="runs per timing (the best counts)")
@@ -31,6 +32,8 @@ def main():
                     help="native: the ntcomp binary (ntcomp_main.cpp); python: python -m ntcomp_amd")
     a = ap.parse_args()
     a.gpus_arg = ["--devices", a.devices] if a.devices else ["--gpus", str(a.gpus)]
+    if a.contexts_per_gpu:
+        a.gpus_arg += ["--contexts-per-gpu", str(a.contexts_per_gpu)]
     import numpy as np
     import ntcomp_amd as nt
     os.makedirs(a.dir, exist_ok=True)
@@ -117,7 +120,8 @@ def main():
                       "encode_s": round(te, 3), "encode_mbases_s": round(bases / te / 1e6, 1),
                       "encoded_bytes": os.path.getsize(enc), "bits_per_base": round(8 * os.path.getsize(enc) / bases, 4),
                       "decode_s": round(td, 3), "decode_mbases_s": round(bases / td / 1e6, 1),
-                      "gpus": a.gpus, "devices": a.devices, "cli": a.cli, "reps": a.reps,
+                      "gpus": a.gpus, "devices": a.devices, "contexts_per_gpu": a.contexts_per_gpu, "cli": a.cli,
+                      "reps": a.reps,
                       "pipeline_mbases_s": {s: round(bases / st["pipeline_wall_s"] / 1e6, 1)
                                             if st and st.get("pipeline_wall_s") else None
                                             for s, st in (("encode", enc_stats), ("decode", dec_stats))},

@@ -5,7 +5,7 @@ set -e
 mkdir -p gpurun_out/e2e
 timeout -k 10 400 python -u scripts/e2e_bench.py --reads 10000000 --deflate libdeflate ${E2E_ARGS:-} \
     > gpurun_out/e2e/plain_ld.json 2> gpurun_out/e2e/plain_ld.err
-timeout -k 10 300 python -u scripts/e2e_bench.py --reads 10000000 --deflate libdeflate --keep --devices 0,0 \
+timeout -k 10 300 python -u scripts/e2e_bench.py --reads 10000000 --deflate libdeflate --keep --contexts-per-gpu 2 \
     > gpurun_out/e2e/plain_ld_2ctx.json 2> gpurun_out/e2e/plain_ld_2ctx.err
 timeout -k 10 300 python -u scripts/e2e_bench.py --reads 10000000 --deflate libdeflate --keep --cli python \
     > gpurun_out/e2e/plain_ld_python.json 2> gpurun_out/e2e/plain_ld_python.err

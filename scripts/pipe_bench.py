@@ -25,11 +25,9 @@ def main():
     a = ap.parse_args()
     import ntcomp_amd as nt
     ix = nt.Index.load(os.path.join(a.dir, "idx"))
-    pool = []
-    for _ in range(max(a.contexts)):
-        c = nt.GpuContext(0)
-        c.upload(ix)
-        pool.append(c)
+    pool = [nt.GpuContext(0).upload(ix)]
+    for _ in range(max(a.contexts) - 1):  # further contexts share the first one's index
+        pool.append(nt.GpuContext(0).share_index(pool[0]))
     fq = os.path.join(a.dir, "reads.fq")
     for bpb, bb, nc in [(x, y, z) for x in a.bpb for y in a.batch_bases for z in a.contexts]:
         ctxs = pool[:nc]

@@ -235,3 +235,32 @@ def test_cli_decode_appends_and_shares_a_redirect(setup, tmp_path):
         for _ in range(2):
             _cli("decode", "-i", str(d / "idx"), str(path), "--blocks-per-batch", "2", stdout=f)
     assert shared.read_bytes() == exp + exp
+
+
+def test_contexts_share_one_index(setup, tmp_path):
+    """ntc_index_share: a second context on the GPU uses the first one's device index (no
+    second upload); both encode the same records, the shared index outlives the context that
+    uploaded it, and the CLI's --contexts-per-gpu 2 writes the same file as one context."""
+    d, genome, ix = setup
+    a = nt.GpuContext(0).upload(ix)
+    b = nt.GpuContext(0).share_index(a)
+    reads = nt.synth_reads(genome, 41, 0, 30_000, 150, 10_000)
+    offs = np.arange(0, len(reads) + 1, 150, dtype=np.uint64)
+    ra, oa = a.encode(reads, offs)
+    rb, ob = b.encode(reads, offs)
+    assert np.array_equal(ra, rb) and np.array_equal(oa, ob)
+    a.close()
+    rc, oc = b.encode(reads, offs)
+    assert np.array_equal(rc, ra)
+    out, _ = b.decode(rc)
+    assert np.array_equal(out, reads)
+    b.close()
+    fq = tmp_path / "r.fq"
+    write_fastq(fq, reads, 150)
+    outs = {}
+    for c in (1, 2):
+        with open(tmp_path / f"{c}.dat", "wb") as f:
+            _cli("encode", "-i", str(d / "idx"), str(fq), "--contexts-per-gpu", str(c), "--blocks-per-batch", "1",
+                 "--deflate", "zlib", stdout=f)
+        outs[c] = (tmp_path / f"{c}.dat").read_bytes()
+    assert outs[1] == outs[2]
