@@ -74,6 +74,10 @@ int ntc_pack_block(const uint64_t *recs, uint64_t n_recs, uint64_t num_records, 
  * block is dropped (nothing written).                                                  */
 int ntc_deflate_block(const ntc_block_meta *meta, const uint8_t *payload, int engine, uint8_t **out,
                       uint64_t *out_len);
+/* One stream's part of ntc_deflate_block (its 32-byte header + gzip member): a block's
+ * bytes are streams 0..3 concatenated, so a pool can deflate them in parallel.          */
+int ntc_deflate_stream(const ntc_block_meta *meta, int stream, const uint8_t *payload, int engine, uint8_t **out,
+                       uint64_t *out_len);
 /* Parses one block at data[0..len).  NTC_ERR_IO on a clean end of input (no bytes left),
  * NTC_ERR_FORMAT on a damaged block (decode_block's Err, which ends the reference's
  * decode loop, src/main.rs:202).                                                      */
@@ -109,6 +113,26 @@ int ntc_pack_blocks_device(ntc_ctx *ctx, const uint64_t *d_recs, const uint64_t 
 int ntc_encode_pack_batch(ntc_ctx *ctx, const uint8_t *bases, const uint64_t *read_offsets, uint64_t n_reads,
                           uint32_t block_reads, ntc_block_meta *meta, uint8_t **payload, uint64_t *payload_bytes,
                           int64_t *bad_read);
+
+/* ---- FASTQ parsed on the GPU ------------------------------------------------------------ */
+/* The CLI's ingest (src/main.rs:158-163: needletail records + normalize(true)) for plain
+ * FASTQ, done on the device: fastq[0, fastq_bytes) is the text of exactly n_reads records of
+ * 4 lines each ('@' header, sequence, '+' line, quality as long as the sequence after one
+ * '\r' is stripped from each; the last line may lack its newline) and nothing else -- no
+ * blank lines, which the host parser (ntc_fastx_*) skips between records and the caller
+ * sends there.  Bases are the sequence lines normalised as ntc_fastx does.  Text under
+ * 4 GiB per call.  NTC_ERR_FORMAT (bad_read = the first failing record) if the text is not
+ * that.  Synchronous; fastq should be pinned host memory for full PCIe speed.
+ *   ntc_fastq_parse        bases + read_offsets[n_reads + 1] back to the host (tests, tools);
+ *                          *n_bases = bases parsed (NTC_ERR_CAPACITY past bases_capacity)
+ *   ntc_encode_pack_fastq  ntc_encode_pack_batch on the parsed reads, which never leave
+ *                          HBM: same metas and payload as parsing on the host and calling
+ *                          ntc_encode_pack_batch; *n_bases = bases encoded              */
+int ntc_fastq_parse(ntc_ctx *ctx, const uint8_t *fastq, uint64_t fastq_bytes, uint64_t n_reads, uint8_t *bases_out,
+                    uint64_t bases_capacity, uint64_t *read_offsets_out, uint64_t *n_bases, int64_t *bad_read);
+int ntc_encode_pack_fastq(ntc_ctx *ctx, const uint8_t *fastq, uint64_t fastq_bytes, uint64_t n_reads,
+                          uint32_t block_reads, ntc_block_meta *meta, uint8_t **payload, uint64_t *payload_bytes,
+                          uint64_t *n_bases, int64_t *bad_read);
 
 #ifdef __cplusplus
 }

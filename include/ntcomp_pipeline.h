@@ -4,6 +4,9 @@
  *   ntc_encode_file   src/main.rs:141-181 (`ntcomp encode -i P reads > encoded.dat`):
  *                     FASTX batches -> GPU encode + block packer on every context ->
  *                     deflate on the host pool -> file header + blocks, in file order.
+ *                     A plain FASTQ goes to the GPU as text, cut at block boundaries,
+ *                     and is parsed there (ntc_encode_pack_fastq); a batch with a blank
+ *                     line, and every compressed or FASTA input, is parsed on the host.
  *   ntc_decode_file   src/main.rs:183-211 (`ntcomp decode -i P encoded.dat > out.fasta`):
  *                     blocks inflated + stream-decoded on the host pool -> GPU walk and
  *                     FASTA formatting on every context -> ">seq.N" records in file order.
@@ -30,7 +33,8 @@ typedef struct ntc_pipeline_opts {
     int32_t blocks_per_batch; /* 65,536-read blocks per GPU call; <= 0: 4 (encode), 2 (decode) */
     uint64_t batch_bases;     /* encode: bases per pinned batch buffer; 0: 64 Mi (grows for long reads) */
     int32_t deflate_engine;   /* NTC_DEFLATE_ZLIB (0) or NTC_DEFLATE_LIBDEFLATE (1)           */
-    int32_t reserved;
+    int32_t host_parse;       /* encode, plain FASTQ: 0 = the text goes to the GPU, which parses
+                                 it (ntc_encode_pack_fastq); 1 = parsed by the host pool      */
 } ntc_pipeline_opts;
 
 typedef struct ntc_pipeline_stats {
@@ -40,7 +44,7 @@ typedef struct ntc_pipeline_stats {
     double alloc_s;                            /* seconds spent pinning host buffers        */
     double first_batch_s, reader_done_s, gpu_done_s; /* timeline from the call's start       */
     int32_t threads;
-    int32_t reserved;
+    int32_t gpu_parsed;                        /* encode: batches parsed on the GPU (FASTQ text) */
     int64_t bad_read;                          /* file index of the failing read, or -1     */
     char error[256];
 } ntc_pipeline_stats;

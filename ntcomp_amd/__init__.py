@@ -40,7 +40,8 @@ EXPORTED = [
     "ntc_memcpy_d2h", "ntc_debug_matching_statistics", "ntc_build_index", "ntc_index_free",
     "ntc_index_view_of", "ntc_index_save", "ntc_index_save_as", "ntc_index_load", "ntc_synth_genome", "ntc_synth_strains", "ntc_synth_reads", "ntc_minimizer_keys",
     "ntc_file_header", "ntc_write_block", "ntc_read_block", "ntc_buffer_free", "ntc_pack_block",
-    "ntc_deflate_block", "ntc_pack_blocks_device", "ntc_encode_pack_batch", "ntc_read_block_into",
+    "ntc_deflate_block", "ntc_deflate_stream", "ntc_pack_blocks_device", "ntc_encode_pack_batch", "ntc_fastq_parse",
+    "ntc_encode_pack_fastq", "ntc_read_block_into",
     "ntc_fastx_open", "ntc_fastx_next_batch", "ntc_fastx_close", "ntc_fasta_format", "ntc_fastx_next_batch_into",
     "ntc_fastx_set_threads", "ntc_host_threads", "ntc_encode_file", "ntc_decode_fasta",
     "ntc_decode_file", "ntc_build_index_device", "ntc_build_index_device_ex", "ntc_index_set_prefix_precalc",
@@ -75,7 +76,7 @@ DEFLATE_ENGINES = {"zlib": 0, "libdeflate": 1}
 
 class PipelineOpts(ctypes.Structure):
     _fields_ = [("threads", ctypes.c_int32), ("blocks_per_batch", ctypes.c_int32), ("batch_bases", ctypes.c_uint64),
-                ("deflate_engine", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("deflate_engine", ctypes.c_int32), ("host_parse", ctypes.c_int32)]
 
 
 class PipelineStats(ctypes.Structure):
@@ -83,7 +84,7 @@ class PipelineStats(ctypes.Structure):
                 ("dropped_blocks", ctypes.c_uint64), ("bytes_out", ctypes.c_uint64), ("parse_s", ctypes.c_double),
                 ("gpu_s", ctypes.c_double), ("deflate_s", ctypes.c_double), ("write_s", ctypes.c_double),
                 ("wall_s", ctypes.c_double), ("alloc_s", ctypes.c_double), ("first_batch_s", ctypes.c_double),
-                ("reader_done_s", ctypes.c_double), ("gpu_done_s", ctypes.c_double), ("threads", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("reader_done_s", ctypes.c_double), ("gpu_done_s", ctypes.c_double), ("threads", ctypes.c_int32), ("gpu_parsed", ctypes.c_int32),
                 ("bad_read", ctypes.c_int64), ("error", ctypes.c_char * 256)]
 
 
@@ -200,9 +201,13 @@ def lib():
         "ntc_read_block_into": (I, [P, u64, ctypes.POINTER(u64), P, u64, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "ntc_pack_block": (I, [P, u64, u64, ctypes.POINTER(BlockMeta), ctypes.POINTER(P), ctypes.POINTER(u64)]),
         "ntc_deflate_block": (I, [ctypes.POINTER(BlockMeta), P, I, ctypes.POINTER(P), ctypes.POINTER(u64)]),
+        "ntc_deflate_stream": (I, [ctypes.POINTER(BlockMeta), I, P, I, ctypes.POINTER(P), ctypes.POINTER(u64)]),
         "ntc_pack_blocks_device": (I, [P, P, P, u64, u32, P, u64, P, ctypes.POINTER(u64)]),
         "ntc_encode_pack_batch": (I, [P, P, P, u64, u32, P, ctypes.POINTER(P), ctypes.POINTER(u64),
                                       ctypes.POINTER(i64)]),
+        "ntc_fastq_parse": (I, [P, P, u64, u64, P, u64, P, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_int64)]),
+        "ntc_encode_pack_fastq": (I, [P, P, u64, u64, u32, P, ctypes.POINTER(P), ctypes.POINTER(u64),
+                                      ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_int64)]),
         "ntc_fastx_open": (I, [ctypes.c_char_p, ctypes.POINTER(P)]),
         "ntc_fastx_next_batch": (I, [P, u64, u64, ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(u64)]),
         "ntc_fastx_close": (None, [P]),
@@ -501,6 +506,41 @@ class GpuContext:
             self.L.ntc_buffer_free(out)
         return list(metas)[:nb], payload
 
+    def parse_fastq(self, text, n_reads):
+        """Plain FASTQ text of exactly n_reads 4-line records -> (bases, offsets), parsed on
+        the GPU (ntc_fastq_parse, fastq.hip); NtcError(NTC_ERR_FORMAT) with .bad_read."""
+        t = np.frombuffer(bytes(text), dtype=np.uint8) if len(text) else np.zeros(1, dtype=np.uint8)
+        bases = np.empty(len(text) // 2 + 1, dtype=np.uint8)
+        offs = np.zeros(n_reads + 1, dtype=np.uint64)
+        nb, bad = ctypes.c_uint64(), ctypes.c_int64(-1)
+        rc = self.L.ntc_fastq_parse(self.h, _p(t), len(text), n_reads, _p(bases), len(bases), _p(offs),
+                                    ctypes.byref(nb), ctypes.byref(bad))
+        if rc:
+            e = NtcError(rc, self.L.ntc_last_error(self.h).decode(errors="replace"))
+            e.bad_read = bad.value
+            raise e
+        return bases[:nb.value].copy(), offs
+
+    def encode_pack_fastq(self, text, n_reads, block_reads=65536):
+        """encode_pack on FASTQ text parsed on the GPU (ntc_encode_pack_fastq) -> (list of
+        BlockMeta, payload bytes, bases encoded)."""
+        t = np.frombuffer(bytes(text), dtype=np.uint8) if len(text) else np.zeros(1, dtype=np.uint8)
+        nb = (n_reads + block_reads - 1) // block_reads
+        metas = (BlockMeta * max(nb, 1))()
+        out, used, nbases, bad = ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int64(-1)
+        rc = self.L.ntc_encode_pack_fastq(self.h, _p(t), len(text), n_reads, block_reads, metas, ctypes.byref(out),
+                                          ctypes.byref(used), ctypes.byref(nbases), ctypes.byref(bad))
+        if rc:
+            self.L.ntc_buffer_free(out)
+            e = NtcError(rc, self.L.ntc_last_error(self.h).decode(errors="replace"))
+            e.bad_read = bad.value
+            raise e
+        try:
+            payload = ctypes.string_at(out.value, used.value) if used.value else b""
+        finally:
+            self.L.ntc_buffer_free(out)
+        return list(metas)[:nb], payload, int(nbases.value)
+
     def encode_status(self):
         bad, n = ctypes.c_int64(-1), ctypes.c_uint64()
         self._check(self.L.ntc_encode_status(self.h, ctypes.byref(bad), ctypes.byref(n)), "ntc_encode_status")
@@ -635,6 +675,21 @@ def deflate_block(meta, payload, engine="zlib"):
         lib().ntc_buffer_free(out)
 
 
+def deflate_stream(meta, stream, payload, engine="zlib"):
+    """One stream's header + gzip member (ntc_deflate_stream); the four concatenated are
+    deflate_block's bytes."""
+    buf = np.frombuffer(payload, dtype=np.uint8) if len(payload) else np.zeros(1, dtype=np.uint8)
+    out, n = ctypes.c_void_p(), ctypes.c_uint64()
+    rc = lib().ntc_deflate_stream(ctypes.byref(meta), stream, _p(buf), DEFLATE_ENGINES[engine], ctypes.byref(out),
+                                  ctypes.byref(n))
+    if rc:
+        raise NtcError(rc, "ntc_deflate_stream")
+    try:
+        return ctypes.string_at(out.value, n.value)
+    finally:
+        lib().ntc_buffer_free(out)
+
+
 def read_block(data):
     """One block of decode_block (lib.rs:320-363) -> (u64 records, bytes consumed,
     num_records header field).  NtcError(NTC_ERR_IO) at a clean end of input."""
@@ -653,12 +708,15 @@ def read_block(data):
 
 
 # ---- FASTX ingest ---------------------------------------------------------------------
-def encode_file(ctxs, in_path, out_fd, threads=0, blocks_per_batch=4, batch_bases=0, deflate="zlib"):
+def encode_file(ctxs, in_path, out_fd, threads=0, blocks_per_batch=4, batch_bases=0, deflate="zlib",
+                host_parse=False):
     """`ntcomp encode` file to file (ntc_encode_file, include/ntcomp_pipeline.h): FASTX ->
     GPU encode + block packer on every context -> deflate pool -> encoded.dat on out_fd.
-    Returns the per-stage stats as a dict; raises NtcError (with .bad_read)."""
+    A plain FASTQ is parsed on the GPU unless host_parse.  Returns the per-stage stats as
+    a dict (gpu_parsed = batches parsed on the GPU); raises NtcError (with .bad_read)."""
     return _run_pipeline("ntc_encode_file", ctxs, in_path, out_fd,
-                         PipelineOpts(threads, blocks_per_batch, batch_bases, DEFLATE_ENGINES[deflate], 0))
+                         PipelineOpts(threads, blocks_per_batch, batch_bases, DEFLATE_ENGINES[deflate],
+                                      1 if host_parse else 0))
 
 
 def decode_file(ctxs, in_path, out_fd, threads=0, blocks_per_batch=2):
@@ -675,7 +733,7 @@ def _run_pipeline(fn, ctxs, in_path, out_fd, o):
     st = PipelineStats()
     rc = getattr(lib(), fn)(arr, len(ctxs), os.fsencode(in_path), out_fd, ctypes.byref(o), ctypes.byref(st))
     d = {k: (getattr(st, k).decode(errors="replace") if k == "error" else getattr(st, k))
-         for k, _ in PipelineStats._fields_ if k != "reserved"}
+         for k, _ in PipelineStats._fields_}
     if rc:
         e = NtcError(rc, d["error"])
         e.bad_read = d["bad_read"]

@@ -153,9 +153,9 @@ def _devices(args):
 
 
 def cmd_encode(args):
-    """main.rs:141-181 through the native pipeline (ntc_encode_file): FASTX parse on the
-    host pool, GPU encode + block packer per context, deflate on the host pool, blocks
-    written in file order."""
+    """main.rs:141-181 through the native pipeline (ntc_encode_file): plain FASTQ parsed
+    on the GPU (--host-parse: on the host pool, as every other input is), GPU encode +
+    block packer per context, deflate on the host pool, blocks written in file order."""
     import ntcomp_amd as nt
     st = _Stats(args.stats)
     log("Loading SBWT index...")
@@ -168,7 +168,8 @@ def cmd_encode(args):
     out.flush()
     try:
         res = st.wrap("pipeline", nt.encode_file)(ctxs, args.query_file, out.fileno(), threads=args.threads,
-                                                  blocks_per_batch=args.blocks_per_batch, deflate=args.deflate)
+                                                  blocks_per_batch=args.blocks_per_batch, deflate=args.deflate,
+                                                  host_parse=args.host_parse)
     except nt.NtcError as e:
         bad = getattr(e, "bad_read", -1)
         raise SystemExit(f"ntcomp encode: {e}" + (f" (read {bad + 1})" if bad is not None and bad >= 0 else ""))
@@ -182,7 +183,8 @@ def cmd_encode(args):
         for k in ("parse_s", "gpu_s", "deflate_s", "write_s"):
             st.acc[k[:-2]] = res[k]
     st.report(command="encode", gpus=len(ctxs), threads=res["threads"], reads=res["reads"], blocks=res["blocks"],
-              dropped_blocks=res["dropped_blocks"], pipeline_wall_s=round(res["wall_s"], 3), deflate=args.deflate)
+              dropped_blocks=res["dropped_blocks"], pipeline_wall_s=round(res["wall_s"], 3), deflate=args.deflate,
+              gpu_parsed_batches=res["gpu_parsed"])
 
 
 def cmd_decode(args):
@@ -258,6 +260,8 @@ def main(argv=None):
                         "zlib.  The deflate bytes differ, the inflated streams do not; neither engine "
                         "reproduces the reference's zlib-rs bytes")
     e.add_argument("--stats", action="store_true", help="print per-stage seconds to stderr")
+    e.add_argument("--host-parse", action="store_true",
+                   help="parse a plain FASTQ on the host pool instead of the GPU")
     d = sub.add_parser("decode", help="Decode data written with Encode")
     d.add_argument("input_path", help="File with encoded fastX data.")
     d.add_argument("-i", "--index", dest="index_prefix", required=True, help="Prefix for prebuilt <prefix>.sbwt and <prefix>.lcs")

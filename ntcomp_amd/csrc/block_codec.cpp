@@ -500,8 +500,30 @@ int ntc_pack_block(const uint64_t *recs, uint64_t n_recs, uint64_t num_records, 
 }
 
 // compress_block's header + deflate_bytes for each stream (encode.rs:96-127)
-int ntc_deflate_block(const ntc_block_meta *meta, const uint8_t *payload, int engine, uint8_t **out,
-                      uint64_t *out_len) {
+}  // extern "C"
+
+namespace {
+// stream s of a block: its 32-byte header (write_block_to's fields) + gzip member, appended
+int deflate_stream_into(const ntc_block_meta *meta, int s, const uint8_t *payload, int engine,
+                        std::vector<uint8_t> &buf) {
+    const ntc_stream_meta &m = meta->stream[s];
+    const size_t hpos = buf.size();
+    buf.resize(hpos + 32);
+    if (!gzip_append(payload + m.offset, m.encoded_size * 8, engine, buf)) return NTC_ERR_FORMAT;
+    BlockHeader h{};
+    h.block_size = (uint32_t)(buf.size() - hpos - 32);
+    h.num_records = (uint32_t)meta->num_records;
+    h.num_u64 = (uint32_t)m.num_u64;
+    h.encoded_size = (uint32_t)m.encoded_size;
+    h.rice_param = m.param;
+    h.bitpacker_exponent = 8;
+    std::vector<uint8_t> hb;
+    write_header(hb, h);
+    std::memcpy(buf.data() + hpos, hb.data(), 32);
+    return NTC_OK;
+}
+
+int deflate_checks(const ntc_block_meta *meta, const uint8_t *payload, int engine, uint8_t **out, uint64_t *out_len) {
     if (!meta || !out || !out_len) return NTC_ERR_INVALID_ARG;
     *out = nullptr;
     *out_len = 0;
@@ -509,32 +531,43 @@ int ntc_deflate_block(const ntc_block_meta *meta, const uint8_t *payload, int en
     if (!payload) return NTC_ERR_INVALID_ARG;
     if (engine != NTC_DEFLATE_ZLIB && engine != NTC_DEFLATE_LIBDEFLATE) return NTC_ERR_INVALID_ARG;
     if (engine == NTC_DEFLATE_LIBDEFLATE && !libdeflate().ok) return NTC_ERR_UNSUPPORTED;
-    std::vector<uint8_t> buf;
-    uint64_t est = 0;
-    for (int s = 0; s < 4; s++) est += meta->stream[s].encoded_size * 8 + 64;
-    buf.reserve(est + est / 16);
-    for (int s = 0; s < 4; s++) {
-        const ntc_stream_meta &m = meta->stream[s];
-        const size_t hpos = buf.size();
-        buf.resize(hpos + 32);
-        if (!gzip_append(payload + m.offset, m.encoded_size * 8, engine, buf)) return NTC_ERR_FORMAT;
-        BlockHeader h{};
-        h.block_size = (uint32_t)(buf.size() - hpos - 32);
-        h.num_records = (uint32_t)meta->num_records;
-        h.num_u64 = (uint32_t)m.num_u64;
-        h.encoded_size = (uint32_t)m.encoded_size;
-        h.rice_param = m.param;
-        h.bitpacker_exponent = 8;
-        std::vector<uint8_t> hb;
-        write_header(hb, h);
-        std::memcpy(buf.data() + hpos, hb.data(), 32);
-    }
+    return NTC_OK;
+}
+
+int hand_out(const std::vector<uint8_t> &buf, uint8_t **out, uint64_t *out_len) {
     uint8_t *o = (uint8_t *)std::malloc(buf.size() ? buf.size() : 1);
     if (!o) return NTC_ERR_CAPACITY;
     std::memcpy(o, buf.data(), buf.size());
     *out = o;
     *out_len = buf.size();
     return NTC_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int ntc_deflate_block(const ntc_block_meta *meta, const uint8_t *payload, int engine, uint8_t **out,
+                      uint64_t *out_len) {
+    int rc = deflate_checks(meta, payload, engine, out, out_len);
+    if (rc) return rc;
+    std::vector<uint8_t> buf;
+    uint64_t est = 0;
+    for (int s = 0; s < 4; s++) est += meta->stream[s].encoded_size * 8 + 64;
+    buf.reserve(est + est / 16);
+    for (int s = 0; s < 4; s++)
+        if ((rc = deflate_stream_into(meta, s, payload, engine, buf))) return rc;
+    return hand_out(buf, out, out_len);
+}
+
+int ntc_deflate_stream(const ntc_block_meta *meta, int stream, const uint8_t *payload, int engine, uint8_t **out,
+                       uint64_t *out_len) {
+    if (stream < 0 || stream > 3) return NTC_ERR_INVALID_ARG;
+    int rc = deflate_checks(meta, payload, engine, out, out_len);
+    if (rc) return rc;
+    std::vector<uint8_t> buf;
+    buf.reserve(meta->stream[stream].encoded_size * 8 + meta->stream[stream].encoded_size / 2 + 128);
+    if ((rc = deflate_stream_into(meta, stream, payload, engine, buf))) return rc;
+    return hand_out(buf, out, out_len);
 }
 
 int ntc_write_block(const uint64_t *recs, uint64_t n_recs, uint64_t num_records, uint8_t **out, uint64_t *out_len) {

@@ -39,7 +39,8 @@ enum WsSlot {
     WS_D = 0, WS_S, WS_F, WS_R, WS_RECCOUNT, WS_SCANTMP, WS_TILEBASE, WS_TILEROWS,
     WS_STAGE_BASES, WS_STAGE_OFFS, WS_STAGE_RECS, WS_E, WS_DEC_A, WS_DEC_B, WS_DEC_C,
     WS_DEC_D, WS_Q, WS_E3, WS_NE, WS_COUNTER, WS_R2, WS_ED, WS_WAVECNT, WS_PACK_CHUNKS, WS_PACK_META,
-    WS_PACK_PAYLOAD, WS_FA_BASES, WS_FA_OFFS, WS_FA_SCAN, WS_ES, WS_OBASE, WS_COUNT
+    WS_PACK_PAYLOAD, WS_FA_BASES, WS_FA_OFFS, WS_FA_SCAN, WS_ES, WS_OBASE,
+    WS_FQ_RAW, WS_FQ_TILES, WS_FQ_NL, WS_FQ_KEPT, WS_COUNT
 };
 
 // The device index of one upload: freed with the last context that holds it
@@ -1267,34 +1268,20 @@ int ntc_pack_blocks_device(ntc_ctx *ctx, const uint64_t *d_recs, const uint64_t 
                             payload_bytes);
 }
 
-int ntc_encode_pack_batch(ntc_ctx *ctx, const uint8_t *bases, const uint64_t *read_offsets, uint64_t n_reads,
-                          uint32_t block_reads, ntc_block_meta *meta, uint8_t **payload, uint64_t *payload_bytes,
-                          int64_t *bad_read) {
-    if (bad_read) *bad_read = -1;
-    if (!ctx || !read_offsets || !meta || !payload || !payload_bytes || block_reads == 0 || (n_reads && !bases))
-        return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument or block_reads = 0");
-    *payload = nullptr;
-    *payload_bytes = 0;
-    HIP_TRY(ctx, hipSetDevice(ctx->device));
-    if (!ctx->has_index) return set_err(ctx, NTC_ERR_NO_INDEX, "no index uploaded");
-    if (ctx->encode_variant != 4) return set_err(ctx, NTC_ERR_UNSUPPORTED, "encode_pack needs encode_variant 4");
-    for (uint64_t r = 0; r < n_reads; r++)
-        if (read_offsets[r + 1] < read_offsets[r])
-            return set_err(ctx, NTC_ERR_INVALID_ARG, "read offsets must be non-decreasing");
-    if (n_reads == 0) return NTC_OK;
-    const uint64_t o0 = read_offsets[0], total = read_offsets[n_reads] - o0;
-    std::vector<uint64_t> offs(n_reads + 1);
-    for (uint64_t r = 0; r <= n_reads; r++) offs[r] = read_offsets[r] - o0;
-    void *d_bases, *d_offs, *d_recs, *d_payload;
+}  // extern "C"
+
+namespace {
+// encode + GPU block packer over reads already in HBM (d_offs: n_reads + 1 offsets, room for
+// n_reads + 1 more behind them, where the record offsets go); the tail of
+// ntc_encode_pack_batch and ntc_encode_pack_fastq
+int encode_pack_staged(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, uint64_t n_reads, uint64_t total,
+                       uint32_t block_reads, ntc_block_meta *meta, uint8_t **payload, uint64_t *payload_bytes,
+                       int64_t *bad_read) {
+    void *d_recs, *d_payload;
     int rc;
-    if ((rc = ensure(ctx, WS_STAGE_BASES, total + 64, &d_bases))) return rc;
-    if ((rc = ensure(ctx, WS_STAGE_OFFS, (n_reads + 1) * 8 * 2, &d_offs))) return rc;
     if ((rc = ensure(ctx, WS_STAGE_RECS, (total + 1) * 8, &d_recs))) return rc;
     uint64_t *d_roffs = (uint64_t *)d_offs + (n_reads + 1);
-    if (total) HIP_TRY(ctx, hipMemcpyAsync(d_bases, bases + o0, total, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(d_offs, offs.data(), (n_reads + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
-    rc = encode4_impl(ctx, (const uint8_t *)d_bases, (const uint64_t *)d_offs, n_reads, total, (uint64_t *)d_recs,
-                      total + 1, d_roffs);
+    rc = encode4_impl(ctx, d_bases, d_offs, n_reads, total, (uint64_t *)d_recs, total + 1, d_roffs);
     if (rc) return rc;
     int64_t bad = -1;
     if ((rc = read_status(ctx, &bad))) {
@@ -1324,6 +1311,132 @@ int ntc_encode_pack_batch(ntc_ctx *ctx, const uint8_t *bases, const uint64_t *re
     *payload = h;
     *payload_bytes = used;
     return NTC_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int ntc_encode_pack_batch(ntc_ctx *ctx, const uint8_t *bases, const uint64_t *read_offsets, uint64_t n_reads,
+                          uint32_t block_reads, ntc_block_meta *meta, uint8_t **payload, uint64_t *payload_bytes,
+                          int64_t *bad_read) {
+    if (bad_read) *bad_read = -1;
+    if (!ctx || !read_offsets || !meta || !payload || !payload_bytes || block_reads == 0 || (n_reads && !bases))
+        return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument or block_reads = 0");
+    *payload = nullptr;
+    *payload_bytes = 0;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (!ctx->has_index) return set_err(ctx, NTC_ERR_NO_INDEX, "no index uploaded");
+    if (ctx->encode_variant != 4) return set_err(ctx, NTC_ERR_UNSUPPORTED, "encode_pack needs encode_variant 4");
+    for (uint64_t r = 0; r < n_reads; r++)
+        if (read_offsets[r + 1] < read_offsets[r])
+            return set_err(ctx, NTC_ERR_INVALID_ARG, "read offsets must be non-decreasing");
+    if (n_reads == 0) return NTC_OK;
+    const uint64_t o0 = read_offsets[0], total = read_offsets[n_reads] - o0;
+    std::vector<uint64_t> offs(n_reads + 1);
+    for (uint64_t r = 0; r <= n_reads; r++) offs[r] = read_offsets[r] - o0;
+    void *d_bases, *d_offs;
+    int rc;
+    if ((rc = ensure(ctx, WS_STAGE_BASES, total + 64, &d_bases))) return rc;
+    if ((rc = ensure(ctx, WS_STAGE_OFFS, (n_reads + 1) * 8 * 2, &d_offs))) return rc;
+    if (total) HIP_TRY(ctx, hipMemcpyAsync(d_bases, bases + o0, total, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(d_offs, offs.data(), (n_reads + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+    return encode_pack_staged(ctx, (const uint8_t *)d_bases, (const uint64_t *)d_offs, n_reads, total, block_reads,
+                              meta, payload, payload_bytes, bad_read);
+}
+
+}  // extern "C"
+
+namespace {
+// FASTQ text -> bases (WS_STAGE_BASES) + read offsets (WS_STAGE_OFFS, room for the record
+// offsets behind them) in HBM, parsed on the device (fastq.hip); synchronous, so the
+// structure checks are answered before anything is encoded.  *total = bases kept.
+int fastq_stage(ntc_ctx *ctx, const uint8_t *fastq, uint64_t bytes, uint64_t n_reads, void **d_bases, void **d_offs,
+                uint64_t *total, int64_t *bad_read) {
+    if (bad_read) *bad_read = -1;
+    *total = 0;
+    if (bytes >= (1ull << 32)) return set_err(ctx, NTC_ERR_CAPACITY, "FASTQ text of 4 GiB or more: split the batch");
+    if (n_reads == 0 && bytes) return set_err(ctx, NTC_ERR_FORMAT, "FASTQ text given for zero reads");
+    const uint64_t tiles = fastq_tiles(bytes);
+    void *raw, *tl, *nl, *kept, *tmp;
+    int rc;
+    if ((rc = ensure(ctx, WS_FQ_RAW, bytes + 64, &raw))) return rc;
+    if ((rc = ensure(ctx, WS_FQ_TILES, tiles * 4 + (tiles + 1) * 8 + 8, &tl))) return rc;
+    if ((rc = ensure(ctx, WS_FQ_NL, 4 * n_reads * 4 + 4, &nl))) return rc;
+    if ((rc = ensure(ctx, WS_FQ_KEPT, n_reads * 4 + 4, &kept))) return rc;
+    if ((rc = ensure(ctx, WS_SCANTMP, scan_tmp_words(std::max(tiles, n_reads) + 1) * 8, &tmp))) return rc;
+    // a sequence line is no longer than its quality line, so bases <= bytes / 2
+    if ((rc = ensure(ctx, WS_STAGE_BASES, bytes / 2 + 64, d_bases))) return rc;
+    if ((rc = ensure(ctx, WS_STAGE_OFFS, (n_reads + 1) * 8 * 2, d_offs))) return rc;
+    FastqArgs a{};
+    a.raw = (const uint8_t *)raw;
+    a.n_raw = bytes;
+    a.n_reads = n_reads;
+    a.tile_base = (uint64_t *)tl;
+    a.tile_cnt = (uint32_t *)(a.tile_base + tiles + 1);
+    a.nl = (uint32_t *)nl;
+    a.kept = (uint32_t *)kept;
+    a.offs = (uint64_t *)*d_offs;
+    a.tmp = (uint64_t *)tmp;
+    a.bases = (uint8_t *)*d_bases;
+    a.status = ctx->d_status;
+    HIP_TRY(ctx, hipMemsetAsync(ctx->d_status, 0xFF, 8, ctx->stream));
+    if (bytes) HIP_TRY(ctx, hipMemcpyAsync(raw, fastq, bytes, hipMemcpyHostToDevice, ctx->stream));
+    launch_fastq_parse(a, ctx->stream);
+    HIP_TRY(ctx, hipGetLastError());
+    launch_status_box(ctx->d_status, a.offs + n_reads, nullptr, nullptr, ctx->h_box, ctx->stream);
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    const uint64_t st = ((volatile uint64_t *)ctx->h_box)[0];
+    if (st != ~0ULL) {
+        if (bad_read) *bad_read = (int64_t)(st >> 8);
+        char buf[160];
+        std::snprintf(buf, sizeof(buf), "malformed FASTQ record at index %lld", (long long)(st >> 8));
+        return set_err(ctx, (int)(st & 0xFF), buf);
+    }
+    *total = ((volatile uint64_t *)ctx->h_box)[1];
+    return NTC_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int ntc_fastq_parse(ntc_ctx *ctx, const uint8_t *fastq, uint64_t fastq_bytes, uint64_t n_reads, uint8_t *bases_out,
+                    uint64_t bases_capacity, uint64_t *read_offsets_out, uint64_t *n_bases, int64_t *bad_read) {
+    if (bad_read) *bad_read = -1;
+    if (!ctx || (fastq_bytes && !fastq) || !read_offsets_out) return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    void *d_bases, *d_offs;
+    uint64_t total = 0;
+    int rc = fastq_stage(ctx, fastq, fastq_bytes, n_reads, &d_bases, &d_offs, &total, bad_read);
+    if (rc) return rc;
+    if (n_bases) *n_bases = total;
+    if (total > bases_capacity || (total && !bases_out))
+        return set_err(ctx, NTC_ERR_CAPACITY, "bases_capacity smaller than the bases parsed");
+    HIP_TRY(ctx, hipMemcpy(read_offsets_out, d_offs, (n_reads + 1) * 8, hipMemcpyDeviceToHost));
+    if (total) HIP_TRY(ctx, hipMemcpy(bases_out, d_bases, total, hipMemcpyDeviceToHost));
+    return NTC_OK;
+}
+
+int ntc_encode_pack_fastq(ntc_ctx *ctx, const uint8_t *fastq, uint64_t fastq_bytes, uint64_t n_reads,
+                          uint32_t block_reads, ntc_block_meta *meta, uint8_t **payload, uint64_t *payload_bytes,
+                          uint64_t *n_bases, int64_t *bad_read) {
+    if (bad_read) *bad_read = -1;
+    if (!ctx || (fastq_bytes && !fastq) || !meta || !payload || !payload_bytes || block_reads == 0)
+        return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument or block_reads = 0");
+    *payload = nullptr;
+    *payload_bytes = 0;
+    if (n_bases) *n_bases = 0;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (!ctx->has_index) return set_err(ctx, NTC_ERR_NO_INDEX, "no index uploaded");
+    if (ctx->encode_variant != 4) return set_err(ctx, NTC_ERR_UNSUPPORTED, "encode_pack needs encode_variant 4");
+    void *d_bases, *d_offs;
+    uint64_t total = 0;
+    int rc = fastq_stage(ctx, fastq, fastq_bytes, n_reads, &d_bases, &d_offs, &total, bad_read);
+    if (rc) return rc;
+    if (n_bases) *n_bases = total;
+    if (n_reads == 0) return NTC_OK;
+    return encode_pack_staged(ctx, (const uint8_t *)d_bases, (const uint64_t *)d_offs, n_reads, total, block_reads,
+                              meta, payload, payload_bytes, bad_read);
 }
 
 int ntc_decode_fasta(ntc_ctx *ctx, const uint64_t *recs, uint64_t n_recs, uint64_t n_reads, uint64_t n_bases,

@@ -39,6 +39,7 @@
 #include <vector>
 
 #include "../../include/ntcomp_host.h"
+#include "ntc_internal.h"
 
 namespace {
 
@@ -1072,6 +1073,21 @@ int ntc_fastx_open(const char *path, ntc_fastx **out) {
     *out = fx;
     return NTC_OK;
 }
+
+}  // extern "C"
+
+namespace ntc {
+const uint8_t *fastx_mapped(ntc_fastx *fx, uint64_t *size) {
+    if (!fx || !fx->mm) return nullptr;
+    if (size) *size = fx->mm_n;
+    return (const uint8_t *)fx->mm;
+}
+void fastx_seek_mapped(ntc_fastx *fx, uint64_t pos) {
+    if (fx && fx->mm) fx->mm_pos = std::min<size_t>((size_t)pos, fx->mm_n);
+}
+}  // namespace ntc
+
+extern "C" {
 
 int ntc_fastx_next_batch(ntc_fastx *fx, uint64_t max_reads, uint64_t max_bases, const uint8_t **bases,
                          const uint64_t **offsets, uint64_t *n_reads) {

@@ -140,6 +140,27 @@ void launch_fasta(const uint8_t *d_bases, const uint64_t *d_offs, uint64_t n, ui
                   const unsigned long long *d_status, uint64_t *sizes, uint64_t *out_offs, uint64_t *tmp, uint8_t *out,
                   uint64_t out_cap, hipStream_t s);
 
+// plain FASTQ text of n_reads whole 4-line records -> normalised bases + read offsets
+// (fastq.hip).  tile_cnt: fastq_tiles(n_raw) words, tile_base: tiles + 1 (its last word =
+// the newlines found), nl: 4 n_reads, kept: n_reads, offs: n_reads + 1, tmp:
+// scan_tmp_words(max(tiles, n_reads) + 1), bases: room for the sequence lines' bytes.
+// status (preset to ~0) gets read << 8 | NTC_ERR_FORMAT for the first malformed record;
+// then no base is written.
+struct FastqArgs {
+    const uint8_t *raw;
+    uint64_t n_raw, n_reads;
+    uint32_t *tile_cnt;
+    uint64_t *tile_base;
+    uint32_t *nl;
+    uint32_t *kept;
+    uint64_t *offs;
+    uint64_t *tmp;
+    uint8_t *bases;
+    unsigned long long *status;
+};
+uint64_t fastq_tiles(uint64_t n_raw);
+void launch_fastq_parse(const FastqArgs &a, hipStream_t s);
+
 void launch_encode(const EncodeArgs &a, hipStream_t s);
 void launch_encode4(const Enc4Args &a, uint64_t total, uint32_t ms_blocks, hipStream_t s,
                     hipEvent_t ev_ms_begin, hipEvent_t ev_ms_end);

@@ -29,6 +29,14 @@ bool save_index_as(const HostIndex &ix, const std::string &prefix, int layout, s
 
 }  // namespace ntc
 
+struct ntc_fastx;
+namespace ntc {
+// a plain FASTQ that ntc_fastx_open mapped: its bytes (null for any other input), and
+// moving the mapped parser to byte pos (a record start) -- pipeline.cpp's GPU-parse reader
+const uint8_t *fastx_mapped(ntc_fastx *fx, uint64_t *size);
+void fastx_seek_mapped(ntc_fastx *fx, uint64_t pos);
+}  // namespace ntc
+
 struct ntc_index_host {
     ntc::HostIndex ix;
 };

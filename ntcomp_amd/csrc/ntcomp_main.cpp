@@ -7,7 +7,7 @@
 //   ntcomp build -o P [-k 31] [-p 8] [-d] [-t 1] [-m 4] [--temp-dir D] [--verbose]
 //                [-l LIST] [--builder auto|host|gpu] [--device N] [--index-format own|sbwt-rs] FILES...
 //   ntcomp encode -i P [--gpus N | --devices 0,0,..] [--threads T] [--blocks-per-batch B]
-//                 [--deflate auto|zlib|libdeflate] [--stats] FILE > encoded.dat
+//                 [--deflate auto|zlib|libdeflate] [--host-parse] [--stats] FILE > encoded.dat
 //   ntcomp decode -i P [--gpus N | --devices ..] [--threads T] [--blocks-per-batch B] [--stats] FILE > out.fasta
 #include <dlfcn.h>
 #include <unistd.h>
@@ -157,6 +157,7 @@ int cmd_encode(const Args &a) {
     o.threads = std::atoi(a.get("--threads", nullptr, "0").c_str());
     o.blocks_per_batch = std::atoi(a.get("--blocks-per-batch", nullptr, "4").c_str());
     o.deflate_engine = engine == "libdeflate" ? NTC_DEFLATE_LIBDEFLATE : NTC_DEFLATE_ZLIB;
+    o.host_parse = a.flag("--host-parse") ? 1 : 0;
     ntc_pipeline_stats st{};
     std::fflush(stdout);
     const int rc = ntc_encode_file(ctxs.data(), (int)ctxs.size(), a.pos[0].c_str(), 1, &o, &st);
@@ -176,10 +177,10 @@ int cmd_encode(const Args &a) {
                      "{\"stats\": {\"index_load\": %.3f, \"gpu_init_upload\": %.3f, \"parse\": %.3f, \"gpu\": %.3f, "
                      "\"deflate\": %.3f, \"write\": %.3f}, \"command\": \"encode\", \"native\": true, \"gpus\": %zu, "
                      "\"threads\": %d, \"reads\": %llu, \"blocks\": %llu, \"dropped_blocks\": %llu, "
-                     "\"pipeline_wall_s\": %.3f, \"deflate\": \"%s\", \"process_s\": %.3f}\n",
+                     "\"pipeline_wall_s\": %.3f, \"deflate\": \"%s\", \"gpu_parsed_batches\": %d, \"process_s\": %.3f}\n",
                      t_load, t_gpu - t_load, st.parse_s, st.gpu_s, st.deflate_s, st.write_s, ctxs.size(), st.threads,
                      (unsigned long long)st.reads, (unsigned long long)st.blocks,
-                     (unsigned long long)st.dropped_blocks, st.wall_s, engine.c_str(), since(t0));
+                     (unsigned long long)st.dropped_blocks, st.wall_s, engine.c_str(), st.gpu_parsed, since(t0));
     return 0;
 }
 

@@ -1,20 +1,27 @@
 // Native encode pipeline of the CLI: `ntcomp encode -i P reads.fq > encoded.dat`
 // (src/main.rs:141-181), file in, encoded.dat out, with every stage overlapped:
 //
-//   reader   FASTX batches of blocks_per_batch x 65,536 reads (main.rs:152) into a ring of
-//            pinned host buffers (ntc_fastx_next_batch_into: plain FASTQ is mapped and
-//            parsed by the host pool).  Reads past the last whole block of a batch carry
-//            into the next buffer, so every block but the file's last holds exactly 65,536
-//            reads, and the last holds num_records % 65,536 (main.rs:174-177).
+//   reader   batches of blocks_per_batch x 65,536 reads (main.rs:152) into a ring of
+//            pinned host buffers.  A plain FASTQ (mapped) goes as text: the reader's gang
+//            copies it into the buffer while counting newlines and looking for blank lines
+//            (fq_copy_scan), and cuts the batch after the last whole block's last line, so
+//            the GPU parses it (ntc_encode_pack_fastq).  Anything else -- compressed input,
+//            FASTA, a batch with a blank line from there on -- is parsed by the host pool
+//            (ntc_fastx_next_batch_into); reads past the last whole block of a batch carry
+//            into the next buffer.  Either way every block but the file's last holds
+//            exactly 65,536 reads, and the last holds num_records % 65,536 (main.rs:174-177).
 //   GPU      one driver thread per context, batches dealt round-robin:
-//            ntc_encode_pack_batch = H2D, encode kernels, GPU block packer, D2H of the four
-//            coded streams per block (the u64 records never leave HBM).
+//            ntc_encode_pack_fastq / ntc_encode_pack_batch = H2D, (parse,) encode kernels,
+//            GPU block packer, D2H of the four coded streams per block (the u64 records
+//            never leave HBM).
 //   deflate  the host pool gzips each block's streams (ntc_deflate_block) -- the only
 //            codec step left on the CPU.
 //   writer   the calling thread writes the file header (lib.rs:52-67) and the blocks in
 //            file order; a block the reference drops (no long or no short record,
 //            write_block_to errs and main.rs:170 ignores it -- App. B.3) is skipped.
+#include <emmintrin.h>
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -25,6 +32,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -36,16 +44,40 @@
 #include "../../include/ntcomp_gpu.h"
 #include "../../include/ntcomp_host.h"
 #include "../../include/ntcomp_pipeline.h"
+#include "ntc_internal.h"
 
 namespace {
 
 using Clock = std::chrono::steady_clock;
 double secs(Clock::time_point a, Clock::time_point b) { return std::chrono::duration<double>(b - a).count(); }
 
+// Pinned host memory: 2 MB pages, registered with HIP (hipHostRegister runs at ~25 GB/s,
+// hipHostMalloc at ~4 GB/s on the box: scripts/ingest_bw.cpp, profiles/round4)
+void *pinned_alloc(size_t n) {
+    const size_t sz = (std::max<size_t>(n, 1) + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+    void *p = std::aligned_alloc(2u << 20, sz);
+    if (!p) return nullptr;
+    madvise(p, sz, MADV_HUGEPAGE);
+    if (hipHostRegister(p, sz, hipHostRegisterPortable) != hipSuccess) {
+        (void)hipGetLastError();
+        std::free(p);
+        return nullptr;
+    }
+    return p;
+}
+void pinned_free(void *p) {
+    if (!p) return;
+    (void)hipHostUnregister(p);
+    std::free(p);
+}
+
 struct Batch {  // one pinned buffer of the ring
     uint8_t *bases = nullptr;
     uint64_t *offs = nullptr;
     uint64_t cap_bases = 0, cap_reads = 0;
+    uint8_t *text = nullptr;  // plain FASTQ text for the GPU parse (text_len bytes, n_process records)
+    uint64_t text_cap = 0, text_len = 0;
+    bool is_text = false;
     uint64_t n_reads = 0;    // reads in the buffer (carry + new)
     uint64_t n_process = 0;  // reads handed to the GPU (whole blocks, or all at the end)
     uint64_t first_read = 0; // file index of the buffer's first read
@@ -53,10 +85,121 @@ struct Batch {  // one pinned buffer of the ring
     bool busy = false;
 };
 
-struct BlockOut {  // a deflated block, or a dropped one
-    uint8_t *data = nullptr;
-    uint64_t len = 0;
+// T - 1 helper threads that run one job at a time together with the caller (the reader's
+// copy + scan of each batch; spawning threads per batch costs ~1 ms a batch)
+struct Gang {
+    std::mutex mu;
+    std::condition_variable go, done;
+    std::function<void(int)> job;
+    uint64_t gen = 0;
+    int running = 0;
+    bool stop = false;
+    std::vector<std::thread> th;
+    explicit Gang(int T) {
+        for (int t = 1; t < T; t++)
+            th.emplace_back([this, t] {
+                uint64_t seen = 0;
+                for (;;) {
+                    std::function<void(int)> j;
+                    {
+                        std::unique_lock<std::mutex> g(mu);
+                        go.wait(g, [&] { return stop || gen != seen; });
+                        if (stop) return;
+                        seen = gen;
+                        j = job;
+                    }
+                    j(t);
+                    std::lock_guard<std::mutex> g(mu);
+                    if (--running == 0) done.notify_all();
+                }
+            });
+    }
+    int size() const { return (int)th.size() + 1; }
+    void run(const std::function<void(int)> &f) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            job = f;
+            running = (int)th.size();
+            gen++;
+        }
+        go.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> g(mu);
+        done.wait(g, [&] { return running == 0; });
+    }
+    ~Gang() {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            stop = true;
+        }
+        go.notify_all();
+        for (auto &x : th) x.join();
+    }
+};
+
+// Copy n bytes of FASTQ text into dst (16-byte aligned) and scan them on the way: the
+// newlines, and the first line inside the piece that starts with '\n' or '\r' (a blank
+// line, which the host parser skips between records; the piece's first byte is the caller's).
+struct FqScan {
+    uint64_t nl = 0;
+    size_t blank = SIZE_MAX;  // offset of the first blank line's first byte, or SIZE_MAX
+};
+FqScan fq_copy_scan(const uint8_t *src, uint8_t *dst, size_t n) {
+    FqScan r;
+    const __m128i NL = _mm_set1_epi8('\n'), CR = _mm_set1_epi8('\r');
+    uint64_t carry = 0;  // the byte before this 64-byte block is '\n'
+    size_t i = 0;
+    for (; i + 64 <= n; i += 64) {
+        uint64_t mnl = 0, mcr = 0;
+        for (int k = 0; k < 4; k++) {
+            const __m128i x = _mm_loadu_si128((const __m128i *)(src + i + 16 * k));
+            _mm_stream_si128((__m128i *)(dst + i + 16 * k), x);
+            mnl |= (uint64_t)(uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(x, NL)) << (16 * k);
+            mcr |= (uint64_t)(uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(x, CR)) << (16 * k);
+        }
+        const uint64_t bad = ((mnl << 1) | carry) & (mnl | mcr);
+        if (bad && r.blank == SIZE_MAX) r.blank = i + (size_t)__builtin_ctzll(bad);
+        carry = mnl >> 63;
+        r.nl += (uint64_t)__builtin_popcountll(mnl);
+    }
+    _mm_sfence();
+    for (; i < n; i++) {
+        const uint8_t c = src[i];
+        dst[i] = c;
+        if (carry && (c == '\n' || c == '\r') && r.blank == SIZE_MAX) r.blank = i;
+        carry = c == '\n';
+        r.nl += c == '\n';
+    }
+    return r;
+}
+
+// byte position just past the target-th newline (1-based) of p[0, n), or n
+size_t nth_newline_end(const uint8_t *p, size_t n, uint64_t target) {
+    const __m128i NL = _mm_set1_epi8('\n');
+    size_t i = 0;
+    for (; i + 64 <= n; i += 64) {
+        uint64_t m = 0;
+        for (int k = 0; k < 4; k++)
+            m |= (uint64_t)(uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_loadu_si128((const __m128i *)(p + i + 16 * k)), NL))
+                 << (16 * k);
+        const uint64_t c = (uint64_t)__builtin_popcountll(m);
+        if (c < target) {
+            target -= c;
+            continue;
+        }
+        for (; target > 1; target--) m &= m - 1;
+        return i + (size_t)__builtin_ctzll(m) + 1;
+    }
+    for (; i < n; i++)
+        if (p[i] == '\n' && --target == 0) return i + 1;
+    return n;
+}
+
+struct BlockOut {  // a deflated block (its four streams' parts), or a dropped one
+    uint8_t *part[4] = {nullptr, nullptr, nullptr, nullptr};
+    uint64_t len[4] = {0, 0, 0, 0};
     int status = NTC_OK;
+    int left = 0;  // parts not yet deflated
 };
 
 struct Shared {
@@ -102,6 +245,9 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
     int rc = ntc_fastx_open(in_path, &fx);
     if (rc) return rc;
     ntc_fastx_set_threads(fx, T);
+    // a mapped plain FASTQ goes to the GPU as text
+    uint64_t text_n = 0;
+    const uint8_t *text = o.host_parse ? nullptr : ntc::fastx_mapped(fx, &text_n);
 
     // pinned ring: the GPU threads hold at most n_ctx buffers, the reader fills one more.
     // A slot's base buffer (the large part, ~320 MB) is pinned by the reader when it first
@@ -112,9 +258,8 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
     for (auto &b : ring) {
         b.cap_bases = cap_bases + BR * 1024ull;  // a carry of < 65,536 reads sits in front
         b.cap_reads = per_batch + BR + 1;
-        if (hipHostMalloc((void **)&b.offs, b.cap_reads * 8, hipHostMallocDefault) != hipSuccess) {
-            for (auto &x : ring)
-                if (x.offs) (void)hipHostFree(x.offs);
+        if (!(b.offs = (uint64_t *)pinned_alloc(b.cap_reads * 8))) {
+            for (auto &x : ring) pinned_free(x.offs);
             ntc_fastx_close(fx);
             return NTC_ERR_HIP;
         }
@@ -126,11 +271,12 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
     bool reader_done = false;
     uint64_t total_blocks = 0;    // known once the reader is done
     std::atomic<double> t_parse{0}, t_gpu{0}, t_deflate{0}, t_write{0};
-    // deflate tasks and finished blocks
+    // deflate tasks (one per stream of a block: ntc_deflate_stream) and blocks in progress
     struct Task {
-        std::shared_ptr<std::vector<uint8_t>> payload;
+        std::shared_ptr<uint8_t> payload;  // the GPU call's host payload (ntc_buffer_free)
         ntc_block_meta meta;
         uint64_t block;
+        int stream;
     };
     std::deque<Task> tasks;
     std::map<uint64_t, BlockOut> done;
@@ -149,19 +295,103 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
     auto grow = [&](Batch &b, uint64_t need_bases, uint64_t keep_bases, uint64_t keep_reads) -> bool {
         if (need_bases <= b.cap_bases) return true;
         const uint64_t cap = std::max(need_bases, b.cap_bases * 2);
-        uint8_t *nbuf = nullptr;
-        if (hipHostMalloc((void **)&nbuf, cap, hipHostMallocDefault) != hipSuccess) return false;
+        uint8_t *nbuf = (uint8_t *)pinned_alloc(cap);
+        if (!nbuf) return false;
         if (keep_bases) std::memcpy(nbuf, b.bases, keep_bases);
-        (void)hipHostFree(b.bases);
+        pinned_free(b.bases);
         b.bases = nbuf;
         b.cap_bases = cap;
         (void)keep_reads;
         return true;
     };
+    // GPU-parse reader state: the next batch's text starts at text_pos (a record start)
+    uint64_t text_pos = 0;
+    double rec_bytes = 0;  // text bytes per record so far
+    std::atomic<uint64_t> text_batches{0};
+    const char *rt_env = std::getenv("NTC_READ_THREADS");  // A/B hook for the reader's gang
+    const int RT = std::max(1, rt_env ? std::atoi(rt_env) : T);
+    if (text) {  // bytes per record from the first MiB
+        const size_t m = (size_t)std::min<uint64_t>(text_n, 1u << 20);
+        uint64_t nl = 0;
+        for (size_t i = 0; i < m; i++) nl += text[i] == '\n';
+        rec_bytes = nl >= 4 ? 4.0 * (double)m / (double)nl : (double)m + 1;
+    }
+    // Fill b with the text of the next whole blocks (or the file's end): 1 = filled, 0 = no
+    // input left, -1 = hand over to the host parser at text_pos (a blank line before the
+    // cut, a line count that is not a multiple of 4 at the end, a block too large for one call)
+    auto fill_text = [&](Gang &gang, Batch &b, bool &eof) -> int {
+        const uint64_t kMaxText = (1ull << 32) - (64u << 20);  // ntc_encode_pack_fastq takes < 4 GiB
+        uint64_t want_cap = (uint64_t)((double)per_batch * rec_bytes * 1.03) + (256u << 10);
+        std::vector<FqScan> sc;
+        for (;;) {
+            if (text_pos >= text_n) return 0;
+            if (text[text_pos] != '@') return -1;
+            want_cap = std::min(want_cap, kMaxText);
+            if (b.text_cap < want_cap) {
+                const auto ta = Clock::now();
+                pinned_free(b.text);
+                b.text_cap = 0;
+                if (!(b.text = (uint8_t *)pinned_alloc(want_cap))) return -1;
+                b.text_cap = want_cap;
+                t_pin = t_pin.load() + secs(ta, Clock::now());
+            }
+            const uint64_t len = std::min(text_n - text_pos, want_cap);
+            const uint8_t *src = text + text_pos;
+            constexpr uint64_t kPiece = 1u << 20;
+            const uint64_t np = (len + kPiece - 1) / kPiece;
+            sc.assign(np, FqScan{});
+            std::atomic<uint64_t> next{0};
+            gang.run([&](int) {
+                for (uint64_t q; (q = next.fetch_add(1)) < np;) {
+                    const uint64_t a = q * kPiece;
+                    sc[q] = fq_copy_scan(src + a, b.text + a, std::min(len, a + kPiece) - a);
+                }
+            });
+            uint64_t nl = 0, blank = UINT64_MAX;  // the first blank line in the text read
+            for (uint64_t q = 0; q < np; q++) {
+                const uint64_t a = q * kPiece;
+                if (blank == UINT64_MAX && a && src[a - 1] == '\n' && (src[a] == '\n' || src[a] == '\r')) blank = a;
+                if (blank == UINT64_MAX && sc[q].blank != SIZE_MAX) blank = a + sc[q].blank;
+                nl += sc[q].nl;
+            }
+            eof = text_pos + len == text_n;
+            // the text read ends the file with whole records and no blank line: all of it goes;
+            // otherwise whole blocks of the complete records, cut after the last one's last line
+            const uint64_t lines = nl + (eof && src[len - 1] != '\n');
+            const bool whole = eof && lines % 4 == 0 && blank == UINT64_MAX;
+            const uint64_t recs = whole ? lines / 4 : nl / 4;
+            uint64_t n = 0, cut = len;
+            if (whole && recs <= per_batch) {
+                n = recs;
+            } else {
+                n = std::min<uint64_t>(recs, per_batch) / BR * BR;
+                if (n == 0) {  // not one whole block in the text read: read more, or give up
+                    if (eof || len < want_cap || want_cap >= kMaxText) return -1;
+                    want_cap *= 2;
+                    continue;
+                }
+                // the batch ends after newline 4 n: find the piece holding it
+                uint64_t before = 0, q = 0;
+                while (before + sc[q].nl < 4 * n) before += sc[q++].nl;
+                const uint64_t a = q * kPiece;
+                cut = a + nth_newline_end(src + a, std::min(len, a + kPiece) - a, 4 * n - before);
+                eof = false;
+            }
+            if (blank < cut) return -1;  // the batch holds a blank line: the host parser takes it
+            b.text_len = cut;
+            b.n_reads = b.n_process = n;
+            text_pos += cut;
+            rec_bytes = (double)cut / (double)std::max<uint64_t>(n, 1);
+            eof = eof || text_pos == text_n;
+            return 1;
+        }
+    };
     std::thread reader([&] {
         uint64_t next_read = 0, next_block = 0, batch_no = 0;
         int prev = -1;
         uint64_t carry = 0;  // reads at the tail of ring[prev] past its processed blocks
+        bool as_text = text != nullptr;
+        std::unique_ptr<Gang> gang(as_text ? new Gang(RT) : nullptr);
         for (;;) {
             int bi;
             {
@@ -171,10 +401,37 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
                 if (sh.error != NTC_OK) break;
             }
             Batch &b = ring[(size_t)bi];
+            b.is_text = false;
+            if (as_text) {
+                const auto tp = Clock::now();
+                bool eof = false;
+                const int r = fill_text(*gang, b, eof);
+                add_time(t_parse, secs(tp, Clock::now()));
+                if (r > 0) {
+                    if (batch_no == 0) S.first_batch_s = secs(t0, Clock::now());
+                    b.is_text = true;
+                    b.first_read = next_read;
+                    b.first_block = next_block;
+                    next_read += b.n_process;
+                    next_block += (b.n_process + BR - 1) / BR;
+                    text_batches++;
+                    {
+                        std::lock_guard<std::mutex> g(sh.mu);
+                        b.busy = true;
+                        gpu_q[(size_t)(batch_no % (uint64_t)n_ctx)].push_back(bi);
+                        batch_no++;
+                        sh.cv.notify_all();
+                    }
+                    if (eof) break;
+                    continue;
+                }
+                if (r == 0) break;
+                as_text = false;  // the host parser goes on from the record at text_pos
+                ntc::fastx_seek_mapped(fx, text_pos);
+            }
             if (!b.bases) {
                 const auto ta = Clock::now();
-                if (hipHostMalloc((void **)&b.bases, b.cap_bases, hipHostMallocDefault) != hipSuccess) {
-                    b.bases = nullptr;
+                if (!(b.bases = (uint8_t *)pinned_alloc(b.cap_bases))) {
                     sh.fail(NTC_ERR_HIP, "pinned host allocation failed");
                     break;
                 }
@@ -282,24 +539,37 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
                 uint8_t *payload = nullptr;
                 uint64_t plen = 0;
                 int64_t bad = -1;
+                uint64_t nb = 0;
                 const auto tg = Clock::now();
-                const int r = ntc_encode_pack_batch(ctxs[c], b.bases, b.offs, b.n_process, BR, metas.data(), &payload,
-                                                    &plen, &bad);
+                const int r = b.is_text ? ntc_encode_pack_fastq(ctxs[c], b.text, b.text_len, b.n_process, BR,
+                                                                metas.data(), &payload, &plen, &nb, &bad)
+                                        : ntc_encode_pack_batch(ctxs[c], b.bases, b.offs, b.n_process, BR,
+                                                                metas.data(), &payload, &plen, &bad);
                 add_time(t_gpu, secs(tg, Clock::now()));
                 if (r) {
                     ntc_buffer_free(payload);
-                    sh.fail(r, std::string("encode: ") + ntc_last_error(ctxs[c]),
-                            bad >= 0 ? (int64_t)b.first_read + bad : -1);
+                    if (b.is_text && r == NTC_ERR_FORMAT)  // as the host parser reports it
+                        sh.fail(r, "FASTX input: malformed or unreadable");
+                    else
+                        sh.fail(r, std::string("encode: ") + ntc_last_error(ctxs[c]),
+                                bad >= 0 ? (int64_t)b.first_read + bad : -1);
                     return;
                 }
-                auto pl = std::make_shared<std::vector<uint8_t>>(payload, payload + plen);
-                ntc_buffer_free(payload);
+                std::shared_ptr<uint8_t> pl(payload, ntc_buffer_free);
                 std::lock_guard<std::mutex> g(sh.mu);
                 S.gpu_done_s = secs(t0, Clock::now());
-                S.bases += b.offs[b.n_process] - b.offs[0];
+                S.bases += b.is_text ? nb : b.offs[b.n_process] - b.offs[0];
                 b.busy = false;
-                for (uint64_t k = 0; k < nblk; k++) {
-                    tasks.push_back(Task{pl, metas[k], b.first_block + k});
+                for (uint64_t k = 0; k < nblk; k++) {  // streams of the largest payload first
+                    const bool ok = metas[k].status == NTC_OK;
+                    BlockOut &bo = done[b.first_block + k];
+                    bo.status = metas[k].status;
+                    bo.left = ok ? 4 : 1;
+                    int order[4] = {0, 1, 2, 3};
+                    std::sort(order, order + 4, [&](int x, int y) {
+                        return metas[k].stream[x].encoded_size > metas[k].stream[y].encoded_size;
+                    });
+                    for (int q = 0; q < (ok ? 4 : 1); q++) tasks.push_back(Task{pl, metas[k], b.first_block + k, order[q]});
                     pending_tasks++;
                 }
                 sh.cv.notify_all();
@@ -320,24 +590,27 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
                     task = std::move(tasks.front());
                     tasks.pop_front();
                 }
-                BlockOut out;
+                uint8_t *data = nullptr;
+                uint64_t len = 0;
                 const auto td = Clock::now();
-                out.status = task.meta.status;
-                if (out.status == NTC_OK) {
-                    const int r = ntc_deflate_block(&task.meta, task.payload->data(), engine, &out.data, &out.len);
+                const int status = task.meta.status;
+                if (status == NTC_OK) {
+                    const int r = ntc_deflate_stream(&task.meta, task.stream, task.payload.get(), engine, &data, &len);
                     if (r) {
                         sh.fail(r, "deflate failed");
                         return;
                     }
-                } else if (out.status != NTC_ERR_EMPTY_READ) {
-                    sh.fail(out.status, "malformed block");
+                } else if (status != NTC_ERR_EMPTY_READ) {
+                    sh.fail(status, "malformed block");
                     return;
                 }
                 task.payload.reset();
                 add_time(t_deflate, secs(td, Clock::now()));
                 std::lock_guard<std::mutex> g(sh.mu);
-                done[task.block] = out;
-                sh.cv.notify_all();
+                BlockOut &bo = done[task.block];
+                bo.part[task.stream] = data;
+                bo.len[task.stream] = len;
+                if (--bo.left == 0) sh.cv.notify_all();
             }
         });
 
@@ -359,7 +632,10 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
         BlockOut out;
         {
             std::unique_lock<std::mutex> g(sh.mu);
-            sh.cv.wait(g, [&] { return sh.error != NTC_OK || done.count(blk) || (reader_done && blk >= total_blocks); });
+            sh.cv.wait(g, [&] {
+                return sh.error != NTC_OK || (done.count(blk) && done[blk].left == 0) ||
+                       (reader_done && blk >= total_blocks && !done.count(blk));
+            });
             if (sh.error != NTC_OK) break;
             if (!done.count(blk)) break;  // all blocks written
             out = done[blk];
@@ -370,13 +646,15 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
         }
         const auto tw = Clock::now();
         if (out.status == NTC_OK) {
-            if (!write_all(out.data, out.len)) sh.fail(NTC_ERR_IO, "write failed");
-            S.bytes_out += out.len;
+            for (int q = 0; q < 4; q++) {
+                if (!write_all(out.part[q], out.len[q])) sh.fail(NTC_ERR_IO, "write failed");
+                S.bytes_out += out.len[q];
+            }
             S.blocks++;
         } else {
             S.dropped_blocks++;
         }
-        ntc_buffer_free(out.data);
+        for (int q = 0; q < 4; q++) ntc_buffer_free(out.part[q]);
         add_time(t_write, secs(tw, Clock::now()));
     }
     {
@@ -389,10 +667,12 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
     reader.join();
     for (auto &t : gpus) t.join();
     for (auto &t : pool) t.join();
-    for (auto &kv : done) ntc_buffer_free(kv.second.data);
+    for (auto &kv : done)
+        for (int q = 0; q < 4; q++) ntc_buffer_free(kv.second.part[q]);
     for (auto &b : ring) {
-        if (b.bases) (void)hipHostFree(b.bases);
-        (void)hipHostFree(b.offs);
+        pinned_free(b.bases);
+        pinned_free(b.offs);
+        pinned_free(b.text);
     }
     ntc_fastx_close(fx);
     const int result = sh.error == -1 ? NTC_OK : sh.error;
@@ -403,6 +683,7 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
     S.write_s = t_write.load();
     S.wall_s = secs(t0, Clock::now());
     S.threads = T;
+    S.gpu_parsed = (int32_t)text_batches.load();
     S.bad_read = sh.bad_read;
     std::snprintf(S.error, sizeof(S.error), "%s", result == NTC_OK ? "" : sh.msg.c_str());
     if (stats) *stats = S;
@@ -564,11 +845,11 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
                 }
             }
         } acc{t_pin, tp};
-        if (*p) (void)hipHostFree(*p);
+        pinned_free(*p);
         *p = nullptr;
         *cap = 0;
         const uint64_t want = need + need / 8 + 4096;
-        if (hipHostMalloc(p, want, hipHostMallocDefault) != hipSuccess) return false;
+        if (!(*p = pinned_alloc(want))) return false;
         *cap = want;
         return true;
     };
@@ -781,8 +1062,8 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
     for (auto &t : pool) t.join();
     for (auto &t : gpus) t.join();
     for (auto &sl : slots) {
-        if (sl.recs) (void)hipHostFree(sl.recs);
-        if (sl.text) (void)hipHostFree(sl.text);
+        pinned_free(sl.recs);
+        pinned_free(sl.text);
     }
     if (data) munmap((void *)data, fsize);
     if (seekable) (void)lseek(out_fd, out_pos, SEEK_SET);

@@ -30,10 +30,12 @@ def main():
     ap.add_argument("--reps", type=int, default=3, help="runs per timing (the best counts)")
     ap.add_argument("--cli", default="native", choices=["native", "python"],
                     help="native: the ntcomp binary (ntcomp_main.cpp); python: python -m ntcomp_amd")
+    ap.add_argument("--host-parse", action="store_true", help="CLI --host-parse (FASTQ parsed on the host pool)")
     a = ap.parse_args()
     a.gpus_arg = ["--devices", a.devices] if a.devices else ["--gpus", str(a.gpus)]
     if a.contexts_per_gpu:
         a.gpus_arg += ["--contexts-per-gpu", str(a.contexts_per_gpu)]
+    a.enc_arg = ["--host-parse"] if a.host_parse else []
     import numpy as np
     import ntcomp_amd as nt
     os.makedirs(a.dir, exist_ok=True)
@@ -88,7 +90,7 @@ def main():
     def run_encode(src, dst):
         t0 = time.time()
         with open(dst, "wb") as f:
-            r = subprocess.run(cmd + ["encode", "-i", prefix, src, "--stats", "--deflate", a.deflate] + a.gpus_arg,
+            r = subprocess.run(cmd + ["encode", "-i", prefix, src, "--stats", "--deflate", a.deflate] + a.gpus_arg + a.enc_arg,
                                stdout=f, stderr=subprocess.PIPE, check=True, cwd=REPO)
         return time.time() - t0, stats_line(r.stderr)
 

@@ -1,16 +1,15 @@
 #!/bin/bash
-# End-to-end encode on one box: the CLI (scripts/e2e_bench.py, plain FASTQ, libdeflate) and
-# the native pipeline alone over calls per batch x contexts per GPU (scripts/pipe_bench.py).
+# End-to-end encode on one box: the native CLI (scripts/e2e_bench.py, plain FASTQ, libdeflate)
+# with the FASTQ parsed on the GPU (default) and on the host pool, two contexts on one GPU,
+# and the native pipeline alone over calls per batch x contexts x parse (scripts/pipe_bench.py).
 set -e
 mkdir -p gpurun_out/e2e
 timeout -k 10 400 python -u scripts/e2e_bench.py --reads 10000000 --deflate libdeflate ${E2E_ARGS:-} \
     > gpurun_out/e2e/plain_ld.json 2> gpurun_out/e2e/plain_ld.err
+timeout -k 10 300 python -u scripts/e2e_bench.py --reads 10000000 --deflate libdeflate --keep --host-parse \
+    > gpurun_out/e2e/plain_ld_hostparse.json 2> gpurun_out/e2e/plain_ld_hostparse.err
 timeout -k 10 300 python -u scripts/e2e_bench.py --reads 10000000 --deflate libdeflate --keep --contexts-per-gpu 2 \
     > gpurun_out/e2e/plain_ld_2ctx.json 2> gpurun_out/e2e/plain_ld_2ctx.err
-timeout -k 10 300 python -u scripts/e2e_bench.py --reads 10000000 --deflate libdeflate --keep --cli python \
-    > gpurun_out/e2e/plain_ld_python.json 2> gpurun_out/e2e/plain_ld_python.err
 timeout -k 10 300 python -u scripts/pipe_bench.py --dir /tmp/ntc_e2e --deflate libdeflate --bpb 4 8 16 \
-    --contexts 1 2 --reps 2 > gpurun_out/e2e/pipe_sweep.jsonl 2> gpurun_out/e2e/pipe_sweep.err
-timeout -k 10 300 python -u scripts/pipe_bench.py --dir /tmp/ntc_e2e --mode decode --bpb 2 4 \
-    --contexts 1 2 --reps 2 > gpurun_out/e2e/pipe_sweep_dec.jsonl 2> gpurun_out/e2e/pipe_sweep_dec.err
+    --contexts 1 2 --parse gpu host --reps 2 > gpurun_out/e2e/pipe_sweep.jsonl 2> gpurun_out/e2e/pipe_sweep.err
 rm -rf /tmp/ntc_e2e

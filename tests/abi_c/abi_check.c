@@ -48,10 +48,11 @@ _Static_assert(offsetof(ntc_block_meta, stream) == 0 && offsetof(ntc_block_meta,
 /* #[repr(C)] NtcPipelineOpts: i32, i32, u64, i32, i32; NtcPipelineStats: 5 x u64, 9 x f64, i32,
  * i32, i64, [c_char; 256] */
 _Static_assert(offsetof(ntc_pipeline_opts, batch_bases) == 8 && offsetof(ntc_pipeline_opts, deflate_engine) == 16 &&
-                   sizeof(ntc_pipeline_opts) == 24,
+                   offsetof(ntc_pipeline_opts, host_parse) == 20 && sizeof(ntc_pipeline_opts) == 24,
                "ntc_pipeline_opts");
 _Static_assert(offsetof(ntc_pipeline_stats, parse_s) == 40 && offsetof(ntc_pipeline_stats, wall_s) == 72 &&
                    offsetof(ntc_pipeline_stats, alloc_s) == 80 && offsetof(ntc_pipeline_stats, threads) == 112 &&
+                   offsetof(ntc_pipeline_stats, gpu_parsed) == 116 &&
                    offsetof(ntc_pipeline_stats, bad_read) == 120 && offsetof(ntc_pipeline_stats, error) == 128 &&
                    sizeof(ntc_pipeline_stats) == 384,
                "ntc_pipeline_stats");

@@ -1,6 +1,7 @@
 // Test stub (tests/san only): the GPU stage of the native pipelines on the CPU, so that
 // ntc_encode_file / ntc_decode_file (pipeline.cpp) run their host threads under the
-// sanitizers.  ntc_encode_pack_batch = the C oracle's encode (oracle/ntcomp_oracle.c, the
+// sanitizers.  ntc_encode_pack_fastq = a host restatement of fastq.hip's 4-line parse, then
+// ntc_encode_pack_batch; ntc_encode_pack_batch = the C oracle's encode (oracle/ntcomp_oracle.c, the
 // test checker) + the host packer (ntc_pack_block); ntc_decode_fasta = the oracle's decode
 // + ">seq.N" lines.  Nothing here ships: the product path is capi.cpp + the HIP kernels.
 #include <cstdio>
@@ -101,6 +102,54 @@ int ntc_decode_fasta(ntc_ctx *ctx, const uint64_t *recs, uint64_t n_recs, uint64
     }
     std::memcpy(out, text.data(), text.size());
     return NTC_OK;
+}
+
+// fastq.hip restated: exactly n_reads 4-line records, the last line possibly without its
+// newline; '@' / '+' / equal lengths after one '\r' stripped; sequence lines normalised
+int ntc_encode_pack_fastq(ntc_ctx *ctx, const uint8_t *fastq, uint64_t bytes, uint64_t n_reads, uint32_t block_reads,
+                          ntc_block_meta *meta, uint8_t **payload, uint64_t *payload_bytes, uint64_t *n_bases,
+                          int64_t *bad_read) {
+    *payload = nullptr;
+    *payload_bytes = 0;
+    if (bad_read) *bad_read = -1;
+    std::vector<uint64_t> nl;
+    for (uint64_t i = 0; i < bytes; i++)
+        if (fastq[i] == '\n') nl.push_back(i);
+    const uint64_t nn = nl.size();
+    if (nn + 1 < 4 * n_reads || nn > 4 * n_reads || (nn == 4 * n_reads && n_reads && fastq[bytes - 1] != '\n') ||
+        (!n_reads && bytes)) {
+        if (bad_read) *bad_read = (int64_t)(n_reads ? std::min(nn / 4, n_reads - 1) : 0);
+        return NTC_ERR_FORMAT;
+    }
+    static const char *keep = "ACGTN-BDHVRYSWKM";
+    auto norm = [](uint8_t c) -> uint8_t {
+        if (std::strchr(keep, c) && c) return c;
+        if (c >= 'a' && c <= 'z' && std::strchr(keep, c - 'a' + 'A') && c != 'u') return (uint8_t)(c - 'a' + 'A');
+        if (c == 'u' || c == 'U') return 'T';
+        if (c == '.' || c == '~') return '-';
+        if (c == ' ' || c == '\t' || c == '\r' || c == '\n') return 0;
+        return 'N';
+    };
+    std::vector<uint8_t> bases;
+    std::vector<uint64_t> offs(n_reads + 1, 0);
+    for (uint64_t r = 0; r < n_reads; r++) {
+        const uint64_t L = 4 * r, h0 = r ? nl[L - 1] + 1 : 0, s0 = nl[L] + 1, s1 = nl[L + 1], q0 = nl[L + 2] + 1,
+                       q1 = L + 3 < nn ? nl[L + 3] : bytes;
+        const uint64_t ls = s1 - s0 - (s1 > s0 && fastq[s1 - 1] == '\r');
+        const uint64_t lq = q1 - q0 - (q1 > q0 && fastq[q1 - 1] == '\r');
+        if (fastq[h0] != '@' || fastq[s1 + 1] != '+' || ls != lq) {
+            if (bad_read) *bad_read = (int64_t)r;
+            return NTC_ERR_FORMAT;
+        }
+        for (uint64_t i = s0; i < s1; i++)
+            if (const uint8_t v = norm(fastq[i])) bases.push_back(v);
+        offs[r + 1] = bases.size();
+    }
+    if (n_bases) *n_bases = bases.size();
+    if (!n_reads) return NTC_OK;
+    bases.push_back(0);
+    return ntc_encode_pack_batch(ctx, bases.data(), offs.data(), n_reads, block_reads, meta, payload, payload_bytes,
+                                 bad_read);
 }
 
 }  // extern "C"

@@ -156,7 +156,7 @@ static int cmd_build(char **a) {
     return 0;
 }
 
-// encode|decode PREFIX IN OUT THREADS BPB NCTX [DEFLATE]
+// encode|decode PREFIX IN OUT THREADS BPB NCTX [DEFLATE [HOST_PARSE]]
 static int cmd_pipe(bool enc, char **a, int n) {
     ntc::HostIndex ix;
     std::string err;
@@ -175,15 +175,16 @@ static int cmd_pipe(bool enc, char **a, int n) {
     opts.blocks_per_batch = std::atoi(a[4]);
     opts.batch_bases = enc ? (1u << 20) : 0;  // small ring buffers: many batches, buffer growth
     opts.deflate_engine = n >= 7 ? std::atoi(a[6]) : NTC_DEFLATE_ZLIB;
+    opts.host_parse = n >= 8 ? std::atoi(a[7]) : 0;
     ntc_pipeline_stats st{};
     const int rc = enc ? ntc_encode_file(ctxs.data(), nctx, a[1], fd, &opts, &st)
                        : ntc_decode_file(ctxs.data(), nctx, a[1], fd, &opts, &st);
     ::close(fd);
     for (auto *c : ctxs) stub_ctx_free(c);
     orc_index_free(o);
-    std::printf("rc=%d reads=%llu bases=%llu blocks=%llu dropped=%llu bad=%lld\n", rc, (unsigned long long)st.reads,
-                (unsigned long long)st.bases, (unsigned long long)st.blocks, (unsigned long long)st.dropped_blocks,
-                (long long)st.bad_read);
+    std::printf("rc=%d reads=%llu bases=%llu blocks=%llu dropped=%llu bad=%lld text=%d\n", rc,
+                (unsigned long long)st.reads, (unsigned long long)st.bases, (unsigned long long)st.blocks,
+                (unsigned long long)st.dropped_blocks, (long long)st.bad_read, st.gpu_parsed);
     return 0;
 }
 

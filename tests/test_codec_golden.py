@@ -152,3 +152,21 @@ def test_short_record_past_32_bases_is_malformed():
     with pytest.raises(nt.NtcError) as e:
         nt.pack_block(recs, 1)
     assert e.value.code == 8
+
+
+@pytest.mark.parametrize("engine", ["zlib", "libdeflate"])
+@pytest.mark.parametrize("name", sorted(n for n in CASES if not CASES[n]["dropped"]))
+def test_deflate_streams_concatenate_to_the_block(name, engine):
+    """ntc_deflate_stream (the pipeline deflates a block's four streams in parallel): the four
+    parts back to back are ntc_deflate_block's bytes; a dropped block's status comes back."""
+    c = CASES[name]
+    meta, payload = nt.pack_block(recs_of(c), c["num_records"])
+    try:
+        whole = nt.deflate_block(meta, payload, engine)
+    except nt.NtcError as e:
+        if e.code == 10:
+            pytest.skip("libdeflate.so.0 not on this host")
+        raise
+    assert b"".join(nt.deflate_stream(meta, s, payload, engine) for s in range(4)) == whole
+    with pytest.raises(nt.NtcError):
+        nt.deflate_stream(meta, 4, payload, engine)

@@ -239,3 +239,45 @@ def test_pipelines_under_sanitizers(san, encoded, tmp_path, kind):
     (tmp_path / "n.fq").write_bytes(b"\n".join(lines))
     got = run(san[kind], "encode", d / "idx", tmp_path / "n.fq", tmp_path / "n.dat", 4, 1, 2, 0)
     assert int(got["rc"]) == 2 and int(got["bad"]) == 70001, got
+
+
+def test_pipeline_text_reader_edge_cases_under_sanitizers(san, encoded, tmp_path):
+    """The encode reader's GPU-parse path (pipeline.cpp fill_text: copy + newline scan, cuts
+    after the last whole block, hand-over to the host parser) against the host parser
+    (host_parse = 1) on FASTQ shapes the host parser accepts or rejects: CRLF, lower case,
+    no final newline, blank lines mid-file / at either end, a truncated last record.  Same
+    rc, counts and encoded.dat bytes either way (the stub's GPU parse restates fastq.hip)."""
+    d, ix, _, _ = encoded
+    genome = nt.synth_genome(8, 40_000)
+    n, L = 65536 + 300, 40
+    body = nt.synth_reads(genome, 5, 0, n, L, 20_000).reshape(n, L)
+    recs = [b"@r%d\n" % i + body[i].tobytes() + b"\n+\n" + b"I" * L + b"\n" for i in range(n)]
+    plain = b"".join(recs)
+    lower = b"".join(r.replace(body[i].tobytes(), body[i].tobytes().lower()) if i % 7 == 0 else r
+                     for i, r in enumerate(recs))
+    mid_blank = b"".join(recs[:65600]) + b"\n\r\n" + b"".join(recs[65600:])
+    cases = {
+        "plain": (plain, True),
+        "crlf": (plain.replace(b"\n", b"\r\n"), True),
+        "lower": (lower, True),
+        "no_final_newline": (plain[:-1], True),
+        "mid_blank": (mid_blank, True),
+        "trailing_blank": (plain + b"\n\n\n", True),
+        "leading_blank": (b"\n" + plain, False),
+        "truncated": (plain[:plain.rindex(b"\n+\n")], True),
+    }
+    for name, (blob, text_first) in cases.items():
+        (tmp_path / f"{name}.fq").write_bytes(blob)
+        got = {}
+        for hp in (0, 1):
+            got[hp] = run(san["asan"], "encode", d / "idx", tmp_path / f"{name}.fq", tmp_path / f"{name}{hp}.dat",
+                          4, 1, 2, 0, hp)
+        assert int(got[1]["text"]) == 0
+        assert (int(got[0]["text"]) > 0) == text_first, (name, got[0])
+        for k in ("rc", "reads", "bases", "blocks", "bad"):
+            assert got[0][k] == got[1][k], (name, k, got)
+        if int(got[0]["rc"]) == 0:
+            assert int(got[0]["reads"]) == n, name
+            assert (tmp_path / f"{name}0.dat").read_bytes() == (tmp_path / f"{name}1.dat").read_bytes(), name
+        else:
+            assert name == "truncated" and int(got[0]["rc"]) == 8, (name, got)
