@@ -120,6 +120,14 @@ int ntc_ctx_get_option(const ntc_ctx *ctx, const char *key, int64_t *value);
  * bitvector, the path cover, the suffix table (+ presence bitmaps) and the inverse-walk
  * jump table in HBM (DESIGN.md "Data layout in HBM").  About 3 GB at n = 10 M, k = 91. */
 int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *ix);
+/* ntc_index_upload in two halves, so a caller can derive the host tables (no GPU) while
+ * contexts are being created: ntc_index_prepare copies the view and builds them;
+ * ntc_index_upload_prepared puts them on ctx's device (any number of contexts / devices;
+ * same device index as ntc_index_upload).  Free with ntc_index_prep_free.              */
+typedef struct ntc_index_prep ntc_index_prep;
+int ntc_index_prepare(const ntc_index_view *ix, ntc_index_prep **out);
+int ntc_index_upload_prepared(ntc_ctx *ctx, const ntc_index_prep *prep);
+void ntc_index_prep_free(ntc_index_prep *prep);
 /* dst uses src's device index (both contexts on one GPU): no second upload, no second copy
  * in HBM; the index is freed with the last context holding it.  Each context keeps its own
  * stream and workspace, so two contexts on one GPU overlap one call's copies and host work

@@ -45,7 +45,7 @@ EXPORTED = [
     "ntc_fastx_open", "ntc_fastx_next_batch", "ntc_fastx_close", "ntc_fasta_format", "ntc_fastx_next_batch_into",
     "ntc_fastx_set_threads", "ntc_host_threads", "ntc_encode_file", "ntc_decode_fasta",
     "ntc_decode_file", "ntc_build_index_device", "ntc_build_index_device_ex", "ntc_index_set_prefix_precalc",
-    "ntc_index_prefix_table", "ntc_index_share",
+    "ntc_index_prefix_table", "ntc_index_share", "ntc_index_prepare", "ntc_index_upload_prepared", "ntc_index_prep_free",
 ]
 
 
@@ -165,6 +165,9 @@ def lib():
         "ntc_ctx_get_option": (I, [P, ctypes.c_char_p, ctypes.POINTER(i64)]),
         "ntc_index_upload": (I, [P, ctypes.POINTER(IndexView)]),
         "ntc_index_share": (I, [P, P]),
+        "ntc_index_prepare": (I, [ctypes.POINTER(IndexView), ctypes.POINTER(P)]),
+        "ntc_index_upload_prepared": (I, [P, P]),
+        "ntc_index_prep_free": (None, [P]),
         "ntc_index_info": (I, [P, P, P, P]),
         "ntc_encode_batch": (I, [P, P, P, u64, P, u64, P, P]),
         "ntc_encode_batch_device": (I, [P, P, P, u64, u32, P, u64, P]),

@@ -19,7 +19,9 @@ import sys
 
 
 BLOCK_READS = 65536  # main.rs:152
-CONTEXTS_PER_GPU = 1  # encode / decode contexts per device (--contexts-per-gpu)
+# contexts per device (--contexts-per-gpu): encode 2 (one call's H2D of FASTQ text overlaps
+# the other's kernels), decode 1 -- as the native CLI (ntcomp_main.cpp)
+ENCODE_CONTEXTS_PER_GPU, DECODE_CONTEXTS_PER_GPU = 2, 1
 
 
 def log(*a):
@@ -251,7 +253,7 @@ def main(argv=None):
                                      "overrides --gpus")
     e.add_argument("--threads", type=int, default=0,
                    help="host pool for FASTQ parse and deflate (0: CPUs available to the process)")
-    e.add_argument("--contexts-per-gpu", type=int, default=CONTEXTS_PER_GPU,
+    e.add_argument("--contexts-per-gpu", type=int, default=ENCODE_CONTEXTS_PER_GPU,
                    help="contexts per device sharing one index copy; calls alternate over them")
     e.add_argument("--blocks-per-batch", type=int, default=4, help="65,536-read blocks per GPU call")
     e.add_argument("--deflate", choices=["auto", "zlib", "libdeflate"], default="auto",
@@ -268,7 +270,7 @@ def main(argv=None):
     d.add_argument("--gpus", type=int, default=1, help="GPUs to decode on (batches dealt round-robin).")
     d.add_argument("--devices", help="comma-separated device list, one context each; overrides --gpus")
     d.add_argument("--threads", type=int, default=0, help="block unzip / format threads (0: CPUs available)")
-    d.add_argument("--contexts-per-gpu", type=int, default=CONTEXTS_PER_GPU,
+    d.add_argument("--contexts-per-gpu", type=int, default=DECODE_CONTEXTS_PER_GPU,
                    help="contexts per device sharing one index copy; calls alternate over them")
     d.add_argument("--blocks-per-batch", type=int, default=2, help="blocks per GPU call")
     d.add_argument("--stats", action="store_true", help="print per-stage seconds to stderr")

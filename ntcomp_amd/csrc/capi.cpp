@@ -412,16 +412,21 @@ int read_status(ntc_ctx *ctx, int64_t *bad_index) {
 // host (glibc f64 math, codec_params.h), pass 2 on the device.  Synchronous.
 int pack_blocks_impl(ntc_ctx *ctx, const uint64_t *d_recs, const uint64_t *d_roffs, uint64_t n_reads,
                      uint32_t block_reads, uint8_t *d_payload, uint64_t payload_capacity, ntc_block_meta *meta,
-                     uint64_t *payload_bytes) {
+                     uint64_t *payload_bytes, const uint64_t *known_ends = nullptr) {
     *payload_bytes = 0;
     const uint64_t n_blocks = (n_reads + block_reads - 1) / block_reads;
     if (n_blocks == 0) return NTC_OK;
     for (int i = 0; i < 3; i++)
         if (!ctx->pack_ev[i]) HIP_TRY(ctx, hipEventCreate(&ctx->pack_ev[i]));
-    uint64_t ends[2] = {0, 0};
-    HIP_TRY(ctx, hipMemcpyAsync(&ends[0], d_roffs, 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(&ends[1], d_roffs + n_reads, 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    uint64_t ends[2] = {0, 0};  // the record offsets' first and last values
+    if (known_ends) {
+        ends[0] = known_ends[0];
+        ends[1] = known_ends[1];
+    } else {
+        HIP_TRY(ctx, hipMemcpyAsync(&ends[0], d_roffs, 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(&ends[1], d_roffs + n_reads, 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    }
     if (ends[1] < ends[0]) return set_err(ctx, NTC_ERR_INVALID_ARG, "record offsets decrease");
     void *d_chunks, *d_meta;
     int rc;
@@ -608,29 +613,87 @@ int ntc_index_share(ntc_ctx *dst, const ntc_ctx *src) {
     return NTC_OK;
 }
 
-int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
-    if (!ctx || !v || !v->lcs) return set_err(ctx, NTC_ERR_INVALID_ARG, "null index view");
+}  // extern "C"
+
+// the host half of an upload: the index copied out of the view and its derived tables
+// (derived.cpp build_derived), no GPU involved
+struct ntc_index_prep {
+    HostIndex hx;
+    Derived dv;
+    int64_t host_us = 0;
+};
+
+namespace {
+int prepare_index(const ntc_index_view *v, ntc_index_prep &p, std::string &err) {
+    const auto t0 = std::chrono::steady_clock::now();
+    p.hx.n = v->n_nodes;
+    p.hx.k = v->k;
+    const uint64_t nw = (v->n_nodes + 63) / 64;
+    for (int c = 0; c < 4; c++) {
+        p.hx.rows[c].assign(v->rows[c], v->rows[c] + nw);
+        p.hx.C[c] = v->C[c];
+    }
+    p.hx.lcs.assign(v->lcs, v->lcs + v->n_nodes);
+    if (!build_derived(p.hx, p.dv, err, false)) return NTC_ERR_FORMAT;
+    p.host_us = (int64_t)std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0)
+                    .count();
+    return NTC_OK;
+}
+bool view_ok(const ntc_index_view *v) {
+    if (!v || !v->lcs) return false;
     for (int c = 0; c < 4; c++)
-        if (!v->rows[c]) return set_err(ctx, NTC_ERR_INVALID_ARG, "null subset-matrix row");
+        if (!v->rows[c]) return false;
+    return true;
+}
+int upload_prepared(ntc_ctx *ctx, const ntc_index_prep &prep);
+}  // namespace
+
+extern "C" {
+
+int ntc_index_prepare(const ntc_index_view *v, ntc_index_prep **out) {
+    if (!out || !view_ok(v)) return NTC_ERR_INVALID_ARG;
+    *out = nullptr;
+    auto *p = new (std::nothrow) ntc_index_prep();
+    if (!p) return NTC_ERR_CAPACITY;
+    std::string err;
+    const int rc = prepare_index(v, *p, err);
+    if (rc) {
+        delete p;
+        return rc;
+    }
+    *out = p;
+    return NTC_OK;
+}
+
+void ntc_index_prep_free(ntc_index_prep *p) { delete p; }
+
+int ntc_index_upload_prepared(ntc_ctx *ctx, const ntc_index_prep *p) {
+    if (!ctx || !p) return set_err(ctx, NTC_ERR_INVALID_ARG, "null context or prepared index");
+    return upload_prepared(ctx, *p);
+}
+
+int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
+    if (!ctx || !view_ok(v)) return set_err(ctx, NTC_ERR_INVALID_ARG, "null index view");
+    ntc_index_prep p;
+    std::string err;
+    const int rc = prepare_index(v, p, err);
+    if (rc) return set_err(ctx, rc, err);
+    return upload_prepared(ctx, p);
+}
+
+}  // extern "C"
+
+namespace {
+int upload_prepared(ntc_ctx *ctx, const ntc_index_prep &prep) {
+    const HostIndex &hx = prep.hx;
+    const Derived &dv = prep.dv;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     const auto t_start = std::chrono::steady_clock::now();
     auto us_since = [&] {
-        return (int64_t)std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() -
-                                                                              t_start).count();
+        return prep.host_us + (int64_t)std::chrono::duration_cast<std::chrono::microseconds>(
+                                  std::chrono::steady_clock::now() - t_start).count();
     };
-    HostIndex hx;
-    hx.n = v->n_nodes;
-    hx.k = v->k;
-    const uint64_t nw = (v->n_nodes + 63) / 64;
-    for (int c = 0; c < 4; c++) {
-        hx.rows[c].assign(v->rows[c], v->rows[c] + nw);
-        hx.C[c] = v->C[c];
-    }
-    hx.lcs.assign(v->lcs, v->lcs + v->n_nodes);
-    Derived dv;
-    std::string err;
-    if (!build_derived(hx, dv, err, false)) return set_err(ctx, NTC_ERR_FORMAT, err);
-    ctx->upload_host_us = us_since();
+    ctx->upload_host_us = prep.host_us;
     // free a previous index
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     ctx->index_mem = std::make_shared<IndexMem>(ctx->device);  // the previous one goes with its last holder
@@ -851,6 +914,9 @@ int ntc_index_upload(ntc_ctx *ctx, const ntc_index_view *v) {
     ctx->upload_total_us = us_since();
     return NTC_OK;
 }
+}  // namespace
+
+extern "C" {
 
 int ntc_ctx_set_option(ntc_ctx *ctx, const char *key, int64_t value) {
     if (!ctx || !key) return NTC_ERR_INVALID_ARG;
@@ -1291,13 +1357,15 @@ int encode_pack_staged(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_o
     // the payload never exceeds the records' 8 B each plus per-stream rounding, except for
     // malformed unary runs: size the device buffer for that and let the packer check
     const uint64_t n_blocks = (n_reads + block_reads - 1) / block_reads;
-    uint64_t nrec = 0;
-    HIP_TRY(ctx, hipMemcpy(&nrec, d_roffs + n_reads, 8, hipMemcpyDeviceToHost));
+    uint64_t nrec = 0;  // the status box of the encode call holds it (k_emit4 wrote offsets from 0)
+    if (ctx->box_valid) nrec = ((volatile uint64_t *)ctx->h_box)[1];
+    else HIP_TRY(ctx, hipMemcpy(&nrec, d_roffs + n_reads, 8, hipMemcpyDeviceToHost));
+    const uint64_t ends[2] = {0, nrec};
     uint64_t cap = nrec * 10 + n_blocks * 64 + 64, used = 0;
     for (int attempt = 0;; attempt++) {
         if ((rc = ensure(ctx, WS_PACK_PAYLOAD, cap, &d_payload))) return rc;
         rc = pack_blocks_impl(ctx, (const uint64_t *)d_recs, d_roffs, n_reads, block_reads, (uint8_t *)d_payload,
-                              ctx->ws[WS_PACK_PAYLOAD].bytes, meta, &used);
+                              ctx->ws[WS_PACK_PAYLOAD].bytes, meta, &used, ends);
         if (rc != NTC_ERR_CAPACITY || attempt) break;
         cap = used;  // exact requirement from the first pass
     }

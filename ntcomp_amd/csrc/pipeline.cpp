@@ -308,8 +308,11 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
     uint64_t text_pos = 0;
     double rec_bytes = 0;  // text bytes per record so far
     std::atomic<uint64_t> text_batches{0};
-    const char *rt_env = std::getenv("NTC_READ_THREADS");  // A/B hook for the reader's gang
-    const int RT = std::max(1, rt_env ? std::atoi(rt_env) : T);
+    // the reader's gang: 8 threads copy + scan at ~45 GB/s on the box, as fast as 16 for the
+    // pipeline and at less CPU beside the deflate pool (scripts/rt_sweep.sh); NTC_READ_THREADS
+    // is the A/B hook
+    const char *rt_env = std::getenv("NTC_READ_THREADS");
+    const int RT = std::max(1, rt_env ? std::atoi(rt_env) : std::min(T, 8));
     if (text) {  // bytes per record from the first MiB
         const size_t m = (size_t)std::min<uint64_t>(text_n, 1u << 20);
         uint64_t nl = 0;

@@ -10,6 +10,7 @@ for rt in ${RT_LIST:-8 16}; do
     --bpb ${BPB_LIST:-4 8} --contexts 1 2 --parse gpu --reps 3 | sed "s/^{/{\"read_threads\": $rt, /" \
     >> gpurun_out/e2e/rt_sweep.jsonl
 done
+timeout -k 10 60 python -u scripts/init_cost.py /tmp/ntc_e2e/idx > gpurun_out/e2e/init_cost.json && timeout -k 10 60 python -u scripts/init_cost.py /tmp/ntc_e2e/idx >> gpurun_out/e2e/init_cost.json
 timeout -k 10 200 python -u scripts/pipe_bench.py --dir /tmp/ntc_e2e --mode decode --bpb 2 4 --contexts 1 2 --reps 3 \
     > gpurun_out/e2e/dec_sweep.jsonl
 rm -rf /tmp/ntc_e2e
