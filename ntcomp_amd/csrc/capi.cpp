@@ -530,6 +530,15 @@ int ntc_ctx_create(int device, ntc_ctx **out) {
     if (device < 0 || device >= ndev) return NTC_ERR_INVALID_ARG;
     ntc_ctx *ctx = new ntc_ctx();
     ctx->device = device;
+    // how a host thread waits for the device (A/B hook; HIP's default is auto): "spin",
+    // "yield" or "blocking".  Takes effect only before the device's first use in the process.
+    if (const char *v = std::getenv("NTC_DEVICE_SCHEDULE")) {
+        const unsigned f = std::strcmp(v, "spin") == 0       ? hipDeviceScheduleSpin
+                           : std::strcmp(v, "yield") == 0    ? hipDeviceScheduleYield
+                           : std::strcmp(v, "blocking") == 0 ? hipDeviceScheduleBlockingSync
+                                                             : hipDeviceScheduleAuto;
+        if (hipSetDevice(device) == hipSuccess && hipSetDeviceFlags(f) != hipSuccess) (void)hipGetLastError();
+    }
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc((void **)&ctx->d_status, 64) != hipSuccess ||
