@@ -59,6 +59,13 @@ typedef struct ntc_block_meta {
 #define NTC_DEFLATE_ZLIB 0       /* system zlib, level 6                                  */
 #define NTC_DEFLATE_LIBDEFLATE 1 /* libdeflate.so.0, level 6 (~3x faster; other deflate
                                     bytes, same inflated content)                       */
+#define NTC_DEFLATE_ADAPTIVE 2   /* libdeflate level 6 where it compresses: a stream whose
+                                    first 32 KiB carry >= 7.9 bits of order-0 entropy per
+                                    byte (s1's colex ids and s4's bases are such: level 6
+                                    shrinks them by < 0.1 %) goes out as stored deflate
+                                    blocks, as zlib's own stored-block fallback would write
+                                    it; half the CPU of NTC_DEFLATE_LIBDEFLATE, same streams
+                                    after inflate, within 0.1 % of its size              */
 
 void ntc_file_header(uint8_t out[32]);
 /* NTC_ERR_EMPTY_READ when the block has no long or no short records (see above). */
@@ -69,7 +76,7 @@ int ntc_write_block(const uint64_t *recs, uint64_t n_recs, uint64_t num_records,
 int ntc_pack_block(const uint64_t *recs, uint64_t n_recs, uint64_t num_records, ntc_block_meta *meta,
                    uint8_t **payload, uint64_t *payload_len);
 /* Header + gzip member per stream, the bytes write_block_to writes.  payload is the base
- * the meta offsets are relative to.  engine: NTC_DEFLATE_ZLIB or NTC_DEFLATE_LIBDEFLATE
+ * the meta offsets are relative to.  engine: NTC_DEFLATE_ZLIB, _LIBDEFLATE or _ADAPTIVE
  * (NTC_ERR_UNSUPPORTED if libdeflate.so.0 is missing).  Returns meta->status when the
  * block is dropped (nothing written).                                                  */
 int ntc_deflate_block(const ntc_block_meta *meta, const uint8_t *payload, int engine, uint8_t **out,

@@ -32,7 +32,7 @@ typedef struct ntc_pipeline_opts {
     int32_t threads;          /* host pool (parse, deflate); <= 0: ntc_host_threads()        */
     int32_t blocks_per_batch; /* 65,536-read blocks per GPU call; <= 0: 4 (encode), 2 (decode) */
     uint64_t batch_bases;     /* encode: bases per pinned batch buffer; 0: 64 Mi (grows for long reads) */
-    int32_t deflate_engine;   /* NTC_DEFLATE_ZLIB (0) or NTC_DEFLATE_LIBDEFLATE (1)           */
+    int32_t deflate_engine;   /* NTC_DEFLATE_ZLIB (0), _LIBDEFLATE (1) or _ADAPTIVE (2)        */
     int32_t host_parse;       /* encode, plain FASTQ: 0 = the text goes to the GPU, which parses
                                  it (ntc_encode_pack_fastq); 1 = parsed by the host pool      */
 } ntc_pipeline_opts;

@@ -71,7 +71,7 @@ class BlockMeta(ctypes.Structure):
                 ("status", ctypes.c_int32), ("reserved", ctypes.c_uint32)]
 
 
-DEFLATE_ENGINES = {"zlib": 0, "libdeflate": 1}
+DEFLATE_ENGINES = {"zlib": 0, "libdeflate": 1, "adaptive": 2}  # NTC_DEFLATE_* (include/ntcomp_codec.h)
 
 
 class PipelineOpts(ctypes.Structure):

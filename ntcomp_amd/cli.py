@@ -165,7 +165,7 @@ def cmd_encode(args):
     ctxs = _open_gpus(index, _devices(args), st, args.contexts_per_gpu)
     log("Encoding fastX data...")
     if args.deflate == "auto":
-        args.deflate = "libdeflate" if nt.libdeflate_available() else "zlib"
+        args.deflate = "adaptive" if nt.libdeflate_available() else "zlib"
     out = sys.stdout.buffer
     out.flush()
     try:
@@ -256,11 +256,11 @@ def main(argv=None):
     e.add_argument("--contexts-per-gpu", type=int, default=ENCODE_CONTEXTS_PER_GPU,
                    help="contexts per device sharing one index copy; calls alternate over them")
     e.add_argument("--blocks-per-batch", type=int, default=4, help="65,536-read blocks per GPU call")
-    e.add_argument("--deflate", choices=["auto", "zlib", "libdeflate"], default="auto",
-                   help="gzip engine for the block streams, level 6 either way (the reference's "
-                        "Compression::default()): libdeflate (auto, when libdeflate.so.0 loads; ~3x faster) or "
-                        "zlib.  The deflate bytes differ, the inflated streams do not; neither engine "
-                        "reproduces the reference's zlib-rs bytes")
+    e.add_argument("--deflate", choices=["auto", "zlib", "libdeflate", "adaptive"], default="auto",
+                   help="gzip engine for the block streams, level 6 (the reference's Compression::default()): "
+                        "adaptive (auto, when libdeflate.so.0 loads: libdeflate, with streams of >= 7.9 bits of "
+                        "entropy per byte stored), libdeflate (~3x faster than zlib) or zlib.  The deflate bytes "
+                        "differ, the inflated streams do not; no engine reproduces the reference's zlib-rs bytes")
     e.add_argument("--stats", action="store_true", help="print per-stage seconds to stderr")
     e.add_argument("--host-parse", action="store_true",
                    help="parse a plain FASTQ on the host pool instead of the GPU")

@@ -30,6 +30,7 @@
 #include <dlfcn.h>
 #include <zlib.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -193,6 +194,7 @@ struct LibDeflate {
     void (*free_c)(void *) = nullptr;
     size_t (*deflate_c)(void *, const void *, size_t, void *, size_t) = nullptr;
     size_t (*bound_c)(void *, size_t) = nullptr;
+    uint32_t (*crc32_c)(uint32_t, const void *, size_t) = nullptr;  // libdeflate_crc32 (optional)
     bool ok = false;
     LibDeflate() {
         void *h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
@@ -201,6 +203,7 @@ struct LibDeflate {
         free_c = (void (*)(void *))dlsym(h, "libdeflate_free_compressor");
         deflate_c = (size_t(*)(void *, const void *, size_t, void *, size_t))dlsym(h, "libdeflate_deflate_compress");
         bound_c = (size_t(*)(void *, size_t))dlsym(h, "libdeflate_deflate_compress_bound");
+        crc32_c = (uint32_t(*)(uint32_t, const void *, size_t))dlsym(h, "libdeflate_crc32");
         ok = alloc_c && free_c && deflate_c && bound_c;
     }
 };
@@ -228,15 +231,55 @@ bool libdeflate_deflate(const uint8_t *data, size_t n, std::vector<uint8_t> &out
     return true;
 }
 
+// order-0 entropy of p[0, n) in bits per byte
+double entropy0(const uint8_t *p, size_t n) {
+    if (!n) return 0;
+    uint32_t h[4][256] = {};
+    size_t i = 0;
+    for (; i + 4 <= n; i += 4) h[0][p[i]]++, h[1][p[i + 1]]++, h[2][p[i + 2]]++, h[3][p[i + 3]]++;
+    for (; i < n; i++) h[0][p[i]]++;
+    double e = 0;
+    for (int c = 0; c < 256; c++) {
+        const uint32_t k = h[0][c] + h[1][c] + h[2][c] + h[3][c];
+        if (k) e -= (double)k * std::log2((double)k / (double)n);
+    }
+    return e / (double)n;
+}
+
+// raw deflate of stored blocks (BTYPE 00, at most 65,535 bytes each; one empty final block
+// for n = 0), appended to out
+void stored_deflate(const uint8_t *data, size_t n, std::vector<uint8_t> &out) {
+    size_t i = 0;
+    do {
+        const size_t len = std::min<size_t>(n - i, 65535);
+        const bool last = i + len == n;
+        const uint8_t h[5] = {(uint8_t)(last ? 1 : 0), (uint8_t)len, (uint8_t)(len >> 8), (uint8_t)~len,
+                              (uint8_t)(~len >> 8)};
+        out.insert(out.end(), h, h + 5);
+        out.insert(out.end(), data + i, data + i + len);
+        i += len;
+    } while (i < n);
+}
+
+constexpr size_t kEntropySample = 32u << 10;
+constexpr double kStoreEntropy = 7.9;
+
 // one gzip member (flate2 GzEncoder shape) appended to out
 bool gzip_append(const uint8_t *data, size_t n, int engine, std::vector<uint8_t> &out) {
     static const uint8_t hdr[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, 0, 0xff};
     const size_t start = out.size();
     out.insert(out.end(), hdr, hdr + 10);
-    const bool ok = engine == NTC_DEFLATE_LIBDEFLATE ? libdeflate_deflate(data, n, out, start + 10)
-                                                     : zlib_deflate(data, n, out, start + 10);
+    bool ok = true;
+    if (engine == NTC_DEFLATE_ADAPTIVE && n >= 4096 && entropy0(data, std::min(n, kEntropySample)) >= kStoreEntropy)
+        stored_deflate(data, n, out);
+    else if (engine == NTC_DEFLATE_LIBDEFLATE || engine == NTC_DEFLATE_ADAPTIVE)
+        ok = libdeflate_deflate(data, n, out, start + 10);
+    else
+        ok = zlib_deflate(data, n, out, start + 10);
     if (!ok) return false;
-    const uint32_t crc = (uint32_t)crc32(0L, data, (uInt)n), isize = (uint32_t)n;
+    LibDeflate &L = libdeflate();  // the same CRC-32 either way; libdeflate's is ~10x faster
+    const uint32_t crc = L.ok && L.crc32_c ? L.crc32_c(0, data, n) : (uint32_t)crc32(0L, data, (uInt)n),
+                   isize = (uint32_t)n;
     for (int i = 0; i < 4; i++) out.push_back((uint8_t)(crc >> (8 * i)));
     for (int i = 0; i < 4; i++) out.push_back((uint8_t)(isize >> (8 * i)));
     return true;
@@ -529,8 +572,9 @@ int deflate_checks(const ntc_block_meta *meta, const uint8_t *payload, int engin
     *out_len = 0;
     if (meta->status != NTC_OK) return meta->status;
     if (!payload) return NTC_ERR_INVALID_ARG;
-    if (engine != NTC_DEFLATE_ZLIB && engine != NTC_DEFLATE_LIBDEFLATE) return NTC_ERR_INVALID_ARG;
-    if (engine == NTC_DEFLATE_LIBDEFLATE && !libdeflate().ok) return NTC_ERR_UNSUPPORTED;
+    if (engine != NTC_DEFLATE_ZLIB && engine != NTC_DEFLATE_LIBDEFLATE && engine != NTC_DEFLATE_ADAPTIVE)
+        return NTC_ERR_INVALID_ARG;
+    if (engine != NTC_DEFLATE_ZLIB && !libdeflate().ok) return NTC_ERR_UNSUPPORTED;
     return NTC_OK;
 }
 

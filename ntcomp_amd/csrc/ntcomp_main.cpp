@@ -7,7 +7,7 @@
 //   ntcomp build -o P [-k 31] [-p 8] [-d] [-t 1] [-m 4] [--temp-dir D] [--verbose]
 //                [-l LIST] [--builder auto|host|gpu] [--device N] [--index-format own|sbwt-rs] FILES...
 //   ntcomp encode -i P [--gpus N | --devices 0,0,..] [--threads T] [--blocks-per-batch B]
-//                 [--deflate auto|zlib|libdeflate] [--host-parse] [--stats] FILE > encoded.dat
+//                 [--deflate auto|zlib|libdeflate|adaptive] [--host-parse] [--stats] FILE > encoded.dat
 //   ntcomp decode -i P [--gpus N | --devices ..] [--threads T] [--blocks-per-batch B] [--stats] FILE > out.fasta
 #include <dlfcn.h>
 #include <unistd.h>
@@ -173,11 +173,15 @@ int cmd_encode(const Args &a) {
     const double t_gpu = since(t0);
     info("Encoding fastX data...");
     std::string engine = a.get("--deflate", nullptr, "auto");
-    if (engine == "auto") engine = libdeflate_present() ? "libdeflate" : "zlib";
+    if (engine == "auto") engine = libdeflate_present() ? "adaptive" : "zlib";
     ntc_pipeline_opts o{};
     o.threads = std::atoi(a.get("--threads", nullptr, "0").c_str());
     o.blocks_per_batch = std::atoi(a.get("--blocks-per-batch", nullptr, "4").c_str());
-    o.deflate_engine = engine == "libdeflate" ? NTC_DEFLATE_LIBDEFLATE : NTC_DEFLATE_ZLIB;
+    o.deflate_engine = engine == "adaptive"     ? NTC_DEFLATE_ADAPTIVE
+                       : engine == "libdeflate" ? NTC_DEFLATE_LIBDEFLATE
+                       : engine == "zlib"       ? NTC_DEFLATE_ZLIB
+                                                : -1;
+    if (o.deflate_engine < 0) die("--deflate: auto, zlib, libdeflate or adaptive");
     o.host_parse = a.flag("--host-parse") ? 1 : 0;
     ntc_pipeline_stats st{};
     std::fflush(stdout);

@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--devices", help="CLI --devices list (several contexts may share a GPU)")
     ap.add_argument("--contexts-per-gpu", type=int, default=0, help="CLI --contexts-per-gpu (0: the CLI default)")
-    ap.add_argument("--deflate", default="zlib", choices=["zlib", "libdeflate"])
+    ap.add_argument("--deflate", default="zlib", choices=["zlib", "libdeflate", "adaptive", "auto"])
     ap.add_argument("--keep", action="store_true", help="reuse an existing FASTQ + index in --dir")
     ap.add_argument("--reps", type=int, default=3, help="runs per timing (the best counts)")
     ap.add_argument("--cli", default="native", choices=["native", "python"],

@@ -170,3 +170,44 @@ def test_deflate_streams_concatenate_to_the_block(name, engine):
     assert b"".join(nt.deflate_stream(meta, s, payload, engine) for s in range(4)) == whole
     with pytest.raises(nt.NtcError):
         nt.deflate_stream(meta, 4, payload, engine)
+
+
+def test_adaptive_deflate_stores_incompressible_streams():
+    """NTC_DEFLATE_ADAPTIVE: a stream of >= 7.9 bits of order-0 entropy per byte (checked on
+    its first 32 KiB) goes out as stored deflate blocks (5 bytes per <= 65,535, so the member
+    is 18 bytes of gzip framing longer than the data plus those), anything else as
+    libdeflate level 6 -- the same bytes as NTC_DEFLATE_LIBDEFLATE.  Both inflate to the
+    streams (Python's zlib checks the CRC and ISIZE too)."""
+    if not nt.libdeflate_available():
+        pytest.skip("libdeflate.so.0 not on this host")
+    rng = np.random.default_rng(5)
+    # long records with random colex ids (s1 near 8 bits/byte) and short ones with random bases
+    n = 20000
+    recs = np.zeros(2 * n, dtype=np.uint64)
+    ids = rng.integers(0, 1 << 31, n, dtype=np.uint64)
+    lens = rng.integers(12, 40, n, dtype=np.uint64)
+    recs[0::2] = ids | (lens << np.uint64(32)) | (np.uint64(1) << np.uint64(56))
+    sl = rng.integers(1, 12, n, dtype=np.uint64)
+    bases = rng.integers(0, 1 << 22, n, dtype=np.uint64) & ((np.uint64(1) << (np.uint64(2) * sl)) - np.uint64(1))
+    recs[1::2] = bases | (((np.uint64(2) | (sl << np.uint64(2)))) << np.uint64(56))
+    meta, payload = nt.pack_block(recs, n)
+    streams = nt.stream_payloads(meta, payload)
+    ad = parse_container(nt.deflate_block(meta, payload, "adaptive"))
+    ld = parse_container(nt.deflate_block(meta, payload, "libdeflate"))
+    stored = 0
+    for s, ((h, m), (_, m_ld)) in enumerate(zip(ad, ld)):
+        raw = streams[s]
+        assert zlib.decompress(m, 31) == raw and zlib.decompress(m_ld, 31) == raw
+        if len(raw) >= 4096 and entropy0(raw[:32768]) >= 7.9:
+            stored += 1
+            assert len(m) == 18 + len(raw) + 5 * max(1, -(-len(raw) // 65535)), s
+            assert len(m) <= len(m_ld) * 1.001 + 64, s
+        else:
+            assert m == m_ld, s
+    assert stored >= 1
+
+
+def entropy0(b):
+    c = np.bincount(np.frombuffer(b, dtype=np.uint8), minlength=256).astype(float)
+    p = c[c > 0] / len(b)
+    return float(-(p * np.log2(p)).sum())
