@@ -110,6 +110,9 @@ std::vector<int> devices_of(const Args &a) {
 // H2D of FASTQ text overlaps the other's kernels (10 M x 150 bp, pipeline 6.2 -> 7.9 Gbases/s,
 // profiles/round4/pipe_encode_gpu_parse_r04.jsonl); decode: 1 (2 measured no better).
 constexpr int kEncodeContextsPerGpu = 2, kDecodeContextsPerGpu = 1;
+// what encode / decode hand to main for the exit
+std::vector<ntc_ctx *> g_ctxs;
+ntc_index_host *g_ix = nullptr;
 std::vector<ntc_ctx *> open_gpus(const ntc_index_host *ix, const std::vector<int> &devs, int per_gpu) {
     ntc_index_view v;
     if (ntc_index_view_of(ix, &v)) die("index view");
@@ -186,7 +189,8 @@ int cmd_encode(const Args &a) {
     ntc_pipeline_stats st{};
     std::fflush(stdout);
     const int rc = ntc_encode_file(ctxs.data(), (int)ctxs.size(), a.pos[0].c_str(), 1, &o, &st);
-    // contexts and the host index are left to the process exit (main)
+    g_ctxs = ctxs;  // main frees the contexts and the host index before leaving
+    g_ix = ix;
     if (rc) {
         std::string m = std::string("encode: ") + st.error;
         if (st.bad_read >= 0) m += " (read " + std::to_string(st.bad_read + 1) + ")";
@@ -225,7 +229,8 @@ int cmd_decode(const Args &a) {
     ntc_pipeline_stats st{};
     std::fflush(stdout);
     const int rc = ntc_decode_file(ctxs.data(), (int)ctxs.size(), a.pos[0].c_str(), 1, &o, &st);
-    // contexts and the host index are left to the process exit (main)
+    g_ctxs = ctxs;  // main frees the contexts and the host index before leaving
+    g_ix = ix;
     if (rc) die(std::string("decode: ") + st.error);
     if (st.dropped_blocks)  // the reference's `while let Ok(..) = decode_block` just ends here (main.rs:202)
         std::fprintf(stderr, "warning: %s; %llu block(s) not decoded\n", st.error,
@@ -348,10 +353,13 @@ int main(int argc, char **argv) {
     if (cmd == "build") return cmd_build(a);
     if (cmd == "encode" || cmd == "decode") {
         const int rc = cmd == "encode" ? cmd_encode(a) : cmd_decode(a);
-        // The output is complete and every device call has returned; leave without the HIP
-        // runtime's teardown (freeing each workspace, the index, the queues), which the
-        // driver does for the process anyway: ~0.1 s of an encode of 10 M reads.
+        // The output is complete and every device call has returned.  Free the contexts
+        // (their device memory: ~15 ms) and leave without the rest of the HIP runtime's
+        // teardown.  Exiting with the contexts alive cost more (wall clock after main 0.10-0.13 s
+        // against 0.05-0.08 s with them freed first, 10 M-read encode, scripts/exit_cost.py).
         std::fflush(stdout);
+        for (auto *c : g_ctxs) ntc_ctx_destroy(c);
+        ntc_index_free(g_ix);
         std::fflush(stderr);
         _exit(rc);
     }
