@@ -26,6 +26,7 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <cstdint>
 #include <cstdio>
@@ -209,6 +210,17 @@ constexpr size_t kRing = 4;
 struct ByteReader {  // read up to n decoded bytes: > 0 bytes, 0 at the end, < 0 on error
     virtual ~ByteReader() {}
     virtual int read(char *dst, unsigned n) = 0;
+    // cap bytes into dst (fewer only at the end): 1 filled, 0 the end was met, -1 error
+    virtual int read_into(char *dst, size_t cap, size_t *got) {
+        *got = 0;
+        while (*got < cap) {
+            const int r = read(dst + *got, (unsigned)std::min<size_t>(cap - *got, 1u << 30));
+            if (r < 0) return -1;
+            if (r == 0) return 0;
+            *got += (size_t)r;
+        }
+        return 1;
+    }
 };
 
 struct GzReader : ByteReader {  // plain or gzip (zlib's transparent gz* reader)
@@ -600,6 +612,77 @@ struct DeflateReader : ByteReader {
             want = want * 2 + (1u << 20);
         }
     }
+    // BGZF straight into the caller's buffer: the whole members from ci whose inflated sizes
+    // (ISIZE) fit in room, inflated in parallel at their offsets (one pass over up to ~one
+    // window); bytes written, 0 when the next member does not fit or is not BGZF, -1 on error
+    int64_t inflate_members_into(char *dst, size_t room) {
+        if (comp_end - ci < kWindow / 2 && !in_eof && !refill()) return -1;
+        std::vector<size_t> at, sz, off(1, 0);
+        for (size_t c = ci; c < comp_end;) {
+            const size_t b = bgzf_size(comp.data() + c, comp_end - c);
+            if (!b || b > comp_end - c) break;  // not BGZF here, or past the window
+            const uint32_t isz = le32(comp.data() + c + b - 4);
+            if (off.back() + isz > room) break;
+            at.push_back(c);
+            sz.push_back(b);
+            off.push_back(off.back() + isz);
+            c += b;
+        }
+        if (at.empty()) return 0;
+        const unsigned T = (unsigned)std::max(1, std::min(16, ntc_host_threads()));
+        while (pool.size() < T) {
+            void *d = alloc_fn();
+            if (!d) return -1;
+            pool.push_back(d);
+        }
+        std::atomic<bool> bad{false};
+        std::atomic<size_t> next{0};
+        auto work = [&](unsigned t) {
+            for (size_t i; (i = next.fetch_add(8)) < at.size();)  // 8 members (~0.5 MB) a grab
+                for (size_t j = i; j < std::min(at.size(), i + 8); j++) {
+                    size_t used = 0, got = 0;
+                    const int rc = gz_fn(pool[t], comp.data() + at[j], sz[j], dst + off[j], off[j + 1] - off[j], &used,
+                                         &got);
+                    if (rc != 0 || used != sz[j] || got != off[j + 1] - off[j]) bad = true;
+                }
+        };
+        std::vector<std::thread> th;
+        for (unsigned t = 1; t < T && t * 8 < at.size(); t++) th.emplace_back(work, t);
+        work(0);
+        for (auto &x : th) x.join();
+        if (bad) return -1;
+        ci = at.back() + sz.back();
+        members += at.size();
+        delivered += off.back();
+        return (int64_t)off.back();
+    }
+    int read_into(char *dst, size_t cap, size_t *got) override {
+        *got = 0;
+        while (*got < cap) {
+            if (out_pos < out_n) {  // the rest of a batch the buffered path inflated
+                const size_t t = std::min(cap - *got, out_n - out_pos);
+                std::memcpy(dst + *got, out + out_pos, t);
+                out_pos += t;
+                *got += t;
+                delivered += t;
+                continue;
+            }
+            if (bgzf && !zfall) {
+                const int64_t w = inflate_members_into(dst + *got, cap - *got);
+                if (w < 0) return -1;
+                if (w > 0) {
+                    *got += (size_t)w;
+                    continue;
+                }
+            }
+            // the buffered path: a member larger than the room, a non-BGZF tail, the end
+            const int r = read(dst + *got, (unsigned)std::min<size_t>(cap - *got, 1u << 30));
+            if (r < 0) return -1;
+            if (r == 0) return 0;
+            *got += (size_t)r;
+        }
+        return 1;
+    }
     // hand the rest of the stream to zlib: reopen, skip what was delivered
     bool to_zlib() {
         gzFile g = gzopen(path.c_str(), "rb");
@@ -700,14 +783,59 @@ struct ChunkSource {
     std::vector<std::vector<char>> spare;
     bool done = false, stop = false, error = false;
 
+    bool direct = false;    // the producer stopped: the consumer reads f itself (read_direct)
+    size_t front_off = 0;   // direct: bytes of full.front() already handed out
+
     explicit ChunkSource(ByteReader *reader) : f(reader) { th = std::thread([this] { run(); }); }
     ~ChunkSource() {
+        if (direct) return;
         {
             std::lock_guard<std::mutex> g(mu);
             stop = true;
         }
         cv.notify_all();
         th.join();
+    }
+    // Stop the producer; the chunks it made are handed out first.  Then the consumer's own
+    // thread decodes straight into its buffer (the GPU-parse reader: BGZF members inflate in
+    // parallel into the pinned batch, no chunk copies).
+    void go_direct() {
+        if (direct) return;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            stop = true;
+        }
+        cv.notify_all();
+        th.join();
+        direct = true;
+    }
+    // direct: up to cap bytes into dst (fewer only at the end of input); -1 on error
+    int64_t read_direct(char *dst, size_t cap) {
+        go_direct();
+        size_t got = 0;
+        while (got < cap && !full.empty()) {
+            std::vector<char> &c = full.front();
+            const size_t t = std::min(cap - got, c.size() - front_off);
+            std::memcpy(dst + got, c.data() + front_off, t);
+            got += t;
+            front_off += t;
+            if (front_off == c.size()) {
+                full.pop_front();
+                front_off = 0;
+            }
+        }
+        if (error) return -1;
+        if (got < cap && !done) {
+            size_t g = 0;
+            const int rc = f->read_into(dst + got, cap - got, &g);
+            got += g;
+            if (rc < 0) {
+                error = true;
+                return -1;
+            }
+            if (rc == 0) done = true;
+        }
+        return (int64_t)got;
     }
     void run() {
         for (;;) {
@@ -737,6 +865,27 @@ struct ChunkSource {
     }
     // next chunk into `out` (swapped); false at end of input
     bool take(std::vector<char> &out, bool &err) {
+        if (direct) {  // the producer is gone: hand out what it left, then read here
+            err = error;
+            if (!full.empty()) {
+                if (front_off) full.front().erase(full.front().begin(), full.front().begin() + (long)front_off);
+                front_off = 0;
+                out.swap(full.front());
+                full.pop_front();
+                return true;
+            }
+            if (done || error) return false;
+            out.resize(kChunk);
+            const int got = f->read(out.data(), (unsigned)kChunk);
+            if (got < 0) error = true;
+            if (got <= 0) {
+                done = true;
+                err = error;
+                return false;
+            }
+            out.resize((size_t)got);
+            return true;
+        }
         std::unique_lock<std::mutex> g(mu);
         cv.wait(g, [&] { return !full.empty() || done; });
         err = error;
@@ -747,6 +896,7 @@ struct ChunkSource {
         return true;
     }
     void give_back(std::vector<char> &c) {
+        if (direct) return;
         std::lock_guard<std::mutex> g(mu);
         if (spare.size() < kRing) spare.push_back(std::move(c));
     }
@@ -1084,6 +1234,42 @@ const uint8_t *fastx_mapped(ntc_fastx *fx, uint64_t *size) {
 }
 void fastx_seek_mapped(ntc_fastx *fx, uint64_t pos) {
     if (fx && fx->mm) fx->mm_pos = std::min<size_t>((size_t)pos, fx->mm_n);
+}
+bool fastx_streamed_fastq(ntc_fastx *fx) { return fx && !fx->mm && fx->src && fx->format == '@'; }
+uint64_t fastx_stream_read(ntc_fastx *fx, uint8_t *dst, uint64_t cap, bool *io_error) {
+    uint64_t got = 0;
+    while (got < cap) {
+        if (fx->pos < fx->end) {  // what the format check (or an unread) left in the buffer
+            const size_t t = (size_t)std::min<uint64_t>(fx->end - fx->pos, cap - got);
+            std::memcpy(dst + got, fx->buf.data() + fx->pos, t);
+            fx->pos += t;
+            got += t;
+            continue;
+        }
+        if (fx->eof) break;
+        const int64_t r = fx->src->read_direct((char *)dst + got, (size_t)(cap - got));
+        if (r < 0) {
+            fx->io_error = true;
+            fx->eof = true;
+            break;
+        }
+        got += (uint64_t)r;
+        if (got < cap) fx->eof = true;  // read_direct fills the room unless the input ended
+    }
+    if (io_error) *io_error = fx->io_error;
+    return got;
+}
+void fastx_stream_unread(ntc_fastx *fx, const uint8_t *src, uint64_t n) {
+    const size_t tail = fx->end - fx->pos;
+    std::vector<char> nb((size_t)n + tail + 1 + (1u << 16));
+    std::memcpy(nb.data(), src, (size_t)n);
+    std::memcpy(nb.data() + n, fx->buf.data() + fx->pos, tail);
+    fx->buf.swap(nb);
+    fx->pos = 0;
+    fx->end = (size_t)n + tail;
+    // fill() supplies a missing final newline when it meets the end of input; the end was
+    // met already, so supply it here
+    if (fx->eof && fx->end && fx->buf[fx->end - 1] != '\n') fx->buf[fx->end++] = '\n';
 }
 }  // namespace ntc
 

@@ -35,6 +35,12 @@ namespace ntc {
 // moving the mapped parser to byte pos (a record start) -- pipeline.cpp's GPU-parse reader
 const uint8_t *fastx_mapped(ntc_fastx *fx, uint64_t *size);
 void fastx_seek_mapped(ntc_fastx *fx, uint64_t pos);
+// a FASTQ read through a decoder (gzip, BGZF, bz2, xz, zstd) or a pipe: the next decoded
+// bytes into dst (up to cap; fewer only at the end of input), and bytes handed back so the
+// host parser goes on from them (the GPU-parse reader's fallback)
+bool fastx_streamed_fastq(ntc_fastx *fx);
+uint64_t fastx_stream_read(ntc_fastx *fx, uint8_t *dst, uint64_t cap, bool *io_error);
+void fastx_stream_unread(ntc_fastx *fx, const uint8_t *src, uint64_t n);
 }  // namespace ntc
 
 struct ntc_index_host {

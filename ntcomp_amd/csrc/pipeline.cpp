@@ -144,6 +144,7 @@ struct FqScan {
     uint64_t nl = 0;
     size_t blank = SIZE_MAX;  // offset of the first blank line's first byte, or SIZE_MAX
 };
+template <bool kCopy>
 FqScan fq_copy_scan(const uint8_t *src, uint8_t *dst, size_t n) {
     FqScan r;
     const __m128i NL = _mm_set1_epi8('\n'), CR = _mm_set1_epi8('\r');
@@ -153,7 +154,7 @@ FqScan fq_copy_scan(const uint8_t *src, uint8_t *dst, size_t n) {
         uint64_t mnl = 0, mcr = 0;
         for (int k = 0; k < 4; k++) {
             const __m128i x = _mm_loadu_si128((const __m128i *)(src + i + 16 * k));
-            _mm_stream_si128((__m128i *)(dst + i + 16 * k), x);
+            if (kCopy) _mm_stream_si128((__m128i *)(dst + i + 16 * k), x);
             mnl |= (uint64_t)(uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(x, NL)) << (16 * k);
             mcr |= (uint64_t)(uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(x, CR)) << (16 * k);
         }
@@ -162,10 +163,10 @@ FqScan fq_copy_scan(const uint8_t *src, uint8_t *dst, size_t n) {
         carry = mnl >> 63;
         r.nl += (uint64_t)__builtin_popcountll(mnl);
     }
-    _mm_sfence();
+    if (kCopy) _mm_sfence();
     for (; i < n; i++) {
         const uint8_t c = src[i];
-        dst[i] = c;
+        if (kCopy) dst[i] = c;
         if (carry && (c == '\n' || c == '\r') && r.blank == SIZE_MAX) r.blank = i;
         carry = c == '\n';
         r.nl += c == '\n';
@@ -304,9 +305,15 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
         (void)keep_reads;
         return true;
     };
-    // GPU-parse reader state: the next batch's text starts at text_pos (a record start)
+    // GPU-parse reader state.  Mapped: the next batch's text starts at text_pos (a record
+    // start).  Streamed (a decoder's output): the text after the last cut, carry_n bytes at
+    // carry_p in the previous batch's buffer, goes first into the next one.
+    const bool streamed = !text && !o.host_parse && ntc::fastx_streamed_fastq(fx);
     uint64_t text_pos = 0;
-    double rec_bytes = 0;  // text bytes per record so far
+    const uint8_t *carry_p = nullptr;
+    uint64_t carry_n = 0;
+    bool stream_eof = false;
+    double rec_bytes = 320;  // text bytes per record so far (a guess for 150 bp reads until known)
     std::atomic<uint64_t> text_batches{0};
     // the reader's gang: 8 threads copy + scan at ~45 GB/s on the box, as fast as 16 for the
     // pipeline and at less CPU beside the deflate pool (scripts/rt_sweep.sh); NTC_READ_THREADS
@@ -319,35 +326,63 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
         for (size_t i = 0; i < m; i++) nl += text[i] == '\n';
         rec_bytes = nl >= 4 ? 4.0 * (double)m / (double)nl : (double)m + 1;
     }
-    // Fill b with the text of the next whole blocks (or the file's end): 1 = filled, 0 = no
-    // input left, -1 = hand over to the host parser at text_pos (a blank line before the
-    // cut, a line count that is not a multiple of 4 at the end, a block too large for one call)
+    // Fill b with the text of the next whole blocks (or the input's end): 1 = filled, 0 = no
+    // input left, -1 = hand over to the host parser (a blank line before the cut, a line
+    // count that is not a multiple of 4 at the end, a block too large for one call), -2 = the
+    // decoder failed
     auto fill_text = [&](Gang &gang, Batch &b, bool &eof) -> int {
         const uint64_t kMaxText = (1ull << 32) - (64u << 20);  // ntc_encode_pack_fastq takes < 4 GiB
         uint64_t want_cap = (uint64_t)((double)per_batch * rec_bytes * 1.03) + (256u << 10);
         std::vector<FqScan> sc;
         for (;;) {
-            if (text_pos >= text_n) return 0;
-            if (text[text_pos] != '@') return -1;
+            if (!streamed) {
+                if (text_pos >= text_n) return 0;
+                if (text[text_pos] != '@') return -1;
+            }
+            // room for the carried text plus more (a batch read with a doubled buffer can leave a
+            // carry larger than this batch's estimate)
+            if (streamed) want_cap = std::max<uint64_t>(want_cap, carry_n + (4u << 20));
             want_cap = std::min(want_cap, kMaxText);
+            if (streamed && carry_n >= want_cap) return -1;  // more than 4 GiB without one block
             if (b.text_cap < want_cap) {
                 const auto ta = Clock::now();
+                uint8_t *nt = (uint8_t *)pinned_alloc(want_cap);
+                if (!nt) return -1;
+                if (carry_n && carry_p == b.text) {  // growing the buffer that holds the carry
+                    std::memcpy(nt, carry_p, carry_n);
+                    carry_p = nt;
+                }
                 pinned_free(b.text);
-                b.text_cap = 0;
-                if (!(b.text = (uint8_t *)pinned_alloc(want_cap))) return -1;
+                b.text = nt;
                 b.text_cap = want_cap;
                 t_pin = t_pin.load() + secs(ta, Clock::now());
             }
-            const uint64_t len = std::min(text_n - text_pos, want_cap);
-            const uint8_t *src = text + text_pos;
+            uint64_t len;
+            const uint8_t *src;
+            if (!streamed) {
+                len = std::min(text_n - text_pos, want_cap);
+                src = text + text_pos;
+            } else {
+                if (carry_n && carry_p != b.text) std::memcpy(b.text, carry_p, carry_n);
+                bool io_err = false;
+                len = carry_n + ntc::fastx_stream_read(fx, b.text + carry_n, want_cap - carry_n, &io_err);
+                if (io_err) return -2;
+                stream_eof = len < want_cap;
+                carry_p = b.text;  // all of it unused until the cut
+                carry_n = len;
+                if (len == 0) return 0;
+                if (b.text[0] != '@') return -1;
+                src = b.text;
+            }
             constexpr uint64_t kPiece = 1u << 20;
             const uint64_t np = (len + kPiece - 1) / kPiece;
             sc.assign(np, FqScan{});
             std::atomic<uint64_t> next{0};
             gang.run([&](int) {
                 for (uint64_t q; (q = next.fetch_add(1)) < np;) {
-                    const uint64_t a = q * kPiece;
-                    sc[q] = fq_copy_scan(src + a, b.text + a, std::min(len, a + kPiece) - a);
+                    const uint64_t a = q * kPiece, e = std::min(len, a + kPiece);
+                    sc[q] = streamed ? fq_copy_scan<false>(src + a, nullptr, e - a)
+                                     : fq_copy_scan<true>(src + a, b.text + a, e - a);
                 }
             });
             uint64_t nl = 0, blank = UINT64_MAX;  // the first blank line in the text read
@@ -357,9 +392,10 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
                 if (blank == UINT64_MAX && sc[q].blank != SIZE_MAX) blank = a + sc[q].blank;
                 nl += sc[q].nl;
             }
-            eof = text_pos + len == text_n;
-            // the text read ends the file with whole records and no blank line: all of it goes;
-            // otherwise whole blocks of the complete records, cut after the last one's last line
+            eof = streamed ? stream_eof : text_pos + len == text_n;
+            // the text read ends the input with whole records and no blank line: all of it
+            // goes; otherwise whole blocks of the complete records, cut after the last one's
+            // last line
             const uint64_t lines = nl + (eof && src[len - 1] != '\n');
             const bool whole = eof && lines % 4 == 0 && blank == UINT64_MAX;
             const uint64_t recs = whole ? lines / 4 : nl / 4;
@@ -383,9 +419,15 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
             if (blank < cut) return -1;  // the batch holds a blank line: the host parser takes it
             b.text_len = cut;
             b.n_reads = b.n_process = n;
-            text_pos += cut;
             rec_bytes = (double)cut / (double)std::max<uint64_t>(n, 1);
-            eof = eof || text_pos == text_n;
+            if (streamed) {
+                carry_p = b.text + cut;
+                carry_n = len - cut;
+                eof = eof || (stream_eof && carry_n == 0);
+            } else {
+                text_pos += cut;
+                eof = eof || text_pos == text_n;
+            }
             return 1;
         }
     };
@@ -393,7 +435,7 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
         uint64_t next_read = 0, next_block = 0, batch_no = 0;
         int prev = -1;
         uint64_t carry = 0;  // reads at the tail of ring[prev] past its processed blocks
-        bool as_text = text != nullptr;
+        bool as_text = text != nullptr || streamed;
         std::unique_ptr<Gang> gang(as_text ? new Gang(RT) : nullptr);
         for (;;) {
             int bi;
@@ -429,8 +471,17 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
                     continue;
                 }
                 if (r == 0) break;
-                as_text = false;  // the host parser goes on from the record at text_pos
-                ntc::fastx_seek_mapped(fx, text_pos);
+                if (r == -2) {
+                    sh.fail(NTC_ERR_IO, "FASTX input: malformed or unreadable");
+                    break;
+                }
+                as_text = false;  // the host parser goes on from the first record not sent
+                if (streamed) {
+                    ntc::fastx_stream_unread(fx, carry_p, carry_n);
+                    carry_n = 0;
+                } else {
+                    ntc::fastx_seek_mapped(fx, text_pos);
+                }
             }
             if (!b.bases) {
                 const auto ta = Clock::now();

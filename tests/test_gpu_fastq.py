@@ -3,6 +3,7 @@ host parser (fastx.cpp, ntc_fastx_*: needletail's records + normalize(true) as t
 them, src/main.rs:158-163), and the encode pipeline's text path (pipeline.cpp fill_text)
 against its host-parse path: same bases and offsets, same metas and payload, same
 encoded.dat bytes, same errors."""
+import gzip
 import os
 
 import numpy as np
@@ -119,9 +120,9 @@ def test_gpu_encode_pack_fastq_equals_encode_pack(ctx):
 
 @pytest.mark.parametrize("bpb", [1, 4])
 def test_encode_file_text_path_equals_host_parse(ctx, tmp_path, bpb):
-    """ntc_encode_file on a plain FASTQ: GPU parse (default) and host parse write the same
-    encoded.dat; a blank line mid-file hands the rest to the host parser; a truncated last
-    record is NTC_ERR_FORMAT either way."""
+    """ntc_encode_file on a FASTQ, mapped or through gzip / BGZF: GPU parse (default) and host
+    parse write the same encoded.dat; a blank line mid-file hands the rest to the host parser;
+    a truncated last record is NTC_ERR_FORMAT either way."""
     genome = nt.synth_genome(31, 100_000)
     ix = nt.Index.build([genome.tobytes()], 31)
     ctx.upload(ix)
@@ -129,8 +130,12 @@ def test_encode_file_text_path_equals_host_parse(ctx, tmp_path, bpb):
     body = nt.synth_reads(genome, 32, 0, n, L, 10_000).reshape(n, L)
     recs = [b"@r%d\n" % i + body[i].tobytes() + b"\n+\n" + b"F" * L + b"\n" for i in range(n)]
     plain = b"".join(recs)
+    from test_cli import _bgzf_member
     files = {"plain": plain, "crlf": plain.replace(b"\n", b"\r\n"),
-             "mid_blank": b"".join(recs[:4 * 65536 + 5]) + b"\n" + b"".join(recs[4 * 65536 + 5:])}
+             "mid_blank": b"".join(recs[:4 * 65536 + 5]) + b"\n" + b"".join(recs[4 * 65536 + 5:]),
+             # through a decoder: the streamed text path (carried tails between batches)
+             "plain_gz": gzip.compress(plain, 1),
+             "plain_bgzf": b"".join(_bgzf_member(plain[i:i + 65000]) for i in range(0, len(plain), 65000))}
     for name, blob in files.items():
         (tmp_path / f"{name}.fq").write_bytes(blob)
         outs = {}

@@ -266,6 +266,17 @@ def test_pipeline_text_reader_edge_cases_under_sanitizers(san, encoded, tmp_path
         "leading_blank": (b"\n" + plain, False),
         "truncated": (plain[:plain.rindex(b"\n+\n")], True),
     }
+    # read lengths changing mid-file (the batch-size estimate and the carried text disagree)
+    long_body = nt.synth_reads(genome, 6, 0, 300, 400, 20_000).reshape(300, 400)
+    ragged = b"".join(recs[:65536 + 100]) + b"".join(
+        b"@l%d\n" % i + long_body[i].tobytes() + b"\n+\n" + b"I" * 400 + b"\n" for i in range(300))
+    cases["ragged"] = (ragged, True)
+    # the same through a decoder (the streamed text path): gzip and BGZF
+    from test_cli import _bgzf_member
+    for name in ("plain", "crlf", "mid_blank", "truncated", "no_final_newline", "ragged"):
+        blob, tf = cases[name]
+        cases[name + ".gz"] = (gzip.compress(blob, 1), tf)
+        cases[name + ".bgzf"] = (b"".join(_bgzf_member(blob[i:i + 60000]) for i in range(0, len(blob), 60000)), tf)
     for name, (blob, text_first) in cases.items():
         (tmp_path / f"{name}.fq").write_bytes(blob)
         got = {}
@@ -274,10 +285,15 @@ def test_pipeline_text_reader_edge_cases_under_sanitizers(san, encoded, tmp_path
                           4, 1, 2, 0, hp)
         assert int(got[1]["text"]) == 0
         assert (int(got[0]["text"]) > 0) == text_first, (name, got[0])
+        if name.endswith(".bgzf"):  # BGZF inflated in parallel straight into the batch: under TSan too
+            t = run(san["tsan"], "encode", d / "idx", tmp_path / f"{name}.fq", tmp_path / f"{name}t.dat", 4, 1, 2, 0, 0)
+            assert t == got[0], (name, t)
+            if int(t["rc"]) == 0:
+                assert (tmp_path / f"{name}t.dat").read_bytes() == (tmp_path / f"{name}0.dat").read_bytes()
         for k in ("rc", "reads", "bases", "blocks", "bad"):
             assert got[0][k] == got[1][k], (name, k, got)
         if int(got[0]["rc"]) == 0:
-            assert int(got[0]["reads"]) == n, name
+            assert int(got[0]["reads"]) == (65536 + 400 if name.startswith("ragged") else n), name
             assert (tmp_path / f"{name}0.dat").read_bytes() == (tmp_path / f"{name}1.dat").read_bytes(), name
         else:
-            assert name == "truncated" and int(got[0]["rc"]) == 8, (name, got)
+            assert name.startswith("truncated") and int(got[0]["rc"]) == 8, (name, got)
