@@ -51,24 +51,70 @@ namespace {
 using Clock = std::chrono::steady_clock;
 double secs(Clock::time_point a, Clock::time_point b) { return std::chrono::duration<double>(b - a).count(); }
 
-// Pinned host memory: 2 MB pages, registered with HIP (hipHostRegister runs at ~25 GB/s,
-// hipHostMalloc at ~4 GB/s on the box: scripts/ingest_bw.cpp, profiles/round4)
+// Pinned host memory: 2 MB pages, touched, then registered with HIP (hipHostRegister runs at
+// ~25 GB/s, hipHostMalloc at ~4 GB/s on the box: scripts/ingest_bw.cpp, profiles/round4).
+// Freed buffers stay registered in a process-wide pool (up to kPinnedPoolMax bytes) and are
+// handed out again, so pipelines that grow and drop buffers per batch neither pay the
+// registration again nor register a range the process just unregistered.
+constexpr size_t kPinnedPoolMax = 8ull << 30;
+struct PinnedPool {
+    std::mutex mu;
+    std::map<void *, size_t> size_of;       // every buffer handed out or pooled
+    std::multimap<size_t, void *> idle;     // pooled: size -> buffer
+    size_t idle_bytes = 0;
+};
+PinnedPool &pinned_pool() {
+    static PinnedPool *p = new PinnedPool();  // never destroyed: buffers live until the process ends
+    return *p;
+}
 void *pinned_alloc(size_t n) {
     const size_t sz = (std::max<size_t>(n, 1) + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
-    void *p = std::aligned_alloc(2u << 20, sz);
-    if (!p) return nullptr;
-    madvise(p, sz, MADV_HUGEPAGE);
-    if (hipHostRegister(p, sz, hipHostRegisterPortable) != hipSuccess) {
+    PinnedPool &P = pinned_pool();
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        auto it = P.idle.lower_bound(sz);
+        if (it != P.idle.end() && it->first <= 2 * sz + (64u << 20)) {  // not a far larger one
+            void *q = it->second;
+            P.idle_bytes -= it->first;
+            P.idle.erase(it);
+            return q;
+        }
+    }
+    void *q = mmap(nullptr, sz, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (q == MAP_FAILED) return nullptr;
+    madvise(q, sz, MADV_HUGEPAGE);
+    std::memset(q, 0, sz);  // real pages before they are pinned
+    if (hipHostRegister(q, sz, hipHostRegisterPortable) != hipSuccess) {
         (void)hipGetLastError();
-        std::free(p);
+        munmap(q, sz);
         return nullptr;
     }
-    return p;
+    std::lock_guard<std::mutex> g(P.mu);
+    P.size_of[q] = sz;
+    return q;
 }
-void pinned_free(void *p) {
-    if (!p) return;
-    (void)hipHostUnregister(p);
-    std::free(p);
+void pinned_free(void *q) {
+    if (!q) return;
+    PinnedPool &P = pinned_pool();
+    std::vector<std::pair<void *, size_t>> drop;
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        auto it = P.size_of.find(q);
+        if (it == P.size_of.end()) return;
+        P.idle.emplace(it->second, q);
+        P.idle_bytes += it->second;
+        while (P.idle_bytes > kPinnedPoolMax && !P.idle.empty()) {  // the largest idle ones go
+            auto big = std::prev(P.idle.end());
+            drop.emplace_back(big->second, big->first);
+            P.idle_bytes -= big->first;
+            P.size_of.erase(big->second);
+            P.idle.erase(big);
+        }
+    }
+    for (auto &d : drop) {
+        (void)hipHostUnregister(d.first);
+        munmap(d.first, d.second);
+    }
 }
 
 struct Batch {  // one pinned buffer of the ring
