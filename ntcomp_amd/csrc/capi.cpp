@@ -40,7 +40,7 @@ enum WsSlot {
     WS_STAGE_BASES, WS_STAGE_OFFS, WS_STAGE_RECS, WS_E, WS_DEC_A, WS_DEC_B, WS_DEC_C,
     WS_DEC_D, WS_Q, WS_E3, WS_NE, WS_COUNTER, WS_R2, WS_ED, WS_WAVECNT, WS_PACK_CHUNKS, WS_PACK_META,
     WS_PACK_PAYLOAD, WS_FA_BASES, WS_FA_OFFS, WS_FA_SCAN, WS_ES, WS_OBASE,
-    WS_FQ_RAW, WS_FQ_TILES, WS_FQ_NL, WS_FQ_KEPT, WS_COUNT
+    WS_FQ_RAW, WS_FQ_TILES, WS_FQ_NL, WS_FQ_KEPT, WS_PACK_SEGS, WS_COUNT
 };
 
 // The device index of one upload: freed with the last context that holds it
@@ -490,12 +490,34 @@ int pack_blocks_impl(ntc_ctx *ctx, const uint64_t *d_recs, const uint64_t *d_rof
     }
     *payload_bytes = words * 8;
     if (words * 8 > payload_capacity) return set_err(ctx, NTC_ERR_CAPACITY, "payload_capacity too small");
-    HIP_TRY(ctx, hipMemsetAsync(d_payload, 0, words * 8, ctx->stream));  // fallback tiles OR into zeros
+    // pass 2 in segments (pack.hip k_pack_write): each block's records, then its s4 chunks
+    std::vector<PackSeg> segs;
+    for (uint64_t b = 0; b < n_blocks; b++) {
+        PackParams &P = pp[b];
+        P.seg0 = (uint32_t)segs.size();
+        if (!P.skip) {
+            const PackStats &S = st[b];
+            for (uint64_t f = S.rec_begin; f < S.rec_begin + S.n_recs; f += kPackSegRecs)
+                segs.push_back(PackSeg{(uint32_t)b, 0u, f, std::min<uint64_t>(kPackSegRecs, S.rec_begin + S.n_recs - f)});
+            const uint64_t nch = (S.T + 30) / 31;
+            for (uint64_t f = 0; f < nch; f += kPackSegChunks)
+                segs.push_back(PackSeg{(uint32_t)b, 1u, f, std::min<uint64_t>(kPackSegChunks, nch - f)});
+        }
+        P.nseg = (uint32_t)segs.size() - P.seg0;
+    }
+    void *d_segs;
+    if ((rc = ensure(ctx, WS_PACK_SEGS, segs.size() * (sizeof(PackSeg) + 48) + 64, &d_segs))) return rc;
+    uint64_t *d_seg_bits = (uint64_t *)((uint8_t *)d_segs + segs.size() * sizeof(PackSeg));
+    uint64_t *d_seg_start = d_seg_bits + 3 * segs.size();
+    HIP_TRY(ctx, hipMemsetAsync(d_payload, 0, words * 8, ctx->stream));  // shared words and fallback tiles OR into zeros
     HIP_TRY(ctx, hipMemcpyAsync(d_params, pp.data(), n_blocks * sizeof(PackParams), hipMemcpyHostToDevice,
                                 ctx->stream));
+    if (!segs.empty())
+        HIP_TRY(ctx, hipMemcpyAsync(d_segs, segs.data(), segs.size() * sizeof(PackSeg), hipMemcpyHostToDevice,
+                                    ctx->stream));
     HIP_TRY(ctx, hipEventRecord(ctx->pack_ev[2], ctx->stream));
-    launch_pack_write(d_recs, (const uint64_t *)d_chunks, d_stats, d_params, n_blocks, (uint64_t *)d_payload, d_bits,
-                      ctx->stream);
+    launch_pack_write(d_recs, (const uint64_t *)d_chunks, d_stats, d_params, n_blocks, (const PackSeg *)d_segs,
+                      segs.size(), d_seg_bits, d_seg_start, (uint64_t *)d_payload, d_bits, ctx->stream);
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipEventRecord(ctx->pack_ev[1], ctx->stream));
     std::vector<uint64_t> bits(n_blocks * 4);

@@ -126,11 +126,22 @@ struct PackParams {
     uint64_t lim1, lim4;  // minimal-binary limits 2^(l+1) - max
     int32_t p2, p3, l1, l4;
     uint32_t skip, pad;   // skip: the block is dropped (App. B.3) or malformed
+    uint32_t seg0, nseg;  // the block's pass-2 segments [seg0, seg0 + nseg): records first, then s4 chunks
 };
+// a workgroup's share of pass 2: kind 0 = records [first, first + count) (absolute indices,
+// streams s1-s3), kind 1 = s4 chunks [first, first + count) of the block
+struct PackSeg {
+    uint32_t block, kind;
+    uint64_t first, count;
+};
+constexpr uint64_t kPackSegRecs = 16384, kPackSegChunks = 16384;
 void launch_pack_stats(const uint64_t *recs, const uint64_t *roffs, uint64_t n_reads, uint32_t block_reads,
                        uint64_t n_blocks, uint64_t *chunks, PackStats *stats, hipStream_t s);
+// pass 2 over n_segs segments: their code lengths, each block's segment offsets (seg_bits /
+// seg_start: 3 words per segment), then every segment's codes in parallel
 void launch_pack_write(const uint64_t *recs, const uint64_t *chunks, const PackStats *stats,
-                       const PackParams *params, uint64_t n_blocks, uint64_t *payload, uint64_t *bits_out,
+                       const PackParams *params, uint64_t n_blocks, const PackSeg *segs, uint64_t n_segs,
+                       uint64_t *seg_bits, uint64_t *seg_start, uint64_t *payload, uint64_t *bits_out,
                        hipStream_t s);
 
 // decode output as FASTA text on the GPU (fasta.hip): ">seq.{first_id + r}\n{read r}\n";

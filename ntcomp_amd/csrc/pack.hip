@@ -8,8 +8,8 @@
 //   compress_block's bytes     src/encode.rs:107-109   words stored big-endian (the MSB-first
 //                                                      bit stream of dsi-bitstream's BE writer)
 //
-// One workgroup (1024 threads, 16 waves) per block; a block is walked in tiles of 4096
-// records (4 consecutive records per thread: two 16-byte loads per lane, coalesced):
+// Workgroups of 1024 threads (16 waves), tiles of 4096 records (4 consecutive records per
+// thread: two 16-byte loads per lane, coalesced); pass 1 one workgroup per block:
 //
 //   k_pack_stats  stream totals (long records, max colex, length / flag sums, short bases)
 //                 and the s4 chunk values: a block scan gives every short record its base
@@ -20,13 +20,18 @@
 //                 f64 math; the device's libm may differ in the last ulp, and the parameter
 //                 is a ceil), minimal-binary widths, per-block payload offsets from exact
 //                 upper bounds, capacity check.
-//   k_pack_write  per tile: code lengths, a 3-way block scan (s1, s2, s3) gives every code
-//                 its bit position, codes are OR-ed into per-stream LDS word buffers (a
-//                 unary run of zeros costs nothing: only the terminating one and the
-//                 remainder are written), then complete words are stored once (big-endian),
-//                 the partial last word carries into the next tile.  A tile whose bits do
-//                 not fit its LDS buffer (pathological unary runs) ORs straight into the
-//                 zeroed payload with global atomics.  Then s4 the same way over the chunks.
+//   k_pack_seglen / k_pack_segscan   pass 2 runs in segments of 16,384 records (or s4
+//                 chunks), each its own workgroup: their bits per stream, then each
+//                 segment's first bit within its block's streams (and the streams' totals).
+//   k_pack_write  per segment, per tile: code lengths, a 3-way block scan (s1, s2, s3) gives
+//                 every code its bit position, codes are OR-ed into per-stream LDS word
+//                 buffers (a unary run of zeros costs nothing: only the terminating one and
+//                 the remainder are written), then complete words are stored once
+//                 (big-endian), the partial last word carries into the next tile; a segment's
+//                 first and last words, shared with the neighbouring segments, are OR-ed into
+//                 the zeroed payload.  A tile whose bits do not fit its LDS buffer
+//                 (pathological unary runs) ORs straight into the payload with global
+//                 atomics.  s4 the same way over the chunk segments.
 //
 // Bound: HBM bytes -- reads 8 B per record twice + 8 B per s4 chunk, writes the payload
 // (about 1 B per record at C91) and the chunks.
@@ -132,18 +137,6 @@ __device__ __forceinline__ void load_tile(const uint64_t *recs, uint64_t i0, uin
         const uint64_t i = i0 + j;
         r[j] = i < end ? recs[i] : 0;
     }
-}
-
-// One stream's tile: codes already OR-ed into buf (buf[0] held the carry word of the
-// previous tile); [bit0, bit1) is the tile's span in the stream.  Stores the complete words,
-// keeps the partial last one in carry (or stores it too at the end of the block).
-__device__ void flush_tile(uint64_t *buf, uint64_t bit0, uint64_t bit1, bool last, uint64_t *out, uint64_t *carry) {
-    const uint64_t w0 = bit0 >> 6;
-    const uint64_t wend = last ? (bit1 + 63) >> 6 : bit1 >> 6;  // words to store: [w0, wend)
-    for (uint64_t i = w0 + threadIdx.x; i < wend; i += kPackThreads) out[i] = bswap64(buf[i - w0]);
-    __syncthreads();
-    if (threadIdx.x == 0) *carry = (!last && (bit1 & 63)) ? buf[(bit1 >> 6) - w0] : 0;
-    __syncthreads();
 }
 
 // A fallback tile's partial last word lives in HBM (atomics): read it back as the carry
@@ -277,102 +270,197 @@ __device__ __forceinline__ Code rice_code(uint64_t x, int p) {  // unary(x >> p)
     return Code{v, q, p + 1, q + 1 + (uint64_t)p};
 }
 
-__global__ void __launch_bounds__(kPackThreads) k_pack_write(const uint64_t *recs, const uint64_t *chunks,
-                                                             const PackStats *stats, const PackParams *params,
-                                                             uint64_t *payload, uint64_t *bits_out) {
-    __shared__ uint64_t buf1[kBuf1], buf2[kBuf2], buf3[kBuf3];
-    __shared__ uint64_t sh[64];
-    __shared__ uint64_t carry[4];
-    const uint64_t b = blockIdx.x;
-    const PackParams P = params[b];
-    if (P.skip) return;
-    const PackStats S = stats[b];
-    const uint64_t beg = S.rec_begin, end = beg + S.n_recs;
-    uint64_t *out1 = payload + P.off[0], *out2 = payload + P.off[1], *out3 = payload + P.off[2],
-             *out4 = payload + P.off[3];
-    if (threadIdx.x < 4) carry[threadIdx.x] = 0;
-    uint64_t pos[3] = {0, 0, 0};  // bits written per stream (same in every thread)
-    __syncthreads();
-    for (uint64_t t0 = beg; t0 < end; t0 += kPackTile) {
-        uint64_t r[kPackPer];
-        load_tile(recs, t0 + threadIdx.x * kPackPer, end, r);
-        uint64_t v[3] = {0, 0, 0};
-#pragma unroll
-        for (int j = 0; j < kPackPer; j++) {
-            const uint64_t i = t0 + threadIdx.x * kPackPer + j;
-            if (i >= end) continue;
-            const uint64_t w = r[j], flag = w >> 56;
+// pass 2a: every segment's bits per stream (the code lengths k_pack_write will write)
+__global__ void __launch_bounds__(kPackThreads) k_pack_seglen(const uint64_t *recs, const uint64_t *chunks,
+                                                              const PackStats *stats, const PackParams *params,
+                                                              const PackSeg *segs, uint64_t *seg_bits) {
+    __shared__ uint64_t rs[16][3];
+    const PackSeg g = segs[blockIdx.x];
+    const PackParams P = params[g.block];
+    uint64_t v[3] = {0, 0, 0};
+    if (g.kind == 0) {
+        for (uint64_t i = g.first + threadIdx.x; i < g.first + g.count; i += kPackThreads) {
+            const uint64_t w = recs[i], flag = w >> 56;
             v[2] += rice_code(flag, P.p3).len;
             if ((flag & 2) == 0) {
                 v[0] += mb_code(w & 0xFFFFFFFFULL, P.l1, P.lim1).len;
                 v[1] += rice_code((w >> 32) & 0xFFFFFFULL, P.p2).len;
             }
         }
-        uint64_t ex[3], tot[3];
-        block_scan3(v, ex, tot, sh);
-        const bool last = t0 + kPackTile >= end;
-        // spans in words of each stream's LDS buffer: fits?  (uniform across the block)
-        bool fit[3];
-        for (int s = 0; s < 3; s++) {
-            uint64_t *buf = s == 0 ? buf1 : s == 1 ? buf2 : buf3;
-            uint64_t *out = s == 0 ? out1 : s == 1 ? out2 : out3;
-            const uint64_t cap = s == 0 ? kBuf1 : s == 1 ? kBuf2 : kBuf3;
-            const uint64_t w0 = pos[s] >> 6, w1 = (pos[s] + tot[s] + 63) >> 6;
-            fit[s] = w1 - w0 + 1 <= cap;
-            if (fit[s]) {
-                for (uint64_t i = threadIdx.x; i < cap; i += kPackThreads) buf[i] = i ? 0 : carry[s];
-            } else if (threadIdx.x == 0 && carry[s]) {
-                atomicOr((unsigned long long *)&out[w0], (unsigned long long)bswap64(carry[s]));
-            }
-        }
-        __syncthreads();
-        uint64_t at[3] = {pos[0] + ex[0], pos[1] + ex[1], pos[2] + ex[2]};
-        const uint64_t base[3] = {(pos[0] >> 6) << 6, (pos[1] >> 6) << 6, (pos[2] >> 6) << 6};
-#pragma unroll
-        for (int j = 0; j < kPackPer; j++) {
-            const uint64_t i = t0 + threadIdx.x * kPackPer + j;
-            if (i >= end) continue;
-            const uint64_t w = r[j], flag = w >> 56;
-            Code c[3];
-            int ns = 0;
-            c[2] = rice_code(flag, P.p3);
-            const bool lng = (flag & 2) == 0;
-            if (lng) {
-                c[0] = mb_code(w & 0xFFFFFFFFULL, P.l1, P.lim1);
-                c[1] = rice_code((w >> 32) & 0xFFFFFFULL, P.p2);
-            }
-            ns = lng ? 0 : 2;
-            for (int s = ns; s < 3; s++) {
-                if (fit[s]) or_bits_lds(s == 0 ? buf1 : s == 1 ? buf2 : buf3, at[s] + c[s].skip - base[s], c[s].v,
-                                        c[s].nb);
-                else or_bits_hbm(s == 0 ? out1 : s == 1 ? out2 : out3, at[s] + c[s].skip, c[s].v, c[s].nb);
-                at[s] += c[s].len;
-            }
-        }
-        __syncthreads();
-        for (int s = 0; s < 3; s++) {
-            uint64_t *out = s == 0 ? out1 : s == 1 ? out2 : out3;
-            if (fit[s]) flush_tile(s == 0 ? buf1 : s == 1 ? buf2 : buf3, pos[s], pos[s] + tot[s], last, out, &carry[s]);
-            else flush_tile_hbm(pos[s] + tot[s], last, out, &carry[s]);
-            pos[s] += tot[s];
-        }
+    } else {
+        const uint64_t *ch = chunks + chunk_base(stats[g.block].rec_begin, g.block);
+        for (uint64_t i = g.first + threadIdx.x; i < g.first + g.count; i += kPackThreads)
+            v[0] += mb_code(ch[i], P.l4, P.lim4).len;
     }
-    // s4: minimal binary over the block's chunks, 2 chunks per thread per tile, in buf1
-    const uint64_t *ch = chunks + chunk_base(beg, b);
-    const uint64_t nch = (S.T + 30) / 31;
-    uint64_t p4 = 0;
-    for (uint64_t t0 = 0; t0 < nch; t0 += kS4Tile) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int k = 0; k < 3; k++) v[k] = wave_sum(v[k]);
+    if (lane == 0)
+        for (int k = 0; k < 3; k++) rs[wid][k] = v[k];
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        uint64_t t = 0;
+        for (int w = 0; w < kPackThreads / 64; w++) t += rs[w][threadIdx.x];
+        seg_bits[3 * blockIdx.x + threadIdx.x] = t;
+    }
+}
+
+// pass 2b: per block, each segment's first bit in each stream and the streams' totals
+__global__ void __launch_bounds__(256) k_pack_segscan(const PackParams *params, const PackSeg *segs,
+                                                      uint64_t n_blocks, const uint64_t *seg_bits,
+                                                      uint64_t *seg_start, uint64_t *bits_out) {
+    const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (b >= n_blocks) return;
+    const PackParams P = params[b];
+    uint64_t pos[4] = {0, 0, 0, 0};
+    if (!P.skip)
+        for (uint32_t j = P.seg0; j < P.seg0 + P.nseg; j++) {
+            if (segs[j].kind == 0) {
+                for (int k = 0; k < 3; k++) {
+                    seg_start[3 * j + k] = pos[k];
+                    pos[k] += seg_bits[3 * j + k];
+                }
+            } else {
+                seg_start[3 * j] = pos[3];
+                pos[3] += seg_bits[3 * j];
+            }
+        }
+    for (int k = 0; k < 4; k++) bits_out[b * 4 + k] = pos[k];
+}
+
+// Store the words [w0, wend) of a tile's LDS buffer (big-endian); the segment's first and last
+// words may hold bits of the neighbouring segments' workgroups: OR-ed into the zeroed payload
+__device__ __forceinline__ void store_words(const uint64_t *buf, uint64_t w0, uint64_t wend, uint64_t first_w,
+                                            uint64_t last_w, uint64_t *out) {
+    for (uint64_t i = w0 + threadIdx.x; i < wend; i += kPackThreads) {
+        const uint64_t x = bswap64(buf[i - w0]);
+        if (i == first_w || i == last_w) atomicOr((unsigned long long *)&out[i], (unsigned long long)x);
+        else out[i] = x;
+    }
+}
+
+// One stream's tile within a segment: codes already OR-ed into buf (buf[0] held the carry
+// word of the previous tile); [bit0, bit1) is the tile's span in the stream.  Stores the
+// complete words, keeps the partial last one in carry (or stores it too at the segment end).
+__device__ void flush_seg_tile(uint64_t *buf, uint64_t bit0, uint64_t bit1, bool last, uint64_t first_w,
+                               uint64_t last_w, uint64_t *out, uint64_t *carry) {
+    const uint64_t w0 = bit0 >> 6;
+    const uint64_t wend = last ? (bit1 + 63) >> 6 : bit1 >> 6;  // words to store: [w0, wend)
+    store_words(buf, w0, wend, first_w, last_w, out);
+    __syncthreads();
+    if (threadIdx.x == 0) *carry = (!last && (bit1 & 63)) ? buf[(bit1 >> 6) - w0] : 0;
+    __syncthreads();
+}
+
+// pass 2c: one workgroup per segment (a block's records in kPackSegRecs pieces, then its s4
+// chunks in kPackSegChunks pieces), all in parallel: tiles of the segment in order, codes into
+// LDS word buffers at the bit positions a block scan gives, complete words stored once.  (One
+// workgroup per block walked all 60-odd tiles of a C91 block in order: 2.1 ms per 4-block call
+// of the encode pipeline, where 64 workgroups now share it.)
+__global__ void __launch_bounds__(kPackThreads) k_pack_write(const uint64_t *recs, const uint64_t *chunks,
+                                                             const PackStats *stats, const PackParams *params,
+                                                             const PackSeg *segs, const uint64_t *seg_bits,
+                                                             const uint64_t *seg_start, uint64_t *payload) {
+    __shared__ uint64_t buf1[kBuf1], buf2[kBuf2], buf3[kBuf3];
+    __shared__ uint64_t sh[64];
+    __shared__ uint64_t carry[4];
+    const uint64_t sg = blockIdx.x;
+    const PackSeg g = segs[sg];
+    const PackParams P = params[g.block];
+    if (threadIdx.x < 4) carry[threadIdx.x] = 0;
+    __syncthreads();
+    if (g.kind == 0) {
+        uint64_t *out[3] = {payload + P.off[0], payload + P.off[1], payload + P.off[2]};
+        uint64_t pos[3], first_w[3], last_w[3];  // the same in every thread
+        for (int s = 0; s < 3; s++) {
+            pos[s] = seg_start[3 * sg + s];
+            const uint64_t e = pos[s] + seg_bits[3 * sg + s];
+            first_w[s] = pos[s] >> 6;
+            last_w[s] = e ? (e - 1) >> 6 : 0;
+        }
+        const uint64_t beg = g.first, end = g.first + g.count;
+        for (uint64_t t0 = beg; t0 < end; t0 += kPackTile) {
+            uint64_t r[kPackPer];
+            load_tile(recs, t0 + threadIdx.x * kPackPer, end, r);
+            uint64_t v[3] = {0, 0, 0};
+#pragma unroll
+            for (int j = 0; j < kPackPer; j++) {
+                const uint64_t i = t0 + threadIdx.x * kPackPer + j;
+                if (i >= end) continue;
+                const uint64_t w = r[j], flag = w >> 56;
+                v[2] += rice_code(flag, P.p3).len;
+                if ((flag & 2) == 0) {
+                    v[0] += mb_code(w & 0xFFFFFFFFULL, P.l1, P.lim1).len;
+                    v[1] += rice_code((w >> 32) & 0xFFFFFFULL, P.p2).len;
+                }
+            }
+            uint64_t ex[3], tot[3];
+            block_scan3(v, ex, tot, sh);
+            const bool last = t0 + kPackTile >= end;
+            // spans in words of each stream's LDS buffer: fits?  (uniform across the workgroup)
+            bool fit[3];
+            for (int s = 0; s < 3; s++) {
+                uint64_t *buf = s == 0 ? buf1 : s == 1 ? buf2 : buf3;
+                const uint64_t cap = s == 0 ? kBuf1 : s == 1 ? kBuf2 : kBuf3;
+                const uint64_t w0 = pos[s] >> 6, w1 = (pos[s] + tot[s] + 63) >> 6;
+                fit[s] = w1 - w0 + 1 <= cap;
+                if (fit[s]) {
+                    for (uint64_t i = threadIdx.x; i < cap; i += kPackThreads) buf[i] = i ? 0 : carry[s];
+                } else if (threadIdx.x == 0 && carry[s]) {
+                    atomicOr((unsigned long long *)&out[s][w0], (unsigned long long)bswap64(carry[s]));
+                }
+            }
+            __syncthreads();
+            uint64_t at[3] = {pos[0] + ex[0], pos[1] + ex[1], pos[2] + ex[2]};
+            const uint64_t base[3] = {(pos[0] >> 6) << 6, (pos[1] >> 6) << 6, (pos[2] >> 6) << 6};
+#pragma unroll
+            for (int j = 0; j < kPackPer; j++) {
+                const uint64_t i = t0 + threadIdx.x * kPackPer + j;
+                if (i >= end) continue;
+                const uint64_t w = r[j], flag = w >> 56;
+                Code c[3];
+                c[2] = rice_code(flag, P.p3);
+                const bool lng = (flag & 2) == 0;
+                if (lng) {
+                    c[0] = mb_code(w & 0xFFFFFFFFULL, P.l1, P.lim1);
+                    c[1] = rice_code((w >> 32) & 0xFFFFFFULL, P.p2);
+                }
+                for (int s = lng ? 0 : 2; s < 3; s++) {
+                    if (fit[s]) or_bits_lds(s == 0 ? buf1 : s == 1 ? buf2 : buf3, at[s] + c[s].skip - base[s], c[s].v,
+                                            c[s].nb);
+                    else or_bits_hbm(out[s], at[s] + c[s].skip, c[s].v, c[s].nb);
+                    at[s] += c[s].len;
+                }
+            }
+            __syncthreads();
+            for (int s = 0; s < 3; s++) {
+                if (fit[s])
+                    flush_seg_tile(s == 0 ? buf1 : s == 1 ? buf2 : buf3, pos[s], pos[s] + tot[s], last, first_w[s],
+                                   last_w[s], out[s], &carry[s]);
+                else
+                    flush_tile_hbm(pos[s] + tot[s], last, out[s], &carry[s]);
+                pos[s] += tot[s];
+            }
+        }
+        return;
+    }
+    // s4: minimal binary over the segment's chunks, 2 chunks per thread per tile, in buf1
+    uint64_t *out4 = payload + P.off[3];
+    const uint64_t *ch = chunks + chunk_base(stats[g.block].rec_begin, g.block);
+    uint64_t p4 = seg_start[3 * sg];
+    const uint64_t e4 = p4 + seg_bits[3 * sg], first_w = p4 >> 6, last_w = e4 ? (e4 - 1) >> 6 : 0;
+    const uint64_t c0 = g.first, c1 = g.first + g.count;
+    for (uint64_t t0 = c0; t0 < c1; t0 += kS4Tile) {
         uint64_t x[kS4Per];
         uint64_t v[3] = {0, 0, 0};
 #pragma unroll
         for (int j = 0; j < kS4Per; j++) {
             const uint64_t i = t0 + threadIdx.x * kS4Per + j;
-            x[j] = i < nch ? ch[i] : 0;
-            if (i < nch) v[0] += mb_code(x[j], P.l4, P.lim4).len;
+            x[j] = i < c1 ? ch[i] : 0;
+            if (i < c1) v[0] += mb_code(x[j], P.l4, P.lim4).len;
         }
         uint64_t ex[3], tot[3];
         block_scan3(v, ex, tot, sh);
-        const bool last = t0 + kS4Tile >= nch;
+        const bool last = t0 + kS4Tile >= c1;
         for (uint64_t i = threadIdx.x; i < (uint64_t)kBuf1; i += kPackThreads) buf1[i] = i ? 0 : carry[3];
         __syncthreads();
         uint64_t at = p4 + ex[0];
@@ -380,20 +468,14 @@ __global__ void __launch_bounds__(kPackThreads) k_pack_write(const uint64_t *rec
 #pragma unroll
         for (int j = 0; j < kS4Per; j++) {
             const uint64_t i = t0 + threadIdx.x * kS4Per + j;
-            if (i >= nch) continue;
+            if (i >= c1) continue;
             const Code c = mb_code(x[j], P.l4, P.lim4);
             or_bits_lds(buf1, at - base, c.v, c.nb);
             at += c.len;
         }
         __syncthreads();
-        flush_tile(buf1, p4, p4 + tot[0], last, out4, &carry[3]);
+        flush_seg_tile(buf1, p4, p4 + tot[0], last, first_w, last_w, out4, &carry[3]);
         p4 += tot[0];
-    }
-    if (threadIdx.x == 0) {
-        bits_out[b * 4 + 0] = pos[0];
-        bits_out[b * 4 + 1] = pos[1];
-        bits_out[b * 4 + 2] = pos[2];
-        bits_out[b * 4 + 3] = p4;
     }
 }
 
@@ -406,10 +488,17 @@ void launch_pack_stats(const uint64_t *recs, const uint64_t *roffs, uint64_t n_r
 }
 
 void launch_pack_write(const uint64_t *recs, const uint64_t *chunks, const PackStats *stats,
-                       const PackParams *params, uint64_t n_blocks, uint64_t *payload, uint64_t *bits_out,
+                       const PackParams *params, uint64_t n_blocks, const PackSeg *segs, uint64_t n_segs,
+                       uint64_t *seg_bits, uint64_t *seg_start, uint64_t *payload, uint64_t *bits_out,
                        hipStream_t s) {
-    hipLaunchKernelGGL(k_pack_write, dim3((uint32_t)n_blocks), dim3(kPackThreads), 0, s, recs, chunks, stats, params,
-                       payload, bits_out);
+    if (n_segs)
+        hipLaunchKernelGGL(k_pack_seglen, dim3((uint32_t)n_segs), dim3(kPackThreads), 0, s, recs, chunks, stats,
+                           params, segs, seg_bits);
+    hipLaunchKernelGGL(k_pack_segscan, dim3((uint32_t)((n_blocks + 255) / 256)), dim3(256), 0, s, params, segs,
+                       n_blocks, (const uint64_t *)seg_bits, seg_start, bits_out);
+    if (n_segs)
+        hipLaunchKernelGGL(k_pack_write, dim3((uint32_t)n_segs), dim3(kPackThreads), 0, s, recs, chunks, stats,
+                           params, segs, (const uint64_t *)seg_bits, (const uint64_t *)seg_start, payload);
 }
 
 }  // namespace ntc
