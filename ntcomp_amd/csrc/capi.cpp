@@ -432,14 +432,17 @@ int pack_blocks_impl(ntc_ctx *ctx, const uint64_t *d_recs, const uint64_t *d_rof
     int rc;
     // chunks of block b at rec_begin + rec_begin / 31 + 2 b (pack.hip chunk_base: room for
     // 32 bases in every short record)
-    if ((rc = ensure(ctx, WS_PACK_CHUNKS, (ends[1] + ends[1] / 31 + 2 * n_blocks + 2) * 8, &d_chunks))) return rc;
-    const uint64_t meta_bytes = n_blocks * (sizeof(PackStats) + sizeof(PackParams) + 32);
+    const uint64_t chunk_words = ends[1] + ends[1] / 31 + 2 * n_blocks + 2;
+    if ((rc = ensure(ctx, WS_PACK_CHUNKS, chunk_words * 8, &d_chunks))) return rc;
+    const uint64_t meta_bytes = n_blocks * (sizeof(PackStats) + sizeof(PackParams) + 32) +
+                                pack_stats_scratch_words(n_blocks, block_reads) * 8;
     if ((rc = ensure(ctx, WS_PACK_META, meta_bytes, &d_meta))) return rc;
     PackStats *d_stats = (PackStats *)d_meta;
     PackParams *d_params = (PackParams *)(d_stats + n_blocks);
     uint64_t *d_bits = (uint64_t *)(d_params + n_blocks);
     HIP_TRY(ctx, hipEventRecord(ctx->pack_ev[0], ctx->stream));
-    launch_pack_stats(d_recs, d_roffs, n_reads, block_reads, n_blocks, (uint64_t *)d_chunks, d_stats, ctx->stream);
+    launch_pack_stats(d_recs, d_roffs, n_reads, block_reads, n_blocks, (uint64_t *)d_chunks, chunk_words,
+                      d_bits + 4 * n_blocks, d_stats, ctx->stream);
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipEventRecord(ctx->pack_ev[1], ctx->stream));
     std::vector<PackStats> st(n_blocks);

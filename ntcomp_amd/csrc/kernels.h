@@ -135,8 +135,12 @@ struct PackSeg {
     uint64_t first, count;
 };
 constexpr uint64_t kPackSegRecs = 16384, kPackSegChunks = 16384;
+// pass 1 (stream totals + s4 chunks) in segments of 4096 reads: chunks (chunk_words words,
+// zeroed here) as pack.hip chunk_base lays them out, scratch: pack_stats_scratch_words()
+uint64_t pack_stats_scratch_words(uint64_t n_blocks, uint32_t block_reads);
 void launch_pack_stats(const uint64_t *recs, const uint64_t *roffs, uint64_t n_reads, uint32_t block_reads,
-                       uint64_t n_blocks, uint64_t *chunks, PackStats *stats, hipStream_t s);
+                       uint64_t n_blocks, uint64_t *chunks, uint64_t chunk_words, uint64_t *scratch,
+                       PackStats *stats, hipStream_t s);
 // pass 2 over n_segs segments: their code lengths, each block's segment offsets (seg_bits /
 // seg_start: 3 words per segment), then every segment's codes in parallel
 void launch_pack_write(const uint64_t *recs, const uint64_t *chunks, const PackStats *stats,

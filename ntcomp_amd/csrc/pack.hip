@@ -152,17 +152,103 @@ __device__ void flush_tile_hbm(uint64_t bit1, bool last, uint64_t *out, uint64_t
     __syncthreads();
 }
 
-__global__ void __launch_bounds__(kPackThreads) k_pack_stats(const uint64_t *recs, const uint64_t *roffs,
-                                                             uint64_t n_reads, uint32_t block_reads,
-                                                             uint64_t *chunks, PackStats *stats) {
+// Pass 1 in segments of kPackSegReads reads (a block's reads in order), each its own
+// workgroup.  Segment sg of block b = sg / spb (spb = segments per block) covers reads
+// [b * block_reads + (sg % spb) * kPackSegReads, ...) within the block; the last block's
+// trailing segments may be empty.
+constexpr uint64_t kPackSegReads = 4096;
+struct SegRange {
+    uint64_t b, r0, r1;
+};
+__device__ __forceinline__ SegRange seg_range(uint64_t sg, uint64_t spb, uint32_t block_reads, uint64_t n_reads) {
+    SegRange g;
+    g.b = sg / spb;
+    const uint64_t bend = g.b * block_reads + block_reads < n_reads ? g.b * block_reads + block_reads : n_reads;
+    g.r0 = g.b * block_reads + (sg % spb) * kPackSegReads;
+    g.r1 = g.r0 + kPackSegReads < bend ? g.r0 + kPackSegReads : bend;
+    if (g.r0 > g.r1) g.r0 = g.r1;
+    return g;
+}
+// per-segment words of the scratch: n_long, max1, sum2, sum3, short bases, bad, first short base
+constexpr int kSegStat = 8;
+
+// 1a: a segment's stream totals
+__global__ void __launch_bounds__(kPackThreads) k_pstat_seg(const uint64_t *recs, const uint64_t *roffs,
+                                                            uint64_t n_reads, uint32_t block_reads, uint64_t spb,
+                                                            uint64_t *seg) {
+    const SegRange g = seg_range(blockIdx.x, spb, block_reads, n_reads);
+    const uint64_t beg = roffs[g.r0], end = roffs[g.r1];
+    uint64_t n_long = 0, max1 = 0, sum2 = 0, sum3 = 0, nb = 0, bad = 0;
+    for (uint64_t i = beg + threadIdx.x; i < end; i += kPackThreads) {
+        const uint64_t w = recs[i], flag = w >> 56;
+        sum3 += flag;
+        if ((flag & 2) == 0) {
+            n_long++;
+            const uint64_t c = w & 0xFFFFFFFFULL;
+            max1 = c > max1 ? c : max1;
+            sum2 += (w >> 32) & 0xFFFFFFULL;
+        } else {
+            const uint64_t len = flag >> 2;
+            if (len > 32) bad = 1;  // from_2bit panics past 32 bases (encode.rs:220)
+            else nb += len;
+        }
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint64_t red[6] = {wave_sum(n_long), wave_max(max1), wave_sum(sum2), wave_sum(sum3), wave_sum(nb), wave_max(bad)};
+    __shared__ uint64_t rs[16][6];
+    if (lane == 0)
+        for (int k = 0; k < 6; k++) rs[wid][k] = red[k];
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const int k = threadIdx.x;
+        uint64_t t = 0;
+        for (int w = 0; w < kPackThreads / 64; w++) t = (k == 1 || k == 5) ? (rs[w][k] > t ? rs[w][k] : t) : t + rs[w][k];
+        seg[blockIdx.x * kSegStat + k] = t;
+    }
+}
+
+// 1b: per block (one thread each), the segments combined and each segment's first short base
+__global__ void __launch_bounds__(256) k_pstat_block(const uint64_t *roffs, uint64_t n_reads, uint32_t block_reads,
+                                                     uint64_t n_blocks, uint64_t spb, uint64_t *seg,
+                                                     PackStats *stats) {
+    const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (b >= n_blocks) return;
+    const uint64_t r0 = b * block_reads, r1 = r0 + block_reads < n_reads ? r0 + block_reads : n_reads;
+    PackStats S{};
+    uint64_t T = 0;
+    for (uint64_t j = b * spb; j < (b + 1) * spb; j++) {
+        uint64_t *x = seg + j * kSegStat;
+        S.n_long += x[0];
+        S.max1 = x[1] > S.max1 ? x[1] : S.max1;
+        S.sum2 += x[2];
+        S.sum3 += x[3];
+        S.bad |= x[5];
+        x[6] = T;
+        T += x[4];
+    }
+    S.rec_begin = roffs[r0];
+    S.n_recs = roffs[r1] - roffs[r0];
+    S.T = T;
+    stats[b] = S;
+}
+
+// 1c: a segment's s4 chunks -- a block scan gives every short record its base position, its
+// 2-bit bases are OR-ed into an LDS chunk buffer, finished chunks go out; the segment's first
+// and last chunks, shared with the neighbouring segments, are OR-ed into the zeroed array
+__global__ void __launch_bounds__(kPackThreads) k_pstat_chunks(const uint64_t *recs, const uint64_t *roffs,
+                                                               uint64_t n_reads, uint32_t block_reads, uint64_t spb,
+                                                               const uint64_t *seg, const PackStats *stats,
+                                                               uint64_t *chunks) {
     __shared__ uint64_t cbuf[kChunkBufWords];
     __shared__ uint64_t sh[64];
-    const uint64_t b = blockIdx.x;
-    const uint64_t r0 = b * block_reads, r1 = r0 + block_reads < n_reads ? r0 + block_reads : n_reads;
-    const uint64_t beg = roffs[r0], end = roffs[r1];
-    uint64_t *ch = chunks + chunk_base(beg, b);  // block b's chunks (up to 32 bases per short record)
-    uint64_t n_long = 0, max1 = 0, sum2 = 0, sum3 = 0, max4 = 0, bad = 0;
-    uint64_t T = 0;  // short bases so far
+    const uint64_t sg = blockIdx.x;
+    const uint64_t nbs = seg[sg * kSegStat + 4];
+    if (nbs == 0) return;  // no short base in this segment
+    const SegRange g = seg_range(sg, spb, block_reads, n_reads);
+    const uint64_t beg = roffs[g.r0], end = roffs[g.r1];
+    uint64_t *ch = chunks + chunk_base(stats[g.b].rec_begin, g.b);  // block b's chunks
+    uint64_t T = seg[sg * kSegStat + 6];                              // the segment's first short base
+    const uint64_t first_c = T / 31, last_c = (T + nbs - 1) / 31;
     for (uint64_t i = threadIdx.x; i < kChunkBufWords; i += kPackThreads) cbuf[i] = 0;
     __syncthreads();
     for (uint64_t t0 = beg; t0 < end; t0 += kPackTile) {
@@ -171,20 +257,8 @@ __global__ void __launch_bounds__(kPackThreads) k_pack_stats(const uint64_t *rec
         uint64_t nb = 0;
 #pragma unroll
         for (int j = 0; j < kPackPer; j++) {
-            const uint64_t i = t0 + threadIdx.x * kPackPer + j;
-            if (i >= end) continue;
-            const uint64_t w = r[j], flag = w >> 56;
-            sum3 += flag;
-            if ((flag & 2) == 0) {
-                n_long++;
-                const uint64_t c = w & 0xFFFFFFFFULL;
-                max1 = c > max1 ? c : max1;
-                sum2 += (w >> 32) & 0xFFFFFFULL;
-            } else {
-                const uint64_t len = flag >> 2;
-                if (len > 32) bad = 1;  // from_2bit panics past 32 bases (encode.rs:220)
-                else nb += len;
-            }
+            const uint64_t i = t0 + threadIdx.x * kPackPer + j, flag = r[j] >> 56;
+            if (i < end && (flag & 2) && (flag >> 2) <= 32) nb += flag >> 2;
         }
         uint64_t v[3] = {nb, 0, 0}, ex[3], tot[3];
         block_scan3(v, ex, tot, sh);
@@ -210,12 +284,12 @@ __global__ void __launch_bounds__(kPackThreads) k_pack_stats(const uint64_t *rec
         __syncthreads();
         const uint64_t T1 = T + tot[0];
         const bool last = t0 + kPackTile >= end;
-        // finished chunks: [c0, T1 / 31), plus the partial last one at the end of the block
+        // finished chunks: [c0, T1 / 31), plus the partial last one at the end of the segment
         const uint64_t cend = last ? (T1 + 30) / 31 : T1 / 31;
         for (uint64_t c = c0 + threadIdx.x; c < cend; c += kPackThreads) {
             const uint64_t x = cbuf[c - c0];
-            ch[c] = x;
-            max4 = x > max4 ? x : max4;
+            if (c == first_c || c == last_c) atomicOr((unsigned long long *)&ch[c], (unsigned long long)x);
+            else ch[c] = x;
         }
         __syncthreads();
         // carry the unfinished chunk to slot 0, clear the rest
@@ -225,28 +299,23 @@ __global__ void __launch_bounds__(kPackThreads) k_pack_stats(const uint64_t *rec
         __syncthreads();
         T = T1;
     }
-    // block reductions
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint64_t red[6] = {wave_sum(n_long), wave_max(max1), wave_sum(sum2), wave_sum(sum3), wave_max(max4),
-                       wave_max(bad)};
-    __shared__ uint64_t rs[16][6];
-    if (lane == 0)
-        for (int k = 0; k < 6; k++) rs[wid][k] = red[k];
+}
+
+// 1d: per block, the largest s4 chunk (after every segment's chunks are in)
+__global__ void __launch_bounds__(kPackThreads) k_pstat_max4(const uint64_t *chunks, PackStats *stats) {
+    const uint64_t b = blockIdx.x;
+    const PackStats S = stats[b];
+    const uint64_t *ch = chunks + chunk_base(S.rec_begin, b);
+    const uint64_t nch = (S.T + 30) / 31;
+    uint64_t m = 0;
+    for (uint64_t c = threadIdx.x; c < nch; c += kPackThreads) m = ch[c] > m ? ch[c] : m;
+    m = wave_max(m);
+    __shared__ uint64_t rs[16];
+    if ((threadIdx.x & 63) == 0) rs[threadIdx.x >> 6] = m;
     __syncthreads();
     if (threadIdx.x == 0) {
-        PackStats s{};
-        for (int w = 0; w < kPackThreads / 64; w++) {
-            s.n_long += rs[w][0];
-            s.max1 = rs[w][1] > s.max1 ? rs[w][1] : s.max1;
-            s.sum2 += rs[w][2];
-            s.sum3 += rs[w][3];
-            s.max4 = rs[w][4] > s.max4 ? rs[w][4] : s.max4;
-            s.bad |= rs[w][5];
-        }
-        s.n_recs = end - beg;
-        s.T = T;
-        s.rec_begin = beg;
-        stats[b] = s;
+        for (int w = 0; w < kPackThreads / 64; w++) m = rs[w] > m ? rs[w] : m;
+        stats[b].max4 = m;
     }
 }
 
@@ -481,10 +550,24 @@ __global__ void __launch_bounds__(kPackThreads) k_pack_write(const uint64_t *rec
 
 }  // namespace
 
+uint64_t pack_stats_scratch_words(uint64_t n_blocks, uint32_t block_reads) {
+    return n_blocks * ((block_reads + kPackSegReads - 1) / kPackSegReads) * kSegStat + 8;
+}
+
 void launch_pack_stats(const uint64_t *recs, const uint64_t *roffs, uint64_t n_reads, uint32_t block_reads,
-                       uint64_t n_blocks, uint64_t *chunks, PackStats *stats, hipStream_t s) {
-    hipLaunchKernelGGL(k_pack_stats, dim3((uint32_t)n_blocks), dim3(kPackThreads), 0, s, recs, roffs, n_reads,
-                       block_reads, chunks, stats);
+                       uint64_t n_blocks, uint64_t *chunks, uint64_t chunk_words, uint64_t *scratch,
+                       PackStats *stats, hipStream_t s) {
+    if (!n_blocks) return;
+    const uint64_t spb = (block_reads + kPackSegReads - 1) / kPackSegReads, n_segs = n_blocks * spb;
+    (void)hipMemsetAsync(chunks, 0, chunk_words * 8, s);  // shared chunks are OR-ed in
+    hipLaunchKernelGGL(k_pstat_seg, dim3((uint32_t)n_segs), dim3(kPackThreads), 0, s, recs, roffs, n_reads,
+                       block_reads, spb, scratch);
+    hipLaunchKernelGGL(k_pstat_block, dim3((uint32_t)((n_blocks + 255) / 256)), dim3(256), 0, s, roffs, n_reads,
+                       block_reads, n_blocks, spb, scratch, stats);
+    hipLaunchKernelGGL(k_pstat_chunks, dim3((uint32_t)n_segs), dim3(kPackThreads), 0, s, recs, roffs, n_reads,
+                       block_reads, spb, (const uint64_t *)scratch, (const PackStats *)stats, chunks);
+    hipLaunchKernelGGL(k_pstat_max4, dim3((uint32_t)n_blocks), dim3(kPackThreads), 0, s, (const uint64_t *)chunks,
+                       stats);
 }
 
 void launch_pack_write(const uint64_t *recs, const uint64_t *chunks, const PackStats *stats,
