@@ -382,6 +382,12 @@ class GpuContext:
         self._check(self.L.ntc_index_upload(self.h, ctypes.byref(index.view)), "ntc_index_upload")
         return self
 
+    def upload_prepared(self, prep):
+        """Upload an IndexPrep (ntc_index_prepare's host tables, built once for any number of
+        contexts / devices): ntc_index_upload_prepared."""
+        self._check(self.L.ntc_index_upload_prepared(self.h, prep.h), "ntc_index_upload_prepared")
+        return self
+
     def share_index(self, other):
         """Use other's device index (same GPU, ntc_index_share): no second upload or copy."""
         self._check(self.L.ntc_index_share(self.h, other.h), "ntc_index_share")
@@ -657,6 +663,30 @@ def pack_block(records, num_records):
         return meta, (ctypes.string_at(out.value, n.value) if out.value else b"")
     finally:
         lib().ntc_buffer_free(out)
+
+
+class IndexPrep:
+    """The host half of an upload (ntc_index_prepare): the index's derived tables, built
+    without a GPU -- e.g. while contexts are created -- and uploaded to each context with
+    GpuContext.upload_prepared."""
+
+    def __init__(self, index):
+        self.h = ctypes.c_void_p()
+        self._index = index  # the view's arrays stay alive
+        rc = lib().ntc_index_prepare(ctypes.byref(index.view), ctypes.byref(self.h))
+        if rc:
+            raise NtcError(rc, "ntc_index_prepare")
+
+    def close(self):
+        if self.h:
+            lib().ntc_index_prep_free(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def stream_payloads(meta, payload):

@@ -50,3 +50,16 @@ def test_synth_is_deterministic_and_shardable():
     a = nt.synth_reads(g, 2, 0, 100, 150, 10_000, threads=3)
     b = nt.synth_reads(g, 2, 40, 60, 150, 10_000, threads=1)
     assert np.array_equal(a.reshape(100, 150)[40:], b.reshape(60, 150))
+
+
+def test_index_prepare_needs_no_gpu():
+    """ntc_index_prepare (the host half of an upload) runs without a GPU and rejects a null
+    view; ntc_index_upload_prepared fails loudly without a context."""
+    g = nt.synth_genome(3, 50_000)
+    ix = nt.Index.build([g.tobytes()], 31)
+    p = nt.IndexPrep(ix)
+    assert p.h
+    p.close()
+    out = ctypes.c_void_p()
+    assert nt.lib().ntc_index_prepare(None, ctypes.byref(out)) == 1
+    assert nt.lib().ntc_index_upload_prepared(None, None) == 1

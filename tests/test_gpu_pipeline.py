@@ -264,3 +264,26 @@ def test_contexts_share_one_index(setup, tmp_path):
                  "--deflate", "zlib", stdout=f)
         outs[c] = (tmp_path / f"{c}.dat").read_bytes()
     assert outs[1] == outs[2]
+
+
+def test_prepared_upload_equals_upload(setup):
+    """ntc_index_prepare + ntc_index_upload_prepared (the native CLI derives the host tables
+    while HIP starts): the same device index as ntc_index_upload -- same sizes, same records,
+    exact round trip -- and one prepared index serves several contexts."""
+    d, genome, ix = setup
+    reads = nt.synth_reads(genome, 43, 0, 20_000, 150, 10_000)
+    offs = np.arange(0, len(reads) + 1, 150, dtype=np.uint64)
+    a = nt.GpuContext(0).upload(ix)
+    prep = nt.IndexPrep(ix)
+    b = nt.GpuContext(0).upload_prepared(prep)
+    c = nt.GpuContext(0).upload_prepared(prep)
+    prep.close()
+    assert a.index_info() == b.index_info() == c.index_info()
+    ra, oa = a.encode(reads, offs)
+    for x in (b, c):
+        r, o = x.encode(reads, offs)
+        assert np.array_equal(r, ra) and np.array_equal(o, oa)
+        out, _ = x.decode(r)
+        assert np.array_equal(out, reads)
+    for x in (a, b, c):
+        x.close()
