@@ -728,6 +728,14 @@ int upload_prepared(ntc_ctx *ctx, const ntc_index_prep &prep) {
                                   std::chrono::steady_clock::now() - t_start).count();
     };
     ctx->upload_host_us = prep.host_us;
+    // NTC_UPLOAD_TRACE=1: seconds since the start of the device half at each stage (stderr)
+    static const bool trace = std::getenv("NTC_UPLOAD_TRACE") != nullptr;
+    auto mark = [&](const char *what, bool sync) {
+        if (!trace) return;
+        if (sync) (void)hipStreamSynchronize(ctx->stream);
+        std::fprintf(stderr, "[upload] %-28s %.4f s\n", what,
+                     std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count());
+    };
     // free a previous index
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     ctx->index_mem = std::make_shared<IndexMem>(ctx->device);  // the previous one goes with its last holder
@@ -756,9 +764,11 @@ int upload_prepared(ntc_ctx *ctx, const ntc_index_prep &prep) {
     HIP_TRY(ctx, hipMemcpy(d_uniq, dv.uniq.data(), dv.uniq.size() * 4, hipMemcpyHostToDevice));
     HIP_TRY(ctx, hipMemcpy(d_pred, dv.pred.data(), n * 4, hipMemcpyHostToDevice));
     HIP_TRY(ctx, hipMemcpy(d_code, dv.code.data(), n, hipMemcpyHostToDevice));
+    mark("allocations + H2D", false);
     launch_walk_build((const uint32_t *)d_pred, (const uint8_t *)d_code, n, (WalkStep *)d_walk_a,
                       (WalkStep *)d_walk_b, (WalkEntry *)d_walk, ctx->stream);
     HIP_TRY(ctx, hipGetLastError());
+    mark("walk table", true);
     // path cover, built on the device (kernels.hip "path cover"; derived.cpp build_paths is
     // the same cover on the host, for emulation)
     void *d_pstream = nullptr, *d_colex_at = nullptr, *d_pos = nullptr, *d_puniq = nullptr;
@@ -833,6 +843,7 @@ int upload_prepared(ntc_ctx *ctx, const ntc_index_prep &prep) {
         }
         free_tmp();
     }
+    mark("path cover", true);
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     HIP_TRY(ctx, hipFree(d_walk_a));
     HIP_TRY(ctx, hipFree(d_walk_b));
@@ -903,7 +914,9 @@ int upload_prepared(ntc_ctx *ctx, const ntc_index_prep &prep) {
     d.filt_f = F;
     d.tab_u = U;
     d.tab_pos = (has_paths && U >= dv.t_jump && n < (1ULL << 31)) ? 1u : 0u;
+    mark("suffix table allocation", false);
     launch_tab_build(d, U, (uint2 *)d_tab, (uint32_t *)d_bits, F, (uint32_t *)d_fbits, ctx->stream);
+    mark("suffix table", true);
     d.win_w = nullptr;
     // SCAN window words (a (U-3)-mer keyed 32-byte entry answers four positions): two lines
     // answer the eight positions of a SCAN unit.  k_ms4 is bound by its lane loads in the
@@ -945,6 +958,7 @@ int upload_prepared(ntc_ctx *ctx, const ntc_index_prep &prep) {
     ctx->n_paths = n_paths;
     ctx->path_text_len = tlen;
     ctx->has_index = true;
+    mark("done", false);
     ctx->upload_total_us = us_since();
     return NTC_OK;
 }
