@@ -835,9 +835,9 @@ int upload_prepared(ntc_ctx *ctx, const ntc_index_prep &prep) {
             HIP_TRY(ctx, hipMemsetAsync(d_pos, 0xFF, n * 4, ctx->stream));
             launch_path_place(pa, st, prv, (const uint64_t *)d_base, (uint32_t *)d_colex_at, (uint32_t *)d_pos,
                               (uint4 *)d_pstream, (uint64_t *)d_puniq, ctx->stream);
-            if (hx.k >= 4)
+            if (hx.k >= kForkBlockMinK)
                 launch_path_forks(pa, st, (const uint32_t *)d_len, (const uint64_t *)d_base, (const uint32_t *)d_pos,
-                                  (uint32_t *)d_colex_at, ctx->stream);
+                                  (const uint4 *)d_pstream, (uint32_t *)d_colex_at, ctx->stream);
             HIP_TRY(ctx, hipGetLastError());
             has_paths = true;
         }
@@ -865,7 +865,7 @@ int upload_prepared(ntc_ctx *ctx, const ntc_index_prep &prep) {
     d.colex_at = (const uint32_t *)d_colex_at;
     d.pos_of_node = (const uint32_t *)d_pos;
     d.puniq = (const uint64_t *)d_puniq;
-    d.forks = has_paths && hx.k >= 4 ? 1u : 0u;
+    d.forks = has_paths && hx.k >= kForkBlockMinK ? 1u : 0u;
     d.absent = dv.absent;
     // Joint path runs pay off when MS intervals above U hold several nodes for long stretches:
     // genome collections, whose shared regions split the path cover into short unitigs (S91:

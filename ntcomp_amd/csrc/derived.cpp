@@ -299,17 +299,28 @@ void build_paths(const HostIndex &ix, Derived &dv) {
         }
         b += (e - a) + k;  // last node at b+(e-a)-1; positions up to b+(e-a)+k-1 hold no node
     }
-    // Fork words (k >= 4): the k free positions after a path's last node v hold, at
-    // v's position + 1 + c, the path position of the node v[1..k]c (from the labels of v's
-    // (k-1)-suffix group head), or kNoNode.  k_ms4's joint-run build follows a run across
-    // the path end with them (MsLaneT::fork_hop) instead of colex_at + extension + pos_of_node.
-    if (k >= 4) {
+    // Fork blocks (encode_core.h fork_block, k >= kForkBlockMinK): in the k free positions
+    // after a path's last node v, per character c the path position of the node v[1..k]c
+    // (from the labels of v's (k-1)-suffix group head) and the 32 path characters from its
+    // k-mer end.  k_ms4's joint-run build follows a run across the path end with one load
+    // (MsLaneT::hop) instead of colex_at + extension + pos_of_node + the path text.
+    if (k >= kForkBlockMinK) {
         b = 0;
         for (uint64_t p = 0; p < np; p++) {
             const uint64_t a = path_start[p], e = path_start[p + 1];
-            const uint32_t v = order[e - 1];
             const uint64_t pos = b + (e - a) - 1;
-            fork_words(ix, dv, dummy, v, dv.colex_at.data() + pos + 1);
+            uint32_t w[4];
+            fork_words(ix, dv, dummy, order[e - 1], w);
+            uint32_t *blk = dv.colex_at.data() + fork_block(pos + 1);
+            for (int c = 0; c < 4; c++) {
+                uint64_t chars = 0;
+                uint32_t ends = 0;
+                if (w[c] != kNoNode) path_text32(dv.pstream.data(), (uint64_t)w[c] + k - 1, chars, ends);
+                blk[4 * c] = w[c];
+                blk[4 * c + 1] = (uint32_t)chars;
+                blk[4 * c + 2] = (uint32_t)(chars >> 32);
+                blk[4 * c + 3] = ends;
+            }
             b += (e - a) + k;
         }
     }
@@ -371,7 +382,7 @@ DevIndex host_dev_index(const HostIndex &ix, const Derived &dv, const std::vecto
     d.colex_at = dv.colex_at.empty() ? nullptr : dv.colex_at.data();
     d.pos_of_node = dv.pos_of_node.empty() ? nullptr : dv.pos_of_node.data();
     d.puniq = dv.puniq.empty() ? nullptr : dv.puniq.data();
-    d.forks = dv.has_paths && ix.k >= 4 ? 1u : 0u;
+    d.forks = dv.has_paths && ix.k >= kForkBlockMinK ? 1u : 0u;
     d.absent = dv.absent;
     d.tab = nullptr;  // see build_tab_host
     d.tab_u = 0;

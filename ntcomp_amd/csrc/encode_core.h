@@ -127,8 +127,26 @@ struct DevIndex {
     const Rank2Chunk *rank2;      // [4][rank2_blocks(n)] two-character rank chunks, or null
     uint32_t joint;               // 1: encode with joint path runs (k_ms4<true>, MsLaneT)
     const uint32_t *win_w;        // window words of each (U-3)-mer (see win_word), or null
-    uint32_t forks;               // 1: colex_at holds fork words after each path end (derived.cpp)
+    uint32_t forks;               // 1: colex_at holds fork blocks after each path end (fork_block)
 };
+
+// Fork blocks (k >= kForkBlockMinK, derived.cpp build_paths, kernels.hip k_path_forks).  A
+// path's last node at position t - 1 is followed by k free colex_at slots; the 16 from
+// fork_block(t) (16-byte aligned, so each entry is one load inside one line) hold, per
+// character c, the entry {y, the 32 path characters from y's k-mer end (2 bits each), their
+// k-mer end bits} of the node y = v[1..k]c's path position (y = 0xFFFFFFFF: none).  A run
+// that stops at the path end hops to y with one load, and the entry's characters are the
+// first 32 positions of the run from y (MsLaneT::step, the run block).
+constexpr uint32_t kForkBlockMinK = 19;
+NTC_HD uint64_t fork_block(uint64_t t) { return (t + 3) & ~3ull; }
+// 32 path characters from text position T and the k-mer end bits there (pstream groups)
+NTC_HD void path_text32(const uint4 *pstream, uint64_t T, uint64_t &chars, uint32_t &ends) {
+    const uint4 g0 = pstream[T >> 5], g1 = pstream[(T >> 5) + 1];
+    const uint32_t sh = (uint32_t)(T & 31);
+    const uint64_t c0 = (uint64_t)g0.x | ((uint64_t)g0.y << 32), c1 = (uint64_t)g1.x | ((uint64_t)g1.y << 32);
+    chars = sh ? ((c0 >> (2 * sh)) | (c1 << (64 - 2 * sh))) : c0;
+    ends = sh ? ((g0.z >> sh) | (g1.z << (32 - sh))) : g0.z;
+}
 
 // per-read status codes (values of ntc_status)
 enum : int {
@@ -678,6 +696,28 @@ NTC_HD uint32_t path_lim(const uint4 &g0, const uint4 &g1, const uint4 &g2, uint
     return la == 32 ? 32 + lb : la;
 }
 
+// path_lim, and in end whether the k-mer end bit at the stop is clear (a path end) when the
+// stop is inside the 64 positions
+NTC_HD uint32_t path_lim_end(const uint4 &g0, const uint4 &g1, const uint4 &g2, uint32_t sh, uint64_t qa, uint64_t qb,
+                             bool &end) {
+    const uint64_t c0 = (uint64_t)g0.x | ((uint64_t)g0.y << 32);
+    const uint64_t c1 = (uint64_t)g1.x | ((uint64_t)g1.y << 32);
+    const uint64_t c2 = (uint64_t)g2.x | ((uint64_t)g2.y << 32);
+    const uint64_t pa = sh ? ((c0 >> (2 * sh)) | (c1 << (64 - 2 * sh))) : c0;
+    const uint64_t pb = sh ? ((c1 >> (2 * sh)) | (c2 << (64 - 2 * sh))) : c1;
+    const uint32_t va = sh ? ((g0.z >> sh) | (g1.z << (32 - sh))) : g0.z;
+    const uint32_t vb = sh ? ((g1.z >> sh) | (g2.z << (32 - sh))) : g1.z;
+    const uint64_t xa = qa ^ pa, xb = qb ^ pb;
+    uint32_t la = xa ? (uint32_t)(__builtin_ctzll(xa) >> 1) : 32u;
+    const uint32_t ia = ~va ? (uint32_t)__builtin_ctz(~va) : 32u;
+    if (ia < la) la = ia;
+    uint32_t lb = xb ? (uint32_t)(__builtin_ctzll(xb) >> 1) : 32u;
+    const uint32_t ib = ~vb ? (uint32_t)__builtin_ctz(~vb) : 32u;
+    if (ib < lb) lb = ib;
+    end = la < 32 ? la == ia : lb < 32 && lb == ib;
+    return la == 32 ? 32 + lb : la;
+}
+
 struct Entry {       // 16 bytes, one uint4 store
     uint32_t p;      // first position
     uint32_t v;      // SBWT entry: colex start S; run entry: path position of node at p
@@ -1165,52 +1205,6 @@ struct MsLaneT {
         return true;
 #endif
     }
-    // Path position of the node at the next query position on the side whose last covered
-    // node is at path position t - 1, the read's character there being c: the path's next
-    // node when the path goes on with c (a mid-path node's only successor), the fork word
-    // colex_at[t + c] when the path ended at t - 1 (k-mer end bit clear), else none.
-    NTC_HD uint32_t fork_next(const DevIndex &ix, uint32_t t, uint32_t c) const {
-        const uint64_t te = (uint64_t)t + ix.k - 1;  // the k-mer end of path position t
-        NTC_TOUCH(kTrPst, ix.pstream + (te >> 5));
-        const uint4 g = ld4<4>(ix.pstream + (te >> 5));  // the group the run just read (L1/L2)
-        const uint32_t o = (uint32_t)(te & 31);
-        const uint32_t pc = (o < 16 ? g.x >> (2 * o) : g.y >> (2 * (o - 16))) & 3u;
-        if ((g.z >> o) & 1u) return pc == c ? t : 0xFFFFFFFFu;
-        NTC_TOUCH(kTrColex, ix.colex_at + t + c);
-        return ix.colex_at[t + c];
-    }
-    // (joint-run build) A run over m >= 1 positions stopped at p + m < len.  If every side of
-    // the interval goes on with the read's character c there, the extension is the interval
-    // of those next nodes (the first and last node of an interval with edge c extend to the
-    // first and last node of the extension, see note_path) at depth d + m + 1 (capped at k):
-    // a single node (or both sides at one node) or, below k - 1, a joint interval.  The run
-    // then goes on from there as a new run entry (the same (d, S) per position as the SBWT
-    // entry + run of the path through colex_at, EXT and pos_of_node it replaces).
-    NTC_HD bool fork_hop(const DevIndex &ix, const MsBufs &b, uint32_t &m) {
-        const uint32_t k = ix.k;
-        const uint64_t qq = qo + p + m;
-        const uint32_t c = (uint32_t)(b.Q[qq >> 5] >> (2 * (qq & 31))) & 3u;
-        const bool joint = jy() != 0xFFFFFFFFu;
-        // (a next node at path position 0 would make j = nx - 1 the "none" value: left to EXT)
-        const uint32_t nx = fork_next(ix, j + m + 1, c);
-        if (nx == 0xFFFFFFFFu || nx == 0) return false;
-        uint32_t ny = nx;
-        if (joint) {
-            ny = fork_next(ix, jy() + m + 1, c);
-            if (ny == 0xFFFFFFFFu || ny == 0) return false;
-        }
-        const uint32_t d1 = d + m + 1 < k ? d + m + 1 : k;
-        const bool single = ny == nx;
-
-        if (d1 < ix.t_jump || (!single && d1 + 1 >= k)) return false;  // as note_single would decide
-        put_entry(b, p, j + 1, m, (d + 1 < k ? d + 1 : k) | kRunTag);
-        p += m;
-        d = d + m < k ? d + m : k;
-        j = nx - 1;
-        jy() = single ? 0xFFFFFFFFu : ny - 1;
-        m = 0;
-        return true;
-    }
     // after a commit: look for the path position of a single-node interval.  A multi-node
     // interval [l, r) (d < k: strains sharing the read's suffix) starts a JOINT run when both
     // its first and its last node lie on paths: while both paths go on with the query's next
@@ -1281,7 +1275,13 @@ struct MsLaneT {
         }
         if (try_run) {
             try_run = false;
-            uint32_t m = 0, pre = vfy;
+            uint32_t pre = vfy & 0xFFu, m = 0;
+            // (joint-run build) hop pending: the run before stopped inside its window at p - 1
+            // with the read going on, its entry written; j (and jy() for a joint run) is the path
+            // position of the last node it covered on each side, vfy >> 8 = 4 + the read's
+            // character c at p (see the stop below)
+            uint32_t hopc = kJoint ? vfy >> 8 : 0u;
+            bool nohop = false;
             vfy = 0;
             for (;;) {
                 // 64 path characters after node j's k-mer (from pre characters before its end
@@ -1294,15 +1294,39 @@ struct MsLaneT {
                 NTC_TOUCH(kTrQ, Q + ((qo + p + m - pre) >> 5) + 2);
                 const uint4 g0 = ld4<4>(ix.pstream + (T >> 5)), g1 = ld4<4>(ix.pstream + (T >> 5) + 1),
                             g2 = ld4<4>(ix.pstream + (T >> 5) + 2);
+                // a hop loads the fork block entry of c with the path text: one round trip
+                uint4 ex = make_uint4(0, 0, 0, 0);
+                if (kJoint && hopc) {
+                    NTC_TOUCH(kTrColex, ix.colex_at + fork_block((uint64_t)j + 1) + 4 * (hopc & 3u));
+                    ex = ld4<0>(reinterpret_cast<const uint4 *>(ix.colex_at + fork_block((uint64_t)j + 1)) + (hopc & 3u));
+                }
                 const uint32_t sh = (uint32_t)(T & 31);
                 const uint64_t c0 = (uint64_t)g0.x | ((uint64_t)g0.y << 32);
                 const uint64_t c1 = (uint64_t)g1.x | ((uint64_t)g1.y << 32);
                 const uint64_t c2 = (uint64_t)g2.x | ((uint64_t)g2.y << 32);
-                const uint64_t pa = sh ? ((c0 >> (2 * sh)) | (c1 << (64 - 2 * sh))) : c0;
-                const uint64_t pb = sh ? ((c1 >> (2 * sh)) | (c2 << (64 - 2 * sh))) : c1;
+                uint64_t pa = sh ? ((c0 >> (2 * sh)) | (c1 << (64 - 2 * sh))) : c0;
+                uint64_t pb = sh ? ((c1 >> (2 * sh)) | (c2 << (64 - 2 * sh))) : c1;
                 uint32_t va = sh ? ((g0.z >> sh) | (g1.z << (32 - sh))) : g0.z;
                 if (pre) va |= (1u << (pre - 1)) - 1u;  // of the verified k-mers only node j's must exist
-                const uint32_t vb = sh ? ((g1.z >> sh) | (g2.z << (32 - sh))) : g1.z;
+                uint32_t vb = sh ? ((g1.z >> sh) | (g2.z << (32 - sh))) : g1.z;
+                // hop, x side: the path's next node when the path goes on with c (mid-path: a
+                // node's only successor), the fork block's node and characters at a path end
+                // (k-mer end bit clear), else none
+                uint32_t nx = j + 1, cap = 64;
+                if (kJoint && hopc) {
+                    NTC_STAT(0);
+                    if (!(va & 1u)) {
+                        NTC_STAT(1);
+                        nx = ex.x;
+                        pa = (uint64_t)ex.y | ((uint64_t)ex.z << 32);
+                        va = ex.w;
+                        pb = 0;
+                        vb = 0;
+                        cap = 32;
+                    } else if ((uint32_t)(pa & 3u) != (hopc & 3u)) {
+                        nx = 0xFFFFFFFFu;
+                    }
+                }
                 const uint64_t q = qo + p + m - pre;
                 const uint64_t qi = q >> 5;
                 const uint32_t qs = (uint32_t)(q & 31) * 2;
@@ -1320,6 +1344,10 @@ struct MsLaneT {
                 const uint32_t ib = ~vb ? (uint32_t)__builtin_ctz(~vb) : 32u;
                 if (ib < lb) lb = ib;
                 uint32_t lim = la == 32 ? 32 + lb : la;
+                const uint32_t lx = lim;
+                const bool xend = la < 32 ? la == ia : lb < 32 && lb == ib;  // x's stop (at lx) is a path end
+                uint32_t ny = nx, ly = 64;
+                bool yend = false;  // the y side's stop (at ly) is a path end
                 if (kJoint && jy() != 0xFFFFFFFFu) {  // joint run: the interval's last node follows its path too
 #if defined(__HIP_DEVICE_COMPILE__)
                     __asm__ volatile("" ::: "memory");  // after lim: the loads below must not overlap the x path's
@@ -1329,8 +1357,52 @@ struct MsLaneT {
                     NTC_TOUCH(kTrPst, ix.pstream + (Ty >> 5) + 2);
                     const uint4 h0 = ld4<4>(ix.pstream + (Ty >> 5)), h1 = ld4<4>(ix.pstream + (Ty >> 5) + 1),
                                 h2 = ld4<4>(ix.pstream + (Ty >> 5) + 2);
-                    const uint32_t ly = path_lim(h0, h1, h2, (uint32_t)(Ty & 31), qa, qb2, 0);
+                    uint4 ey = make_uint4(0, 0, 0, 0);
+                    if (hopc) {
+                        NTC_TOUCH(kTrColex, ix.colex_at + fork_block((uint64_t)jy() + 1) + 4 * (hopc & 3u));
+                        ey = ld4<0>(reinterpret_cast<const uint4 *>(ix.colex_at + fork_block((uint64_t)jy() + 1)) +
+                                    (hopc & 3u));
+                    }
+                    const uint32_t shy = (uint32_t)(Ty & 31);
+                    ny = jy() + 1;
+                    if (hopc) NTC_STAT(2);
+                    if (hopc && !((h0.z >> shy) & 1u)) {  // hop, y side at its path end
+                        NTC_STAT(3);
+                        ny = ey.x;
+                        const uint64_t x = qa ^ ((uint64_t)ey.y | ((uint64_t)ey.z << 32));
+                        ly = x ? ctz64(x) >> 1 : 32u;
+                        const uint32_t iv = ~ey.w ? (uint32_t)__builtin_ctz(~ey.w) : 32u;
+                        yend = iv <= ly;
+                        if (iv < ly) ly = iv;
+                        cap = 32;
+                    } else {
+                        if (hopc && ((shy < 16 ? h0.x >> (2 * shy) : h0.y >> (2 * (shy - 16))) & 3u) != (hopc & 3u))
+                            ny = 0xFFFFFFFFu;
+                        ly = path_lim_end(h0, h1, h2, shy, qa, qb2, yend);
+                    }
                     if (ly < lim) lim = ly;
+                }
+                if (kJoint && hopc) {
+                    // the extension of the interval is the interval of the sides' next nodes (the
+                    // first and last node of an interval with edge c extend to the first and last
+                    // node of the extension) at depth d + 1: a single node (or both sides at one
+                    // node) or, below k - 1, a joint interval, under the conditions note_single
+                    // applies.  The run goes on from there as a new run entry (the same (d, S) per
+                    // position as the SBWT entry + run of the path through colex_at, EXT and
+                    // pos_of_node it replaces).  (A next node at path position 0 would make
+                    // j = nx - 1 the "none" value: left to EXT.)
+                    hopc = 0;
+                    const bool joint = jy() != 0xFFFFFFFFu, single = !joint || ny == nx;
+                    const uint32_t d1 = d + 1 < k ? d + 1 : k;
+                    if (nx == 0xFFFFFFFFu || nx == 0 || ny == 0xFFFFFFFFu || ny == 0 || d1 < ix.t_jump ||
+                        (!single && d1 + 1 >= k)) {
+                        NTC_STAT(4);
+                        nohop = true;
+                        break;
+                    }
+                    NTC_STAT(cap == 32 ? (lim < 32 ? 5 : 6) : 7);
+                    j = nx - 1;
+                    if (joint) jy() = single ? 0xFFFFFFFFu : ny - 1;
                 }
                 if (len + pre - p - m < lim) lim = len + pre - p - m;
                 if (lim < pre) {  // the guessed node is not the U-mer's: take it from the table
@@ -1343,14 +1415,27 @@ struct MsLaneT {
                 }
                 m += lim - pre;
                 pre = 0;
-                if (lim < 64) {
+                if (lim < cap) {  // (cap 32: a fork block's characters, the run going on past them)
                     if constexpr (kJoint) {
-                        // the run stopped inside its window with the read going on: across a
-                        // path end (or both sides' next nodes), the run going on in the next
-                        // call.  Hops chained in one call hold the whole wave on this lane's
-                        // dependent loads (A/B, S91 k_ms4: 12.3 ms before, 16.3 ms with every
-                        // hop chained, 12.4 with one, 12.0 with none)
-                        if (ix.forks && m > 0 && p + m < len && fork_hop(ix, b, m)) {
+                        // the run stopped inside its window with the read going on: its entry
+                        // now, the hop across the path end (or to both sides' next nodes) with
+                        // the next call's run.  Hops chained in one call hold the whole wave on
+                        // this lane's dependent loads (round 3, A/B, S91 k_ms4: 12.3 ms before,
+                        // 16.3 ms with every hop chained, 12.4 with one, 12.0 with none)
+                        // A hop needs each side at a path end or going on with the read's
+                        // character c (else: a mismatch, mostly a sequencing error, on with EXT
+                        // or the break now) and the depth note_single asks for
+                        // (a side whose own stop lies past lim goes on with c)
+                        const uint32_t c = (uint32_t)((lim < 32 ? qa >> (2 * lim) : qb2 >> (2 * (lim - 32))) & 3u);
+                        const uint32_t d1 = d + m + 1 < k ? d + m + 1 : k;
+                        if (ix.forks && m > 0 && p + m < len && (lx > lim || xend) && (ly > lim || yend) &&
+                            d1 >= ix.t_jump && (jy() == 0xFFFFFFFFu || d1 + 1 < k)) {
+                            put_entry(b, p, j + 1, m, (d + 1 < k ? d + 1 : k) | kRunTag);
+                            p += m;
+                            d = d + m < k ? d + m : k;
+                            j += m;
+                            if (jy() != 0xFFFFFFFFu) jy() += m;
+                            vfy = (4u + c) << 8;
                             try_run = true;
                             return 0;
                         }
@@ -1361,12 +1446,15 @@ struct MsLaneT {
             if (kJoint && jy() != 0xFFFFFFFFu) {
                 // joint run over a multi-node interval [l, r) (its first and last nodes followed
                 // along their paths): the interval at p + m - 1 is [node at j + m, node at jy + m
-                // + 1) and the extension at p + m goes on from it (see note_path)
+                // + 1) and the extension at p + m goes on from it (see note_path); no hop after
+                // a run (nohop): its entry is written, the interval at p - 1 the same way
                 if (m > 0) {
                     put_entry(b, p, j + 1, m, (d + 1 < k ? d + 1 : k) | kRunTag);
                     p += m;
                     d = d + m < k ? d + m : k;
                     if (p >= len) { jy() = 0xFFFFFFFFu; return 1; }
+                }
+                if (m > 0 || nohop) {
                     NTC_TOUCH(kTrColex, ix.colex_at + j + m);
                     NTC_TOUCH(kTrColex, ix.colex_at + jy() + m);
                     l = ix.colex_at[j + m] & 0x7FFFFFFFu;
@@ -1374,13 +1462,16 @@ struct MsLaneT {
                 }
                 jy() = 0xFFFFFFFFu;
                 m = 0;  // on into the EXT block below, in this same call
+                nohop = false;
             }
-            if (m > 0) {
-                put_entry(b, p, j + 1, m, (d + 1 < k ? d + 1 : k) | kRunTag);
-                p += m;
-                j += m;
-                d = d + m < k ? d + m : k;
-                if (p >= len) return 1;
+            if (m > 0 || nohop) {
+                if (m > 0) {
+                    put_entry(b, p, j + 1, m, (d + 1 < k ? d + 1 : k) | kRunTag);
+                    p += m;
+                    j += m;
+                    d = d + m < k ? d + m : k;
+                    if (p >= len) return 1;
+                }
                 gj = j;
                 ge = p;
                 // the run broke at p (mostly a sequencing error): table first

@@ -221,9 +221,9 @@ void launch_path_edges(const PathArgs &a, uint32_t *prv, hipStream_t s);
 // list ranking by pointer jumping: st[z] = {start node, distance, min node on the way, 0};
 // returns the buffer (a or b) holding the result
 uint4 *launch_path_rank(const uint32_t *prv, uint32_t n, uint4 *a, uint4 *b, hipStream_t s);
-// fork words after each path end (k >= 4), after launch_path_place
+// fork blocks after each path end (k >= kForkBlockMinK), after launch_path_place
 void launch_path_forks(const PathArgs &a, const uint4 *st, const uint32_t *len, const uint64_t *base,
-                       const uint32_t *pos_of_node, uint32_t *colex_at, hipStream_t s);
+                       const uint32_t *pos_of_node, const uint4 *pstream, uint32_t *colex_at, hipStream_t s);
 // cut every cycle at its smallest node (prv[min] = none); *flag = 1 if any was cut
 void launch_path_cut(const PathArgs &a, const uint4 *st, uint32_t *prv, uint32_t *flag, hipStream_t s);
 // len[start] = path length (len zeroed first); vals[z] = len + k at starts, else 0;

@@ -1166,11 +1166,11 @@ __global__ __launch_bounds__(256) void k_path_place(PathArgs a, const uint4 *st,
     }
 }
 
-// fork words after each path end (derived.cpp fork_words): run after k_path_place, so that
-// every real node's path position is known
+// fork blocks after each path end (derived.cpp build_paths, encode_core.h fork_block): run
+// after k_path_place, so that every real node's path position and all path text are known
 __global__ __launch_bounds__(256) void k_path_forks(PathArgs a, const uint4 *st, const uint32_t *len,
                                                     const uint64_t *base, const uint32_t *pos_of_node,
-                                                    uint32_t *colex_at) {
+                                                    const uint4 *pstream, uint32_t *colex_at) {
     const uint32_t z = blockIdx.x * 256u + threadIdx.x;
     if (z == 0 || z >= a.n || path_dummy(a.dummy, z)) return;
     const uint4 e = st[z];
@@ -1178,6 +1178,7 @@ __global__ __launch_bounds__(256) void k_path_forks(PathArgs a, const uint4 *st,
     const uint64_t pos = base[e.x] + e.y;
     uint32_t h = z;
     while (h > 0 && a.lcs[h] >= a.k - 1) h--;  // the (k-1)-suffix group's first node holds the labels
+    uint4 *blk = reinterpret_cast<uint4 *>(colex_at + fork_block(pos + 1));
 #pragma unroll
     for (int c = 0; c < 4; c++) {
         const uint2 w = a.rank[(uint64_t)c * a.rwords + (h >> 5)];
@@ -1186,13 +1187,16 @@ __global__ __launch_bounds__(256) void k_path_forks(PathArgs a, const uint4 *st,
             const uint32_t y = rank_word(w, h);
             if (!path_dummy(a.dummy, y)) v = pos_of_node[y];
         }
-        colex_at[pos + 1 + c] = v;
+        uint64_t chars = 0;
+        uint32_t ends = 0;
+        if (v != 0xFFFFFFFFu) path_text32(pstream, (uint64_t)v + a.k - 1, chars, ends);
+        blk[c] = make_uint4(v, (uint32_t)chars, (uint32_t)(chars >> 32), ends);
     }
 }
 
 void launch_path_forks(const PathArgs &a, const uint4 *st, const uint32_t *len, const uint64_t *base,
-                       const uint32_t *pos_of_node, uint32_t *colex_at, hipStream_t s) {
-    hipLaunchKernelGGL(k_path_forks, grid_for(a.n), dim3(256), 0, s, a, st, len, base, pos_of_node, colex_at);
+                       const uint32_t *pos_of_node, const uint4 *pstream, uint32_t *colex_at, hipStream_t s) {
+    hipLaunchKernelGGL(k_path_forks, grid_for(a.n), dim3(256), 0, s, a, st, len, base, pos_of_node, pstream, colex_at);
 }
 
 void launch_path_edges(const PathArgs &a, uint32_t *prv, hipStream_t s) {

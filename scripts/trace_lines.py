@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--group", type=int, default=1, help="count distinct lines per this many consecutive reads")
     ap.add_argument("--order", choices=["input", "minimizer"], default="input",
                     help="process reads as generated, or grouped by their minimizer (locality experiment)")
+    ap.add_argument("--waves", action="store_true",
+                    help="also run one 64-lane wave in lock step (emu_wave_modes): iterations and steps per read")
     args = ap.parse_args()
     so = os.path.join(REPO, "tests", "emu", "libntc_emu_trace.so")
     subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "tests", "emu"), "libntc_emu_trace.so"])
@@ -74,6 +76,9 @@ def main():
     ov = np.zeros(K, dtype=np.uint64)
     L.emu_trace_report(out.ctypes.data)
     L.emu_trace_overlap(ov.ctypes.data)
+    st = np.zeros(16, dtype=np.uint64)
+    L.emu_stats.argtypes = [ctypes.c_void_p]
+    L.emu_stats(st.ctypes.data)
     n = int(out[0])
     req = out[1:1 + 2 * K].reshape(2, K) / n
     lines = out[1 + 2 * K:].reshape(2, K) / n
@@ -85,6 +90,15 @@ def main():
             if req[ph][i] > 0:
                 extra = f"  (also touched by ms: {ov[i] / n:5.2f})" if ph == 1 else ""
                 print(f"   {KINDS[i]:12s} loads {req[ph][i]:7.2f}  lines {lines[ph][i]:6.2f}{extra}")
+    if st.any():  # NTC_STAT counters of the MS lanes (encode_core.h), per read
+        print("-- unit counters per read: " + ", ".join(f"[{i}] {st[i] / n:.2f}" for i in range(16) if st[i]))
+    if args.waves:
+        w = emu_lib.emu_wave_modes(ix.n, args.k, ix.rows, ix.C, ix.lcs, reads, offs)
+        modes = ["Scan", "Ext", "P1", "Bs", "Brk", "First", "Enter", "BrkLong", "ExtFail", "run"]
+        nr = args.reads
+        print(f"-- wave (64 lanes, lock step): iterations per 64 reads {64 * w[0] / nr:.2f}, "
+              f"lane steps per read {w[2] / nr:.2f}, distinct modes per iteration {w[1] / max(w[0], 1):.2f}")
+        print("   steps per read: " + ", ".join(f"{m} {w[3 + i] / nr:.2f}" for i, m in enumerate(modes) if w[3 + i]))
 
 
 if __name__ == "__main__":

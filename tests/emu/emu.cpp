@@ -59,6 +59,13 @@ extern "C" void emu_trace_report(uint64_t *out) {  // [reads, req[2][K], lines[2
     memset(g_ltot, 0, sizeof g_ltot);
     g_reads = 0;
 }
+#if defined(NTC_STATS) && !defined(__HIP_DEVICE_COMPILE__)
+uint64_t ntc::ntc_stats[16];
+extern "C" void emu_stats(uint64_t *out) {  // [16]: NTC_STAT counters (encode_core.h), then cleared
+    for (int i = 0; i < 16; i++) out[i] = ntc_stats[i];
+    memset(ntc_stats, 0, sizeof ntc_stats);
+}
+#endif
 extern "C" void emu_trace_overlap(uint64_t *out) {  // [K]: parse lines also touched by the MS phase
     for (int b = 0; b < kTrKinds; b++) out[b] = g_over[b];
     memset(g_over, 0, sizeof g_over);
@@ -378,25 +385,18 @@ extern "C" int emu_decode(const ntc_index_view *v, const uint64_t *recs, uint64_
     return NTC_OK;
 }
 
-// Wave divergence of k_ms4 (diagnostic): one wave of 64 lanes runs MsLane::step in lock step
-// over the reads, idle lanes taking the next read as the kernel's pool hands them out.  out:
-// [0] wave iterations, [1] sum over iterations of the distinct entry modes among busy lanes
-// (a "run" pending counts as its own mode), [2] lane steps, [3..12] steps per entry mode
-// (Scan, Ext, P1, Bs, Brk, First, Enter, BrkLong, ExtFail, run), [13..22] iterations by
-// number of distinct modes (1..10).
-extern "C" int emu_wave_modes(const ntc_index_view *v, const uint8_t *bases, const uint64_t *offs, uint64_t n_reads,
-                              uint64_t *out) {
-    HostIndex hx;
-    Derived dv;
-    std::vector<WalkEntry> walk;
-    std::vector<uint2> tab;
-    std::vector<uint32_t> bits, fbits;
-    std::vector<uint16_t> pairb;
-    DevIndex d;
-    if (!load(v, hx, dv, walk, d, tab, bits, fbits, pairb, 0)) return NTC_ERR_FORMAT;
-    memset(out, 0, 23 * sizeof(uint64_t));
+// Wave divergence of k_ms4 (diagnostic): one wave of 64 lanes runs MsLaneT::step (the build
+// the upload would pick: joint unless NTC_EMU_JOINT=0) in lock step over the reads, idle
+// lanes taking the next read as the kernel's pool hands them out.  out: [0] wave
+// iterations, [1] sum over iterations of the distinct entry modes among busy lanes (a "run"
+// pending counts as its own mode), [2] lane steps, [3..12] steps per entry mode (Scan, Ext,
+// P1, Bs, Brk, First, Enter, BrkLong, ExtFail, run), [13..22] iterations by number of
+// distinct modes (1..10).
+constexpr int kWaveModes = 10;
+template <bool kJoint>
+void wave_modes(const DevIndex &d, const uint8_t *bases, const uint64_t *offs, uint64_t n_reads, uint64_t *out) {
     struct Lane {
-        MsLane ms;
+        MsLaneT<kJoint> ms;
         std::vector<uint64_t> Q;
         std::vector<Entry> Ed, Es, Ep;
         unsigned long long pcnt = 0, status = ~0ull;
@@ -427,7 +427,7 @@ extern "C" int emu_wave_modes(const ntc_index_view *v, const uint8_t *bases, con
             if (!l.busy) continue;
             ntc_host_lane = li;
             any = true;
-            const uint32_t m = l.ms.try_run ? 9u : l.ms.mode;
+            const uint32_t m = l.ms.try_run ? (uint32_t)kWaveModes - 1 : l.ms.mode;
             modes |= 1u << m;
             out[3 + m]++;
             out[2]++;
@@ -440,7 +440,22 @@ extern "C" int emu_wave_modes(const ntc_index_view *v, const uint8_t *bases, con
         out[0]++;
         const uint32_t dm = (uint32_t)__builtin_popcount(modes);
         out[1] += dm;
-        out[12 + dm]++;
+        out[3 + kWaveModes + dm - 1]++;
     }
+}
+
+extern "C" int emu_wave_modes(const ntc_index_view *v, const uint8_t *bases, const uint64_t *offs, uint64_t n_reads,
+                              uint64_t *out) {
+    HostIndex hx;
+    Derived dv;
+    std::vector<WalkEntry> walk;
+    std::vector<uint2> tab;
+    std::vector<uint32_t> bits, fbits;
+    std::vector<uint16_t> pairb;
+    DevIndex d;
+    if (!load(v, hx, dv, walk, d, tab, bits, fbits, pairb, 0)) return NTC_ERR_FORMAT;
+    memset(out, 0, (3 + 2 * kWaveModes) * sizeof(uint64_t));
+    if (d.joint) wave_modes<true>(d, bases, offs, n_reads, out);
+    else wave_modes<false>(d, bases, offs, n_reads, out);
     return 0;
 }
