@@ -1296,7 +1296,7 @@ struct MsLaneT {
                             g2 = ld4<4>(ix.pstream + (T >> 5) + 2);
                 // a hop loads the fork block entry of c with the path text: one round trip
                 uint4 ex = make_uint4(0, 0, 0, 0);
-                if (kJoint && hopc) {
+                if (kJoint && (hopc & 8u)) {
                     NTC_TOUCH(kTrColex, ix.colex_at + fork_block((uint64_t)j + 1) + 4 * (hopc & 3u));
                     ex = ld4<0>(reinterpret_cast<const uint4 *>(ix.colex_at + fork_block((uint64_t)j + 1)) + (hopc & 3u));
                 }
@@ -1358,7 +1358,7 @@ struct MsLaneT {
                     const uint4 h0 = ld4<4>(ix.pstream + (Ty >> 5)), h1 = ld4<4>(ix.pstream + (Ty >> 5) + 1),
                                 h2 = ld4<4>(ix.pstream + (Ty >> 5) + 2);
                     uint4 ey = make_uint4(0, 0, 0, 0);
-                    if (hopc) {
+                    if (hopc & 16u) {
                         NTC_TOUCH(kTrColex, ix.colex_at + fork_block((uint64_t)jy() + 1) + 4 * (hopc & 3u));
                         ey = ld4<0>(reinterpret_cast<const uint4 *>(ix.colex_at + fork_block((uint64_t)jy() + 1)) +
                                     (hopc & 3u));
@@ -1435,7 +1435,7 @@ struct MsLaneT {
                             d = d + m < k ? d + m : k;
                             j += m;
                             if (jy() != 0xFFFFFFFFu) jy() += m;
-                            vfy = (4u + c) << 8;
+                            vfy = (4u + c + (lx > lim ? 0u : 8u) + (ly > lim ? 0u : 16u)) << 8;
                             try_run = true;
                             return 0;
                         }
