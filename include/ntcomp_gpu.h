@@ -105,7 +105,11 @@ int ntc_ctx_synchronize(ntc_ctx *ctx);
  * get_option returns the setting in use).  "win" (-1 auto = on for U >= 4 / 0 / 1): SCAN
  * window words, 4^(U-3) x 32 B, four positions per line.  Also "filter" (-1 auto = on only
  * without window words and below 60 % density / 0 / 1: SCAN pre-filter), "ext2" (0 / 1:
- * two-character rank chunks), "pair_bytes" (0 / 1), same rules.
+ * two-character rank chunks), "pair_bytes" (0 / 1), same rules.  "decode_only" (0 default
+ * / 1) for the NEXT upload: build only what decoding reads (the walk table), none of the
+ * encoder's path cover, suffix table or SCAN words; encode calls on that index then fail
+ * with NTC_ERR_NO_INDEX (after the upload get_option returns whether the index in use is
+ * decode-only; ntc_index_share passes it on).
  * Read-only: "n_paths", "path_text_len" (the path cover built on the device at upload),
  * "path_hash" (test hook: FNV-1a of the cover arrays, derived.h path_cover_hash),
  * "tab_u" (after an upload: the depth in use), "tab_u_fallback" (1: the default depth 15

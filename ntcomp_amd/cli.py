@@ -125,11 +125,12 @@ def cmd_build(args):
     ix.save(args.output_prefix, layout=args.index_format)
 
 
-def _open_gpus(index, devices, st=None, per_gpu=1):
+def _open_gpus(index, devices, st=None, per_gpu=1, decode_only=False):
     """per_gpu contexts per entry of devices; an int n means devices
     0..n-1.  The first context of a device uploads the index, the others on that device share
     it (ntc_index_share): calls alternate over the contexts, so one call's copies and host
-    work overlap another's kernels."""
+    work overlap another's kernels.  decode_only: the upload builds only the walk table
+    (ctx option decode_only)."""
     import ntcomp_amd as nt
     ctxs, first = [], {}
     for d in (range(devices) if isinstance(devices, int) else devices):
@@ -138,6 +139,8 @@ def _open_gpus(index, devices, st=None, per_gpu=1):
             if d in first:
                 c.share_index(first[d])
             else:
+                if decode_only:
+                    c.set_option("decode_only", 1)
                 (st.wrap("index_upload", c.upload) if st else c.upload)(index)
                 first[d] = c
                 if st and st.on:
@@ -196,7 +199,7 @@ def cmd_decode(args):
     import ntcomp_amd as nt
     st = _Stats(args.stats)
     index = st.wrap("index_load", nt.Index.load)(args.index_prefix)
-    ctxs = _open_gpus(index, _devices(args), st, args.contexts_per_gpu)
+    ctxs = _open_gpus(index, _devices(args), st, args.contexts_per_gpu, decode_only=True)
     log("Decoding encoded data...")
     out = sys.stdout.buffer
     out.flush()

@@ -103,6 +103,9 @@ struct ntc_ctx {
     int64_t filter_density_ppm = -1;  // presence density of the filter level at the last upload
     int joint_opt = -1;      // joint path runs at the next upload: -1 auto (fragmented path cover), 0 off, 1 on
     int win_opt = -1;        // SCAN window words at the next upload: -1 auto (U >= 4), 0 off, 1 on
+    int decode_only_opt = 0;  // the next upload builds only what decode needs (walk table): no path
+                              // cover, suffix table or SCAN words; encode calls then fail
+    bool index_decode_only = false;  // the index in use was uploaded that way
     int ext2_opt = 0;        // build the two-character rank chunks at the next upload (A/B option: 1 measured
                              // slower -- 8 B/node from HBM against 1 B/node of Infinity-Cache-resident rank words)
     uint64_t n_paths = 0, path_text_len = 0;
@@ -216,6 +219,8 @@ uint32_t ent_slots(const ntc_ctx *ctx) {
 // total_bases = offs[n] - offs[0] (known to the caller).
 int encode4_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, uint64_t n_reads,
                  uint64_t total_bases, uint64_t *d_rec_out, uint64_t cap, uint64_t *d_rec_offs) {
+    if (ctx->index_decode_only)
+        return set_err(ctx, NTC_ERR_NO_INDEX, "the index was uploaded for decode only (ctx option decode_only)");
     Enc4Args a{};
     a.ix = ctx->dix;
     a.bases = d_bases;
@@ -310,6 +315,8 @@ int encode_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, ui
                 const Layout &lay, uint64_t *d_rec_out, uint64_t cap, uint64_t *d_rec_offs,
                 uint64_t units) {
     if (!ctx->has_index) return set_err(ctx, NTC_ERR_NO_INDEX, "no index uploaded");
+    if (ctx->index_decode_only)
+        return set_err(ctx, NTC_ERR_NO_INDEX, "the index was uploaded for decode only (ctx option decode_only)");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     ctx->last_variant = ctx->encode_variant;
     EncodeArgs a{};
@@ -642,6 +649,7 @@ int ntc_index_share(ntc_ctx *dst, const ntc_ctx *src) {
     dst->path_text_len = src->path_text_len;
     dst->filter_density_ppm = src->filter_density_ppm;
     dst->tab_u_fallback = src->tab_u_fallback;
+    dst->index_decode_only = src->index_decode_only;
     dst->upload_host_us = dst->upload_total_us = 0;
     dst->has_index = true;
     return NTC_OK;
@@ -774,7 +782,9 @@ int upload_prepared(ntc_ctx *ctx, const ntc_index_prep &prep) {
     void *d_pstream = nullptr, *d_colex_at = nullptr, *d_pos = nullptr, *d_puniq = nullptr;
     bool has_paths = false;
     uint64_t tlen = 0, n_paths = 0;
-    if (n < (1ULL << 31)) {
+    const bool dec_only = ctx->decode_only_opt != 0;
+    ctx->index_decode_only = false;
+    if (!dec_only && n < (1ULL << 31)) {
         const std::vector<uint8_t> dummy = dummy_nodes(hx, dv);
         std::vector<uint32_t> dbits(n / 32 + 2, 0);
         for (uint64_t z = 0; z < n; z++)
@@ -873,6 +883,26 @@ int upload_prepared(ntc_ctx *ctx, const ntc_index_prep &prep) {
     // the lighter k_ms4 build.
     d.joint = has_paths && (ctx->joint_opt == 1 || (ctx->joint_opt < 0 && (uint64_t)n_paths * kJointAutoNodesPerPath > n))
                   ? 1u : 0u;
+    if (dec_only) {  // decode reads the walk table alone: no suffix table, SCAN words or rank chunks
+        d.rank2 = nullptr;
+        d.tab = nullptr;
+        d.tab_bits = nullptr;
+        d.filt_bits = nullptr;
+        d.filt_f = 0;
+        d.pair_w = nullptr;
+        d.win_w = nullptr;
+        d.tab_u = 0;
+        d.tab_pos = 0;
+        HIP_TRY(ctx, hipGetLastError());
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        ctx->n_paths = 0;
+        ctx->path_text_len = 0;
+        ctx->index_decode_only = true;
+        ctx->has_index = true;
+        mark("done (decode only)", false);
+        ctx->upload_total_us = us_since();
+        return NTC_OK;
+    }
     d.rank2 = nullptr;
     if (ctx->ext2_opt) {  // two-character rank lines (8 B per node)
         void *d_r2;
@@ -994,6 +1024,11 @@ int ntc_ctx_set_option(ntc_ctx *ctx, const char *key, int64_t value) {
         ctx->win_opt = (int)value;
         return NTC_OK;
     }
+    if (std::strcmp(key, "decode_only") == 0) {  // applies to the next ntc_index_upload
+        if (value != 0 && value != 1) return set_err(ctx, NTC_ERR_INVALID_ARG, "decode_only must be 0 or 1");
+        ctx->decode_only_opt = (int)value;
+        return NTC_OK;
+    }
     if (std::strcmp(key, "ext2") == 0) {  // applies to the next ntc_index_upload
         if (value != 0 && value != 1) return set_err(ctx, NTC_ERR_INVALID_ARG, "ext2 must be 0 or 1");
         ctx->ext2_opt = (int)value;
@@ -1031,6 +1066,7 @@ int ntc_ctx_get_option(const ntc_ctx *ctx, const char *key, int64_t *value) {
     else if (std::strcmp(key, "tab_u") == 0) *value = ctx->has_index ? ctx->dix.tab_u : ctx->tab_u_opt;
     else if (std::strcmp(key, "pair_bytes") == 0) *value = ctx->has_index ? (ctx->dix.pair_w != nullptr) : ctx->pair_bytes_opt;
     else if (std::strcmp(key, "ext2") == 0) *value = ctx->has_index ? (ctx->dix.rank2 != nullptr) : ctx->ext2_opt;
+    else if (std::strcmp(key, "decode_only") == 0) *value = ctx->has_index ? ctx->index_decode_only : ctx->decode_only_opt;
     else if (std::strcmp(key, "filter") == 0) *value = ctx->has_index ? (ctx->dix.filt_f != 0) : ctx->filter_opt;
     else if (std::strcmp(key, "joint") == 0) *value = ctx->has_index ? (int64_t)ctx->dix.joint : ctx->joint_opt;
     else if (std::strcmp(key, "win") == 0) *value = ctx->has_index ? (ctx->dix.win_w != nullptr) : ctx->win_opt;

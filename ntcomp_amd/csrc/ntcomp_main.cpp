@@ -113,7 +113,10 @@ constexpr int kEncodeContextsPerGpu = 2, kDecodeContextsPerGpu = 1;
 // what encode / decode hand to main for the exit
 std::vector<ntc_ctx *> g_ctxs;
 ntc_index_host *g_ix = nullptr;
-std::vector<ntc_ctx *> open_gpus(const ntc_index_host *ix, const std::vector<int> &devs, int per_gpu) {
+// decode_only: the upload builds what decode reads (the walk table), not the encoder's path
+// cover, suffix table and SCAN words (ctx option decode_only)
+std::vector<ntc_ctx *> open_gpus(const ntc_index_host *ix, const std::vector<int> &devs, int per_gpu,
+                                 bool decode_only = false) {
     ntc_index_view v;
     if (ntc_index_view_of(ix, &v)) die("index view");
     // the HIP runtime starts (~0.1 s) while this thread derives the index's host tables
@@ -146,6 +149,7 @@ std::vector<ntc_ctx *> open_gpus(const ntc_index_host *ix, const std::vector<int
         if (src) {
             if (ntc_index_share(c, src)) die(std::string("index share: ") + ntc_last_error(c));
         } else {
+            if (decode_only && ntc_ctx_set_option(c, "decode_only", 1)) die("ctx option decode_only");
             if (ntc_index_upload_prepared(c, prep)) die(std::string("index upload: ") + ntc_last_error(c));
             first.push_back({dev_of[i], c});
         }
@@ -220,7 +224,7 @@ int cmd_decode(const Args &a) {
     ntc_index_host *ix = nullptr;
     if (ntc_index_load(prefix.c_str(), &ix)) die("cannot load index " + prefix);
     const double t_load = since(t0);
-    auto ctxs = open_gpus(ix, devices_of(a), per_gpu_of(a, kDecodeContextsPerGpu));
+    auto ctxs = open_gpus(ix, devices_of(a), per_gpu_of(a, kDecodeContextsPerGpu), true);
     const double t_gpu = since(t0);
     info("Decoding encoded data...");
     ntc_pipeline_opts o{};

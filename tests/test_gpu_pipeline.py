@@ -287,3 +287,33 @@ def test_prepared_upload_equals_upload(setup):
         assert np.array_equal(out, reads)
     for x in (a, b, c):
         x.close()
+
+
+def test_decode_only_upload(setup):
+    """ctx option decode_only: the upload builds the walk table alone (no path cover, suffix
+    table or SCAN words, a smaller device index); decode is the same as on a full index, the
+    option passes on through ntc_index_share, and encode calls fail with NTC_ERR_NO_INDEX."""
+    d, genome, ix = setup
+    reads = nt.synth_reads(genome, 44, 0, 20_000, 150, 10_000)
+    offs = np.arange(0, len(reads) + 1, 150, dtype=np.uint64)
+    full = nt.GpuContext(0).upload(ix)
+    recs, _ = full.encode(reads, offs)
+    dec = nt.GpuContext(0)
+    dec.set_option("decode_only", 1)
+    dec.upload(ix)
+    assert dec.get_option("decode_only") == 1 and full.get_option("decode_only") == 0
+    assert dec.index_info()[2] < full.index_info()[2]
+    shared = nt.GpuContext(0)
+    shared.share_index(dec)
+    for x in (dec, shared):
+        out, o2 = x.decode(recs)
+        assert np.array_equal(out, reads) and np.array_equal(o2, offs)
+        with pytest.raises(nt.NtcError) as e:
+            x.encode(reads, offs)
+        assert e.value.code == 7  # NTC_ERR_NO_INDEX
+    dec.set_option("decode_only", 0)
+    dec.upload(ix)  # a full upload again: encode works
+    r2, _ = dec.encode(reads, offs)
+    assert np.array_equal(r2, recs)
+    for x in (full, dec, shared):
+        x.close()
