@@ -19,8 +19,15 @@ def emu_lib():
                 os.path.join(REPO, "ntcomp_amd", "csrc", "derived.h"),
                 os.path.join(REPO, "ntcomp_amd", "csrc", "encode_core.h"),
                 os.path.join(REPO, "ntcomp_amd", "csrc", "derived.cpp")]
-        if (not os.path.exists(EMU_SO)) or any(os.path.getmtime(EMU_SO) < os.path.getmtime(d) for d in deps):
-            subprocess.check_call(["make", "-s", "-B", "-C", os.path.join(REPO, "tests", "emu")])
+        stale = lambda: (not os.path.exists(EMU_SO)) or any(os.path.getmtime(EMU_SO) < os.path.getmtime(d)
+                                                             for d in deps)
+        if stale():
+            import fcntl  # one build at a time across pytest-xdist workers (re-checked under the lock)
+            with open(os.path.join(REPO, "tests", "emu", ".build.lock"), "w") as lock:
+                fcntl.flock(lock, fcntl.LOCK_EX)
+                if stale():
+                    subprocess.check_call(["make", "-s", "-B", "-C", os.path.join(REPO, "tests", "emu")])
+                fcntl.flock(lock, fcntl.LOCK_UN)
         L = ctypes.CDLL(EMU_SO)
         P, u64 = ctypes.c_void_p, ctypes.c_uint64
         L.emu_encode.restype = ctypes.c_int

@@ -32,7 +32,13 @@ MASK = (1 << 64) - 1
 
 @pytest.fixture(scope="module")
 def san():
-    subprocess.check_call(["make", "-s", "-j2", "-C", SAN])
+    # one build at a time (pytest-xdist workers share tests/san: a relink under a binary
+    # another worker is running fails with a permission error)
+    import fcntl
+    with open(os.path.join(SAN, ".build.lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        subprocess.check_call(["make", "-s", "-j2", "-C", SAN])
+        fcntl.flock(lock, fcntl.LOCK_UN)
     return {"asan": os.path.join(SAN, "san_asan"), "tsan": os.path.join(SAN, "san_tsan")}
 
 
