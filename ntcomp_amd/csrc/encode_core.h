@@ -20,7 +20,8 @@
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 #ifndef NTC_NT
 #define NTC_NT 17  // streaming (nontemporal) hints, bit mask: 1 table entries, 16 entry stores,
-                   // 2 exact presence bits, 4 path stream, 8 query words, 32 pair words (k_ms4)
+                   // 2 exact presence bits, 4 path stream, 8 query words, 32 pair words (k_ms4),
+                   // 64 fork block entries
 #endif
 
 // Line tracing for the test-only emulator (tests/emu, -DNTC_TRACE): every index load
@@ -1298,7 +1299,7 @@ struct MsLaneT {
                 uint4 ex = make_uint4(0, 0, 0, 0);
                 if (kJoint && (hopc & 8u)) {
                     NTC_TOUCH(kTrColex, ix.colex_at + fork_block((uint64_t)j + 1) + 4 * (hopc & 3u));
-                    ex = ld4<0>(reinterpret_cast<const uint4 *>(ix.colex_at + fork_block((uint64_t)j + 1)) + (hopc & 3u));
+                    ex = ld4<64>(reinterpret_cast<const uint4 *>(ix.colex_at + fork_block((uint64_t)j + 1)) + (hopc & 3u));
                 }
                 const uint32_t sh = (uint32_t)(T & 31);
                 const uint64_t c0 = (uint64_t)g0.x | ((uint64_t)g0.y << 32);
@@ -1360,7 +1361,7 @@ struct MsLaneT {
                     uint4 ey = make_uint4(0, 0, 0, 0);
                     if (hopc & 16u) {
                         NTC_TOUCH(kTrColex, ix.colex_at + fork_block((uint64_t)jy() + 1) + 4 * (hopc & 3u));
-                        ey = ld4<0>(reinterpret_cast<const uint4 *>(ix.colex_at + fork_block((uint64_t)jy() + 1)) +
+                        ey = ld4<64>(reinterpret_cast<const uint4 *>(ix.colex_at + fork_block((uint64_t)jy() + 1)) +
                                     (hopc & 3u));
                     }
                     const uint32_t shy = (uint32_t)(Ty & 31);
