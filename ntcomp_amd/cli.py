@@ -10,9 +10,10 @@ per context, deflate on the host pool, blocks in file order.  Decode: blocks unz
 thread pool (ctypes releases the GIL), batches decode on the GPU contexts, FASTA
 formatting on the pool, output in file order.
 
-Index files: <prefix>.sbwt / <prefix>.lcs in this library's own layout, or (--index-format
-sbwt-rs) a recalled restatement of the sbwt 0.3.11 layout with the -p prefix lookup table
-(unpinned offline -- DESIGN.md section 8).
+Index files: <prefix>.sbwt / <prefix>.lcs written by default in a recalled restatement of
+the sbwt 0.3.11 / kbo 0.5.1 layout the reference always writes (kbo::index::serialize_sbwt,
+main.rs:138), with the -p prefix lookup table (unpinned offline -- DESIGN.md section 8);
+--index-format own writes this library's own layout.  encode/decode read either.
 """
 import argparse
 import sys
@@ -104,13 +105,16 @@ def cmd_build(args):
             builder = "host"
     if builder == "gpu":
         # the same index built on the GPU (build.hip; tests/test_gpu_build.py: equal to the host
-        # build) in passes that fit -m/--mem-gb of device memory, sorted partitions past the same
-        # amount of host memory spilled to --temp-dir (kbo's BuildOpts, main.rs:111-134)
-        budget = int(args.mem_gb * (1 << 30))
+        # build).  kbo's BuildOpts (main.rs:111-134; cli.rs:55-60: --temp-dir builds "on temporary
+        # disk space instead of in-memory", -m is the memory for that): -m given bounds the device
+        # memory of a pass (else 85 % of the free HBM); with --temp-dir, sorted partitions past -m GB
+        # of host memory go to files there, without it nothing spills.
+        mem = int((args.mem_gb if args.mem_gb is not None else 4) * (1 << 30))
         stats = {}
         try:
-            ix = nt.Index.build_gpu(ctx, seqs, args.kmer_size, add_revcomp=True, device_budget=budget,
-                                    host_budget=budget, temp_dir=args.temp_dir, stats=stats)
+            ix = nt.Index.build_gpu(ctx, seqs, args.kmer_size, add_revcomp=True,
+                                    device_budget=mem if args.mem_gb is not None else 0,
+                                    host_budget=mem if args.temp_dir else 0, temp_dir=args.temp_dir, stats=stats)
         finally:
             ctx.close()
         if args.verbose:
@@ -235,19 +239,20 @@ def main(argv=None):
     b.add_argument("-d", "--dedup-batches", action="store_true",
                    help="Deduplicate k-mers per batch (the GPU build always deduplicates a full pass in place).")
     b.add_argument("-t", "--threads", dest="num_threads", type=int, default=1)
-    b.add_argument("-m", "--mem-gb", type=float, default=4,
-                   help="Memory budget in GB: device memory per GPU build pass, and host memory for sorted "
-                        "partitions (past it they spill to --temp-dir).")
-    b.add_argument("--temp-dir", help="Directory for partitions past the memory budget (default $TMPDIR or /tmp).")
+    b.add_argument("-m", "--mem-gb", type=float, default=None,
+                   help="Memory budget in GB (default 4 for --temp-dir): device memory per GPU build pass when given "
+                        "(else 85%% of the free HBM), and with --temp-dir the host memory for sorted partitions.")
+    b.add_argument("--temp-dir", help="Build on temporary disk space at this path: sorted partitions past -m GB of "
+                                      "host memory spill there (without it nothing spills).")
     b.add_argument("--verbose", action="store_true")
     b.add_argument("--builder", choices=["auto", "host", "gpu"], default="auto",
                    help="auto (default): the GPU when one is usable, else the host; host: threaded C++ builder "
                         "(in memory); gpu: k-mer sort, dummies, LCS and labels on the GPU in memory-bounded "
                         "passes (same index)")
     b.add_argument("--device", type=int, default=0, help="GPU for --builder gpu")
-    b.add_argument("--index-format", choices=["own", "sbwt-rs"], default="own",
-                   help="own layout (default) or a restatement of sbwt 0.3.11/kbo 0.5.1 files (parity unpinned); "
-                        "encode/decode read either")
+    b.add_argument("--index-format", choices=["own", "sbwt-rs"], default="sbwt-rs",
+                   help="sbwt-rs (default): a restatement of the sbwt 0.3.11/kbo 0.5.1 files the reference writes "
+                        "(parity unpinned); own: this library's layout. encode/decode read either")
     e = sub.add_parser("encode", help="Encode fastX data using an SBWT index")
     e.add_argument("query_file", help="Query file with sequence data.")
     e.add_argument("-i", "--index", dest="index_prefix", required=True, help="Prefix for prebuilt <prefix>.sbwt and <prefix>.lcs")

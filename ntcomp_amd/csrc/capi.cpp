@@ -1506,6 +1506,10 @@ int fastq_stage(ntc_ctx *ctx, const uint8_t *fastq, uint64_t bytes, uint64_t n_r
                 uint64_t *total, int64_t *bad_read) {
     if (bad_read) *bad_read = -1;
     *total = 0;
+    // The parse reuses d_status and the mailbox: whatever an earlier encode or decode
+    // left there is gone, so its status / counts must not be reported any more.
+    ctx->box_valid = false;
+    ctx->last = kNone;
     if (bytes >= (1ull << 32)) return set_err(ctx, NTC_ERR_CAPACITY, "FASTQ text of 4 GiB or more: split the batch");
     if (n_reads == 0 && bytes) return set_err(ctx, NTC_ERR_FORMAT, "FASTQ text given for zero reads");
     const uint64_t tiles = fastq_tiles(bytes);

@@ -650,7 +650,9 @@ struct DeflateReader : ByteReader {
         for (unsigned t = 1; t < T && t * 8 < at.size(); t++) th.emplace_back(work, t);
         work(0);
         for (auto &x : th) x.join();
-        if (bad) return -1;
+        // libdeflate rejected a member (or its sizes disagree): nothing is delivered, and the
+        // buffered path takes the same members, falling back to zlib as read() does
+        if (bad) return 0;
         ci = at.back() + sz.back();
         members += at.size();
         delivered += off.back();

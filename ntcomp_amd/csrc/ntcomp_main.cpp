@@ -53,12 +53,20 @@ struct Args {
     }
 };
 
-// options taking a value; everything else starting with '-' is a switch
+// options taking a value, and switches; anything else starting with '-' is a usage error
+// (clap rejects unknown arguments, src/cli.rs)
 bool takes_value(const std::string &o) {
     static const char *v[] = {"-o", "--output-prefix", "-k", "-p", "--prefix-precalc", "-t", "--threads", "-m",
                               "--mem-gb", "--temp-dir", "-l", "--input-list", "--builder", "--device",
                               "--index-format", "-i", "--index", "--gpus", "--devices", "--blocks-per-batch",
                               "--deflate", "--contexts-per-gpu"};
+    for (const char *x : v)
+        if (o == x) return true;
+    return false;
+}
+
+bool is_switch(const std::string &o) {
+    static const char *v[] = {"-d", "--dedup-batches", "--verbose", "--stats", "--host-parse"};
     for (const char *x : v)
         if (o == x) return true;
     return false;
@@ -71,12 +79,16 @@ Args parse(int argc, char **argv, int from) {
         if (s.size() > 1 && s[0] == '-') {
             const size_t eq = s.find('=');
             if (eq != std::string::npos && s.rfind("--", 0) == 0) {
-                a.kv.push_back({s.substr(0, eq), s.substr(eq + 1)});
+                const std::string name = s.substr(0, eq);
+                if (!takes_value(name)) die("unexpected argument '" + s + "'");
+                a.kv.push_back({name, s.substr(eq + 1)});
             } else if (takes_value(s)) {
                 if (i + 1 >= argc) die("option " + s + " needs a value");
                 a.kv.push_back({s, argv[++i]});
-            } else {
+            } else if (is_switch(s)) {
                 a.kv.push_back({s, "1"});
+            } else {
+                die("unexpected argument '" + s + "'");
             }
         } else {
             a.pos.push_back(s);
@@ -275,9 +287,10 @@ int cmd_build(const Args &a) {
     const uint32_t pre = (uint32_t)std::atoi(a.get("-p", "--prefix-precalc", "8").c_str());
     const int threads = std::atoi(a.get("-t", "--threads", "1").c_str());
     const double mem_gb = std::atof(a.get("-m", "--mem-gb", "4").c_str());
+    const bool mem_given = a.flag("-m", "--mem-gb");
     const std::string temp = a.get("--temp-dir", nullptr, "");
     const std::string builder = a.get("--builder", nullptr, "auto");
-    const std::string layout = a.get("--index-format", nullptr, "own");
+    const std::string layout = a.get("--index-format", nullptr, "sbwt-rs");
     const int device = std::atoi(a.get("--device", nullptr, "0").c_str());
     const bool verbose = a.flag("--verbose");
     std::fprintf(stderr, "Building SBWT index from %zu files...\n", files.size());
@@ -307,11 +320,14 @@ int cmd_build(const Args &a) {
         ctx = nullptr;
     }
     if (ctx) {
-        // kbo's BuildOpts { mem_gb, temp_dir } (main.rs:111-134): -m bounds the device memory of a
-        // pass and the host memory of sorted partitions (past it: files under --temp-dir)
+        // kbo's BuildOpts { mem_gb, temp_dir } (main.rs:111-134; cli.rs:55-60: --temp-dir builds
+        // "on temporary disk space instead of in-memory", -m is the memory for that).  -m given:
+        // the device memory of a pass; else 85 % of the free HBM.  --temp-dir given: sorted
+        // partitions past -m GB of host memory go to files there; else nothing spills.
         ntc_build_opts o{};
-        o.device_budget_bytes = (uint64_t)(mem_gb * (double)(1ull << 30));
-        o.host_budget_bytes = o.device_budget_bytes;
+        const uint64_t mem = (uint64_t)(mem_gb * (double)(1ull << 30));
+        o.device_budget_bytes = mem_given ? mem : 0;
+        o.host_budget_bytes = temp.empty() ? 0 : mem;
         o.temp_dir = temp.empty() ? nullptr : temp.c_str();
         ntc_build_stats st{};
         const int rc = ntc_build_index_device_ex(ctx, seq.data(), offs.data(), offs.size() - 1, k, 1, &o, &st, &ix);

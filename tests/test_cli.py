@@ -327,6 +327,34 @@ def test_native_cli_build_equals_python_cli(tmp_path):
     assert r.returncode == 2 and b"usage" in r.stderr
 
 
+def test_cli_build_writes_sbwt_rs_layout_by_default(tmp_path):
+    """The reference always writes sbwt-rs files (kbo::index::serialize_sbwt, main.rs:138) with
+    the -p 8 prefix table (cli.rs:46): both CLIs do so by default, `--index-format own` is the
+    opt-in, and Index.load reads either."""
+    g = nt.synth_genome(7, 20_000).tobytes().decode()
+    (tmp_path / "a.fa").write_text(">a\n" + g + "\n")
+    subprocess.run([NATIVE, "build", "-o", str(tmp_path / "n"), "--builder", "host", str(tmp_path / "a.fa")],
+                   check=True, stderr=subprocess.PIPE)
+    _cli("build", "-o", str(tmp_path / "p"), "--builder", "host", str(tmp_path / "a.fa"))
+    _cli("build", "-o", str(tmp_path / "own"), "--builder", "host", "--index-format", "own", str(tmp_path / "a.fa"))
+    for ext in (".sbwt", ".lcs"):
+        assert (tmp_path / ("n" + ext)).read_bytes() == (tmp_path / ("p" + ext)).read_bytes(), ext
+    assert (tmp_path / "n.sbwt").read_bytes()[:8] != b"NTCSBWT1"
+    assert (tmp_path / "own.sbwt").read_bytes()[:8] == b"NTCSBWT1"
+    a, b = nt.Index.load(str(tmp_path / "n")), nt.Index.load(str(tmp_path / "own"))
+    assert a.prefix_table()[0] == 8 and a.k == b.k == 31 and a.n == b.n
+    assert all(np.array_equal(x, y) for x, y in zip(a.rows, b.rows)) and np.array_equal(a.lcs, b.lcs)
+
+
+def test_native_cli_rejects_unknown_options(tmp_path):
+    """clap rejects arguments it does not know (src/cli.rs); so does the native CLI, instead of
+    taking `--gpu 2` as a switch and '2' as the input file."""
+    for args in (["encode", "-i", "x", "--gpu", "2", "r.fq"], ["build", "-o", "x", "--mem", "3", "a.fa"],
+                 ["decode", "-i", "x", "--stat", "e.dat"], ["encode", "-i", "x", "--gpux=2", "r.fq"]):
+        r = subprocess.run([NATIVE, *args], stderr=subprocess.PIPE, cwd=tmp_path)
+        assert r.returncode != 0 and b"unexpected argument" in r.stderr, (args, r.stderr)
+
+
 @pytest.mark.gpu
 def test_native_cli_encode_decode_equal_python_cli(tmp_path):
     """`ntcomp encode|decode` (native) and `python -m ntcomp_amd encode|decode` write the same
@@ -335,6 +363,9 @@ def test_native_cli_encode_decode_equal_python_cli(tmp_path):
     (tmp_path / "g.fa").write_text(">g\n" + genome.tobytes().decode() + "\n")
     subprocess.run([NATIVE, "build", "-o", str(tmp_path / "idx"), "-k", "31", str(tmp_path / "g.fa")], check=True,
                    stderr=subprocess.PIPE)
+    # default flags: the sbwt-rs layout with the -p 8 prefix table, read back by encode/decode
+    assert (tmp_path / "idx.sbwt").read_bytes()[:8] != b"NTCSBWT1"
+    assert nt.Index.load(str(tmp_path / "idx")).prefix_table()[0] == 8
     n, L = 150_000, 100
     reads = nt.synth_reads(genome, 9, 0, n, L, 10_000)
     fq = tmp_path / "r.fq"
@@ -351,3 +382,24 @@ def test_native_cli_encode_decode_equal_python_cli(tmp_path):
                        stderr=subprocess.PIPE, check=True)
     lines = (tmp_path / "n.fa").read_bytes().split(b"\n")
     assert b"".join(lines[1::2]) == reads.tobytes() and lines[0] == b">seq.1"
+
+
+@pytest.mark.gpu
+def test_native_cli_build_budgets(tmp_path):
+    """-m bounds a GPU build pass's device memory; without --temp-dir nothing spills to disk
+    however small -m is (the reference builds on disk only with --temp-dir, cli.rs:58-60);
+    with it, partitions past -m GB of host memory go there.  The same index either way."""
+    genome = nt.synth_genome(3, 400_000)
+    (tmp_path / "g.fa").write_text(">g\n" + genome.tobytes().decode() + "\n")
+    outs = {}
+    for name, extra in (("mem", ["-m", "0.005"]), ("tmp", ["-m", "0.001", "--temp-dir", str(tmp_path)]),
+                        ("def", [])):
+        r = subprocess.run([NATIVE, "build", "-o", str(tmp_path / name), "--builder", "gpu", "--verbose", *extra,
+                            str(tmp_path / "g.fa")], check=True, stderr=subprocess.PIPE)
+        err = r.stderr.decode()
+        line = [x for x in err.splitlines() if x.startswith("build:")][0]
+        outs[name] = (line, (tmp_path / f"{name}.sbwt").read_bytes(), (tmp_path / f"{name}.lcs").read_bytes())
+    assert outs["mem"][1:] == outs["def"][1:] == outs["tmp"][1:]
+    assert "spilled 0 B" in outs["mem"][0] and "spilled 0 B" in outs["def"][0], outs
+    assert " 1 + 1 passes" not in outs["mem"][0], outs["mem"][0]  # -m 5 MB: several passes
+    assert "spilled 0 B" not in outs["tmp"][0], outs["tmp"][0]

@@ -158,3 +158,26 @@ def test_encode_file_text_path_equals_host_parse(ctx, tmp_path, bpb):
         finally:
             os.close(fd)
         assert e.value.code == 8, hp
+
+
+def test_gpu_fastq_parse_does_not_leak_into_encode_status(ctx):
+    """the parse reuses the context's status word and mailbox, so after
+    encode_batch -> fastq_parse, encode_status must not report the parse's base count as
+    the encode's record count: the parse was the last call, so there is no encode to
+    report (NTC_ERR_INVALID_ARG), and a fresh encode reports its own count again."""
+    g = nt.synth_genome(5, 20_000)
+    ix = nt.Index.build([g.tobytes()], 31)
+    ctx.upload(ix)
+    n, L = 300, 150
+    reads = nt.synth_reads(g, 6, 0, n, L, 10_000)
+    offs = np.arange(0, n * L + 1, L, dtype=np.uint64)
+    recs, roff = ctx.encode(reads, offs)
+    assert ctx.encode_status() == len(recs)
+    text = b"".join(b"@r\n" + reads[i * L:(i + 1) * L].tobytes() + b"\n+\n" + b"F" * L + b"\n" for i in range(n))
+    b, o = ctx.parse_fastq(text, n)
+    assert len(b) == n * L
+    with pytest.raises(nt.NtcError) as e:
+        ctx.encode_status()
+    assert e.value.code == 1
+    recs2, _ = ctx.encode(reads, offs)
+    assert np.array_equal(recs2, recs) and ctx.encode_status() == len(recs)
