@@ -725,6 +725,26 @@ struct DeflateReader : ByteReader {
     }
 };
 
+// One gzip member (or several concatenated) that is not BGZF, inflated in parallel
+// (pgzip.cpp): the reference's own `.fastq.gz` input (README.md:30), which one zlib stream
+// inflated at ~0.6 GB/s of text on one thread.
+struct ParallelGzReader : ByteReader {
+    ntc::PgzReader *r;
+    explicit ParallelGzReader(ntc::PgzReader *x) : r(x) {}
+    ~ParallelGzReader() override { ntc::pgz_close(r); }
+    int read_into(char *dst, size_t cap, size_t *got) override { return ntc::pgz_read(r, dst, cap, got); }
+    int read(char *dst, unsigned n) override {
+        size_t got = 0;
+        const int rc = ntc::pgz_read(r, dst, n, &got);
+        return rc < 0 ? -1 : (int)got;
+    }
+};
+// compressed size from which a non-BGZF gzip goes to the parallel inflater (NTC_PGZ_MIN)
+uint64_t pgz_min_bytes() {
+    const char *e = std::getenv("NTC_PGZ_MIN");
+    return e ? (uint64_t)std::atoll(e) : (4ull << 20);
+}
+
 // the reader for a path, by its first bytes; *rc = NTC_ERR_IO / NTC_ERR_UNSUPPORTED on failure
 ByteReader *open_reader(const char *path, int *rc) {
     unsigned char m[6] = {0};
@@ -756,6 +776,12 @@ ByteReader *open_reader(const char *path, int *rc) {
             const long size = std::ftell(f);
             std::rewind(f);
             const bool bgzf = hn == 18 && DeflateReader::bgzf_size(h, 18) != 0;
+            if (!bgzf && size > 0 && (uint64_t)size >= pgz_min_bytes()) {
+                if (ntc::PgzReader *pr = ntc::pgz_open(path, std::max(1, std::min(16, ntc_host_threads())))) {
+                    std::fclose(f);
+                    return new ParallelGzReader(pr);
+                }
+            }
             if (size > 0 && (bgzf || (uint64_t)size <= kWholeMax)) {
                 auto *d = new DeflateReader(path, f, (uint64_t)size, bgzf);  // owns f
                 if (d->ok) return d;

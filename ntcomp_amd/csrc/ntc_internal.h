@@ -1,5 +1,6 @@
 // Host-side internal types shared by the builder, index I/O and the C ABI.
 #pragma once
+#include <cstddef>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -41,6 +42,14 @@ void fastx_seek_mapped(ntc_fastx *fx, uint64_t pos);
 bool fastx_streamed_fastq(ntc_fastx *fx);
 uint64_t fastx_stream_read(ntc_fastx *fx, uint8_t *dst, uint64_t cap, bool *io_error);
 void fastx_stream_unread(ntc_fastx *fx, const uint8_t *src, uint64_t n);
+
+// Parallel inflate of a non-BGZF gzip file (pgzip.cpp): null when the file is not gzip.
+// pgz_read: cap bytes into dst (fewer only at the end), 1 filled, 0 the end, -1 an error
+// (corrupt or truncated data, a CRC or ISIZE mismatch).
+struct PgzReader;
+PgzReader *pgz_open(const char *path, int threads);
+int pgz_read(PgzReader *r, char *dst, size_t cap, size_t *got);
+void pgz_close(PgzReader *r);
 }  // namespace ntc
 
 struct ntc_index_host {

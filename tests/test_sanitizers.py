@@ -315,3 +315,69 @@ def test_pipeline_text_reader_edge_cases_under_sanitizers(san, encoded, tmp_path
             assert (tmp_path / f"{name}0.dat").read_bytes() == (tmp_path / f"{name}1.dat").read_bytes(), name
         else:
             assert name.startswith(("truncated", "bad_crc", "slack")), (name, got)
+
+
+def _gzip_cases():
+    """gzip inputs for the parallel inflater (pgzip.cpp): every deflate block type and zlib
+    strategy, several members, headers with a name, trailing bytes, and damaged members."""
+    import io
+    import zlib
+    rng = np.random.default_rng(3)
+    seqs = _reads(3000, 300, 4)
+    fq = b"".join(b"@r%d x\n%s\n+\n%s\n" % (i, s, b"I" * len(s)) for i, s in enumerate(seqs))
+    homo = b"".join(b"@h%d\n%s\n+\n%s\n" % (i, b"A" * 5000, b"I" * 5000) for i in range(40))
+    junk = bytes(rng.choice(list(b"ACGTNRYKMacgtn-"), 300_000))
+    fa = b"".join(b">s%d\n%s\n" % (i, junk[j:j + 3000]) for i, j in enumerate(range(0, len(junk), 3000)))
+
+    def strat(data, s):
+        c = zlib.compressobj(6, zlib.DEFLATED, 31, 8, s)
+        return c.compress(data) + c.flush()
+
+    def named(data):
+        b = io.BytesIO()
+        with gzip.GzipFile(filename="reads.fq", mode="wb", fileobj=b, mtime=0) as g:
+            g.write(data)
+        return b.getvalue()
+
+    h = len(fq) // 3
+    ok = {"l1.fq.gz": gzip.compress(fq, 1), "l6.fq.gz": gzip.compress(fq, 6), "l9.fq.gz": gzip.compress(fq, 9),
+          "stored.fq.gz": gzip.compress(fq, 0), "multi.fq.gz": gzip.compress(fq[:h], 6) + gzip.compress(fq[h:], 1),
+          "empty_first.fq.gz": gzip.compress(b"") + gzip.compress(fq),
+          "named.fq.gz": named(fq), "tail.fq.gz": gzip.compress(fq) + b"not gzip" * 9,
+          "homo.fq.gz": gzip.compress(homo, 6), "fa.fa.gz": gzip.compress(fa, 6),
+          "fixed.fq.gz": strat(fq, zlib.Z_FIXED), "huff.fq.gz": strat(fq, zlib.Z_HUFFMAN_ONLY),
+          "rle.fq.gz": strat(fq, zlib.Z_RLE), "filtered.fa.gz": strat(fa, zlib.Z_FILTERED)}
+    g6 = bytearray(ok["l6.fq.gz"])
+    crc = bytearray(g6)
+    crc[-6] ^= 1
+    isz = bytearray(g6)
+    isz[-2] ^= 1
+    flip = bytearray(g6)
+    flip[len(flip) // 2] ^= 0x5A
+    bad = {"trunc.fq.gz": bytes(g6[:-100]), "crc.fq.gz": bytes(crc), "isize.fq.gz": bytes(isz),
+           "flip.fq.gz": bytes(flip), "trunc_multi.fq.gz": ok["multi.fq.gz"][:-9]}
+    return ok, bad
+
+
+def test_parallel_gzip_under_sanitizers(san, tmp_path):
+    """Non-BGZF gzip through the parallel inflater (NTC_PGZ_MIN=0, 1-3 KiB chunks: hundreds
+    of speculative chunk starts, false candidates and gaps) under ASan/UBSan and TSan: the
+    same records as the production reader (libdeflate / zlib on one thread) for every block
+    type, and the same error for damaged members."""
+    ok, bad = _gzip_cases()
+    for name, data in {**ok, **bad}.items():
+        (tmp_path / name).write_bytes(data)
+        exp = fastx_digest(str(tmp_path / name), 500)
+        assert (exp[0] == 0) == (name in ok), (name, exp)
+        for kind, chunk in (("asan", 1024), ("tsan", 3000)):
+            env = dict(ENV, NTC_PGZ_MIN="0", NTC_PGZ_CHUNK=str(chunk))
+            r = subprocess.run([san[kind], "fastx", str(tmp_path / name), "4", "500", str(1 << 16), "1"], env=env,
+                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=600)
+            err = r.stderr.decode(errors="replace")
+            assert r.returncode == 0 and "Sanitizer" not in err and "runtime error" not in err, err[-4000:]
+            got = dict(x.split("=", 1) for x in r.stdout.decode().split())
+            if exp[0]:
+                assert int(got["rc"]) == exp[0], (name, kind, got)
+            else:
+                assert (int(got["rc"]), int(got["reads"]), int(got["bases"]), int(got["hash"], 16)) == exp, \
+                    (name, kind)
