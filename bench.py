@@ -32,6 +32,12 @@ time, against 8 TB/s.  Each read request is counted at its own size (32/64/128 B
 TCC_EA0_RDREQ_{32B,64B,128B}), writes at theirs (TCC_EA0_WRREQ, _64B), so random 64 B
 lines are not double-counted.  `line_rate` puts the request rate past L2 (reads and
 writes) against the random-line roof measured by scripts/randbw.hip.
+roofline.algorithmic: the bytes THIS design must move per launch -- encode: the distinct
+128 B lines a read's lanes touch (the emulator's line trace of encode_core.h,
+profiles/algorithmic_lines.json, scripts/trace_lines.py --json) x reads; decode: one 128 B
+walk-table line per 112 bases of each long record, plus 8 B per record in and 1 B per base
+out -- over the kernel time (algorithmic frac), and traffic / algorithmic bytes (waste:
+1.0 = every line fetched once per read).
 cpu_baseline: the faithful C oracle (oracle/ntcomp_oracle.c, test infrastructure) on one
 pinned host core, rank 0 at N = 1, on a bounded sample; it is also the parity checker.  The
 reference encoder is single-threaded (main.rs:162-173), so one core is the faithful figure;
@@ -54,6 +60,8 @@ METRIC = "encode Mbases/sec at k=91, 150bp reads, 1/2/4/8 MI355X; bit-exact vs C
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md "HBM": 8 TB/s spec
 PMC_JSON = os.path.join(REPO, "profiles", "pmc_traffic.json")
 RANDBW_JSONL = os.path.join(REPO, "profiles", "round1", "randbw.jsonl")
+ALG_JSON = os.path.join(REPO, "profiles", "algorithmic_lines.json")
+WALK_SPAN = 112  # characters per walk-table entry (encode_core.h kWalkSpan): one 128 B line each
 
 
 def log(*a):
@@ -190,6 +198,45 @@ def roofline(kname, kernel_ms, kernel_ms_min, units, unit_name, pmc, pmc_note, w
     if extra:
         r.update(extra)
     return r
+
+
+def load_alg(path):
+    try:
+        with open(path) as f:
+            return json.load(f).get("workloads", {})
+    except (OSError, ValueError):
+        return {}
+
+
+def algorithmic(bytes_per_launch, units, unit_name, kernel_ms, traffic, source):
+    """the design's own bytes per launch against the kernel time and the counter traffic"""
+    gbs = bytes_per_launch / (kernel_ms / 1e3) / 1e9
+    return {"bytes_per_launch": int(bytes_per_launch), "bytes_per_" + unit_name: round(bytes_per_launch / units, 2),
+            "achieved": round(gbs, 1), "peak": HBM_PEAK_GBPS, "frac": round(gbs / HBM_PEAK_GBPS, 4),
+            "waste": round(traffic / bytes_per_launch, 3) if traffic else None, "source": source}
+
+
+def alg_encode(alg, wl, units, kernel_ms, traffic):
+    w = alg.get(wl)
+    if not w:
+        return None
+    per = w["k_ms4_lines_per_read"] * 128
+    return algorithmic(per * units, units, "read", kernel_ms, traffic,
+                       f"{w['k_ms4_lines_per_read']} distinct 128 B lines per read (emulator trace of "
+                       f"{w['reads']} reads, encode_core.h {w['encode_core_sha256']}) x reads")
+
+
+def alg_decode(recs, bases, kernel_ms, traffic):
+    """k_dec_rec: ceil(L / 112) walk lines per long record + records in + ASCII out"""
+    import numpy as np
+    flags = recs >> np.uint64(56)
+    long_ = (flags & np.uint64(2)) == 0
+    L = ((recs[long_] >> np.uint64(32)) & np.uint64(0xFFFFFF)).astype(np.int64)
+    walk = int(((L + WALK_SPAN - 1) // WALK_SPAN).sum())
+    b = 128 * walk + 8 * len(recs) + bases
+    return algorithmic(b, bases, "base", kernel_ms, traffic,
+                       f"{walk} walk-table lines (ceil(L/{WALK_SPAN}) per long record) x 128 B + 8 B per record "
+                       f"+ 1 B per base")
 
 
 def io_floor(in_bytes, out_bytes, call_ms):
@@ -505,11 +552,14 @@ def main():
 
     nthreads = max(1, min(16, (os.cpu_count() or 8) // max(1, world)))
     pmc, pmc_note = load_pmc(args.pmc_json, nt.device_source_hash())
+    alg = load_alg(ALG_JSON)
     # counters exist for the profiled workloads only (scripts/profile_bench.sh: the defaults)
     default_wl = (args.read_len, args.err_ppm, args.genome_bp, args.strains, args.strain_snp_ppm) == \
         (150, 10_000, 5_000_000, 10, 10_000)
     if not default_wl and pmc is not None:
         pmc, pmc_note = None, "counters are profiled for the default workloads only"
+    if not default_wl:
+        alg = {}  # so are the line traces
     L, k = args.read_len, args.k
     first, n = shard_mod.read_range(rank, world, reads_per_gpu)
     line = {}
@@ -632,6 +682,7 @@ def main():
                                                   "kernel time / peak: the reference algorithm's bytes this "
                                                   "kernel's suffix table and path runs avoid; not a roofline"})
             rl["io_floor"] = io_floor(b0["bases"], 8 * n_recs * b0["n"] / n, call_ms)
+            rl["algorithmic"] = alg_encode(alg, f"C{kk}", b0["n"], kavg, rl.get("traffic"))
             if world > 1:
                 rl["aggregate"] = aggregate_roofline(gather({"traffic": rl.get("traffic"), "kernel_ms": kavg}), world)
             metric = METRIC if kk == 91 else METRIC.replace("k=91", f"k={kk}")
@@ -662,6 +713,7 @@ def main():
                            {"kernel_ms_inflight": round(kin, 4), "isolated_launches": len(iso["decode"][0])},
                            working_set=index.n * 32)
             drl["io_floor"] = io_floor(8 * n_recs * b0["n"] / n, b0["bases"], call_ms)
+            drl["algorithmic"] = alg_decode(records_of(ctx, b0, 0, b0["n"])[0], b0["bases"], kavg, drl.get("traffic"))
             if world > 1:
                 drl["aggregate"] = aggregate_roofline(gather({"traffic": drl.get("traffic"), "kernel_ms": kavg}),
                                                       world)
@@ -740,6 +792,7 @@ def main():
             srecs = s["config"]["records_per_gpu"]
             srl = roofline("k_ms4", kavg, kmin, b0["n"], "read", pmc, pmc_note, f"S{k}")
             srl["io_floor"] = io_floor(b0["bases"], 8 * srecs * b0["n"] / ns, launch_ms(pe.tms, units, b0["n"])[0])
+            srl["algorithmic"] = alg_encode(alg, f"S{k}", b0["n"], kavg, srl.get("traffic"))
             s.update(value=round(sh.bases * world * args.steps / el / 1e6, 2), unit="Mbases/s",
                      ms_per_step=round(el / args.steps * 1e3, 3), roofline=srl)
             pd = Pipe(sctx, "decode")
@@ -749,6 +802,7 @@ def main():
             sdrl = roofline("k_dec_rec", kavg, kmin, b0["bases"], "base", pmc, pmc_note, f"SD{k}",
                             working_set=index.n * 32)
             sdrl["io_floor"] = io_floor(8 * srecs * b0["n"] / ns, b0["bases"], launch_ms(pd.tms, units, b0["bases"])[0])
+            sdrl["algorithmic"] = alg_decode(records_of(ctx, b0, 0, b0["n"])[0], b0["bases"], kavg, sdrl.get("traffic"))
             s["decode"] = {"value": round(sh.bases * world * args.steps / el / 1e6, 2), "unit": "Mbases/s",
                            "ms_per_step": round(el / args.steps * 1e3, 3), "roofline": sdrl}
         secs = 0 if args.no_cpu else 3.0

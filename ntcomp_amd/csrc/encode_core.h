@@ -1018,6 +1018,7 @@ struct MsBufs {
     unsigned long long *pcnt = nullptr;  // pool entries reserved (zeroed per call)
     uint32_t *obase = nullptr;           // each overflowing read's reservation start
     unsigned long long *status = nullptr;
+    uint2 *bs = nullptr;  // k_ms4 with joint runs: each lane's binary-search best interval in LDS
 };
 // The call ran out of an overflow pool: status 0 (below every read's (read << 8 | code)), the
 // parse and emit skip, and the host grows the pool to the reserved total and runs it again.
@@ -1047,12 +1048,13 @@ NTC_HD uint32_t entry0_count(const Entry &e0) { return (e0.dk >> 8) & kNeInE0; }
 template <bool kJoint>
 struct MsLaneT {
     uint64_t qo;        // this read starts at character qo of Q; its entries at E + qo
-    uint64_t rid;       // read id (dense entry slots)
+    uint32_t rid;       // read id (dense entry slots; a call holds < 2^32 reads)
     uint64_t qw;        // query characters [qb, qb + 32) of this read, cached
     uint32_t qb;
     uint32_t len, p, d, l, r, j, ne, mode, hi, lo, l1, r1, bl, bR;
     uint32_t gj, ge;    // last run break: at position ge, node before it at path position gj (ge = 0: none)
-    uint32_t ob;        // overflow reservation of this read (kNoLimit: none, or the pool ran out)
+    // (the read's overflow reservation is read back from b.obase[rid], which reserve() writes:
+    // a register for it, live across the whole loop, cost the joint build its 7th wave)
     uint32_t vfy;       // the next run first verifies the vfy characters ending at node j
     // Joint run (note_single): path position of the interval's last node, else 0xFFFFFFFF.
     // It lives in l1, which only the binary-search probes use (written before read in
@@ -1064,7 +1066,7 @@ struct MsLaneT {
     // overlaps the other lanes' run loads instead of adding one to the read-start block
     NTC_HD void start(const DevIndex &ix, uint64_t qo_, uint32_t len_, uint64_t rid_ = 0, const uint64_t *Q = nullptr) {
         qo = qo_;
-        rid = rid_;
+        rid = (uint32_t)rid_;
         len = len_;
         qw = 0;
         qb = 0xFFFFFFFFu;
@@ -1078,7 +1080,6 @@ struct MsLaneT {
         mode = kModeFirst; lo = r1 = bl = bR = 0;
         hi = kScanW;  // SCAN width cap (hi is free while scanning)
         gj = ge = vfy = 0;
-        ob = kNoLimit;
         jy() = 0xFFFFFFFFu;
         try_run = false;
     }
@@ -1089,6 +1090,26 @@ struct MsLaneT {
         NTC_TOUCH(kTrQ, Q + ((qo + from) >> 5) + 1);
         qw = window2(Q, qo + from);
     }
+    // the binary search's best interval ext(I_lo, c): in LDS in the joint build on the device
+    // (two registers live across the loop cost it the 7th wave), else in bl / bR
+    NTC_HD void put_best(const MsBufs &b, uint32_t x, uint32_t y) {
+#ifdef __HIP_DEVICE_COMPILE__
+        if constexpr (kJoint) {
+            b.bs[stage_lane()] = make_uint2(x, y);
+            return;
+        }
+#endif
+        (void)b;
+        bl = x;
+        bR = y;
+    }
+    NTC_HD uint2 best(const MsBufs &b) const {
+#ifdef __HIP_DEVICE_COMPILE__
+        if constexpr (kJoint) return b.bs[stage_lane()];
+#endif
+        (void)b;
+        return make_uint2(bl, bR);
+    }
     NTC_HD bool covers(uint32_t x0, uint32_t x1) const { return qb != 0xFFFFFFFFu && x0 >= qb && x1 < qb + 32; }
     NTC_HD uint64_t key_at(uint32_t x, uint32_t U) const {  // U-mer ending at x (cached window)
         return (qw >> (2 * (x + 1 - U - qb))) & ((1ULL << (2 * U)) - 1);
@@ -1096,7 +1117,8 @@ struct MsLaneT {
     // Spilled entry s (entry kEntSlot + s): secondary slot s < S, else the overflow
     // reservation (null when the pool ran out: the call is re-run, nothing is read back).
     NTC_HD Entry *spill_at(const MsBufs &b, uint32_t s) const {
-        if (s < b.S) return b.Es + rid * (uint64_t)b.S + s;
+        if (s < b.S) return b.Es + (uint64_t)rid * b.S + s;
+        const uint32_t ob = b.obase[rid];  // written by reserve() (this lane, earlier)
         return ob == kNoLimit ? nullptr : b.Ep + ob + (s - b.S);
     }
     // First overflow entry, at position p_: the read has at most len - p_ entries from here
@@ -1111,10 +1133,9 @@ struct MsLaneT {
         *b.pcnt += need;
 #endif
         if (at + need <= b.pcap) {
-            ob = (uint32_t)at;
-            b.obase[rid] = ob;
+            b.obase[rid] = (uint32_t)at;
         } else {
-            ob = kNoLimit;
+            b.obase[rid] = kNoLimit;
 #ifdef __HIP_DEVICE_COMPILE__
             atomicMin(b.status, kStatusRegrow);
 #else
@@ -1141,7 +1162,7 @@ struct MsLaneT {
             return;
         }
         if (ne == kEntSlot) {
-            Entry *dst = b.Ed + rid * b.ds;
+            Entry *dst = b.Ed + (uint64_t)rid * b.ds;
 #pragma unroll
             for (uint32_t i = 1; i < kEntSlot; i++) {
                 const uint4 x = b.stage[i * 256 + t];
@@ -1155,7 +1176,7 @@ struct MsLaneT {
         if ((s & (kStageSlots - 1)) == kStageSlots - 1) flush_stage(b);
         return;
 #endif
-        Entry *dst = ne < kEntSlot ? b.Ed + rid * b.ds : spill_at(b, ne - kEntSlot);
+        Entry *dst = ne < kEntSlot ? b.Ed + (uint64_t)rid * b.ds : spill_at(b, ne - kEntSlot);
         if (dst) store_entry(dst, ne < kEntSlot ? (uint64_t)ne * b.es : 0, p_, v, m, dk);
         ne++;
     }
@@ -1185,7 +1206,7 @@ struct MsLaneT {
 #if NTC_ECOMB
         const uint32_t t = stage_lane();
         const uint32_t c = ne < kNeInE0 ? ne : kNeInE0;
-        Entry *dst = b.Ed + rid * b.ds;
+        Entry *dst = b.Ed + (uint64_t)rid * b.ds;
         if (ne > kEntSlot) {
             flush_stage(b);
             const uint4 x = b.stage[kStageSlots * 256 + t];
@@ -1950,7 +1971,8 @@ struct MsLaneT {
             uint32_t tl, tr, tj;
             tab_interval(ix, te, tl, tr, tj);
             if (d == U) return commit(ix, b, tl, tr, U);  // t* = U - 1
-            lo = U - 1; bl = tl; bR = tr;  // ext(I_{U-1}, c) = the U-mer's interval
+            lo = U - 1;  // ext(I_{U-1}, c) = the U-mer's interval
+            put_best(b, tl, tr);
             hi = d - 1;
             mode = kModeP1;
             return 0;
@@ -1964,11 +1986,15 @@ struct MsLaneT {
         extend(ix, c, ql, qr, el, er);
         if (el < er) {
             if (p1) return commit(ix, b, el, er, t + 1);
-            lo = t; bl = el; bR = er;
+            lo = t;
+            put_best(b, el, er);
         } else {
             hi = t; l1 = ql; r1 = qr;
         }
-        if (hi - lo <= 1) return commit(ix, b, bl, bR, lo + 1);
+        if (hi - lo <= 1) {
+            const uint2 bb = best(b);
+            return commit(ix, b, bb.x, bb.y, lo + 1);
+        }
         mode = kModeBs;
         return 0;
     }

@@ -231,7 +231,9 @@ struct WaveQueue {
     __device__ bool grab(uint32_t lane, uint32_t chunk, uint64_t &b, uint64_t &e) const {
         unsigned long long got = 0;
         if (lane == 0) got = atomicAdd(head, (unsigned long long)chunk);
-        got = __shfl(got, 0, 64);
+        // lane 0's value into scalar registers: the pool bounds stay wave-uniform (SGPRs)
+        got = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(got >> 32)) << 32) |
+              __builtin_amdgcn_readfirstlane((uint32_t)got);
         const uint64_t nb = lo + got;
         if (nb >= hi) return false;
         b = nb;
@@ -285,21 +287,32 @@ __device__ __forceinline__ uint32_t parse_one(const Enc4Args &a, uint64_t r) {
     return (uint32_t)rc;
 }
 
+// waves per SIMD k_ms4 is compiled for: without joint runs 8 (64 VGPRs, no scratch: 20 KB of LDS
+// per block, 8 blocks = the CU's 160 KB), with them 7 (72 VGPRs, no scratch, 22 KB of LDS).  The
+// joint build's lane state fits 72 since round 5 (32-bit read id, the overflow reservation read
+// back from obase, the binary search's best interval in LDS, the queue bounds in SGPRs): A/B on
+// one box, S91 k_ms4 10.71 -> 10.42 ms at 7 waves; C91 unchanged at 8 (2.69 -> 2.68 ms)
 #ifndef NTC_MS_WAVES
-#define NTC_MS_WAVES 6  // waves per SIMD k_ms4 is compiled for (VGPR <= 80: the batched SCAN loads fit unspilled)
+#define NTC_MS_WAVES 8
+#endif
+#ifndef NTC_MS_WAVES_J
+#define NTC_MS_WAVES_J 7
 #endif
 template <bool kJoint>
-__global__ __launch_bounds__(256, NTC_MS_WAVES) void k_ms4(Enc4Args a) {
+__global__ __launch_bounds__(256, kJoint ? NTC_MS_WAVES_J : NTC_MS_WAVES) void k_ms4(Enc4Args a) {
     const uint32_t lane = threadIdx.x & 63;
     if (*a.status != ~0ull) return;  // a read failed to pack: nothing to do
     const uint64_t o0 = a.offs[0];
     uint64_t pool_lo = 0, pool_hi = 0;
     bool exhausted = false, idle = true;
-    uint64_t rd = 0;
     const WaveQueue wq(a.counter, a.n_reads);
     __shared__ uint4 s_stage[(kStageSlots + 1) * 256];  // MsLane::put_entry write combining, entry 0
+    // (joint build) the binary search's best interval: 2 KB per block, 7 blocks per CU at 7 waves
+    // per SIMD = 157.5 KB of the 160 KB of LDS
+    __shared__ uint2 s_best[kJoint ? 256 : 1];
     // dense slots read-major, secondary slots and the overflow pool sized by need
-    const MsBufs bufs{a.Q, a.Es, a.Ed, 1, s_stage, kEntSlot, a.S, a.Ep, a.pcap, a.counter + kPoolCntE, a.obase, a.status};
+    const MsBufs bufs{a.Q,    a.Es,    a.Ed,      1,   s_stage, kEntSlot, a.S, a.Ep, a.pcap, a.counter + kPoolCntE,
+                      a.obase, a.status, s_best};
     MsLaneT<kJoint> st;
     for (;;) {
         // ---- hand idle lanes the next reads (wave-uniform control flow) ----------------
@@ -309,7 +322,7 @@ __global__ __launch_bounds__(256, NTC_MS_WAVES) void k_ms4(Enc4Args a) {
             const uint32_t rank = (uint32_t)__popcll(want & ((1ULL << lane) - 1));
             const uint64_t avail = pool_hi - pool_lo;
             if (idle && rank < avail) {
-                rd = pool_lo + rank;
+                const uint64_t rd = pool_lo + rank;
                 idle = false;
                 const uint64_t b = a.offs[rd], e = a.offs[rd + 1];
                 const uint64_t P = b - o0;
@@ -330,10 +343,10 @@ __global__ __launch_bounds__(256, NTC_MS_WAVES) void k_ms4(Enc4Args a) {
             const int rc = st.step(a.ix, bufs);
             if (rc != 0) {
                 if (rc < 0) {
-                    atomicMin(a.status, (unsigned long long)((rd << 8) | (uint64_t)(-rc)));
-                    a.ne[rd] = 0;
+                    atomicMin(a.status, (unsigned long long)(((uint64_t)st.rid << 8) | (uint64_t)(-rc)));
+                    a.ne[st.rid] = 0;
                 } else if (st.finish(bufs)) {
-                    a.ne[rd] = st.ne;
+                    a.ne[st.rid] = st.ne;
                 }
                 idle = true;
             }

@@ -47,6 +47,9 @@ def main():
     ap.add_argument("--group", type=int, default=1, help="count distinct lines per this many consecutive reads")
     ap.add_argument("--order", choices=["input", "minimizer"], default="input",
                     help="process reads as generated, or grouped by their minimizer (locality experiment)")
+    ap.add_argument("--json", help="merge this workload's lines per read into this JSON file "
+                                   "(profiles/algorithmic_lines.json, read by bench.py)")
+    ap.add_argument("--label", help="workload key in --json (C91, C31, S91)")
     ap.add_argument("--waves", action="store_true",
                     help="also run one 64-lane wave in lock step (emu_wave_modes): iterations and steps per read")
     args = ap.parse_args()
@@ -90,6 +93,28 @@ def main():
             if req[ph][i] > 0:
                 extra = f"  (also touched by ms: {ov[i] / n:5.2f})" if ph == 1 else ""
                 print(f"   {KINDS[i]:12s} loads {req[ph][i]:7.2f}  lines {lines[ph][i]:6.2f}{extra}")
+    if args.json:
+        import hashlib
+        import json
+        core = os.path.join(REPO, "ntcomp_amd", "csrc", "encode_core.h")
+        try:
+            with open(args.json) as f:
+                j = json.load(f)
+        except (OSError, ValueError):
+            j = {}
+        j["note"] = ("distinct 128-byte lines each read touches in the encode lanes (tests/emu emulator of "
+                     "encode_core.h, NTC_TRACE), per kernel phase: the algorithmic traffic of this design, "
+                     "scripts/trace_lines.py --json")
+        j.setdefault("workloads", {})[args.label] = {
+            "encode_core_sha256": hashlib.sha256(open(core, "rb").read()).hexdigest()[:16],
+            "reads": n, "k": args.k, "genome_bp": args.genome_bp, "strains": args.strains,
+            "err_ppm": args.err_ppm, "records_per_read": round(len(recs) / n, 4),
+            "k_ms4_lines_per_read": round(float(lines[0].sum()), 4),
+            "k_parse4_lines_per_read": round(float(lines[1].sum()), 4),
+            "k_ms4_by_structure": {KINDS[i]: round(float(lines[0][i]), 4) for i in range(K) if lines[0][i] > 0},
+            "k_parse4_by_structure": {KINDS[i]: round(float(lines[1][i]), 4) for i in range(K) if lines[1][i] > 0}}
+        with open(args.json, "w") as f:
+            json.dump(j, f, indent=1, sort_keys=True)
     if st.any():  # NTC_STAT counters of the MS lanes (encode_core.h), per read
         print("-- unit counters per read: " + ", ".join(f"[{i}] {st[i] / n:.2f}" for i in range(16) if st[i]))
     if args.waves:
