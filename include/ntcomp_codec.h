@@ -121,6 +121,32 @@ int ntc_encode_pack_batch(ntc_ctx *ctx, const uint8_t *bases, const uint64_t *re
                           uint32_t block_reads, ntc_block_meta *meta, uint8_t **payload, uint64_t *payload_bytes,
                           int64_t *bad_read);
 
+/* ---- GPU unpacker (the inverse of the packer) ------------------------------------------ */
+/* decode_block (src/lib.rs:320-368) split at inflate.  ntc_read_block_streams (host): one
+ * block's four stream headers at data[0..len) and their gzip members inflated into
+ * payload[0..capacity) (stream i at meta->stream[i].offset, 8-byte aligned, exactly
+ * encoded_size words each: the big-endian words compress_block wrote); meta->n_recs = the
+ * block's records (its flag stream's values), num_records its header field.  Returns what
+ * ntc_read_block_into returns for a block it cannot read (NTC_ERR_IO at a clean end,
+ * NTC_ERR_FORMAT damaged, NTC_ERR_CAPACITY past capacity).
+ * ntc_unpack_streams (GPU): payload[0..payload_bytes) holding n_blocks blocks' streams at
+ * their metas' offsets -> the blocks' u64 records in the context's device memory, in
+ * block order: rice_decode / minimal_binary_decode / zip_block_contents
+ * (src/decode.rs:51-149) on the device.  *n_blocks_ok = the blocks before the first
+ * damaged one (a meta with status != 0, or one the device cannot decode: decode_block's
+ * Err ends the reference's loop, main.rs:202); *n_reads / *n_bases = what those blocks'
+ * records hold.  Synchronous.
+ * ntc_unpacked_records: those records to the host (tests).  ntc_decode_fasta_unpacked:
+ * ntc_decode_fasta of those records without their trip through host memory (*out_len =
+ * the text's bytes; NTC_ERR_CAPACITY past out_capacity, so capacity 0 asks the size).    */
+int ntc_read_block_streams(const uint8_t *data, uint64_t len, uint64_t *consumed, uint8_t *payload,
+                           uint64_t capacity, ntc_block_meta *meta);
+int ntc_unpack_streams(ntc_ctx *ctx, const uint8_t *payload, uint64_t payload_bytes, const ntc_block_meta *metas,
+                       uint64_t n_blocks, uint64_t *n_blocks_ok, uint64_t *n_reads, uint64_t *n_bases);
+int ntc_unpacked_records(ntc_ctx *ctx, uint64_t *recs, uint64_t capacity, uint64_t *n_recs);
+int ntc_decode_fasta_unpacked(ntc_ctx *ctx, uint64_t first_id, uint8_t *out, uint64_t out_capacity,
+                              uint64_t *out_len);
+
 /* ---- FASTQ parsed on the GPU ------------------------------------------------------------ */
 /* The CLI's ingest (src/main.rs:158-163: needletail records + normalize(true)) for plain
  * FASTQ, done on the device: fastq[0, fastq_bytes) is the text of exactly n_reads records of

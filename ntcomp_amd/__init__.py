@@ -41,7 +41,8 @@ EXPORTED = [
     "ntc_index_view_of", "ntc_index_save", "ntc_index_save_as", "ntc_index_load", "ntc_synth_genome", "ntc_synth_strains", "ntc_synth_reads", "ntc_minimizer_keys",
     "ntc_file_header", "ntc_write_block", "ntc_read_block", "ntc_buffer_free", "ntc_pack_block",
     "ntc_deflate_block", "ntc_deflate_stream", "ntc_pack_blocks_device", "ntc_encode_pack_batch", "ntc_fastq_parse",
-    "ntc_encode_pack_fastq", "ntc_read_block_into",
+    "ntc_encode_pack_fastq", "ntc_read_block_into", "ntc_read_block_streams", "ntc_unpack_streams",
+    "ntc_unpacked_records", "ntc_decode_fasta_unpacked",
     "ntc_fastx_open", "ntc_fastx_next_batch", "ntc_fastx_close", "ntc_fasta_format", "ntc_fastx_next_batch_into",
     "ntc_fastx_set_threads", "ntc_host_threads", "ntc_encode_file", "ntc_decode_fasta",
     "ntc_decode_file", "ntc_build_index_device", "ntc_build_index_device_ex", "ntc_index_set_prefix_precalc",
@@ -221,6 +222,10 @@ def lib():
         "ntc_fasta_format": (I, [P, P, u64, u64, ctypes.POINTER(P), ctypes.POINTER(u64)]),
         "ntc_decode_fasta": (I, [P, P, u64, u64, u64, u64, P, u64, ctypes.POINTER(u64)]),
         "ntc_decode_file": (I, [P, I, ctypes.c_char_p, I, ctypes.POINTER(PipelineOpts), ctypes.POINTER(PipelineStats)]),
+        "ntc_read_block_streams": (I, [P, u64, ctypes.POINTER(u64), P, u64, ctypes.POINTER(BlockMeta)]),
+        "ntc_unpack_streams": (I, [P, P, u64, P, u64, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
+        "ntc_unpacked_records": (I, [P, P, u64, ctypes.POINTER(u64)]),
+        "ntc_decode_fasta_unpacked": (I, [P, u64, P, u64, ctypes.POINTER(u64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -565,6 +570,34 @@ class GpuContext:
         self._check(self.L.ntc_decode_status(self.h, ctypes.byref(nr), ctypes.byref(nb)), "ntc_decode_status")
         return int(nr.value), int(nb.value)
 
+    def unpack(self, metas, payload, n_blocks=None):
+        """GPU unpacker (ntc_unpack_streams): blocks' inflated streams -> records in HBM ->
+        (blocks decoded before the first damaged one, reads, bases)."""
+        n = len(metas) if n_blocks is None else n_blocks
+        buf = np.frombuffer(bytes(payload), dtype=np.uint8) if len(payload) else np.zeros(8, dtype=np.uint8)
+        ok, nr, nb = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(self.L.ntc_unpack_streams(self.h, _p(buf), len(payload), ctypes.cast(metas, ctypes.c_void_p), n,
+                                              ctypes.byref(ok), ctypes.byref(nr), ctypes.byref(nb)),
+                    "ntc_unpack_streams")
+        return int(ok.value), int(nr.value), int(nb.value)
+
+    def unpacked_records(self):
+        n = ctypes.c_uint64()
+        self.L.ntc_unpacked_records(self.h, None, 0, ctypes.byref(n))
+        out = np.zeros(max(1, n.value), dtype=np.uint64)
+        self._check(self.L.ntc_unpacked_records(self.h, _p(out), len(out), ctypes.byref(n)), "ntc_unpacked_records")
+        return out[:n.value]
+
+    def decode_fasta_unpacked(self, first_id=1):
+        need = ctypes.c_uint64()
+        rc = self.L.ntc_decode_fasta_unpacked(self.h, first_id, None, 0, ctypes.byref(need))
+        if rc not in (0, 5):
+            self._check(rc, "ntc_decode_fasta_unpacked")
+        out = np.zeros(max(1, need.value), dtype=np.uint8)
+        self._check(self.L.ntc_decode_fasta_unpacked(self.h, first_id, _p(out), len(out), ctypes.byref(need)),
+                    "ntc_decode_fasta_unpacked")
+        return out[:need.value].tobytes()
+
     def synchronize(self):
         self._check(self.L.ntc_ctx_synchronize(self.h), "ntc_ctx_synchronize")
 
@@ -738,6 +771,45 @@ def read_block(data):
     finally:
         lib().ntc_buffer_free(recs)
     return arr, int(used.value), int(nrec.value)
+
+
+def read_block_streams(data):
+    """The host half of decode_block for the GPU unpacker (ntc_read_block_streams): one
+    block's stream headers + inflated streams -> (BlockMeta, payload bytes, bytes consumed).
+    NtcError(NTC_ERR_IO) at a clean end of input."""
+    buf = np.frombuffer(bytes(data), dtype=np.uint8) if len(data) else np.zeros(1, dtype=np.uint8)
+    used, meta = ctypes.c_uint64(), BlockMeta()
+    # the payload is at most 8x the gzip'd bytes' inflated size; ask the headers first
+    cap = 0
+    pos = 0
+    for _ in range(4):
+        if pos + 32 > len(data):
+            break
+        h = bytes(data[pos:pos + 32])
+        cap += 8 * int.from_bytes(h[12:16], "little")
+        pos += 32 + int.from_bytes(h[0:4], "little")
+    pay = np.zeros(max(cap, 8), dtype=np.uint8)
+    rc = lib().ntc_read_block_streams(_p(buf), len(data), ctypes.byref(used), _p(pay), cap, ctypes.byref(meta))
+    if rc:
+        raise NtcError(rc, "ntc_read_block_streams")
+    return meta, pay[:cap].tobytes(), int(used.value)
+
+
+def concat_streams(blocks):
+    """(meta, payload) pairs -> one payload and the metas with their offsets moved into it
+    (each block's streams stay 8-byte aligned): the input of GpuContext.unpack."""
+    metas = (BlockMeta * max(1, len(blocks)))()
+    parts, off = [], 0
+    for i, (m, pay) in enumerate(blocks):
+        mm = BlockMeta()
+        ctypes.memmove(ctypes.byref(mm), ctypes.byref(m), ctypes.sizeof(BlockMeta))
+        for s in range(4):
+            mm.stream[s].offset = m.stream[s].offset + off
+        metas[i] = mm
+        pad = (-len(pay)) % 8
+        parts.append(bytes(pay) + b"\0" * pad)
+        off += len(pay) + pad
+    return metas, b"".join(parts)
 
 
 # ---- FASTX ingest ---------------------------------------------------------------------

@@ -40,6 +40,7 @@
 #include <vector>
 
 #include "../../include/ntcomp_codec.h"
+#include "ntc_internal.h"
 #include "codec_params.h"
 
 namespace {
@@ -630,24 +631,10 @@ int ntc_write_block(const uint64_t *recs, uint64_t n_recs, uint64_t num_records,
 }  // extern "C"
 
 namespace {
-// decode_block's container half (lib.rs:320-363): the block's four streams, decompressed and
-// zipped back into u64 records (zip_block_contents, decode.rs:102-149), into vec (resized)
-// or out (cap records; NTC_ERR_CAPACITY if more).  *n_recs = the block's record count.
-int read_block_impl(const uint8_t *data, uint64_t len, uint64_t *consumed, std::vector<uint64_t> *vec, uint64_t *out,
-                    uint64_t cap, uint64_t *n_recs, uint64_t *num_records) {
-    *n_recs = 0;
-    *consumed = 0;
-    uint64_t pos = 0;
-    std::vector<uint64_t> parts[4];
-    BlockHeader hs[4];
-    for (int s = 0; s < 4; s++) {
-        if (pos + 32 > len) return s == 0 && pos == len ? NTC_ERR_IO : NTC_ERR_FORMAT;  // IO = clean EOF
-        hs[s] = read_header(data + pos);
-        pos += 32;
-        if (pos + hs[s].block_size > len) return NTC_ERR_FORMAT;
-        if (!decompress_block(data + pos, hs[s], s == 1 || s == 2, parts[s])) return NTC_ERR_FORMAT;
-        pos += hs[s].block_size;
-    }
+// zip_block_contents (decode.rs:102-149): the four decoded streams -> u64 records, into vec
+// (resized) or out (cap records; NTC_ERR_CAPACITY if more).  *n_recs = the block's records.
+int zip_parts(const std::vector<uint64_t> (&parts)[4], std::vector<uint64_t> *vec, uint64_t *out, uint64_t cap,
+              uint64_t *n_recs) {
     const auto &c1 = parts[0], &c2 = parts[1], &fl = parts[2], &bn = parts[3];
     if (c1.size() != c2.size()) return NTC_ERR_FORMAT;
     uint64_t T = 0;
@@ -657,8 +644,6 @@ int read_block_impl(const uint8_t *data, uint64_t len, uint64_t *consumed, std::
     // (Appendix B.4); ((T-1) % 31) + 1 agrees everywhere else
     if (T ? bn.size() != (T + 30) / 31 : false) return NTC_ERR_FORMAT;
     *n_recs = fl.size();
-    if (num_records) *num_records = hs[0].num_records;
-    *consumed = pos;
     if (vec) {
         vec->resize(fl.size());
         out = vec->data();
@@ -690,7 +675,55 @@ int read_block_impl(const uint8_t *data, uint64_t len, uint64_t *consumed, std::
     }
     return NTC_OK;
 }
+
+// decode_block's container half (lib.rs:320-363): the block's four streams, decompressed and
+// zipped back into u64 records (zip_block_contents, decode.rs:102-149), into vec (resized)
+// or out (cap records; NTC_ERR_CAPACITY if more).  *n_recs = the block's record count.
+int read_block_impl(const uint8_t *data, uint64_t len, uint64_t *consumed, std::vector<uint64_t> *vec, uint64_t *out,
+                    uint64_t cap, uint64_t *n_recs, uint64_t *num_records) {
+    *n_recs = 0;
+    *consumed = 0;
+    uint64_t pos = 0;
+    std::vector<uint64_t> parts[4];
+    BlockHeader hs[4];
+    for (int s = 0; s < 4; s++) {
+        if (pos + 32 > len) return s == 0 && pos == len ? NTC_ERR_IO : NTC_ERR_FORMAT;  // IO = clean EOF
+        hs[s] = read_header(data + pos);
+        pos += 32;
+        if (pos + hs[s].block_size > len) return NTC_ERR_FORMAT;
+        if (!decompress_block(data + pos, hs[s], s == 1 || s == 2, parts[s])) return NTC_ERR_FORMAT;
+        pos += hs[s].block_size;
+    }
+    const int rc = zip_parts(parts, vec, out, cap, n_recs);
+    if (rc == NTC_OK || rc == NTC_ERR_CAPACITY) {
+        *consumed = pos;
+        if (num_records) *num_records = hs[0].num_records;
+    }
+    return rc;
+}
 }  // namespace
+
+namespace ntc {
+// The GPU unpacker's work on the host (the sanitizer builds' stand-in for the device): one
+// block's inflated streams (payload at meta's offsets) -> records; NTC_ERR_FORMAT if damaged.
+int unpack_block_host(const ntc_block_meta &m, const uint8_t *payload, std::vector<uint64_t> &recs) {
+    std::vector<uint64_t> parts[4];
+    for (int s = 0; s < 4; s++) {
+        const ntc_stream_meta &st = m.stream[s];
+        std::vector<uint64_t> words(st.encoded_size);
+        for (uint64_t i = 0; i < st.encoded_size; i++) {
+            uint64_t w;
+            std::memcpy(&w, payload + st.offset + 8 * i, 8);
+            words[i] = bswap64(w);
+        }
+        const bool ok = (s == 1 || s == 2) ? rice_decode(words, st.num_u64, st.param, parts[s])
+                                           : minimal_binary_decode(words, st.num_u64, st.param, parts[s]);
+        if (!ok) return NTC_ERR_FORMAT;
+    }
+    uint64_t n = 0;
+    return zip_parts(parts, &recs, nullptr, 0, &n);
+}
+}  // namespace ntc
 
 extern "C" {
 
@@ -711,6 +744,45 @@ int ntc_read_block(const uint8_t *data, uint64_t len, uint64_t *consumed, uint64
     std::memcpy(buf, v.data(), v.size() * 8);
     *recs = buf;
     *consumed = used;
+    return NTC_OK;
+}
+
+int ntc_read_block_streams(const uint8_t *data, uint64_t len, uint64_t *consumed, uint8_t *payload,
+                           uint64_t capacity, ntc_block_meta *meta) {
+    if (!data || !consumed || !meta || (capacity && !payload)) return NTC_ERR_INVALID_ARG;
+    *consumed = 0;
+    std::memset(meta, 0, sizeof(*meta));
+    uint64_t pos = 0, off = 0;
+    BlockHeader hs[4];
+    for (int s = 0; s < 4; s++) {
+        if (pos + 32 > len) return s == 0 && pos == len ? NTC_ERR_IO : NTC_ERR_FORMAT;  // IO = clean EOF
+        hs[s] = read_header(data + pos);
+        pos += 32;
+        if (pos + hs[s].block_size > len) return NTC_ERR_FORMAT;
+        const uint64_t want = (uint64_t)hs[s].encoded_size * 8;
+        if (off + want > capacity) return NTC_ERR_CAPACITY;
+        // libdeflate straight into the payload; zlib through a vector
+        LibInflate &L = libinflate();
+        bool ok = false;
+        if (L.ok && (tl_decompressor.d || (tl_decompressor.d = L.alloc_d()))) {
+            size_t got = 0;
+            ok = L.gz_d(tl_decompressor.d, data + pos, hs[s].block_size, payload + off, want, &got) == 0 && got == want;
+        } else {
+            std::vector<uint8_t> v;
+            ok = gunzip_bytes(data + pos, hs[s].block_size, v) && v.size() == want;
+            if (ok && want) std::memcpy(payload + off, v.data(), want);
+        }
+        if (!ok) return NTC_ERR_FORMAT;
+        meta->stream[s].num_u64 = hs[s].num_u64;
+        meta->stream[s].encoded_size = hs[s].encoded_size;
+        meta->stream[s].param = hs[s].rice_param;
+        meta->stream[s].offset = off;
+        off += want;
+        pos += hs[s].block_size;
+    }
+    meta->num_records = hs[0].num_records;
+    meta->n_recs = hs[2].num_u64;
+    *consumed = pos;
     return NTC_OK;
 }
 

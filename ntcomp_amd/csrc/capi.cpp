@@ -40,7 +40,8 @@ enum WsSlot {
     WS_STAGE_BASES, WS_STAGE_OFFS, WS_STAGE_RECS, WS_E, WS_DEC_A, WS_DEC_B, WS_DEC_C,
     WS_DEC_D, WS_Q, WS_E3, WS_NE, WS_COUNTER, WS_R2, WS_ED, WS_WAVECNT, WS_PACK_CHUNKS, WS_PACK_META,
     WS_PACK_PAYLOAD, WS_FA_BASES, WS_FA_OFFS, WS_FA_SCAN, WS_ES, WS_OBASE,
-    WS_FQ_RAW, WS_FQ_TILES, WS_FQ_NL, WS_FQ_KEPT, WS_PACK_SEGS, WS_COUNT
+    WS_FQ_RAW, WS_FQ_TILES, WS_FQ_NL, WS_FQ_KEPT, WS_PACK_SEGS,
+    WS_UNP_PAY, WS_UNP_MARKS, WS_UNP_ST, WS_UNP_VALS, WS_UNP_RECS, WS_UNP_OUT, WS_COUNT
 };
 
 // The device index of one upload: freed with the last context that holds it
@@ -72,6 +73,9 @@ struct ntc_ctx {
     // at the end of a device call, so *_status() is one stream sync instead of D2H copies
     uint64_t *h_box = nullptr;
     bool box_valid = false;
+    // the records of the last ntc_unpack_streams (in WS_UNP_RECS) and their read / base counts
+    uint64_t *unp_d_recs = nullptr;
+    uint64_t unp_recs = 0, unp_reads = 0, unp_bases = 0;
     // last call
     CallKind last = kNone;
     uint64_t last_n = 0;           // reads (encode) / records (decode)
@@ -1595,13 +1599,11 @@ int ntc_encode_pack_fastq(ntc_ctx *ctx, const uint8_t *fastq, uint64_t fastq_byt
                               meta, payload, payload_bytes, bad_read);
 }
 
-int ntc_decode_fasta(ntc_ctx *ctx, const uint64_t *recs, uint64_t n_recs, uint64_t n_reads, uint64_t n_bases,
-                     uint64_t first_id, uint8_t *out, uint64_t out_capacity, uint64_t *out_len) {
-    if (!ctx || !out_len || (n_recs && !recs) || (n_reads && !out)) return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument");
-    HIP_TRY(ctx, hipSetDevice(ctx->device));
-    *out_len = 0;
-    if (!ctx->has_index) return set_err(ctx, NTC_ERR_NO_INDEX, "no index uploaded");
-    // bytes of ">seq.{id}\n" + read + "\n" for ids first_id .. first_id + n_reads - 1
+}  // extern "C"
+
+namespace {
+// bytes of ">seq.{id}\n" + read + "\n" for ids first_id .. first_id + n_reads - 1
+uint64_t fasta_bytes(uint64_t n_reads, uint64_t n_bases, uint64_t first_id) {
     uint64_t need = n_bases + 7 * n_reads;  // 5 + 2 per read, plus the digits
     for (uint64_t lo = 1, d = 1; lo <= first_id + n_reads - 1 && n_reads; lo *= 10, d++) {
         const uint64_t hi = lo > UINT64_MAX / 10 ? UINT64_MAX : lo * 10 - 1;  // ids with d digits: [lo, hi]
@@ -1609,19 +1611,20 @@ int ntc_decode_fasta(ntc_ctx *ctx, const uint64_t *recs, uint64_t n_recs, uint64
         if (a <= b) need += d * (b - a + 1);
         if (hi == UINT64_MAX) break;
     }
-    *out_len = need;
-    if (need > out_capacity) return set_err(ctx, NTC_ERR_CAPACITY, "out_capacity smaller than the FASTA text");
-    if (n_recs == 0) return n_reads ? set_err(ctx, NTC_ERR_FORMAT, "reads without records") : NTC_OK;
-    void *d_recs, *d_bases, *d_offs, *d_scan, *d_out;
+    return need;
+}
+
+// walk + FASTA text of records already in HBM (d_recs), text D2H into out (need bytes)
+int decode_fasta_dev(ntc_ctx *ctx, const uint64_t *d_recs, uint64_t n_recs, uint64_t n_reads, uint64_t n_bases,
+                     uint64_t first_id, uint8_t *out, uint64_t need) {
+    void *d_bases, *d_offs, *d_scan, *d_out;
     int rc;
-    if ((rc = ensure(ctx, WS_STAGE_RECS, n_recs * 8, &d_recs))) return rc;
     if ((rc = ensure(ctx, WS_FA_BASES, n_bases + 64, &d_bases))) return rc;
     if ((rc = ensure(ctx, WS_FA_OFFS, (n_reads + 2) * 8, &d_offs))) return rc;
     if ((rc = ensure(ctx, WS_FA_SCAN, (2 * (n_reads + 1) + scan_tmp_words(n_reads + 1)) * 8, &d_scan))) return rc;
     if ((rc = ensure(ctx, WS_STAGE_BASES, need + 64, &d_out))) return rc;
-    HIP_TRY(ctx, hipMemcpyAsync(d_recs, recs, n_recs * 8, hipMemcpyHostToDevice, ctx->stream));
-    if ((rc = ntc_decode_batch_device(ctx, (const uint64_t *)d_recs, n_recs, (uint8_t *)d_bases, n_bases + 64,
-                                      (uint64_t *)d_offs, n_reads + 2)))
+    if ((rc = ntc_decode_batch_device(ctx, d_recs, n_recs, (uint8_t *)d_bases, n_bases + 64, (uint64_t *)d_offs,
+                                      n_reads + 2)))
         return rc;
     uint64_t *sizes = (uint64_t *)d_scan, *out_offs = sizes + (n_reads + 1), *tmp = out_offs + (n_reads + 1);
     launch_fasta((const uint8_t *)d_bases, (const uint64_t *)d_offs, n_reads, first_id, ctx->d_status, sizes, out_offs,
@@ -1633,6 +1636,114 @@ int ntc_decode_fasta(ntc_ctx *ctx, const uint64_t *recs, uint64_t n_recs, uint64
     if (nr != n_reads || nb != n_bases)
         return set_err(ctx, NTC_ERR_FORMAT, "records hold other read / base counts than given");
     return NTC_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int ntc_decode_fasta(ntc_ctx *ctx, const uint64_t *recs, uint64_t n_recs, uint64_t n_reads, uint64_t n_bases,
+                     uint64_t first_id, uint8_t *out, uint64_t out_capacity, uint64_t *out_len) {
+    if (!ctx || !out_len || (n_recs && !recs) || (n_reads && !out)) return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    *out_len = 0;
+    if (!ctx->has_index) return set_err(ctx, NTC_ERR_NO_INDEX, "no index uploaded");
+    const uint64_t need = fasta_bytes(n_reads, n_bases, first_id);
+    *out_len = need;
+    if (need > out_capacity) return set_err(ctx, NTC_ERR_CAPACITY, "out_capacity smaller than the FASTA text");
+    if (n_recs == 0) return n_reads ? set_err(ctx, NTC_ERR_FORMAT, "reads without records") : NTC_OK;
+    void *d_recs;
+    int rc;
+    if ((rc = ensure(ctx, WS_STAGE_RECS, n_recs * 8, &d_recs))) return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(d_recs, recs, n_recs * 8, hipMemcpyHostToDevice, ctx->stream));
+    return decode_fasta_dev(ctx, (const uint64_t *)d_recs, n_recs, n_reads, n_bases, first_id, out, need);
+}
+
+int ntc_unpack_streams(ntc_ctx *ctx, const uint8_t *payload, uint64_t payload_bytes, const ntc_block_meta *metas,
+                       uint64_t n_blocks, uint64_t *n_blocks_ok, uint64_t *n_reads, uint64_t *n_bases) {
+    if (!ctx || (n_blocks && (!metas || !payload)) || !n_blocks_ok) return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    *n_blocks_ok = 0;
+    if (n_reads) *n_reads = 0;
+    if (n_bases) *n_bases = 0;
+    ctx->unp_recs = 0;
+    ctx->unp_reads = ctx->unp_bases = 0;
+    if (n_blocks == 0) return NTC_OK;
+    // stream descriptors: word offsets into the payload, value offsets, record offsets
+    std::vector<UnpackStream> st(4 * n_blocks);
+    std::vector<uint64_t> roff(n_blocks + 1, 0);
+    uint64_t nv = 0;
+    const uint64_t pay_words = (payload_bytes + 7) / 8;
+    for (uint64_t b = 0; b < n_blocks; b++) {
+        for (int i = 0; i < 4; i++) {
+            const ntc_stream_meta &m = metas[b].stream[i];
+            if ((m.offset & 7) || m.offset / 8 + m.encoded_size > pay_words)
+                return set_err(ctx, NTC_ERR_INVALID_ARG, "stream outside the payload or not 8-byte aligned");
+            st[4 * b + i] = UnpackStream{m.offset / 8, m.encoded_size, m.num_u64, m.param, nv};
+            nv += m.num_u64;
+        }
+        roff[b + 1] = roff[b] + metas[b].stream[2].num_u64;  // one flag per record
+    }
+    void *d_pay, *d_marks, *d_st, *d_vals, *d_recs, *d_out;
+    int rc;
+    if ((rc = ensure(ctx, WS_UNP_PAY, pay_words * 8 + 16, &d_pay))) return rc;
+    if ((rc = ensure(ctx, WS_UNP_MARKS, pay_words * 8 + 16, &d_marks))) return rc;
+    if ((rc = ensure(ctx, WS_UNP_ST, st.size() * sizeof(UnpackStream) + (n_blocks + 1) * 8, &d_st))) return rc;
+    if ((rc = ensure(ctx, WS_UNP_VALS, nv * 8 + 8, &d_vals))) return rc;
+    if ((rc = ensure(ctx, WS_UNP_RECS, roff[n_blocks] * 8 + 8, &d_recs))) return rc;
+    uint64_t max_recs = 0;
+    for (uint64_t b = 0; b < n_blocks; b++) max_recs = std::max<uint64_t>(max_recs, metas[b].stream[2].num_u64);
+    const uint64_t segw = unpack_seg_words(n_blocks, max_recs);
+    if ((rc = ensure(ctx, WS_UNP_OUT, n_blocks * 3 * 8 + segw * 8 + 4 * n_blocks * 4 + 8, &d_out))) return rc;
+    uint64_t *d_roff = (uint64_t *)((uint8_t *)d_st + st.size() * sizeof(UnpackStream));
+    uint64_t *d_out3 = (uint64_t *)d_out, *d_segc = d_out3 + 3 * n_blocks;
+    int32_t *d_sst = (int32_t *)(d_segc + segw);
+    HIP_TRY(ctx, hipMemcpyAsync(d_pay, payload, payload_bytes, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(d_st, st.data(), st.size() * sizeof(UnpackStream), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(d_roff, roff.data(), (n_blocks + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+    launch_unpack((const uint64_t *)d_pay, (const UnpackStream *)d_st, n_blocks, max_recs, (uint64_t *)d_marks,
+                  (uint64_t *)d_vals, d_sst, d_roff, (uint64_t *)d_recs, d_segc, d_out3, ctx->stream);
+    HIP_TRY(ctx, hipGetLastError());
+    std::vector<uint64_t> o3(3 * n_blocks);
+    HIP_TRY(ctx, hipMemcpyAsync(o3.data(), d_out3, 3 * n_blocks * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    // the blocks before the first damaged one (decode_block's Err ends the reference's loop,
+    // main.rs:202); a block the host already found damaged (meta status) ends it as well
+    uint64_t ok = 0, rd = 0, bs = 0;
+    for (; ok < n_blocks && o3[3 * ok + 2] == 0 && metas[ok].status == 0; ok++) {
+        rd += o3[3 * ok];
+        bs += o3[3 * ok + 1];
+    }
+    *n_blocks_ok = ok;
+    if (n_reads) *n_reads = rd;
+    if (n_bases) *n_bases = bs;
+    ctx->unp_d_recs = (uint64_t *)d_recs;
+    ctx->unp_recs = roff[ok];
+    ctx->unp_reads = rd;
+    ctx->unp_bases = bs;
+    return NTC_OK;
+}
+
+int ntc_unpacked_records(ntc_ctx *ctx, uint64_t *recs, uint64_t capacity, uint64_t *n_recs) {
+    if (!ctx || !n_recs || (capacity && !recs)) return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    *n_recs = ctx->unp_recs;
+    if (ctx->unp_recs > capacity) return set_err(ctx, NTC_ERR_CAPACITY, "capacity smaller than the unpacked records");
+    if (ctx->unp_recs)
+        HIP_TRY(ctx, hipMemcpy(recs, ctx->unp_d_recs, ctx->unp_recs * 8, hipMemcpyDeviceToHost));
+    return NTC_OK;
+}
+
+int ntc_decode_fasta_unpacked(ntc_ctx *ctx, uint64_t first_id, uint8_t *out, uint64_t out_capacity, uint64_t *out_len) {
+    if (!ctx || !out_len) return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    *out_len = 0;
+    if (!ctx->has_index) return set_err(ctx, NTC_ERR_NO_INDEX, "no index uploaded");
+    const uint64_t need = fasta_bytes(ctx->unp_reads, ctx->unp_bases, first_id);
+    *out_len = need;  // (a size query: out_capacity 0)
+    if (need > out_capacity) return set_err(ctx, NTC_ERR_CAPACITY, "out_capacity smaller than the FASTA text");
+    if (need && !out) return set_err(ctx, NTC_ERR_INVALID_ARG, "null argument");
+    if (ctx->unp_recs == 0) return ctx->unp_reads ? set_err(ctx, NTC_ERR_FORMAT, "reads without records") : NTC_OK;
+    return decode_fasta_dev(ctx, ctx->unp_d_recs, ctx->unp_recs, ctx->unp_reads, ctx->unp_bases, first_id, out, need);
 }
 
 int ntc_last_timing(ntc_ctx *ctx, ntc_timing *out) {

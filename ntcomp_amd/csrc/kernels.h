@@ -151,6 +151,22 @@ void launch_pack_write(const uint64_t *recs, const uint64_t *chunks, const PackS
 // decode output as FASTA text on the GPU (fasta.hip): ">seq.{first_id + r}\n{read r}\n";
 // sizes / out_offs: n + 1 words, tmp: scan_tmp_words(n) words; out_offs[n] = total bytes.
 // Nothing is written unless the decode status is clear (~0) and the text fits out_cap.
+// GPU block unpacker (unpack.hip): stream i of block b is entry 4 b + i (s1 colex, s2 length,
+// s3 flag, s4 short-base chunks), its inflated big-endian words at payload[word_off ...]
+struct UnpackStream {
+    uint64_t word_off;  // u64 words into the payload (and into the marks scratch)
+    uint64_t nwords;    // encoded_size
+    uint64_t n;         // num_u64 values
+    uint64_t param;     // Rice parameter / minimal-binary max
+    uint64_t val_off;   // its values at vals[val_off ...]
+};
+// streams -> values (stream_status[4 b + i]), zip -> records of block b at recs[rec_off[b] ...];
+// out3[3 b .. 3 b + 2] = reads, bases, status.  marks: as many words as the payload; segc:
+// unpack_seg_words(n_blocks, the largest block's records) words
+void launch_unpack(const uint64_t *payload, const UnpackStream *st, uint64_t n_blocks, uint64_t max_recs,
+                   uint64_t *marks, uint64_t *vals, int32_t *stream_status, const uint64_t *rec_off, uint64_t *recs,
+                   uint64_t *segc, uint64_t *out3, hipStream_t s);
+uint64_t unpack_seg_words(uint64_t n_blocks, uint64_t max_recs);
 void launch_fasta(const uint8_t *d_bases, const uint64_t *d_offs, uint64_t n, uint64_t first_id,
                   const unsigned long long *d_status, uint64_t *sizes, uint64_t *out_offs, uint64_t *tmp, uint8_t *out,
                   uint64_t out_cap, hipStream_t s);

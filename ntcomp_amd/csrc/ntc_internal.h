@@ -31,6 +31,7 @@ bool save_index_as(const HostIndex &ix, const std::string &prefix, int layout, s
 }  // namespace ntc
 
 struct ntc_fastx;
+struct ntc_block_meta;
 namespace ntc {
 // a plain FASTQ that ntc_fastx_open mapped: its bytes (null for any other input), and
 // moving the mapped parser to byte pos (a record start) -- pipeline.cpp's GPU-parse reader
@@ -46,6 +47,8 @@ void fastx_stream_unread(ntc_fastx *fx, const uint8_t *src, uint64_t n);
 // Parallel inflate of a non-BGZF gzip file (pgzip.cpp): null when the file is not gzip.
 // pgz_read: cap bytes into dst (fewer only at the end), 1 filled, 0 the end, -1 an error
 // (corrupt or truncated data, a CRC or ISIZE mismatch).
+// the GPU unpacker's block decode on the host (block_codec.cpp; the sanitizer stand-in)
+int unpack_block_host(const ::ntc_block_meta &m, const uint8_t *payload, std::vector<uint64_t> &recs);
 struct PgzReader;
 PgzReader *pgz_open(const char *path, int threads);
 int pgz_read(PgzReader *r, char *dst, size_t cap, size_t *got);

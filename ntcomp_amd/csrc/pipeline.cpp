@@ -799,14 +799,20 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
 //   extents  the file is mapped; the blocks' extents and record counts come from their
 //            32-byte headers alone (block_size of each stream; the flag stream's num_u64 =
 //            records).  A truncated block ends the input, as read_exact ends decode_block.
-//   unzip    the host pool turns each block into u64 records (ntc_read_block_into:
-//            inflate, Rice / minimal-binary decode, zip_block_contents) straight into the
-//            batch's pinned buffer, counting its reads (first flags) and bases.
-//   GPU      one driver thread per context, batches dealt round-robin: ntc_decode_fasta =
-//            H2D of the records, the inverse-SBWT walk, the FASTA text formatted on the GPU
-//            (">seq.N" numbering from the reads of the batches before), D2H of the text.
-//   writer   the calling thread writes the batches' text in file order (a regular file:
-//            pwrite from the host pool at the batch's offset; otherwise write).
+//   unzip    the host pool inflates each block's four streams (ntc_read_block_streams)
+//            straight into the batch's pinned payload buffer.
+//   GPU      one driver thread per context, batches dealt round-robin:
+//            ntc_unpack_streams = H2D of the streams, Rice / minimal-binary decode and
+//            zip_block_contents on the device (unpack.hip), the batch's read count back;
+//            then, once the reads of the batches before fix its ">seq.N" numbering,
+//            ntc_decode_fasta_unpacked = the inverse-SBWT walk, the FASTA text formatted on
+//            the GPU, D2H of the text.
+//   writer   the calling thread numbers the batches in file order as their read counts
+//            arrive and writes their text in file order (a regular file: pwrite from the
+//            host pool at the batch's offset; otherwise write), the next batches' GPU work
+//            running meanwhile.
+// NTC_HOST_UNPACK=1 keeps round 4's split: the host pool decodes each block into u64
+// records (ntc_read_block_into), counts its reads, and ntc_decode_fasta takes the records.
 // A damaged block ends the output after the blocks before it (decode_block's Err ends the
 // reference's loop, main.rs:202).
 // ---------------------------------------------------------------------------------------
@@ -819,11 +825,15 @@ namespace {
 struct DBlock {
     uint64_t a, len;   // byte range of the block
     uint64_t n_recs;   // records (the flag stream's num_u64)
+    uint64_t pay;      // bytes of its four inflated streams (8 x encoded_size each)
 };
 
 struct DSlot {  // one batch in flight
     uint64_t *recs = nullptr;
     uint64_t cap_recs = 0;
+    uint8_t *pay = nullptr;  // GPU unpack: the blocks' inflated streams
+    uint64_t cap_pay = 0, n_pay = 0;
+    std::vector<ntc_block_meta> metas;
     uint8_t *text = nullptr;
     uint64_t cap_text = 0;
     uint64_t batch = ~0ULL;  // batch held, ~0 = free
@@ -834,6 +844,7 @@ struct DSlot {  // one batch in flight
     int bad_block = -1;      // first damaged block (index in the batch)
     bool buffer = false;     // recs sized for the batch
     bool ready = false;      // complete + first_id known: the GPU may take it
+    bool unpacked = false;   // GPU unpack: the batch's reads and bases are known
     bool decoded = false;
 };
 
@@ -901,7 +912,7 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
                                          (uint64_t)data[p + 3] << 24; };
     std::vector<DBlock> blocks;
     for (uint64_t pos = 32; pos < fsize;) {  // after the 32-byte file header (main.rs:196-198)
-        uint64_t p = pos, nrec = 0;
+        uint64_t p = pos, nrec = 0, pay = 0;
         bool whole = true;
         for (int s = 0; s < 4 && whole; s++) {
             if (p + 32 > fsize) {
@@ -909,11 +920,12 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
                 break;
             }
             if (s == 2) nrec = le32(p + 8);
+            pay += 8 * le32(p + 12);
             p += 32 + le32(p);
             if (p > fsize) whole = false;
         }
         if (!whole) break;
-        blocks.push_back(DBlock{pos, p - pos, nrec});
+        blocks.push_back(DBlock{pos, p - pos, nrec, pay});
         pos = p;
     }
     const uint64_t n_batches = (blocks.size() + bpb - 1) / bpb;
@@ -921,6 +933,7 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
 
     const int NB = n_ctx + 2;
     std::vector<DSlot> slots((size_t)NB);
+    const bool gpu_unpack = !std::getenv("NTC_HOST_UNPACK");
     Shared sh;
     uint64_t next_task = 0;       // next block to unzip
     uint64_t next_id = 1;         // main.rs:204: seq.{i+1}
@@ -983,16 +996,29 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
                     DSlot &sl = slot_of(b);
                     first = sl.batch != b;
                     if (first) {
-                        sl = DSlot{sl.recs, sl.cap_recs, sl.text, sl.cap_text};
+                        DSlot fresh;
+                        fresh.recs = sl.recs;
+                        fresh.cap_recs = sl.cap_recs;
+                        fresh.pay = sl.pay;
+                        fresh.cap_pay = sl.cap_pay;
+                        fresh.text = sl.text;
+                        fresh.cap_text = sl.cap_text;
+                        fresh.metas.swap(sl.metas);
+                        sl = std::move(fresh);
                         sl.batch = b;
                         sl.first_block = b * bpb;
                         sl.n_blocks = std::min<uint64_t>(bpb, blocks.size() - sl.first_block);
-                        for (uint64_t i = 0; i < sl.n_blocks; i++) sl.n_recs += blocks[sl.first_block + i].n_recs;
+                        for (uint64_t i = 0; i < sl.n_blocks; i++) {
+                            sl.n_recs += blocks[sl.first_block + i].n_recs;
+                            sl.n_pay += blocks[sl.first_block + i].pay;
+                        }
+                        sl.metas.assign(sl.n_blocks, ntc_block_meta{});
                     }
                 }
                 DSlot &sl = slot_of(b);
-                if (first) {  // size the batch's pinned record buffer outside the lock
-                    const bool okp = ensure_pinned((void **)&sl.recs, &sl.cap_recs, sl.n_recs * 8 + 8);
+                if (first) {  // size the batch's pinned record / stream buffer outside the lock
+                    const bool okp = gpu_unpack ? ensure_pinned((void **)&sl.pay, &sl.cap_pay, sl.n_pay + 8)
+                                                : ensure_pinned((void **)&sl.recs, &sl.cap_recs, sl.n_recs * 8 + 8);
                     if (!okp) {
                         sh.fail(NTC_ERR_HIP, "pinned host allocation failed");
                         return;
@@ -1005,14 +1031,26 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
                     sh.cv.wait(g, [&] { return sh.error != NTC_OK || sl.buffer; });
                     if (sh.error != NTC_OK) return;
                 }
-                uint64_t off = 0;
-                for (uint64_t i = sl.first_block; i < blk; i++) off += blocks[i].n_recs;
+                uint64_t off = 0, poff = 0;
+                for (uint64_t i = sl.first_block; i < blk; i++) {
+                    off += blocks[i].n_recs;
+                    poff += blocks[i].pay;
+                }
                 const auto tu = Clock::now();
                 uint64_t used = 0, nr = 0, numr = 0, reads = 0, bases = 0;
                 const DBlock &db = blocks[blk];
-                int rc = ntc_read_block_into(data + db.a, db.len, &used, sl.recs + off, db.n_recs, &nr, &numr);
-                if (rc == NTC_OK && (nr != db.n_recs || used != db.len)) rc = NTC_ERR_FORMAT;
-                if (rc == NTC_OK) count_reads(sl.recs + off, nr, &reads, &bases);
+                int rc;
+                if (gpu_unpack) {  // inflate only: the streams are decoded on the GPU
+                    ntc_block_meta &m = sl.metas[blk - sl.first_block];
+                    rc = ntc_read_block_streams(data + db.a, db.len, &used, sl.pay + poff, db.pay, &m);
+                    if (rc == NTC_OK && (m.n_recs != db.n_recs || used != db.len)) rc = NTC_ERR_FORMAT;
+                    for (int i = 0; i < 4; i++) m.stream[i].offset += poff;
+                    if (rc != NTC_OK) m.status = rc;
+                } else {
+                    rc = ntc_read_block_into(data + db.a, db.len, &used, sl.recs + off, db.n_recs, &nr, &numr);
+                    if (rc == NTC_OK && (nr != db.n_recs || used != db.len)) rc = NTC_ERR_FORMAT;
+                    if (rc == NTC_OK) count_reads(sl.recs + off, nr, &reads, &bases);
+                }
                 add_time(t_unzip, secs(tu, Clock::now()));
                 std::lock_guard<std::mutex> g(sh.mu);
                 const int bi = (int)(blk - sl.first_block);
@@ -1039,6 +1077,61 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
         gpus.emplace_back([&, c] {
             for (uint64_t b = (uint64_t)c;; b += (uint64_t)n_ctx) {
                 DSlot *slp;
+                if (gpu_unpack) {
+                    // the batch's streams decoded on the device as soon as every block of it is
+                    // inflated (or found damaged): its read count numbers the batches after it
+                    {
+                        std::unique_lock<std::mutex> g(sh.mu);
+                        sh.cv.wait(g, [&] {
+                            return sh.error != NTC_OK || b >= n_batches || (stop_batch >= 0 && (int64_t)b > stop_batch) ||
+                                   (slot_of(b).batch == b && slot_of(b).finished == slot_of(b).n_blocks);
+                        });
+                        if (sh.error != NTC_OK || b >= n_batches || (stop_batch >= 0 && (int64_t)b > stop_batch)) return;
+                        slp = &slot_of(b);
+                    }
+                    DSlot &sl = *slp;
+                    const uint64_t nb = sl.bad_block >= 0 ? (uint64_t)sl.bad_block : sl.n_blocks;
+                    const auto tg = Clock::now();
+                    uint64_t ok = 0, nr = 0, nbs = 0;
+                    const int rc = ntc_unpack_streams(ctxs[c], sl.pay, sl.n_pay, sl.metas.data(), nb, &ok, &nr, &nbs);
+                    add_time(t_gpu, secs(tg, Clock::now()));
+                    if (rc) {
+                        sh.fail(rc, std::string("decode: ") + ntc_last_error(ctxs[c]));
+                        return;
+                    }
+                    {
+                        std::unique_lock<std::mutex> g(sh.mu);
+                        if (ok < nb) {  // a block the device could not decode: the output ends before it
+                            sl.bad_block = (int)ok;
+                            if (stop_batch < 0 || (int64_t)b < stop_batch) stop_batch = (int64_t)b;
+                        }
+                        sl.n_reads = nr;
+                        sl.n_bases = nbs;
+                        sl.unpacked = true;
+                        sh.cv.notify_all();
+                        sh.cv.wait(g, [&] { return sh.error != NTC_OK || sl.ready; });
+                        if (sh.error != NTC_OK) return;
+                    }
+                    const uint64_t need = sl.n_bases + 7 * sl.n_reads + digits_total(sl.first_id, sl.n_reads) + 64;
+                    const auto tf = Clock::now();
+                    if (!ensure_pinned((void **)&sl.text, &sl.cap_text, need)) {
+                        sh.fail(NTC_ERR_HIP, "pinned host allocation failed");
+                        return;
+                    }
+                    uint64_t len = 0;
+                    const int rf = ntc_decode_fasta_unpacked(ctxs[c], sl.first_id, sl.text, sl.cap_text, &len);
+                    add_time(t_gpu, secs(tf, Clock::now()));
+                    if (rf) {
+                        sh.fail(rf, std::string("decode: ") + ntc_last_error(ctxs[c]));
+                        return;
+                    }
+                    std::lock_guard<std::mutex> g(sh.mu);
+                    sl.text_len = len;
+                    sl.decoded = true;
+                    S.gpu_done_s = secs(t0, Clock::now());
+                    sh.cv.notify_all();
+                    continue;
+                }
                 {
                     std::unique_lock<std::mutex> g(sh.mu);
                     sh.cv.wait(g, [&] {
@@ -1112,20 +1205,18 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
         }
         return true;
     };
-    for (uint64_t b = 0; b < n_batches; b++) {
-        DSlot *slp;
-        {
-            std::unique_lock<std::mutex> g(sh.mu);
-            // the batch is complete once every block of it is unzipped or found damaged
-            sh.cv.wait(g, [&] {
-                if (sh.error != NTC_OK) return true;
-                if (stop_batch >= 0 && (int64_t)b > stop_batch) return true;
-                const DSlot &sl = slot_of(b);
-                return sl.batch == b && sl.finished == sl.n_blocks;
-            });
-            if (sh.error != NTC_OK || (stop_batch >= 0 && (int64_t)b > stop_batch)) break;
-            DSlot &sl = slot_of(b);
-            if (sl.bad_block >= 0) {  // only the blocks before the damaged one
+    // ">seq.N" numbering: batch a gets first_id once every batch before it has its read count
+    // (host unpack: the batch is complete; GPU unpack: the device has decoded its streams).
+    // Batches are numbered as far ahead as they allow, so their GPU work overlaps the
+    // writes of the batches before them.
+    uint64_t next_assign = 0;
+    auto assign_ahead = [&](uint64_t b) {  // under sh.mu
+        while (next_assign < n_batches && next_assign < b + (uint64_t)NB) {
+            if (stop_batch >= 0 && (int64_t)next_assign > stop_batch) break;
+            DSlot &sl = slot_of(next_assign);
+            if (sl.batch != next_assign || sl.finished != sl.n_blocks) break;
+            if (gpu_unpack && !sl.unpacked) break;
+            if (!gpu_unpack && sl.bad_block >= 0) {  // only the blocks before the damaged one
                 uint64_t n = 0;
                 for (int i = 0; i < sl.bad_block; i++) n += blocks[sl.first_block + (uint64_t)i].n_recs;
                 sl.n_recs = n;
@@ -1135,10 +1226,23 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
             sl.first_id = next_id;
             next_id += sl.n_reads;
             sl.ready = true;
+            next_assign++;
             sh.cv.notify_all();
-            sh.cv.wait(g, [&] { return sh.error != NTC_OK || sl.decoded; });
-            if (sh.error != NTC_OK) break;
-            slp = &sl;
+        }
+    };
+    for (uint64_t b = 0; b < n_batches; b++) {
+        DSlot *slp;
+        {
+            std::unique_lock<std::mutex> g(sh.mu);
+            sh.cv.wait(g, [&] {
+                if (sh.error != NTC_OK) return true;
+                if (stop_batch >= 0 && (int64_t)b > stop_batch) return true;
+                assign_ahead(b);
+                const DSlot &sl = slot_of(b);
+                return sl.batch == b && sl.decoded;
+            });
+            if (sh.error != NTC_OK || (stop_batch >= 0 && (int64_t)b > stop_batch)) break;
+            slp = &slot_of(b);
         }
         const auto tw = Clock::now();
         if (!write_text(slp->text, slp->text_len)) sh.fail(NTC_ERR_IO, "write failed");
@@ -1163,6 +1267,7 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
     for (auto &t : gpus) t.join();
     for (auto &sl : slots) {
         pinned_free(sl.recs);
+        pinned_free(sl.pay);
         pinned_free(sl.text);
     }
     if (data) munmap((void *)data, fsize);

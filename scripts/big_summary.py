@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--bench", help="a bench.py JSON line: S91's numbers go beside this point")
     a = ap.parse_args()
     pt = json.loads(open(os.path.join(a.out_dir, "point.json")).read().strip().splitlines()[-1])
+    pt.setdefault("reps", 3)
     n = pt["reads"]
     rd = per_dispatch(a.out_dir, "pmc_rd")
     wr = per_dispatch(a.out_dir, "pmc_wr")
@@ -40,16 +41,21 @@ def main():
         dur.setdefault(short(r["Kernel_Name"]), []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     kern = {}
     for k in ("k_ms4", "k_parse4", "k_pack", "k_emit4"):
-        r_, w_ = rd.get(k, []), wr.get(k, [])
+        # the last dispatch of each pass is the timed call (the first call learns the pools and
+        # may run twice); the kernel trace's last --reps dispatches are the timed ones
+        c = pt.get("calls_per_rep", 1)
+        r_, w_ = rd.get(k, [])[-c:], wr.get(k, [])[-c:]
+        dur[k] = dur.get(k, [])[-pt.get("reps", 3) * c:]
         if not r_:
             continue
-        rb = mean([32 * x.get("TCC_EA0_RDREQ_32B_sum", 0) + 64 * x.get("TCC_EA0_RDREQ_64B_sum", 0) +
+        # per call (mean over the rep's calls) x calls = per rep; n reads per rep
+        rb = c * mean([32 * x.get("TCC_EA0_RDREQ_32B_sum", 0) + 64 * x.get("TCC_EA0_RDREQ_64B_sum", 0) +
                    128 * x.get("TCC_EA0_RDREQ_128B_sum", 0) for x in r_])
-        rq = mean([x.get("TCC_EA0_RDREQ_sum", 0) for x in r_])
-        wq = mean([x.get("TCC_EA0_WRREQ_sum", 0) for x in w_]) if w_ else None
-        wb = mean([32 * (x.get("TCC_EA0_WRREQ_sum", 0) - x.get("TCC_EA0_WRREQ_64B_sum", 0)) +
+        rq = c * mean([x.get("TCC_EA0_RDREQ_sum", 0) for x in r_])
+        wq = c * mean([x.get("TCC_EA0_WRREQ_sum", 0) for x in w_]) if w_ else None
+        wb = c * mean([32 * (x.get("TCC_EA0_WRREQ_sum", 0) - x.get("TCC_EA0_WRREQ_64B_sum", 0)) +
                    64 * x.get("TCC_EA0_WRREQ_64B_sum", 0) for x in w_]) if w_ else 0
-        ms = mean(dur.get(k, [])) / 1e6 if dur.get(k) else None
+        ms = c * mean(dur.get(k, [])) / 1e6 if dur.get(k) else None
         e = {"avg_ms_trace": round(ms, 4) if ms else None, "read_requests_per_read": round(rq / n, 3),
              "write_requests_per_read": round(wq / n, 3) if wq is not None else None,
              "bytes_per_read": round((rb + wb) / n, 1)}

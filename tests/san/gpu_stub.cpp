@@ -28,6 +28,8 @@ int64_t orc_decode(const orc_index *ix, const uint64_t *recs, uint64_t n_recs, u
 struct ntc_ctx {
     const orc_index *ix = nullptr;
     std::string err;
+    std::vector<uint64_t> unp;  // ntc_unpack_streams' records
+    uint64_t unp_reads = 0, unp_bases = 0;
 };
 
 ntc_ctx *stub_ctx_new(const orc_index *ix) {
@@ -102,6 +104,34 @@ int ntc_decode_fasta(ntc_ctx *ctx, const uint64_t *recs, uint64_t n_recs, uint64
     }
     std::memcpy(out, text.data(), text.size());
     return NTC_OK;
+}
+
+// unpack.hip restated: the blocks before the first damaged one, decoded on the host
+int ntc_unpack_streams(ntc_ctx *ctx, const uint8_t *payload, uint64_t payload_bytes, const ntc_block_meta *metas,
+                       uint64_t n_blocks, uint64_t *n_blocks_ok, uint64_t *n_reads, uint64_t *n_bases) {
+    (void)payload_bytes;
+    ctx->unp.clear();
+    ctx->unp_reads = ctx->unp_bases = 0;
+    uint64_t ok = 0;
+    std::vector<uint64_t> r;
+    for (; ok < n_blocks; ok++) {
+        if (metas[ok].status || ntc::unpack_block_host(metas[ok], payload, r) != NTC_OK) break;
+        for (uint64_t w : r) {
+            const uint32_t flag = (uint32_t)(w >> 56);
+            ctx->unp_reads += flag & 1;
+            ctx->unp_bases += (flag & 2) ? (flag >> 2) : ((w >> 32) & 0xFFFFFFu);
+        }
+        ctx->unp.insert(ctx->unp.end(), r.begin(), r.end());
+    }
+    *n_blocks_ok = ok;
+    if (n_reads) *n_reads = ctx->unp_reads;
+    if (n_bases) *n_bases = ctx->unp_bases;
+    return NTC_OK;
+}
+
+int ntc_decode_fasta_unpacked(ntc_ctx *ctx, uint64_t first_id, uint8_t *out, uint64_t out_capacity, uint64_t *out_len) {
+    return ntc_decode_fasta(ctx, ctx->unp.data(), ctx->unp.size(), ctx->unp_reads, ctx->unp_bases, first_id, out,
+                            out_capacity, out_len);
 }
 
 // fastq.hip restated: exactly n_reads 4-line records, the last line possibly without its
