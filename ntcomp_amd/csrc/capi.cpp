@@ -399,7 +399,10 @@ int read_status(ntc_ctx *ctx, int64_t *bad_index) {
             return NTC_OK;
         }
         if (st == kStatusRegrow) {
-            if (ctx->last == kEncode && ctx->last_variant == 4 && attempt < 2) {
+            // up to 4 re-runs: the first call on a context learns the entry pool (the parse
+            // is skipped while entries overflow), then the record pool; a 10 M-read call on a
+            // 177 M-node collection (L31, profiles/round5/big_point_*) ran out after two
+            if (ctx->last == kEncode && ctx->last_variant == 4 && attempt < 4) {
                 const int rc = regrow_and_rerun(ctx);
                 if (rc) return rc;
                 continue;
@@ -1686,7 +1689,8 @@ int ntc_unpack_streams(ntc_ctx *ctx, const uint8_t *payload, uint64_t payload_by
     void *d_pay, *d_marks, *d_st, *d_vals, *d_recs, *d_out;
     int rc;
     if ((rc = ensure(ctx, WS_UNP_PAY, pay_words * 8 + 16, &d_pay))) return rc;
-    if ((rc = ensure(ctx, WS_UNP_MARKS, pay_words * 8 + 16, &d_marks))) return rc;
+    if ((rc = ensure(ctx, WS_UNP_MARKS, pay_words * 8 + 16 + unpack_chain_words(n_blocks) * 4, &d_marks))) return rc;
+    uint32_t *d_chain = (uint32_t *)((uint8_t *)d_marks + pay_words * 8 + 16);
     if ((rc = ensure(ctx, WS_UNP_ST, st.size() * sizeof(UnpackStream) + (n_blocks + 1) * 8, &d_st))) return rc;
     if ((rc = ensure(ctx, WS_UNP_VALS, nv * 8 + 8, &d_vals))) return rc;
     if ((rc = ensure(ctx, WS_UNP_RECS, roff[n_blocks] * 8 + 8, &d_recs))) return rc;
@@ -1701,7 +1705,7 @@ int ntc_unpack_streams(ntc_ctx *ctx, const uint8_t *payload, uint64_t payload_by
     HIP_TRY(ctx, hipMemcpyAsync(d_st, st.data(), st.size() * sizeof(UnpackStream), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(d_roff, roff.data(), (n_blocks + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
     launch_unpack((const uint64_t *)d_pay, (const UnpackStream *)d_st, n_blocks, max_recs, (uint64_t *)d_marks,
-                  (uint64_t *)d_vals, d_sst, d_roff, (uint64_t *)d_recs, d_segc, d_out3, ctx->stream);
+                  d_chain, (uint64_t *)d_vals, d_sst, d_roff, (uint64_t *)d_recs, d_segc, d_out3, ctx->stream);
     HIP_TRY(ctx, hipGetLastError());
     std::vector<uint64_t> o3(3 * n_blocks);
     HIP_TRY(ctx, hipMemcpyAsync(o3.data(), d_out3, 3 * n_blocks * 8, hipMemcpyDeviceToHost, ctx->stream));

@@ -164,9 +164,10 @@ struct UnpackStream {
 // out3[3 b .. 3 b + 2] = reads, bases, status.  marks: as many words as the payload; segc:
 // unpack_seg_words(n_blocks, the largest block's records) words
 void launch_unpack(const uint64_t *payload, const UnpackStream *st, uint64_t n_blocks, uint64_t max_recs,
-                   uint64_t *marks, uint64_t *vals, int32_t *stream_status, const uint64_t *rec_off, uint64_t *recs,
-                   uint64_t *segc, uint64_t *out3, hipStream_t s);
+                   uint64_t *marks, uint32_t *chainc, uint64_t *vals, int32_t *stream_status, const uint64_t *rec_off,
+                   uint64_t *recs, uint64_t *segc, uint64_t *out3, hipStream_t s);
 uint64_t unpack_seg_words(uint64_t n_blocks, uint64_t max_recs);
+uint64_t unpack_chain_words(uint64_t n_blocks);  // chainc: u32 words
 void launch_fasta(const uint8_t *d_bases, const uint64_t *d_offs, uint64_t n, uint64_t first_id,
                   const unsigned long long *d_status, uint64_t *sizes, uint64_t *out_offs, uint64_t *tmp, uint8_t *out,
                   uint64_t out_cap, hipStream_t s);

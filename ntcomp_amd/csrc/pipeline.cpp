@@ -799,20 +799,19 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
 //   extents  the file is mapped; the blocks' extents and record counts come from their
 //            32-byte headers alone (block_size of each stream; the flag stream's num_u64 =
 //            records).  A truncated block ends the input, as read_exact ends decode_block.
-//   unzip    the host pool inflates each block's four streams (ntc_read_block_streams)
-//            straight into the batch's pinned payload buffer.
-//   GPU      one driver thread per context, batches dealt round-robin:
-//            ntc_unpack_streams = H2D of the streams, Rice / minimal-binary decode and
-//            zip_block_contents on the device (unpack.hip), the batch's read count back;
-//            then, once the reads of the batches before fix its ">seq.N" numbering,
-//            ntc_decode_fasta_unpacked = the inverse-SBWT walk, the FASTA text formatted on
-//            the GPU, D2H of the text.
+//   unzip    the host pool turns each block into u64 records (ntc_read_block_into:
+//            inflate, Rice / minimal-binary decode, zip_block_contents) straight into the
+//            batch's pinned buffer, counting its reads (first flags) and bases.
+//   GPU      one driver thread per context, batches dealt round-robin: ntc_decode_fasta =
+//            H2D of the records, the inverse-SBWT walk, the FASTA text formatted on the GPU
+//            (">seq.N" numbering from the reads of the batches before), D2H of the text.
 //   writer   the calling thread numbers the batches in file order as their read counts
 //            arrive and writes their text in file order (a regular file: pwrite from the
 //            host pool at the batch's offset; otherwise write), the next batches' GPU work
 //            running meanwhile.
-// NTC_HOST_UNPACK=1 keeps round 4's split: the host pool decodes each block into u64
-// records (ntc_read_block_into), counts its reads, and ntc_decode_fasta takes the records.
+// NTC_GPU_UNPACK=1: the pool only inflates each block's streams (ntc_read_block_streams) and
+// the GPU decodes them (ntc_unpack_streams, unpack.hip) before the walk
+// (ntc_decode_fasta_unpacked); the batch's read count comes back from the device.
 // A damaged block ends the output after the blocks before it (decode_block's Err ends the
 // reference's loop, main.rs:202).
 // ---------------------------------------------------------------------------------------
@@ -933,7 +932,12 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
 
     const int NB = n_ctx + 2;
     std::vector<DSlot> slots((size_t)NB);
-    const bool gpu_unpack = !std::getenv("NTC_HOST_UNPACK");
+    // the streams decoded on the GPU (NTC_GPU_UNPACK=1) or on the host pool (default): on one
+    // MI355X box the device path ran the 10 M-read decode pipeline at 2.7 against 6.0 Gbases/s
+    // (profiles/round5/e2e_dec_*): its minimal-binary streams cost l + 1 chains per segment on
+    // one CU per stream, while 16 host threads decode a call's blocks in parallel
+    const char *gu = std::getenv("NTC_GPU_UNPACK");
+    const bool gpu_unpack = gu && std::atoi(gu) > 0;
     Shared sh;
     uint64_t next_task = 0;       // next block to unzip
     uint64_t next_id = 1;         // main.rs:204: seq.{i+1}

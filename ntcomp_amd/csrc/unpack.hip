@@ -10,6 +10,7 @@
 // A code stream is a chain of variable-length codes (Rice: unary quotient + p bits; minimal
 // binary: l or l + 1 bits), so its code boundaries are found in parallel the way a
 // self-synchronising prefix code allows (k_unpack_streams, one workgroup per stream):
+// Rice streams (s2, s3; k_unpack_streams):
 //   A  every thread decodes its segment of the stream from the segment's first bit as if a
 //      code started there, marking the code starts of its chain in a bitmap;
 //   B  each thread goes on past its segment's end into the next segment until its chain
@@ -21,6 +22,9 @@
 //   D  each thread decodes its segment's true codes into place.
 // A chain that never meets the next one within that segment (possible for pathological
 // streams, never seen on ntcomp's) makes the workgroup decode its stream sequentially.
+// Minimal-binary streams (s1, s4; k_unpack_mb) are l- or (l + 1)-bit codes, nearly all of one
+// length, and such chains need not ever meet: there every segment's transfer is computed for
+// each of the l + 1 offsets a code can start at, and one thread follows the true entries.
 //
 // k_zip_count + k_zip_write (a workgroup per 16,384 records of a block) zip the four value
 // streams back into u64 records with two block scans (long records -> s1/s2 index, short
@@ -51,7 +55,7 @@ __device__ __forceinline__ uint64_t bswap64(uint64_t x) { return __builtin_bswap
 struct Bits64 {
     const uint64_t *w;
     uint64_t nwords;
-    uint64_t wi = ~0ull, hi = 0, lo = 0;
+    uint64_t wi = ~0ull - 1, hi = 0, lo = 0;  // (not ~0: ~0 + 1 would look like "the next word" of word 0)
     __device__ __forceinline__ uint64_t load(uint64_t i) const { return i < nwords ? bswap64(w[i]) : 0; }
     __device__ __forceinline__ uint64_t peek(uint64_t pos) {
         const uint64_t i = pos >> 6;
@@ -173,9 +177,11 @@ __device__ __forceinline__ uint64_t block_exscan(uint64_t v, uint64_t *tot, uint
     return base + inc - v;
 }
 
+// Rice streams (s2, s3 of every block: workgroup 2 i + j takes stream 4 i + 1 + j)
 __global__ __launch_bounds__(kUnpThreads) void k_unpack_streams(const uint64_t *payload, const UnpackStream *st,
                                                                uint64_t *marks, uint64_t *vals, int32_t *status) {
-    const UnpackStream s = st[blockIdx.x];
+    const uint32_t si = 4 * (blockIdx.x >> 1) + 1 + (blockIdx.x & 1);
+    const UnpackStream s = st[si];
     const int t = threadIdx.x;
     __shared__ uint64_t sh[kUnpThreads / 64];
     __shared__ uint64_t s_f[kUnpThreads + 1], s_y[kUnpThreads + 1], s_pre[kUnpThreads + 1];
@@ -185,24 +191,23 @@ __global__ __launch_bounds__(kUnpThreads) void k_unpack_streams(const uint64_t *
         s_fail = 0;
         s_err = 0;
     }
-    StreamCoder cd{payload + s.word_off, s.nwords, (blockIdx.x & 3) == 1 || (blockIdx.x & 3) == 2, 0, 0, 0,
-                   Bits64{payload + s.word_off, s.nwords}};
+    StreamCoder cd{payload + s.word_off, s.nwords, true, 0, 0, 0, Bits64{payload + s.word_off, s.nwords}};
     if (cd.rice) {
         if (s.param > 63) {
-            if (t == 0) status[blockIdx.x] = NTC_ERR_FORMAT;
+            if (t == 0) status[si] = NTC_ERR_FORMAT;
             return;
         }
         cd.p = (uint32_t)s.param;
     } else {
         if (s.param < 1) {  // minimal_binary_decode: param 0 decodes no value
-            if (t == 0) status[blockIdx.x] = s.n == 0 ? 0 : NTC_ERR_FORMAT;
+            if (t == 0) status[si] = s.n == 0 ? 0 : NTC_ERR_FORMAT;
             return;
         }
         cd.l = 63u - (uint32_t)__builtin_clzll(s.param);
         cd.limit = (cd.l == 63 ? 0ull : (2ull << cd.l)) - s.param;
     }
     if (s.n == 0) {
-        if (t == 0) status[blockIdx.x] = 0;
+        if (t == 0) status[si] = 0;
         return;
     }
     uint64_t *m = marks + s.word_off;
@@ -284,7 +289,7 @@ __global__ __launch_bounds__(kUnpThreads) void k_unpack_streams(const uint64_t *
                 vals[s.val_off + i] = c.val;
                 p += c.len;
             }
-            status[blockIdx.x] = err;
+            status[si] = err;
         }
         return;
     }
@@ -319,7 +324,97 @@ __global__ __launch_bounds__(kUnpThreads) void k_unpack_streams(const uint64_t *
         }
     }
     __syncthreads();
-    if (t == 0) status[blockIdx.x] = s_err;
+    if (t == 0) status[si] = s_err;
+}
+
+// Minimal-binary streams (s1, s4: workgroup 2 i + j takes stream 4 i + 3 j).  Their codes are
+// l or l + 1 bits, mostly one of the two, and chains started at different offsets rarely
+// meet (fixed-length codes never do), so each segment's transfer is computed for every entry
+// offset a code can start at: thread t decodes its segment from each e < l + 1 bits past its
+// first bit and records where that chain leaves (the first code start past the segment, at
+// most l bits on) and its codes; thread 0 then follows the true entry from segment to segment
+// (one LDS lookup each), and each segment's true codes are decoded into place.
+__global__ __launch_bounds__(kUnpThreads) void k_unpack_mb(const uint64_t *payload, const UnpackStream *st,
+                                                          uint32_t *chainc, uint64_t *vals, int32_t *status) {
+    const uint32_t si = 4 * (blockIdx.x >> 1) + ((blockIdx.x & 1) ? 3 : 0);
+    const UnpackStream s = st[si];
+    const int t = threadIdx.x;
+    __shared__ uint8_t s_x[kUnpThreads * 64];  // exit offset past the segment per entry (255: dead)
+    __shared__ uint8_t s_entry[kUnpThreads];
+    __shared__ uint64_t sh[kUnpThreads / 64];
+    __shared__ int s_err;
+    if (s.param < 1) {  // minimal_binary_decode: param 0 decodes no value
+        if (t == 0) status[si] = s.n == 0 ? 0 : NTC_ERR_FORMAT;
+        return;
+    }
+    if (s.n == 0) {
+        if (t == 0) status[si] = 0;
+        return;
+    }
+    if (t == 0) s_err = 0;
+    StreamCoder cd{payload + s.word_off, s.nwords, false, 0, 0, 0, Bits64{payload + s.word_off, s.nwords}};
+    cd.l = 63u - (uint32_t)__builtin_clzll(s.param);
+    cd.limit = (cd.l == 63 ? 0ull : (2ull << cd.l)) - s.param;
+    const uint32_t L = cd.l + 1;  // entry offsets 0 .. l (codes are at most l + 1 bits)
+    const uint64_t nbits = s.nwords * 64;
+    uint64_t S = (nbits + kUnpThreads - 1) / kUnpThreads;
+    if (S < 64) S = 64;
+    const uint64_t a = (uint64_t)t * S, b = a + S < nbits ? a + S : nbits;
+    const bool active = a < nbits;
+    uint32_t *cc = chainc + (uint64_t)blockIdx.x * kUnpThreads * 64 + (uint64_t)t * 64;
+    // ---- A: the segment's transfer for every entry offset --------------------------------------
+    if (active) {
+        for (uint32_t e = 0; e < L; e++) {
+            uint64_t pos = a + e;
+            uint32_t cnt = 0;
+            bool dead = false;
+            while (pos < b) {
+                const Code c = cd.at(pos);
+                if (!c.len) {
+                    dead = true;
+                    break;
+                }
+                pos += c.len;
+                cnt++;
+            }
+            s_x[t * 64 + e] = dead ? 255 : (uint8_t)(pos - b);
+            cc[e] = cnt;
+        }
+    }
+    __syncthreads();
+    // ---- B: the true entry of every segment (segment 0: the stream's first bit) ----------------
+    if (t == 0) {
+        uint32_t e = 0;
+        for (int u = 0; u < kUnpThreads; u++) {
+            if ((uint64_t)u * S >= nbits || e == 255) {
+                s_entry[u] = 255;
+                continue;
+            }
+            s_entry[u] = (uint8_t)e;
+            e = s_x[u * 64 + e];
+        }
+    }
+    __syncthreads();
+    // ---- C + D: true codes per segment, offsets, decode into place ----------------------------
+    const uint32_t en = s_entry[t];
+    const uint64_t cnt = active && en != 255 ? cc[en] : 0;
+    uint64_t tot;
+    const uint64_t off = block_exscan<kUnpThreads>(cnt, &tot, sh);
+    if (t == 0 && tot < s.n) s_err = NTC_ERR_FORMAT;  // fewer codes than values
+    if (cnt && off < s.n) {
+        uint64_t p = a + en;
+        for (uint64_t j = 0; j < cnt && off + j < s.n; j++) {
+            const Code c = cd.at(p);
+            if (!c.len || c.bad) {
+                atomicExch(&s_err, (int)NTC_ERR_FORMAT);
+                break;
+            }
+            vals[s.val_off + off + j] = c.val;
+            p += c.len;
+        }
+    }
+    __syncthreads();
+    if (t == 0) status[si] = s_err;
 }
 
 // The zip runs in segments of kZipSeg records, one workgroup each, so a call's few blocks
@@ -465,17 +560,21 @@ __global__ __launch_bounds__(kZipThreads) void k_zip_write(const UnpackStream *s
 }  // namespace
 
 void launch_unpack(const uint64_t *payload, const UnpackStream *st, uint64_t n_blocks, uint64_t max_recs,
-                   uint64_t *marks, uint64_t *vals, int32_t *stream_status, const uint64_t *rec_off, uint64_t *recs,
-                   uint64_t *segc, uint64_t *out3, hipStream_t s) {
+                   uint64_t *marks, uint32_t *chainc, uint64_t *vals, int32_t *stream_status, const uint64_t *rec_off,
+                   uint64_t *recs, uint64_t *segc, uint64_t *out3, hipStream_t s) {
     if (!n_blocks) return;
     const uint32_t nseg = (uint32_t)((max_recs + kZipSeg - 1) / kZipSeg) + 1;
-    hipLaunchKernelGGL(k_unpack_streams, dim3((uint32_t)(4 * n_blocks)), dim3(kUnpThreads), 0, s, payload, st, marks,
+    hipLaunchKernelGGL(k_unpack_streams, dim3((uint32_t)(2 * n_blocks)), dim3(kUnpThreads), 0, s, payload, st, marks,
                        vals, stream_status);
+    hipLaunchKernelGGL(k_unpack_mb, dim3((uint32_t)(2 * n_blocks)), dim3(kUnpThreads), 0, s, payload, st, chainc, vals,
+                       stream_status);
     (void)hipMemsetAsync(out3, 0, n_blocks * 3 * 8, s);
     hipLaunchKernelGGL(k_zip_count, dim3((uint32_t)(n_blocks * nseg)), dim3(kZipThreads), 0, s, st, vals, nseg, segc);
     hipLaunchKernelGGL(k_zip_write, dim3((uint32_t)(n_blocks * nseg)), dim3(kZipThreads), 0, s, st, vals, rec_off, recs,
                        stream_status, nseg, segc, (unsigned long long *)out3);
 }
+
+uint64_t unpack_chain_words(uint64_t n_blocks) { return 2 * n_blocks * kUnpThreads * 64; }  // u32 words
 
 uint64_t unpack_seg_words(uint64_t n_blocks, uint64_t max_recs) {
     return 2 * n_blocks * ((max_recs + kZipSeg - 1) / kZipSeg + 1);
