@@ -1689,9 +1689,34 @@ int ntc_unpack_streams(ntc_ctx *ctx, const uint8_t *payload, uint64_t payload_by
     void *d_pay, *d_marks, *d_st, *d_vals, *d_recs, *d_out;
     int rc;
     if ((rc = ensure(ctx, WS_UNP_PAY, pay_words * 8 + 16, &d_pay))) return rc;
-    if ((rc = ensure(ctx, WS_UNP_MARKS, pay_words * 8 + 16 + unpack_chain_words(n_blocks) * 4, &d_marks))) return rc;
-    uint32_t *d_chain = (uint32_t *)((uint8_t *)d_marks + pay_words * 8 + 16);
-    if ((rc = ensure(ctx, WS_UNP_ST, st.size() * sizeof(UnpackStream) + (n_blocks + 1) * 8, &d_st))) return rc;
+    // the tiles of the streams (their tables after the marks)
+    UnpackPlan plan;
+    unpack_plan(st.data(), n_blocks, plan);
+    if ((rc = ensure(ctx, WS_UNP_MARKS, pay_words * 8 + 128 + unpack_ws_bytes(plan), &d_marks))) return rc;
+    void *d_ws = (uint8_t *)d_marks + ((pay_words * 8 + 16 + 63) & ~63ull);
+    // the table upload: streams, record offsets, tile lists, stream lists
+    const std::vector<UnpTile> *tl[2] = {&plan.mb_tiles, &plan.rice_tiles};
+    const std::vector<UnpStreamRef> *sl[2] = {&plan.mb_streams, &plan.rice_streams};
+    uint64_t up_bytes = st.size() * sizeof(UnpackStream) + (n_blocks + 1) * 8;
+    for (int k = 0; k < 2; k++) up_bytes += tl[k]->size() * sizeof(UnpTile) + sl[k]->size() * sizeof(UnpStreamRef);
+    std::vector<uint8_t> up(up_bytes);
+    uint64_t at[4];
+    {
+        uint64_t q = 0;
+        std::memcpy(up.data(), st.data(), st.size() * sizeof(UnpackStream));
+        q += st.size() * sizeof(UnpackStream);
+        std::memcpy(up.data() + q, roff.data(), (n_blocks + 1) * 8);
+        q += (n_blocks + 1) * 8;
+        for (int k = 0; k < 2; k++) {
+            at[2 * k] = q;
+            if (!tl[k]->empty()) std::memcpy(up.data() + q, tl[k]->data(), tl[k]->size() * sizeof(UnpTile));
+            q += tl[k]->size() * sizeof(UnpTile);
+            at[2 * k + 1] = q;
+            if (!sl[k]->empty()) std::memcpy(up.data() + q, sl[k]->data(), sl[k]->size() * sizeof(UnpStreamRef));
+            q += sl[k]->size() * sizeof(UnpStreamRef);
+        }
+    }
+    if ((rc = ensure(ctx, WS_UNP_ST, up.size(), &d_st))) return rc;
     if ((rc = ensure(ctx, WS_UNP_VALS, nv * 8 + 8, &d_vals))) return rc;
     if ((rc = ensure(ctx, WS_UNP_RECS, roff[n_blocks] * 8 + 8, &d_recs))) return rc;
     uint64_t max_recs = 0;
@@ -1702,10 +1727,29 @@ int ntc_unpack_streams(ntc_ctx *ctx, const uint8_t *payload, uint64_t payload_by
     uint64_t *d_out3 = (uint64_t *)d_out, *d_segc = d_out3 + 3 * n_blocks;
     int32_t *d_sst = (int32_t *)(d_segc + segw);
     HIP_TRY(ctx, hipMemcpyAsync(d_pay, payload, payload_bytes, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(d_st, st.data(), st.size() * sizeof(UnpackStream), hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(d_roff, roff.data(), (n_blocks + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
-    launch_unpack((const uint64_t *)d_pay, (const UnpackStream *)d_st, n_blocks, max_recs, (uint64_t *)d_marks,
-                  d_chain, (uint64_t *)d_vals, d_sst, d_roff, (uint64_t *)d_recs, d_segc, d_out3, ctx->stream);
+    HIP_TRY(ctx, hipMemcpyAsync(d_st, up.data(), up.size(), hipMemcpyHostToDevice, ctx->stream));
+    UnpackDev dv{};
+    dv.payload = (const uint64_t *)d_pay;
+    dv.st = (const UnpackStream *)d_st;
+    dv.n_blocks = n_blocks;
+    dv.max_recs = max_recs;
+    dv.marks = (uint64_t *)d_marks;
+    dv.mb_tiles = (const UnpTile *)((uint8_t *)d_st + at[0]);
+    dv.mb_streams = (const UnpStreamRef *)((uint8_t *)d_st + at[1]);
+    dv.rice_tiles = (const UnpTile *)((uint8_t *)d_st + at[2]);
+    dv.rice_streams = (const UnpStreamRef *)((uint8_t *)d_st + at[3]);
+    dv.n_mb_tiles = (uint32_t)plan.mb_tiles.size();
+    dv.n_rice_tiles = (uint32_t)plan.rice_tiles.size();
+    dv.n_mb_streams = (uint32_t)plan.mb_streams.size();
+    dv.n_rice_streams = (uint32_t)plan.rice_streams.size();
+    dv.ws = d_ws;
+    dv.vals = (uint64_t *)d_vals;
+    dv.status = d_sst;
+    dv.rec_off = d_roff;
+    dv.recs = (uint64_t *)d_recs;
+    dv.segc = d_segc;
+    dv.out3 = d_out3;
+    launch_unpack(dv, ctx->stream);
     HIP_TRY(ctx, hipGetLastError());
     std::vector<uint64_t> o3(3 * n_blocks);
     HIP_TRY(ctx, hipMemcpyAsync(o3.data(), d_out3, 3 * n_blocks * 8, hipMemcpyDeviceToHost, ctx->stream));

@@ -4,6 +4,7 @@
 
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "encode_core.h"
 
@@ -160,14 +161,41 @@ struct UnpackStream {
     uint64_t param;     // Rice parameter / minimal-binary max
     uint64_t val_off;   // its values at vals[val_off ...]
 };
-// streams -> values (stream_status[4 b + i]), zip -> records of block b at recs[rec_off[b] ...];
+// The streams run in tiles (a workgroup each): tile k of a list is tile `tile` of stream si,
+// which is entry `stream` of the list's streams; a stream's tiles are contiguous, from
+// first_tile.  unpack_plan lists the minimal-binary (s1, s4) and Rice (s2, s3) tiles from the
+// host copy of the stream table.
+struct UnpTile {
+    uint32_t si, tile, stream, pad;
+};
+struct UnpStreamRef {
+    uint32_t si, first_tile, n_tiles, pad;
+};
+struct UnpackPlan {
+    std::vector<UnpTile> mb_tiles, rice_tiles;
+    std::vector<UnpStreamRef> mb_streams, rice_streams;
+};
+void unpack_plan(const UnpackStream *st, uint64_t n_blocks, UnpackPlan &plan);
+uint64_t unpack_ws_bytes(const UnpackPlan &plan);  // the tiles' tables (ws)
+// streams -> values (status[4 b + i]), zip -> records of block b at recs[rec_off[b] ...];
 // out3[3 b .. 3 b + 2] = reads, bases, status.  marks: as many words as the payload; segc:
 // unpack_seg_words(n_blocks, the largest block's records) words
-void launch_unpack(const uint64_t *payload, const UnpackStream *st, uint64_t n_blocks, uint64_t max_recs,
-                   uint64_t *marks, uint32_t *chainc, uint64_t *vals, int32_t *stream_status, const uint64_t *rec_off,
-                   uint64_t *recs, uint64_t *segc, uint64_t *out3, hipStream_t s);
+struct UnpackDev {
+    const uint64_t *payload;
+    const UnpackStream *st;
+    uint64_t n_blocks, max_recs;
+    uint64_t *marks;
+    const UnpTile *mb_tiles, *rice_tiles;  // the plan's lists, on the device
+    const UnpStreamRef *mb_streams, *rice_streams;
+    uint32_t n_mb_tiles, n_rice_tiles, n_mb_streams, n_rice_streams;
+    void *ws;
+    uint64_t *vals;
+    int32_t *status;
+    const uint64_t *rec_off;
+    uint64_t *recs, *segc, *out3;
+};
+void launch_unpack(const UnpackDev &d, hipStream_t s);
 uint64_t unpack_seg_words(uint64_t n_blocks, uint64_t max_recs);
-uint64_t unpack_chain_words(uint64_t n_blocks);  // chainc: u32 words
 void launch_fasta(const uint8_t *d_bases, const uint64_t *d_offs, uint64_t n, uint64_t first_id,
                   const unsigned long long *d_status, uint64_t *sizes, uint64_t *out_offs, uint64_t *tmp, uint8_t *out,
                   uint64_t out_cap, hipStream_t s);

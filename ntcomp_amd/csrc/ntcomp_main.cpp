@@ -228,6 +228,12 @@ int cmd_encode(const Args &a) {
     return 0;
 }
 
+// the pipeline's stream decode on the host pool (NTC_HOST_UNPACK, pipeline.cpp) -- for --stats
+bool host_unpack_on() {
+    const char *h = std::getenv("NTC_HOST_UNPACK");
+    return h && std::atoi(h) > 0;
+}
+
 int cmd_decode(const Args &a) {
     const auto t0 = Clock::now();
     if (a.pos.size() != 1) die("decode: one input file");
@@ -254,10 +260,13 @@ int cmd_decode(const Args &a) {
     if (a.flag("--stats"))
         std::fprintf(stderr,
                      "{\"stats\": {\"index_load\": %.3f, \"gpu_init_upload\": %.3f, \"unzip\": %.3f, \"gpu\": %.3f, "
-                     "\"write\": %.3f}, \"command\": \"decode\", \"native\": true, \"gpus\": %zu, \"threads\": %d, "
-                     "\"reads\": %llu, \"blocks\": %llu, \"pipeline_wall_s\": %.3f, \"process_s\": %.3f}\n",
-                     t_load, t_gpu - t_load, st.parse_s, st.gpu_s, st.write_s, ctxs.size(), st.threads,
-                     (unsigned long long)st.reads, (unsigned long long)st.blocks, st.wall_s, since(t0));
+                     "\"write\": %.3f, \"alloc\": %.3f}, \"timeline\": {\"first_write\": %.3f, \"unzip_done\": %.3f, "
+                     "\"gpu_done\": %.3f}, \"command\": \"decode\", \"native\": true, \"gpus\": %zu, \"threads\": %d, "
+                     "\"reads\": %llu, \"blocks\": %llu, \"pipeline_wall_s\": %.3f, \"gpu_unpack\": %s, "
+                     "\"process_s\": %.3f}\n",
+                     t_load, t_gpu - t_load, st.parse_s, st.gpu_s, st.write_s, st.alloc_s, st.first_batch_s,
+                     st.reader_done_s, st.gpu_done_s, ctxs.size(), st.threads, (unsigned long long)st.reads,
+                     (unsigned long long)st.blocks, st.wall_s, host_unpack_on() ? "false" : "true", since(t0));
     return 0;
 }
 

@@ -67,6 +67,12 @@ PinnedPool &pinned_pool() {
     static PinnedPool *p = new PinnedPool();  // never destroyed: buffers live until the process ends
     return *p;
 }
+// decode: the streams decoded on the host pool instead of the GPU (NTC_HOST_UNPACK=1)
+bool host_unpack_on() {
+    const char *h = std::getenv("NTC_HOST_UNPACK");
+    return h && std::atoi(h) > 0;
+}
+
 void *pinned_alloc(size_t n) {
     const size_t sz = (std::max<size_t>(n, 1) + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
     PinnedPool &P = pinned_pool();
@@ -799,19 +805,20 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
 //   extents  the file is mapped; the blocks' extents and record counts come from their
 //            32-byte headers alone (block_size of each stream; the flag stream's num_u64 =
 //            records).  A truncated block ends the input, as read_exact ends decode_block.
-//   unzip    the host pool turns each block into u64 records (ntc_read_block_into:
-//            inflate, Rice / minimal-binary decode, zip_block_contents) straight into the
-//            batch's pinned buffer, counting its reads (first flags) and bases.
-//   GPU      one driver thread per context, batches dealt round-robin: ntc_decode_fasta =
-//            H2D of the records, the inverse-SBWT walk, the FASTA text formatted on the GPU
-//            (">seq.N" numbering from the reads of the batches before), D2H of the text.
-//   writer   the calling thread numbers the batches in file order as their read counts
-//            arrive and writes their text in file order (a regular file: pwrite from the
-//            host pool at the batch's offset; otherwise write), the next batches' GPU work
-//            running meanwhile.
-// NTC_GPU_UNPACK=1: the pool only inflates each block's streams (ntc_read_block_streams) and
-// the GPU decodes them (ntc_unpack_streams, unpack.hip) before the walk
-// (ntc_decode_fasta_unpacked); the batch's read count comes back from the device.
+//   unzip    the host pool inflates each block's four streams (ntc_read_block_streams)
+//            straight into the batch's pinned payload buffer.
+//   GPU      one driver thread per context, batches dealt round-robin:
+//            ntc_unpack_streams = H2D of the streams, Rice / minimal-binary decode and
+//            zip_block_contents on the device (unpack.hip), the batch's read count back;
+//            then, once the reads of the batches before fix its ">seq.N" numbering,
+//            ntc_decode_fasta_unpacked = the inverse-SBWT walk, the FASTA text formatted on
+//            the GPU, D2H of the text.
+//   writer   the calling thread writes the batches' text in file order (a regular file:
+//            pwrite at the batch's offset; otherwise write), the next batches' GPU work
+//            running meanwhile.  Batches are numbered by whichever thread completes a read
+//            count.
+// NTC_HOST_UNPACK=1: the pool decodes each block into u64 records (ntc_read_block_into),
+// counting its reads, and ntc_decode_fasta takes the records.
 // A damaged block ends the output after the blocks before it (decode_block's Err ends the
 // reference's loop, main.rs:202).
 // ---------------------------------------------------------------------------------------
@@ -932,12 +939,10 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
 
     const int NB = n_ctx + 2;
     std::vector<DSlot> slots((size_t)NB);
-    // the streams decoded on the GPU (NTC_GPU_UNPACK=1) or on the host pool (default): on one
-    // MI355X box the device path ran the 10 M-read decode pipeline at 2.7 against 6.0 Gbases/s
-    // (profiles/round5/e2e_dec_*): its minimal-binary streams cost l + 1 chains per segment on
-    // one CU per stream, while 16 host threads decode a call's blocks in parallel
-    const char *gu = std::getenv("NTC_GPU_UNPACK");
-    const bool gpu_unpack = gu && std::atoi(gu) > 0;
+    // the streams decoded on the GPU (default) or on the host pool (NTC_HOST_UNPACK=1): the
+    // 10 M-read decode pipeline ran at 8.0 against 7.6 Gbases/s on one MI355X box, the pool's
+    // thread-time 0.11 against 0.64 s (profiles/round5/e2e_dec_*)
+    const bool gpu_unpack = !host_unpack_on();
     Shared sh;
     uint64_t next_task = 0;       // next block to unzip
     uint64_t next_id = 1;         // main.rs:204: seq.{i+1}
@@ -971,6 +976,33 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
         return true;
     };
 
+    // ">seq.N" numbering: batch a gets first_id once every batch before it has its read count
+    // (host unpack: the batch is complete; GPU unpack: the device has decoded its streams).
+    // Whichever thread completes a count numbers the batches as far ahead as they allow, so
+    // their GPU work overlaps the writes of the batches before them (round 5's first version
+    // numbered them in the writer's loop only: a batch's text then waited for the write of
+    // the one before it, 3.1 ms per batch where the write takes 2).
+    uint64_t next_assign = 0;
+    auto assign_ahead = [&]() {  // under sh.mu
+        while (next_assign < n_batches) {
+            if (stop_batch >= 0 && (int64_t)next_assign > stop_batch) break;
+            DSlot &sl = slot_of(next_assign);
+            if (sl.batch != next_assign || sl.finished != sl.n_blocks) break;
+            if (gpu_unpack && !sl.unpacked) break;
+            if (!gpu_unpack && sl.bad_block >= 0) {  // only the blocks before the damaged one
+                uint64_t n = 0;
+                for (int i = 0; i < sl.bad_block; i++) n += blocks[sl.first_block + (uint64_t)i].n_recs;
+                sl.n_recs = n;
+                sl.n_reads = sl.n_bases = 0;
+                count_reads(sl.recs, n, &sl.n_reads, &sl.n_bases);
+            }
+            sl.first_id = next_id;
+            next_id += sl.n_reads;
+            sl.ready = true;
+            next_assign++;
+            sh.cv.notify_all();
+        }
+    };
     // ---- unzip pool ------------------------------------------------------------------------
     // Blocks are taken in file order; the first block of a batch claims the batch's slot
     // (free once the writer is done with batch b - NB) and sizes its record buffer.  Past a
@@ -1068,6 +1100,7 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
                 sl.finished++;
                 if (blk + 1 == blocks.size() || (stop_batch >= 0 && sl.finished == sl.n_blocks))
                     S.reader_done_s = secs(t0, Clock::now());
+                if (!gpu_unpack && sl.finished == sl.n_blocks) assign_ahead();
                 sh.cv.notify_all();
             }
         });
@@ -1112,6 +1145,7 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
                         sl.n_reads = nr;
                         sl.n_bases = nbs;
                         sl.unpacked = true;
+                        assign_ahead();
                         sh.cv.notify_all();
                         sh.cv.wait(g, [&] { return sh.error != NTC_OK || sl.ready; });
                         if (sh.error != NTC_OK) return;
@@ -1178,28 +1212,11 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
     const bool seekable = fstat(out_fd, &ost) == 0 && S_ISREG(ost.st_mode) && fl >= 0 && !(fl & O_APPEND) &&
                           lseek(out_fd, 0, SEEK_CUR) >= 0;
     off_t out_pos = seekable ? lseek(out_fd, 0, SEEK_CUR) : 0;
+    // one writer: buffered writes into one file serialise on its inode lock, and on the GPU
+    // box one thread's pwrite put 1.6 GB into the page cache at 12.6 GB/s against 10.4 from
+    // 8 threads at their own offsets and 1.9 through a shared mapping
+    // (profiles/round5/write_bw_box.jsonl, scripts/write_bw.cpp)
     auto write_text = [&](const uint8_t *p, uint64_t n) -> bool {
-        if (seekable && n > (8u << 20) && T > 1) {  // parallel pwrite into the page cache
-            const int W = std::min<int>(T, 8);
-            std::vector<std::thread> ws;
-            std::atomic<bool> ok{true};
-            for (int w = 0; w < W; w++)
-                ws.emplace_back([&, w] {
-                    const uint64_t a = n * (uint64_t)w / (uint64_t)W, e = n * (uint64_t)(w + 1) / (uint64_t)W;
-                    uint64_t q = a;
-                    while (q < e) {
-                        const ssize_t r = ::pwrite(out_fd, p + q, e - q, out_pos + (off_t)q);
-                        if (r <= 0) {
-                            ok = false;
-                            return;
-                        }
-                        q += (uint64_t)r;
-                    }
-                });
-            for (auto &x : ws) x.join();
-            out_pos += (off_t)n;
-            return ok.load();
-        }
         while (n) {
             const ssize_t w = seekable ? ::pwrite(out_fd, p, n, out_pos) : ::write(out_fd, p, n);
             if (w <= 0) return false;
@@ -1209,31 +1226,6 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
         }
         return true;
     };
-    // ">seq.N" numbering: batch a gets first_id once every batch before it has its read count
-    // (host unpack: the batch is complete; GPU unpack: the device has decoded its streams).
-    // Batches are numbered as far ahead as they allow, so their GPU work overlaps the
-    // writes of the batches before them.
-    uint64_t next_assign = 0;
-    auto assign_ahead = [&](uint64_t b) {  // under sh.mu
-        while (next_assign < n_batches && next_assign < b + (uint64_t)NB) {
-            if (stop_batch >= 0 && (int64_t)next_assign > stop_batch) break;
-            DSlot &sl = slot_of(next_assign);
-            if (sl.batch != next_assign || sl.finished != sl.n_blocks) break;
-            if (gpu_unpack && !sl.unpacked) break;
-            if (!gpu_unpack && sl.bad_block >= 0) {  // only the blocks before the damaged one
-                uint64_t n = 0;
-                for (int i = 0; i < sl.bad_block; i++) n += blocks[sl.first_block + (uint64_t)i].n_recs;
-                sl.n_recs = n;
-                sl.n_reads = sl.n_bases = 0;
-                count_reads(sl.recs, n, &sl.n_reads, &sl.n_bases);
-            }
-            sl.first_id = next_id;
-            next_id += sl.n_reads;
-            sl.ready = true;
-            next_assign++;
-            sh.cv.notify_all();
-        }
-    };
     for (uint64_t b = 0; b < n_batches; b++) {
         DSlot *slp;
         {
@@ -1241,7 +1233,7 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
             sh.cv.wait(g, [&] {
                 if (sh.error != NTC_OK) return true;
                 if (stop_batch >= 0 && (int64_t)b > stop_batch) return true;
-                assign_ahead(b);
+                assign_ahead();
                 const DSlot &sl = slot_of(b);
                 return sl.batch == b && sl.decoded;
             });

@@ -8,23 +8,21 @@
 //                                         31-base 2-bit chunks of s4, App. B.4's ((T-1) % 31) + 1)
 //
 // A code stream is a chain of variable-length codes (Rice: unary quotient + p bits; minimal
-// binary: l or l + 1 bits), so its code boundaries are found in parallel the way a
-// self-synchronising prefix code allows (k_unpack_streams, one workgroup per stream):
-// Rice streams (s2, s3; k_unpack_streams):
-//   A  every thread decodes its segment of the stream from the segment's first bit as if a
-//      code started there, marking the code starts of its chain in a bitmap;
-//   B  each thread goes on past its segment's end into the next segment until its chain
-//      meets a position the next thread's chain marked: from there both chains agree.
-//      Thread 0's chain is the true one (the stream starts with a code), so by induction
-//      every segment's true codes are: the ones the previous thread decoded before the
-//      meeting point, then the next thread's marked starts;
-//   C  true codes per segment (a count + a popcount of the bitmap), block scan -> offsets;
-//   D  each thread decodes its segment's true codes into place.
-// A chain that never meets the next one within that segment (possible for pathological
-// streams, never seen on ntcomp's) makes the workgroup decode its stream sequentially.
-// Minimal-binary streams (s1, s4; k_unpack_mb) are l- or (l + 1)-bit codes, nearly all of one
-// length, and such chains need not ever meet: there every segment's transfer is computed for
-// each of the l + 1 offsets a code can start at, and one thread follows the true entries.
+// binary: l or l + 1 bits), so its code boundaries are found in parallel, segment by segment,
+// with every stream cut into tiles (a workgroup each) so a call's streams fill the GPU:
+// Rice streams (s2, s3; k_rice_*) synchronise the way a self-synchronising prefix code does:
+//   every segment is decoded from its first bit as if a code started there, its starts
+//   marked in a bitmap; each chain then goes on past its segment's end until it meets a
+//   start a later segment's chain marked (nearly always the next one's, within a few codes),
+//   from where both agree.  Segment 0's chain is the true one (the stream starts with a
+//   code), so the true chain is: segment 0's chain, its codes past the end up to the meeting
+//   point, the met segment's marked starts from there, and so on -- true codes per segment
+//   (a popcount + the codes up to the meeting point), a scan, a decode into place.  A chain
+//   that meets none within 8 segments makes one lane decode the stream.
+// Minimal-binary streams (s1, s4; k_mb_*) are l- or (l + 1)-bit codes, nearly all of one
+//   length, and such chains need not ever meet: there every segment's transfer is computed
+//   for each of the l + 1 offsets a code can start at, and the true entries follow from
+//   composed tile transfers.
 //
 // k_zip_count + k_zip_write (a workgroup per 16,384 records of a block) zip the four value
 // streams back into u64 records with two block scans (long records -> s1/s2 index, short
@@ -32,8 +30,8 @@
 // what read_block_impl checks (stream sizes, flags past the streams), and sums the reads
 // (first flags) and bases the FASTA writer needs.
 //
-// Bound: the payload is read ~3x (speculative, continuation, final decode) and the values
-// once; about 1 B per record of payload at C91.
+// Work: Rice bits are decoded ~2x (speculative + final, the continuations are short),
+// minimal-binary bits l + 2 times; the payload (~1 B per record at C91) is L2-resident.
 #include <hip/hip_runtime.h>
 
 #include "../../include/ntcomp_gpu.h"
@@ -43,7 +41,6 @@ namespace ntc {
 
 namespace {
 
-constexpr int kUnpThreads = 1024;  // threads (segments) per stream
 constexpr int kZipThreads = 256;   // threads per block in the zip
 constexpr int kZipPer = 4;         // records per thread per zip tile
 
@@ -52,11 +49,18 @@ __device__ __forceinline__ uint64_t bswap64(uint64_t x) { return __builtin_bswap
 // The 64 stream bits from bit position pos (MSB first), zero past the stream's end.  The
 // cursor keeps the two words under the last position: a thread's positions only grow, so a
 // code costs a load only when it crosses into the next word.
+// A workgroup's words may be staged in LDS (sw: words w0 .. w0 + nl - 1, byte-swapped);
+// positions outside that window read global memory.
 struct Bits64 {
     const uint64_t *w;
     uint64_t nwords;
     uint64_t wi = ~0ull - 1, hi = 0, lo = 0;  // (not ~0: ~0 + 1 would look like "the next word" of word 0)
-    __device__ __forceinline__ uint64_t load(uint64_t i) const { return i < nwords ? bswap64(w[i]) : 0; }
+    const uint64_t *sw = nullptr;
+    uint64_t w0 = 0, nl = 0;
+    __device__ __forceinline__ uint64_t load(uint64_t i) const {
+        if (i - w0 < nl) return sw[i - w0];
+        return i < nwords ? bswap64(w[i]) : 0;
+    }
     __device__ __forceinline__ uint64_t peek(uint64_t pos) {
         const uint64_t i = pos >> 6;
         if (i != wi) {
@@ -121,15 +125,12 @@ __device__ __forceinline__ Code mb_at(Bits64 &bt, uint64_t pos, uint32_t l, uint
     return {len, v ? v - 1 : 0, v == 0};
 }
 
-struct StreamCoder {
-    const uint64_t *w;
-    uint64_t nwords;
-    bool rice;
-    uint32_t p, l;
-    uint64_t limit;
-    Bits64 bt;
-    __device__ Code at(uint64_t pos) { return rice ? rice_at(bt, pos, p) : mb_at(bt, pos, l, limit); }
-};
+
+// the workgroup's window of a stream's words into LDS (zero past the stream's end)
+__device__ __forceinline__ void stage_words(uint64_t *sw, const uint64_t *w, uint64_t nwords, uint64_t w0, uint32_t n) {
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) sw[i] = w0 + i < nwords ? bswap64(w[w0 + i]) : 0;
+    __syncthreads();
+}
 
 __device__ __forceinline__ bool marked(const uint64_t *m, uint64_t pos) { return (m[pos >> 6] >> (pos & 63)) & 1u; }
 
@@ -154,7 +155,7 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
     return x;
 }
 
-// exclusive block scan (kUnpThreads or kZipThreads threads), through sh (>= threads / 64 words)
+// exclusive block scan (kThreads threads), through sh (>= threads / 64 words)
 template <int kThreads>
 __device__ __forceinline__ uint64_t block_exscan(uint64_t v, uint64_t *tot, uint64_t *sh) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -177,199 +178,343 @@ __device__ __forceinline__ uint64_t block_exscan(uint64_t v, uint64_t *tot, uint
     return base + inc - v;
 }
 
-// Rice streams (s2, s3 of every block: workgroup 2 i + j takes stream 4 i + 1 + j)
-__global__ __launch_bounds__(kUnpThreads) void k_unpack_streams(const uint64_t *payload, const UnpackStream *st,
-                                                               uint64_t *marks, uint64_t *vals, int32_t *status) {
-    const uint32_t si = 4 * (blockIdx.x >> 1) + 1 + (blockIdx.x & 1);
-    const UnpackStream s = st[si];
-    const int t = threadIdx.x;
-    __shared__ uint64_t sh[kUnpThreads / 64];
-    __shared__ uint64_t s_f[kUnpThreads + 1], s_y[kUnpThreads + 1], s_pre[kUnpThreads + 1];
-    __shared__ int s_fail, s_err;
-    const uint64_t nbits = s.nwords * 64;
-    if (t == 0) {
-        s_fail = 0;
-        s_err = 0;
-    }
-    StreamCoder cd{payload + s.word_off, s.nwords, true, 0, 0, 0, Bits64{payload + s.word_off, s.nwords}};
-    if (cd.rice) {
-        if (s.param > 63) {
-            if (t == 0) status[si] = NTC_ERR_FORMAT;
-            return;
-        }
-        cd.p = (uint32_t)s.param;
-    } else {
-        if (s.param < 1) {  // minimal_binary_decode: param 0 decodes no value
-            if (t == 0) status[si] = s.n == 0 ? 0 : NTC_ERR_FORMAT;
-            return;
-        }
-        cd.l = 63u - (uint32_t)__builtin_clzll(s.param);
-        cd.limit = (cd.l == 63 ? 0ull : (2ull << cd.l)) - s.param;
-    }
-    if (s.n == 0) {
-        if (t == 0) status[si] = 0;
-        return;
-    }
-    uint64_t *m = marks + s.word_off;
-    // segments of S bits (a multiple of 64: each thread owns whole bitmap words)
-    const uint64_t S = ((nbits + kUnpThreads - 1) / kUnpThreads + 63) & ~63ull;
-    const uint64_t a = (uint64_t)t * S, b = a + S < nbits ? a + S : nbits;
-    const bool active = a < nbits;
-    // ---- A: speculative chain from the segment's first bit, starts marked -------------------
-    uint64_t pos = a, own = 0;
+// ---- Rice streams (s2, s3) ------------------------------------------------------------------
+// Segments of kRiceSegBits bits (whole bitmap words), a wave per tile of kRiceTileSegs
+// segments, so a call's streams spread over the whole GPU.  Per segment (g = the call's
+// segment index; the arrays below are indexed by it):
+//   k_rice_a      the speculative chain from the segment's first bit: its code starts marked
+//                 in the bitmap, END = its first start past the segment (kDeadPos: it ran past
+//                 the stream's end);
+//   k_rice_b      on from END until a start some later segment's chain marked: NEXT = that
+//                 segment, Y = the meeting point, PRE = the codes before it.  Nearly always
+//                 the next segment, within a few codes; otherwise the stream's flags get
+//                 kNotSimple (its true chain is followed by k_rice_walk), and a chain that met
+//                 none within 8 segments gets kSerial (one lane decodes the stream);
+//   k_rice_walk   a wave per stream: the serial decode, or the true chain's segments and the
+//                 points it joins them at (ENTRY, kNoEntry for the segments it runs through);
+//                 a simple stream's segment g is joined at Y[g - 1];
+//   k_rice_count  true codes per segment (marks from its entry to its end + PRE), per tile;
+//   k_rice_scan   a wave per stream: the tiles' first value indices, the stream's status;
+//   k_rice_decode each segment's true codes into place.
+constexpr int kRiceSegBits = 512;
+constexpr int kRiceTileSegs = 64;
+constexpr uint64_t kDeadPos = ~0ull, kNoEntry = ~0ull;
+constexpr uint32_t kNoNext = 0xFFFFFFFFu;
+constexpr uint32_t kNotSimple = 1, kSerial = 2, kBadParam = 4;
+constexpr uint32_t kRiceWin = kRiceTileSegs * kRiceSegBits / 64 + 16;  // LDS words: the tile + 1024 bits
+
+struct RiceWs {
+    uint64_t *Y, *E, *END;
+    uint32_t *NEXT, *PRE, *CNT;
+    uint64_t *TSUM, *TOFF;
+    uint32_t *flags;
+};
+__host__ __device__ inline RiceWs rice_ws(void *base, uint64_t n_tiles, uint64_t n_streams) {
+    const uint64_t ns = n_tiles * kRiceTileSegs;
+    RiceWs w;
+    uint64_t *q = (uint64_t *)base;
+    w.Y = q;
+    w.E = q + ns;
+    w.END = q + 2 * ns;
+    w.TSUM = q + 3 * ns;
+    w.TOFF = w.TSUM + n_tiles;
+    uint32_t *r = (uint32_t *)(w.TOFF + n_tiles);
+    w.NEXT = r;
+    w.PRE = r + ns;
+    w.CNT = r + 2 * ns;
+    w.flags = r + 3 * ns;
+    (void)n_streams;
+    return w;
+}
+static uint64_t rice_ws_bytes(uint64_t n_tiles, uint64_t n_streams) {
+    return n_tiles * kRiceTileSegs * 36 + n_tiles * 16 + n_streams * 4 + 64;
+}
+
+struct RiceSeg {
+    UnpackStream s;
+    uint64_t seg, a, b, g, nbits;
+    uint32_t r;
+    bool active;
+};
+__device__ __forceinline__ RiceSeg rice_seg(const UnpackStream *st, const UnpTile *tiles) {
+    const UnpTile tl = tiles[blockIdx.x];
+    RiceSeg x;
+    x.s = st[tl.si];
+    x.r = tl.stream;
+    x.nbits = x.s.nwords * 64;
+    x.seg = (uint64_t)tl.tile * kRiceTileSegs + threadIdx.x;
+    x.a = x.seg * kRiceSegBits;
+    x.b = x.a + kRiceSegBits < x.nbits ? x.a + kRiceSegBits : x.nbits;
+    x.g = (uint64_t)blockIdx.x * kRiceTileSegs + threadIdx.x;
+    x.active = x.a < x.nbits;
+    return x;
+}
+
+__global__ __launch_bounds__(kRiceTileSegs) void k_rice_a(const uint64_t *payload, const UnpackStream *st,
+                                                         const UnpTile *tiles, uint64_t *marks, RiceWs w) {
+    const RiceSeg x = rice_seg(st, tiles);
+    __shared__ uint64_t sw[kRiceWin];
+    const uint64_t w0 = (uint64_t)tiles[blockIdx.x].tile * kRiceTileSegs * kRiceSegBits / 64;
+    stage_words(sw, payload + x.s.word_off, x.s.nwords, w0, kRiceWin);
+    if (!x.active) return;
+    uint64_t *m = marks + x.s.word_off;
+    Bits64 bt{payload + x.s.word_off, x.s.nwords};
+    bt.sw = sw;
+    bt.w0 = w0;
+    bt.nl = kRiceWin;
+    const uint32_t p = (uint32_t)x.s.param;
+    uint64_t pos = x.a, word = 0, wi = x.a >> 6;
     bool dead = false;
-    if (active) {
-        for (uint64_t i = a >> 6; i < (b + 63) >> 6; i++) m[i] = 0;
-        uint64_t word = 0, wi = a >> 6;
-        while (pos < b) {
-            const Code c = cd.at(pos);
-            if (!c.len) {
-                dead = true;
+    while (pos < x.b) {
+        const Code c = rice_at(bt, pos, p);
+        if (!c.len) {
+            dead = true;
+            break;
+        }
+        while ((pos >> 6) != wi) {  // (a code may skip whole words: they hold no start)
+            m[wi] = word;
+            wi++;
+            word = 0;
+        }
+        word |= 1ull << (pos & 63);
+        pos += c.len;
+    }
+    for (; wi < (x.b + 63) >> 6; wi++) {
+        m[wi] = word;
+        word = 0;
+    }
+    w.END[x.g] = dead ? kDeadPos : pos;
+}
+
+__global__ __launch_bounds__(kRiceTileSegs) void k_rice_b(const uint64_t *payload, const UnpackStream *st,
+                                                         const UnpTile *tiles, const uint64_t *marks, RiceWs w) {
+    const RiceSeg x = rice_seg(st, tiles);
+    __shared__ uint64_t sw[kRiceWin];
+    const uint64_t w0 = (uint64_t)tiles[blockIdx.x].tile * kRiceTileSegs * kRiceSegBits / 64;
+    stage_words(sw, payload + x.s.word_off, x.s.nwords, w0, kRiceWin);
+    if (!x.active) return;
+    const uint64_t *m = marks + x.s.word_off;
+    const uint64_t e = w.END[x.g];
+    uint64_t q = e, pre = 0;
+    uint32_t nx = kNoNext, fl = 0;
+    if (e == kDeadPos) {
+        q = x.nbits;
+        if (x.b < x.nbits) fl |= kNotSimple;  // the stream's codes end inside it
+    } else {
+        Bits64 bt{payload + x.s.word_off, x.s.nwords};
+        bt.sw = sw;
+        bt.w0 = w0;
+        bt.nl = kRiceWin;
+        const uint32_t p = (uint32_t)x.s.param;
+        const uint64_t lim = x.b + 8ull * kRiceSegBits;
+        while (q < x.nbits) {
+            if (marked(m, q)) {
+                nx = (uint32_t)(q / kRiceSegBits);
                 break;
             }
-            if ((pos >> 6) != wi) {
-                m[wi] = word;
-                wi = pos >> 6;
-                word = 0;
+            if (q >= lim) {
+                fl |= kSerial;
+                break;
             }
-            word |= 1ull << (pos & 63);
-            own++;
-            pos += c.len;
+            const Code c = rice_at(bt, q, p);
+            if (!c.len) break;
+            q += c.len;
+            pre++;
         }
-        m[wi] = word;
+        if (x.b < x.nbits && nx != (uint32_t)(x.seg + 1)) fl |= kNotSimple;
     }
-    __syncthreads();
-    // ---- B: on into the next segment until the next thread's chain is met ---------------------
-    // (thread t writes s_f / s_y / s_pre of segment t + 1: its true first start, the meeting
-    // point and the codes before it)
-    if (active && b < nbits) {
-        const uint64_t nb = b + S < nbits ? b + S : nbits;
-        uint64_t q = pos, pre = 0;
-        bool met = false;
-        if (!dead) {
-            while (q < nb) {
-                if (marked(m, q)) {
-                    met = true;
-                    break;
-                }
-                const Code c = cd.at(q);
-                if (!c.len) break;
-                q += c.len;
-                pre++;
-            }
-        }
-        // a chain that ran past the stream's end (dead) ends the stream's codes: the segments
-        // after it hold none (fine when the first n codes all lie before it)
-        if (dead) {
-            s_f[t + 1] = nbits;
-            s_y[t + 1] = nbits;
-            s_pre[t + 1] = 0;
-        } else if (met) {
-            s_f[t + 1] = pos;
-            s_y[t + 1] = q;
-            s_pre[t + 1] = pre;
-        } else if (q >= nb && pos < nb) {
-            s_fail = 1;  // the chains did not meet within the next segment
-        } else {
-            // pos >= nb: a code longer than a segment; or the chain died in the next segment
-            s_fail = 1;
-        }
-    }
-    __syncthreads();
-    if (s_fail) {  // sequential fallback: thread 0 walks the whole stream
+    w.NEXT[x.g] = nx;
+    w.Y[x.g] = q;
+    w.PRE[x.g] = (uint32_t)pre;
+    if (fl) atomicOr(&w.flags[x.r], fl);
+}
+
+__global__ __launch_bounds__(64) void k_rice_walk(const uint64_t *payload, const UnpackStream *st,
+                                                 const UnpStreamRef *rs, uint64_t *vals, int32_t *status, RiceWs w) {
+    const UnpStreamRef ref = rs[blockIdx.x];
+    const UnpackStream s = st[ref.si];
+    const int t = threadIdx.x;
+    if (s.param > 63) {
         if (t == 0) {
+            status[ref.si] = NTC_ERR_FORMAT;
+            w.flags[blockIdx.x] = kBadParam;
+        }
+        return;
+    }
+    if (s.n == 0 || ref.n_tiles == 0) {
+        if (t == 0) status[ref.si] = s.n == 0 ? 0 : NTC_ERR_FORMAT;
+        return;
+    }
+    const uint32_t fl = w.flags[blockIdx.x];
+    if (fl & kSerial) {  // one lane decodes the whole stream
+        if (t == 0) {
+            Bits64 bt{payload + s.word_off, s.nwords};
             uint64_t p = 0;
             int err = 0;
             for (uint64_t i = 0; i < s.n; i++) {
-                const Code c = cd.at(p);
-                if (!c.len || c.bad) {
+                const Code c = rice_at(bt, p, (uint32_t)s.param);
+                if (!c.len) {
                     err = NTC_ERR_FORMAT;
                     break;
                 }
                 vals[s.val_off + i] = c.val;
                 p += c.len;
             }
-            status[si] = err;
+            status[ref.si] = err;
         }
         return;
     }
-    // ---- C: true codes per segment, offsets ----------------------------------------------------
-    uint64_t cnt = 0, f = 0;
-    if (active) {
-        if (t == 0) {
-            cnt = dead ? own : count_marks(m, 0, b);
-            f = 0;
-        } else {
-            f = s_f[t];
-            const uint64_t y = s_y[t];
-            cnt = s_pre[t] + (y < b ? count_marks(m, y, b) : 0);
-            // a dead chain of this thread: its marks after the meeting point run up to where it
-            // died; the codes past that (the stream's tail padding) do not exist
+    if (!(fl & kNotSimple)) return;
+    const uint64_t g0 = (uint64_t)ref.first_tile * kRiceTileSegs, ns = (uint64_t)ref.n_tiles * kRiceTileSegs;
+    for (uint64_t i = t; i < ns; i += 64) w.E[g0 + i] = kNoEntry;
+    __syncthreads();
+    if (t == 0) {
+        uint64_t v = 0, y = 0;
+        for (;;) {
+            w.E[g0 + v] = y;
+            const uint32_t nx = w.NEXT[g0 + v];
+            if (nx == kNoNext) break;
+            y = w.Y[g0 + v];
+            v = nx;
         }
     }
-    uint64_t tot;
-    const uint64_t off = block_exscan<kUnpThreads>(cnt, &tot, sh);
-    if (t == 0 && tot < s.n) s_err = NTC_ERR_FORMAT;  // fewer codes than values
-    // ---- D: decode this segment's true codes into place ---------------------------------------
-    if (active && off < s.n) {
-        uint64_t p = f;
-        for (uint64_t j = 0; j < cnt && off + j < s.n; j++) {
-            const Code c = cd.at(p);
-            if (!c.len || c.bad) {
-                atomicExch(&s_err, (int)NTC_ERR_FORMAT);
+}
+
+__global__ __launch_bounds__(kRiceTileSegs) void k_rice_count(const UnpackStream *st, const UnpTile *tiles,
+                                                             const uint64_t *marks, RiceWs w) {
+    const RiceSeg x = rice_seg(st, tiles);
+    const uint32_t fl = w.flags[x.r];
+    if (fl & (kSerial | kBadParam)) return;
+    uint64_t y = kNoEntry;
+    if (x.active) y = (fl & kNotSimple) ? w.E[x.g] : (x.seg == 0 ? 0 : w.Y[x.g - 1]);
+    const bool on = x.active && y != kNoEntry;
+    const uint64_t cnt = on ? (y < x.b ? count_marks(marks + x.s.word_off, y, x.b) : 0) + w.PRE[x.g] : 0;
+    if (x.active) {
+        w.CNT[x.g] = (uint32_t)cnt;
+        w.E[x.g] = on ? y : kNoEntry;
+    }
+    const uint64_t tot = wave_sum(cnt);
+    if (threadIdx.x == 0) w.TSUM[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(64) void k_rice_scan(const UnpackStream *st, const UnpStreamRef *rs, int32_t *status,
+                                                 RiceWs w) {
+    const UnpStreamRef ref = rs[blockIdx.x];
+    const UnpackStream s = st[ref.si];
+    if (s.n == 0 || ref.n_tiles == 0 || (w.flags[blockIdx.x] & (kSerial | kBadParam))) return;
+    const int lane = threadIdx.x;
+    uint64_t base = 0;
+    for (uint32_t k0 = 0; k0 < ref.n_tiles; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        const uint64_t v = k < ref.n_tiles ? w.TSUM[ref.first_tile + k] : 0;
+        uint64_t inc = v;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t u = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += u;
+        }
+        if (k < ref.n_tiles) w.TOFF[ref.first_tile + k] = base + inc - v;
+        base += __shfl(inc, 63, 64);
+    }
+    if (lane == 0) status[ref.si] = base < s.n ? NTC_ERR_FORMAT : 0;  // fewer codes than values
+}
+
+__global__ __launch_bounds__(kRiceTileSegs) void k_rice_decode(const uint64_t *payload, const UnpackStream *st,
+                                                              const UnpTile *tiles, uint64_t *vals, int32_t *status,
+                                                              RiceWs w) {
+    const RiceSeg x = rice_seg(st, tiles);
+    if (w.flags[x.r] & (kSerial | kBadParam)) return;
+    __shared__ uint64_t sw[kRiceWin];
+    const uint64_t w0 = (uint64_t)tiles[blockIdx.x].tile * kRiceTileSegs * kRiceSegBits / 64;
+    stage_words(sw, payload + x.s.word_off, x.s.nwords, w0, kRiceWin);
+    const uint64_t cnt = x.active ? w.CNT[x.g] : 0;
+    const int lane = threadIdx.x;
+    uint64_t inc = cnt;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t u = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += u;
+    }
+    const uint64_t off = w.TOFF[blockIdx.x] + inc - cnt;
+    int err = 0;
+    if (cnt && off < x.s.n) {
+        Bits64 bt{payload + x.s.word_off, x.s.nwords};
+        bt.sw = sw;
+        bt.w0 = w0;
+        bt.nl = kRiceWin;
+        uint64_t p = w.E[x.g];
+        for (uint64_t j = 0; j < cnt && off + j < x.s.n; j++) {
+            const Code c = rice_at(bt, p, (uint32_t)x.s.param);
+            if (!c.len) {
+                err = NTC_ERR_FORMAT;
                 break;
             }
-            vals[s.val_off + off + j] = c.val;
+            vals[x.s.val_off + off + j] = c.val;
             p += c.len;
         }
     }
-    __syncthreads();
-    if (t == 0) status[si] = s_err;
+    if (err) atomicOr(&status[tiles[blockIdx.x].si], err);
 }
 
-// Minimal-binary streams (s1, s4: workgroup 2 i + j takes stream 4 i + 3 j).  Their codes are
-// l or l + 1 bits, mostly one of the two, and chains started at different offsets rarely
-// meet (fixed-length codes never do), so each segment's transfer is computed for every entry
-// offset a code can start at: thread t decodes its segment from each e < l + 1 bits past its
-// first bit and records where that chain leaves (the first code start past the segment, at
-// most l bits on) and its codes; thread 0 then follows the true entry from segment to segment
-// (one LDS lookup each), and each segment's true codes are decoded into place.
-__global__ __launch_bounds__(kUnpThreads) void k_unpack_mb(const uint64_t *payload, const UnpackStream *st,
-                                                          uint32_t *chainc, uint64_t *vals, int32_t *status) {
-    const uint32_t si = 4 * (blockIdx.x >> 1) + ((blockIdx.x & 1) ? 3 : 0);
-    const UnpackStream s = st[si];
+// Minimal-binary streams (s1, s4).  Their codes are l or l + 1 bits, mostly one of the two,
+// and chains started at different offsets rarely meet (fixed-length codes never do), so a
+// segment's codes are found through its transfer: for each of the L = l + 1 offsets e a code
+// can start at past the segment's first bit, where that chain leaves the segment (the first
+// code start past it, at most l bits on) and how many codes it holds.  Transfers compose, so
+// the true entries come from a two-level walk:
+//   k_mb_tab     a thread per segment (kMbSegBits bits) computes its L transfers; lane e of a
+//                tile (kMbTileSegs segments) follows entry e through the tile's segments in
+//                LDS -> the tile's own transfer;
+//   k_mb_walk    a wave per stream follows the true entry from tile to tile (bit 0 enters
+//                tile 0 at offset 0) -> each tile's entry and its codes' first value index;
+//   k_mb_decode  a tile follows its entry through its segments in LDS, scans the segments'
+//                code counts and decodes each segment's true codes into place.
+// The work is L transfers of every bit, spread over all CUs (a tile per workgroup).
+constexpr int kMbSegBits = 256;   // bits per segment (>= 64 > l + 1)
+constexpr int kMbTileSegs = 256;  // segments (threads) per tile
+constexpr uint8_t kMbDead = 255;  // a chain that ran past the stream's end
+constexpr int kMbWalkTiles = 128; // tiles per LDS chunk of k_mb_walk
+constexpr uint32_t kMbWin = kMbTileSegs * kMbSegBits / 64 + 2;  // LDS words: the tile + the last code
+
+struct MbParams {
+    uint32_t l, L;
+    uint64_t limit, nbits;
+};
+__device__ __forceinline__ MbParams mb_params(const UnpackStream &s) {
+    MbParams q;
+    q.l = 63u - (uint32_t)__builtin_clzll(s.param);
+    q.L = q.l + 1;
+    q.limit = (q.l == 63 ? 0ull : (2ull << q.l)) - s.param;
+    q.nbits = s.nwords * 64;
+    return q;
+}
+
+// transfer tables: X[(tile * 64 + e) * kMbTileSegs + seg] exit offsets, C[...] code counts
+// (entry-major, so a tile's lanes store and load consecutive bytes); TX / TC the tiles' own
+__global__ __launch_bounds__(kMbTileSegs) void k_mb_tab(const uint64_t *payload, const UnpackStream *st,
+                                                       const UnpTile *tiles, uint8_t *X, uint16_t *C, uint8_t *TX,
+                                                       uint32_t *TC) {
+    const UnpTile tl = tiles[blockIdx.x];
+    const UnpackStream s = st[tl.si];
+    const MbParams q = mb_params(s);
     const int t = threadIdx.x;
-    __shared__ uint8_t s_x[kUnpThreads * 64];  // exit offset past the segment per entry (255: dead)
-    __shared__ uint8_t s_entry[kUnpThreads];
-    __shared__ uint64_t sh[kUnpThreads / 64];
-    __shared__ int s_err;
-    if (s.param < 1) {  // minimal_binary_decode: param 0 decodes no value
-        if (t == 0) status[si] = s.n == 0 ? 0 : NTC_ERR_FORMAT;
-        return;
-    }
-    if (s.n == 0) {
-        if (t == 0) status[si] = 0;
-        return;
-    }
-    if (t == 0) s_err = 0;
-    StreamCoder cd{payload + s.word_off, s.nwords, false, 0, 0, 0, Bits64{payload + s.word_off, s.nwords}};
-    cd.l = 63u - (uint32_t)__builtin_clzll(s.param);
-    cd.limit = (cd.l == 63 ? 0ull : (2ull << cd.l)) - s.param;
-    const uint32_t L = cd.l + 1;  // entry offsets 0 .. l (codes are at most l + 1 bits)
-    const uint64_t nbits = s.nwords * 64;
-    uint64_t S = (nbits + kUnpThreads - 1) / kUnpThreads;
-    if (S < 64) S = 64;
-    const uint64_t a = (uint64_t)t * S, b = a + S < nbits ? a + S : nbits;
-    const bool active = a < nbits;
-    uint32_t *cc = chainc + (uint64_t)blockIdx.x * kUnpThreads * 64 + (uint64_t)t * 64;
-    // ---- A: the segment's transfer for every entry offset --------------------------------------
-    if (active) {
-        for (uint32_t e = 0; e < L; e++) {
+    __shared__ uint8_t sX[64 * kMbTileSegs];
+    __shared__ uint16_t sC[64 * kMbTileSegs];
+    __shared__ uint64_t sw[kMbWin];
+    const uint64_t seg0 = (uint64_t)tl.tile * kMbTileSegs;
+    const uint64_t w0 = seg0 * kMbSegBits / 64;
+    stage_words(sw, payload + s.word_off, s.nwords, w0, kMbWin);
+    const uint64_t a = (seg0 + t) * kMbSegBits, b = a + kMbSegBits < q.nbits ? a + kMbSegBits : q.nbits;
+    const uint64_t tbase = (uint64_t)blockIdx.x * 64 * kMbTileSegs;
+    if (a < q.nbits) {
+        Bits64 bt{payload + s.word_off, s.nwords};
+        bt.sw = sw;
+        bt.w0 = w0;
+        bt.nl = kMbWin;
+        for (uint32_t e = 0; e < q.L; e++) {
             uint64_t pos = a + e;
             uint32_t cnt = 0;
             bool dead = false;
             while (pos < b) {
-                const Code c = cd.at(pos);
+                const Code c = mb_at(bt, pos, q.l, q.limit);
                 if (!c.len) {
                     dead = true;
                     break;
@@ -377,36 +522,112 @@ __global__ __launch_bounds__(kUnpThreads) void k_unpack_mb(const uint64_t *paylo
                 pos += c.len;
                 cnt++;
             }
-            s_x[t * 64 + e] = dead ? 255 : (uint8_t)(pos - b);
-            cc[e] = cnt;
+            const uint8_t x = dead ? kMbDead : (uint8_t)(pos - b);
+            sX[e * kMbTileSegs + t] = x;
+            sC[e * kMbTileSegs + t] = (uint16_t)cnt;
+            X[tbase + (uint64_t)e * kMbTileSegs + t] = x;
+            C[tbase + (uint64_t)e * kMbTileSegs + t] = (uint16_t)cnt;
         }
     }
     __syncthreads();
-    // ---- B: the true entry of every segment (segment 0: the stream's first bit) ----------------
-    if (t == 0) {
-        uint32_t e = 0;
-        for (int u = 0; u < kUnpThreads; u++) {
-            if ((uint64_t)u * S >= nbits || e == 255) {
-                s_entry[u] = 255;
-                continue;
+    if ((uint32_t)t < q.L) {
+        const uint64_t segs = (q.nbits + kMbSegBits - 1) / kMbSegBits;
+        const uint32_t ns = (uint32_t)(segs - seg0 < kMbTileSegs ? segs - seg0 : kMbTileSegs);
+        uint32_t ex = (uint32_t)t, cnt = 0;
+        for (uint32_t u = 0; u < ns && ex != kMbDead; u++) {
+            cnt += sC[ex * kMbTileSegs + u];
+            ex = sX[ex * kMbTileSegs + u];
+        }
+        TX[(uint64_t)blockIdx.x * 64 + t] = (uint8_t)ex;
+        TC[(uint64_t)blockIdx.x * 64 + t] = cnt;
+    }
+}
+
+// a wave per minimal-binary stream: tile entries TE and first value indices TP; the stream's
+// status (param 0 decodes no value; fewer codes than values)
+__global__ __launch_bounds__(64) void k_mb_walk(const UnpackStream *st, const UnpStreamRef *mbs, const uint8_t *TX,
+                                               const uint32_t *TC, uint8_t *TE, uint64_t *TP, int32_t *status) {
+    const UnpStreamRef m = mbs[blockIdx.x];
+    const UnpackStream s = st[m.si];
+    const int t = threadIdx.x;
+    if (s.param < 1 || s.n == 0) {
+        if (t == 0) status[m.si] = s.n == 0 ? 0 : NTC_ERR_FORMAT;
+        return;
+    }
+    __shared__ uint8_t sX[kMbWalkTiles * 64];
+    __shared__ uint32_t sC[kMbWalkTiles * 64];
+    uint32_t e = 0;
+    uint64_t p = 0;
+    for (uint32_t k0 = 0; k0 < m.n_tiles; k0 += kMbWalkTiles) {
+        const uint32_t nk = m.n_tiles - k0 < (uint32_t)kMbWalkTiles ? m.n_tiles - k0 : (uint32_t)kMbWalkTiles;
+        const uint64_t g0 = (uint64_t)m.first_tile + k0;
+        for (uint32_t i = t; i < nk * 64; i += 64) {
+            sX[i] = TX[g0 * 64 + i];
+            sC[i] = TC[g0 * 64 + i];
+        }
+        __syncthreads();
+        if (t == 0) {
+            for (uint32_t k = 0; k < nk; k++) {
+                TE[g0 + k] = (uint8_t)e;
+                TP[g0 + k] = p;
+                if (e == kMbDead) continue;
+                p += sC[k * 64 + e];
+                e = sX[k * 64 + e];
             }
-            s_entry[u] = (uint8_t)e;
-            e = s_x[u * 64 + e];
+        }
+        __syncthreads();
+        e = __shfl(e, 0, 64);
+        p = __shfl(p, 0, 64);
+    }
+    if (t == 0) status[m.si] = p < s.n ? NTC_ERR_FORMAT : 0;  // fewer codes than values
+}
+
+__global__ __launch_bounds__(kMbTileSegs) void k_mb_decode(const uint64_t *payload, const UnpackStream *st,
+                                                          const UnpTile *tiles, const uint8_t *X, const uint16_t *C,
+                                                          const uint8_t *TE, const uint64_t *TP, uint64_t *vals,
+                                                          int32_t *status) {
+    const uint8_t e0 = TE[blockIdx.x];
+    if (e0 == kMbDead) return;  // the stream's codes ended in an earlier tile
+    const UnpTile tl = tiles[blockIdx.x];
+    const UnpackStream s = st[tl.si];
+    const MbParams q = mb_params(s);
+    const int t = threadIdx.x;
+    __shared__ uint8_t sX[64 * kMbTileSegs];
+    __shared__ uint8_t sE[kMbTileSegs];
+    __shared__ uint64_t sh[kMbTileSegs / 64];
+    __shared__ uint64_t sw[kMbWin];
+    __shared__ int s_err;
+    const uint64_t tbase = (uint64_t)blockIdx.x * 64 * kMbTileSegs;
+    for (uint32_t e = 0; e < q.L; e++) sX[e * kMbTileSegs + t] = X[tbase + (uint64_t)e * kMbTileSegs + t];
+    if (t == 0) s_err = 0;
+    __syncthreads();
+    const uint64_t seg0 = (uint64_t)tl.tile * kMbTileSegs;
+    const uint64_t w0 = seg0 * kMbSegBits / 64;
+    stage_words(sw, payload + s.word_off, s.nwords, w0, kMbWin);
+    const uint64_t segs = (q.nbits + kMbSegBits - 1) / kMbSegBits;
+    const uint32_t ns = (uint32_t)(segs - seg0 < kMbTileSegs ? segs - seg0 : kMbTileSegs);
+    if (t == 0) {
+        uint32_t e = e0;
+        for (uint32_t u = 0; u < kMbTileSegs; u++) {
+            sE[u] = (uint8_t)(u < ns ? e : kMbDead);
+            if (u < ns && e != kMbDead) e = sX[e * kMbTileSegs + u];
         }
     }
     __syncthreads();
-    // ---- C + D: true codes per segment, offsets, decode into place ----------------------------
-    const uint32_t en = s_entry[t];
-    const uint64_t cnt = active && en != 255 ? cc[en] : 0;
+    const uint32_t en = sE[t];
+    const uint64_t cnt = en != kMbDead ? C[tbase + (uint64_t)en * kMbTileSegs + t] : 0;
     uint64_t tot;
-    const uint64_t off = block_exscan<kUnpThreads>(cnt, &tot, sh);
-    if (t == 0 && tot < s.n) s_err = NTC_ERR_FORMAT;  // fewer codes than values
+    const uint64_t off = TP[blockIdx.x] + block_exscan<kMbTileSegs>(cnt, &tot, sh);
     if (cnt && off < s.n) {
-        uint64_t p = a + en;
+        Bits64 bt{payload + s.word_off, s.nwords};
+        bt.sw = sw;
+        bt.w0 = w0;
+        bt.nl = kMbWin;
+        uint64_t p = (seg0 + t) * kMbSegBits + en;
         for (uint64_t j = 0; j < cnt && off + j < s.n; j++) {
-            const Code c = cd.at(p);
+            const Code c = mb_at(bt, p, q.l, q.limit);
             if (!c.len || c.bad) {
-                atomicExch(&s_err, (int)NTC_ERR_FORMAT);
+                s_err = NTC_ERR_FORMAT;
                 break;
             }
             vals[s.val_off + off + j] = c.val;
@@ -414,12 +635,12 @@ __global__ __launch_bounds__(kUnpThreads) void k_unpack_mb(const uint64_t *paylo
         }
     }
     __syncthreads();
-    if (t == 0) status[si] = s_err;
+    if (t == 0 && s_err) atomicOr(&status[tl.si], (int)NTC_ERR_FORMAT);
 }
 
 // The zip runs in segments of kZipSeg records, one workgroup each, so a call's few blocks
 // fill the GPU.  k_zip_count: per segment, its long records and short bases.
-constexpr uint64_t kZipSeg = 16384;
+constexpr uint64_t kZipSeg = 4096;
 __global__ __launch_bounds__(kZipThreads) void k_zip_count(const UnpackStream *st, const uint64_t *vals, uint32_t nseg,
                                                           uint64_t *segc) {
     const uint32_t b = blockIdx.x / nseg, g = blockIdx.x % nseg;
@@ -532,9 +753,16 @@ __global__ __launch_bounds__(kZipThreads) void k_zip_write(const UnpackStream *s
                 }
                 // bases jb .. jb + L - 1 of the concatenation: chunk q / 31, base q % 31
                 w = 0;
-                for (uint32_t u = 0; u < L; u++) {
-                    const uint64_t q = jb + u;
-                    w |= ((bn[q / 31] >> (2 * (q % 31))) & 3ull) << (2 * u);
+                if (L <= 32) {  // from at most two chunks
+                    const uint64_t c = jb / 31;
+                    const uint32_t o = (uint32_t)(jb - 31 * c), t0 = 31 - o < L ? 31 - o : L;
+                    if (t0) w = (bn[c] >> (2 * o)) & ((1ull << (2 * t0)) - 1);
+                    if (L > t0) w |= (bn[c + 1] & ((1ull << (2 * (L - t0))) - 1)) << (2 * t0);
+                } else {  // (longer than as_2bit takes; the host decoder's shifts)
+                    for (uint32_t u = 0; u < L; u++) {
+                        const uint64_t q = jb + u;
+                        w |= ((bn[q / 31] >> (2 * (q % 31))) & 3ull) << ((2 * u) & 63);
+                    }
                 }
                 w &= 0x00FFFFFFFFFFFFFFull;
                 bases += L;
@@ -559,22 +787,73 @@ __global__ __launch_bounds__(kZipThreads) void k_zip_write(const UnpackStream *s
 
 }  // namespace
 
-void launch_unpack(const uint64_t *payload, const UnpackStream *st, uint64_t n_blocks, uint64_t max_recs,
-                   uint64_t *marks, uint32_t *chainc, uint64_t *vals, int32_t *stream_status, const uint64_t *rec_off,
-                   uint64_t *recs, uint64_t *segc, uint64_t *out3, hipStream_t s) {
-    if (!n_blocks) return;
-    const uint32_t nseg = (uint32_t)((max_recs + kZipSeg - 1) / kZipSeg) + 1;
-    hipLaunchKernelGGL(k_unpack_streams, dim3((uint32_t)(2 * n_blocks)), dim3(kUnpThreads), 0, s, payload, st, marks,
-                       vals, stream_status);
-    hipLaunchKernelGGL(k_unpack_mb, dim3((uint32_t)(2 * n_blocks)), dim3(kUnpThreads), 0, s, payload, st, chainc, vals,
-                       stream_status);
-    (void)hipMemsetAsync(out3, 0, n_blocks * 3 * 8, s);
-    hipLaunchKernelGGL(k_zip_count, dim3((uint32_t)(n_blocks * nseg)), dim3(kZipThreads), 0, s, st, vals, nseg, segc);
-    hipLaunchKernelGGL(k_zip_write, dim3((uint32_t)(n_blocks * nseg)), dim3(kZipThreads), 0, s, st, vals, rec_off, recs,
-                       stream_status, nseg, segc, (unsigned long long *)out3);
+void unpack_plan(const UnpackStream *st, uint64_t n_blocks, UnpackPlan &plan) {
+    plan = UnpackPlan{};
+    for (uint64_t b = 0; b < n_blocks; b++)
+        for (int i = 0; i < 4; i++) {
+            const uint32_t si = (uint32_t)(4 * b + (uint64_t)i);
+            const UnpackStream &s = st[si];
+            const bool mb = i == 0 || i == 3;
+            const uint64_t seg_bits = mb ? kMbSegBits : kRiceSegBits, per = mb ? kMbTileSegs : kRiceTileSegs;
+            const uint64_t segs = (s.nwords * 64 + seg_bits - 1) / seg_bits;
+            const bool run = s.n && (mb ? s.param >= 1 : s.param <= 63);
+            const uint32_t nt = run ? (uint32_t)((segs + per - 1) / per) : 0;
+            auto &tiles = mb ? plan.mb_tiles : plan.rice_tiles;
+            auto &refs = mb ? plan.mb_streams : plan.rice_streams;
+            for (uint32_t k = 0; k < nt; k++) tiles.push_back(UnpTile{si, k, (uint32_t)refs.size(), 0});
+            refs.push_back(UnpStreamRef{si, (uint32_t)(tiles.size() - nt), nt, 0});
+        }
 }
 
-uint64_t unpack_chain_words(uint64_t n_blocks) { return 2 * n_blocks * kUnpThreads * 64; }  // u32 words
+// minimal binary: X (u8) + C (u16) per tile entry and segment, TX (u8) + TC (u32) per tile
+// entry, TE + TP per tile; then the Rice tables
+static uint64_t mb_ws_bytes(uint64_t n_tiles) { return (n_tiles * (64 * kMbTileSegs * 3 + 64 * 5 + 16) + 64) & ~63ull; }
+uint64_t unpack_ws_bytes(const UnpackPlan &plan) {
+    return mb_ws_bytes(plan.mb_tiles.size()) + rice_ws_bytes(plan.rice_tiles.size(), plan.rice_streams.size());
+}
+
+void launch_unpack(const UnpackDev &d, hipStream_t s) {
+    if (!d.n_blocks) return;
+    const uint32_t nseg = (uint32_t)((d.max_recs + kZipSeg - 1) / kZipSeg) + 1;
+    // Rice streams
+    const RiceWs rw = rice_ws((uint8_t *)d.ws + mb_ws_bytes(d.n_mb_tiles), d.n_rice_tiles, d.n_rice_streams);
+    (void)hipMemsetAsync(rw.flags, 0, (uint64_t)d.n_rice_streams * 4, s);
+    if (d.n_rice_tiles) {
+        hipLaunchKernelGGL(k_rice_a, dim3(d.n_rice_tiles), dim3(kRiceTileSegs), 0, s, d.payload, d.st, d.rice_tiles,
+                           d.marks, rw);
+        hipLaunchKernelGGL(k_rice_b, dim3(d.n_rice_tiles), dim3(kRiceTileSegs), 0, s, d.payload, d.st, d.rice_tiles,
+                           (const uint64_t *)d.marks, rw);
+    }
+    hipLaunchKernelGGL(k_rice_walk, dim3(d.n_rice_streams), dim3(64), 0, s, d.payload, d.st, d.rice_streams, d.vals,
+                       d.status, rw);
+    if (d.n_rice_tiles)
+        hipLaunchKernelGGL(k_rice_count, dim3(d.n_rice_tiles), dim3(kRiceTileSegs), 0, s, d.st, d.rice_tiles,
+                           (const uint64_t *)d.marks, rw);
+    hipLaunchKernelGGL(k_rice_scan, dim3(d.n_rice_streams), dim3(64), 0, s, d.st, d.rice_streams, d.status, rw);
+    if (d.n_rice_tiles)
+        hipLaunchKernelGGL(k_rice_decode, dim3(d.n_rice_tiles), dim3(kRiceTileSegs), 0, s, d.payload, d.st,
+                           d.rice_tiles, d.vals, d.status, rw);
+    // minimal-binary streams: X, C, TC, TP, TX, TE
+    const uint64_t nt = d.n_mb_tiles;
+    uint8_t *X = (uint8_t *)d.ws;
+    uint16_t *C = (uint16_t *)(X + nt * 64 * kMbTileSegs);
+    uint32_t *TC = (uint32_t *)(C + nt * 64 * kMbTileSegs);
+    uint64_t *TP = (uint64_t *)(TC + nt * 64);
+    uint8_t *TX = (uint8_t *)(TP + nt);
+    uint8_t *TE = TX + nt * 64;
+    if (nt)
+        hipLaunchKernelGGL(k_mb_tab, dim3(d.n_mb_tiles), dim3(kMbTileSegs), 0, s, d.payload, d.st, d.mb_tiles, X, C, TX,
+                           TC);
+    hipLaunchKernelGGL(k_mb_walk, dim3(d.n_mb_streams), dim3(64), 0, s, d.st, d.mb_streams, TX, TC, TE, TP, d.status);
+    if (nt)
+        hipLaunchKernelGGL(k_mb_decode, dim3(d.n_mb_tiles), dim3(kMbTileSegs), 0, s, d.payload, d.st, d.mb_tiles, X, C,
+                           TE, TP, d.vals, d.status);
+    (void)hipMemsetAsync(d.out3, 0, d.n_blocks * 3 * 8, s);
+    hipLaunchKernelGGL(k_zip_count, dim3((uint32_t)(d.n_blocks * nseg)), dim3(kZipThreads), 0, s, d.st, d.vals, nseg,
+                       d.segc);
+    hipLaunchKernelGGL(k_zip_write, dim3((uint32_t)(d.n_blocks * nseg)), dim3(kZipThreads), 0, s, d.st, d.vals,
+                       d.rec_off, d.recs, d.status, nseg, d.segc, (unsigned long long *)d.out3);
+}
 
 uint64_t unpack_seg_words(uint64_t n_blocks, uint64_t max_recs) {
     return 2 * n_blocks * ((max_recs + kZipSeg - 1) / kZipSeg + 1);

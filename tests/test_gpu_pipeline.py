@@ -154,8 +154,18 @@ def ragged(genome, n, seed, lo=1, hi=400):
     return reads, offs
 
 
+@pytest.fixture(params=["gpu", "host"])
+def unpack(request, monkeypatch):
+    """The decode pipeline's stream decode: on the GPU (default) or the host pool."""
+    if request.param == "host":
+        monkeypatch.setenv("NTC_HOST_UNPACK", "1")
+    else:
+        monkeypatch.delenv("NTC_HOST_UNPACK", raising=False)
+    return request.param
+
+
 @pytest.mark.parametrize("bpb,threads,nctx", [(1, 1, 1), (2, 4, 1), (16, 8, 1), (1, 3, 2)])
-def test_decode_file_equals_reads(setup, tmp_path, bpb, threads, nctx):
+def test_decode_file_equals_reads(setup, tmp_path, bpb, threads, nctx, unpack):
     d, genome, ix = setup
     ctxs = [nt.GpuContext(0) for _ in range(nctx)]
     for c in ctxs:
@@ -172,7 +182,7 @@ def test_decode_file_equals_reads(setup, tmp_path, bpb, threads, nctx):
         c.close()
 
 
-def test_decode_file_truncated_and_damaged_blocks(setup, tmp_path):
+def test_decode_file_truncated_and_damaged_blocks(setup, tmp_path, unpack):
     """A truncated tail ends the input (read_exact, main.rs:199); a damaged gzip member ends
     the output after the blocks before it, without an error (main.rs:202)."""
     d, genome, ix = setup
