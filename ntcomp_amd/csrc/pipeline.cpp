@@ -943,6 +943,13 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
     // 10 M-read decode pipeline ran at 8.0 against 7.6 Gbases/s on one MI355X box, the pool's
     // thread-time 0.11 against 0.64 s (profiles/round5/e2e_dec_*)
     const bool gpu_unpack = !host_unpack_on();
+    // NTC_PIPE_TRACE=n: the first n batches' events on stderr (ms from the call's start)
+    const char *tr = std::getenv("NTC_PIPE_TRACE");
+    const uint64_t trace_n = tr ? (uint64_t)std::atoll(tr) : 0;
+    auto trace = [&](const char *what, uint64_t b) {
+        if (b < trace_n) std::fprintf(stderr, "[pipe] %8.3f ms batch %llu %s\n", 1e3 * secs(t0, Clock::now()),
+                                      (unsigned long long)b, what);
+    };
     Shared sh;
     uint64_t next_task = 0;       // next block to unzip
     uint64_t next_id = 1;         // main.rs:204: seq.{i+1}
@@ -1003,6 +1010,29 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
             sh.cv.notify_all();
         }
     };
+    // ---- pinned buffers of the first batches, allocated in parallel -----------------------------
+    // (each is mapped, touched and registered: ~10 ms for a batch's 21 MB of text, which the
+    // first batch would otherwise wait for in turn; later batches reuse them).  The text size
+    // is a guess from the records (48 bytes each: C91's reads take 41); a batch that needs
+    // more regrows its buffer as before.
+    {
+        std::vector<std::thread> pre;
+        for (uint64_t j = 0; j < (uint64_t)NB && j < n_batches; j++)
+            pre.emplace_back([&, j] {
+                uint64_t nr = 0, np = 0;
+                for (uint64_t i = j * bpb; i < std::min<uint64_t>((j + 1) * bpb, blocks.size()); i++) {
+                    nr += blocks[i].n_recs;
+                    np += blocks[i].pay;
+                }
+                DSlot &sl = slots[(size_t)j];
+                const bool ok = (gpu_unpack ? ensure_pinned((void **)&sl.pay, &sl.cap_pay, np + 8)
+                                            : ensure_pinned((void **)&sl.recs, &sl.cap_recs, nr * 8 + 8)) &&
+                                ensure_pinned((void **)&sl.text, &sl.cap_text, nr * 48 + (1u << 20));
+                if (!ok) sh.fail(NTC_ERR_HIP, "pinned host allocation failed");
+            });
+        for (auto &t : pre) t.join();
+    }
+
     // ---- unzip pool ------------------------------------------------------------------------
     // Blocks are taken in file order; the first block of a batch claims the batch's slot
     // (free once the writer is done with batch b - NB) and sizes its record buffer.  Past a
@@ -1100,6 +1130,7 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
                 sl.finished++;
                 if (blk + 1 == blocks.size() || (stop_batch >= 0 && sl.finished == sl.n_blocks))
                     S.reader_done_s = secs(t0, Clock::now());
+                if (sl.finished == sl.n_blocks) trace("inflated", b);
                 if (!gpu_unpack && sl.finished == sl.n_blocks) assign_ahead();
                 sh.cv.notify_all();
             }
@@ -1145,6 +1176,7 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
                         sl.n_reads = nr;
                         sl.n_bases = nbs;
                         sl.unpacked = true;
+                        trace("unpacked", b);
                         assign_ahead();
                         sh.cv.notify_all();
                         sh.cv.wait(g, [&] { return sh.error != NTC_OK || sl.ready; });
@@ -1166,6 +1198,7 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
                     std::lock_guard<std::mutex> g(sh.mu);
                     sl.text_len = len;
                     sl.decoded = true;
+                    trace("decoded", b);
                     S.gpu_done_s = secs(t0, Clock::now());
                     sh.cv.notify_all();
                     continue;
@@ -1198,6 +1231,7 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
                 std::lock_guard<std::mutex> g(sh.mu);
                 sl.text_len = len;
                 sl.decoded = true;
+                trace("decoded", b);
                 S.gpu_done_s = secs(t0, Clock::now());
                 sh.cv.notify_all();
             }
@@ -1245,6 +1279,7 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
         add_time(t_write, secs(tw, Clock::now()));
         std::lock_guard<std::mutex> g(sh.mu);
         if (b == 0) S.first_batch_s = secs(t0, Clock::now());
+        trace("written", b);
         S.reads += slp->n_reads;
         S.bases += slp->n_bases;
         S.bytes_out += slp->text_len;
