@@ -1642,6 +1642,24 @@ int decode_fasta_dev(ntc_ctx *ctx, const uint64_t *d_recs, uint64_t n_recs, uint
 }
 }  // namespace
 
+namespace ntc {
+int reserve_decode(ntc_ctx *ctx, uint64_t pay_bytes, uint64_t n_recs) {
+    if (!ctx) return NTC_ERR_INVALID_ARG;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const uint64_t pw = (pay_bytes + 7) / 8, n_bases = 40 * n_recs, need = fasta_bytes(n_recs, n_bases, 1);
+    void *p;
+    int rc;
+    if ((rc = ensure(ctx, WS_UNP_PAY, pw * 8 + 16, &p))) return rc;
+    if ((rc = ensure(ctx, WS_UNP_MARKS, pw * 8 * 8 + 128, &p))) return rc;  // marks + tile tables
+    if ((rc = ensure(ctx, WS_UNP_VALS, 3 * n_recs * 8 + 8, &p))) return rc;
+    if ((rc = ensure(ctx, WS_UNP_RECS, n_recs * 8 + 8, &p))) return rc;
+    if ((rc = ensure(ctx, WS_FA_BASES, n_bases + 64, &p))) return rc;
+    if ((rc = ensure(ctx, WS_FA_OFFS, (n_recs + 2) * 8, &p))) return rc;
+    if ((rc = ensure(ctx, WS_FA_SCAN, (2 * (n_recs + 1) + scan_tmp_words(n_recs + 1)) * 8, &p))) return rc;
+    return ensure(ctx, WS_STAGE_BASES, need + 64, &p);
+}
+}  // namespace ntc
+
 extern "C" {
 
 int ntc_decode_fasta(ntc_ctx *ctx, const uint64_t *recs, uint64_t n_recs, uint64_t n_reads, uint64_t n_bases,

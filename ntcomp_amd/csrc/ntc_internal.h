@@ -32,6 +32,7 @@ bool save_index_as(const HostIndex &ix, const std::string &prefix, int layout, s
 
 struct ntc_fastx;
 struct ntc_block_meta;
+struct ntc_ctx;
 namespace ntc {
 // a plain FASTQ that ntc_fastx_open mapped: its bytes (null for any other input), and
 // moving the mapped parser to byte pos (a record start) -- pipeline.cpp's GPU-parse reader
@@ -49,6 +50,11 @@ void fastx_stream_unread(ntc_fastx *fx, const uint8_t *src, uint64_t n);
 // (corrupt or truncated data, a CRC or ISIZE mismatch).
 // the GPU unpacker's block decode on the host (block_codec.cpp; the sanitizer stand-in)
 int unpack_block_host(const ::ntc_block_meta &m, const uint8_t *payload, std::vector<uint64_t> &recs);
+// The decode pipeline's device workspaces sized ahead for a batch of about n_recs records in
+// pay_bytes of inflated streams (capi.cpp): hipMalloc'd while the first batch inflates
+// rather than on its path.  Estimates: at most 3 values and one read per record, 48 bytes of
+// FASTA per record; a batch that needs more grows them as before.
+int reserve_decode(::ntc_ctx *ctx, uint64_t pay_bytes, uint64_t n_recs);
 struct PgzReader;
 PgzReader *pgz_open(const char *path, int threads);
 int pgz_read(PgzReader *r, char *dst, size_t cap, size_t *got);

@@ -1143,6 +1143,27 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
     std::vector<std::thread> gpus;
     for (int c = 0; c < n_ctx; c++)
         gpus.emplace_back([&, c] {
+            // While the pool inflates the first batches: one tiny unpack (an empty block) and
+            // one tiny decode (a one-base read), so the first real calls find the unpacker's
+            // and the formatter's code objects loaded (HIP loads them at a kernel's first
+            // launch: ~10 ms on the first batch's path otherwise)
+            if (gpu_unpack) {
+                ntc_block_meta m0{};
+                uint64_t ok = 0, nr = 0, nbs = 0, len = 0, brecs = 0, bpay = 0;
+                uint8_t pay0[8] = {0}, txt[64];
+                const uint64_t rec1 = (uint64_t)(1u | 2u | (1u << 2)) << 56;  // first, short, 1 base "A"
+                for (uint64_t i = c * bpb; i < std::min<uint64_t>((c + 1) * bpb, blocks.size()); i++) {
+                    brecs += blocks[i].n_recs;
+                    bpay += blocks[i].pay;
+                }
+                // ... and the device workspaces sized for the first batch (hipMalloc'd here)
+                if (ntc_unpack_streams(ctxs[c], pay0, 8, &m0, 1, &ok, &nr, &nbs) ||
+                    ntc_decode_fasta(ctxs[c], &rec1, 1, 1, 1, 1, txt, sizeof(txt), &len) ||
+                    ntc::reserve_decode(ctxs[c], bpay, brecs)) {
+                    sh.fail(NTC_ERR_HIP, std::string("decode: ") + ntc_last_error(ctxs[c]));
+                    return;
+                }
+            }
             for (uint64_t b = (uint64_t)c;; b += (uint64_t)n_ctx) {
                 DSlot *slp;
                 if (gpu_unpack) {
