@@ -110,6 +110,10 @@ int ntc_ctx_synchronize(ntc_ctx *ctx);
  * encoder's path cover, suffix table or SCAN words; encode calls on that index then fail
  * with NTC_ERR_NO_INDEX (after the upload get_option returns whether the index in use is
  * decode-only; ntc_index_share passes it on).
+ * "warm_dma" (bytes, 1 .. 2^30) is an action: one device-to-host and one host-to-device copy
+ * of that size through a temporary pinned buffer, now -- the process's first large copies
+ * start the DMA engines (≈ 8 ms on the MI355X box), which the CLI does beside the index
+ * preparation instead of on the first batch's path.
  * Read-only: "n_paths", "path_text_len" (the path cover built on the device at upload),
  * "path_hash" (test hook: FNV-1a of the cover arrays, derived.h path_cover_hash),
  * "tab_u" (after an upload: the depth in use), "tab_u_fallback" (1: the default depth 15

@@ -1036,6 +1036,26 @@ int ntc_ctx_set_option(ntc_ctx *ctx, const char *key, int64_t value) {
         ctx->decode_only_opt = (int)value;
         return NTC_OK;
     }
+    if (std::strcmp(key, "warm_dma") == 0) {  // an action: copies of `value` bytes each way, now
+        if (value < 1 || value > (1ll << 30)) return set_err(ctx, NTC_ERR_INVALID_ARG, "warm_dma: 1 .. 2^30 bytes");
+        HIP_TRY(ctx, hipSetDevice(ctx->device));
+        void *h = nullptr, *d = nullptr;
+        if (hipHostMalloc(&h, (size_t)value, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            return set_err(ctx, NTC_ERR_HIP, "warm_dma: pinned allocation failed");
+        }
+        int rc = ensure(ctx, WS_STAGE_BASES, (uint64_t)value, &d);
+        if (rc == NTC_OK) {
+            if (hipMemcpyAsync(h, d, (size_t)value, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+                hipMemcpyAsync(d, h, (size_t)value, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+                hipStreamSynchronize(ctx->stream) != hipSuccess) {
+                (void)hipGetLastError();
+                rc = set_err(ctx, NTC_ERR_HIP, "warm_dma: copy failed");
+            }
+        }
+        (void)hipHostFree(h);
+        return rc;
+    }
     if (std::strcmp(key, "ext2") == 0) {  // applies to the next ntc_index_upload
         if (value != 0 && value != 1) return set_err(ctx, NTC_ERR_INVALID_ARG, "ext2 must be 0 or 1");
         ctx->ext2_opt = (int)value;
@@ -1643,7 +1663,7 @@ int decode_fasta_dev(ntc_ctx *ctx, const uint64_t *d_recs, uint64_t n_recs, uint
 }  // namespace
 
 namespace ntc {
-int reserve_decode(ntc_ctx *ctx, uint64_t pay_bytes, uint64_t n_recs) {
+int reserve_decode(ntc_ctx *ctx, uint64_t pay_bytes, uint64_t n_recs, uint8_t *host, uint64_t host_bytes) {
     if (!ctx) return NTC_ERR_INVALID_ARG;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     const uint64_t pw = (pay_bytes + 7) / 8, n_bases = 40 * n_recs, need = fasta_bytes(n_recs, n_bases, 1);
@@ -1656,7 +1676,14 @@ int reserve_decode(ntc_ctx *ctx, uint64_t pay_bytes, uint64_t n_recs) {
     if ((rc = ensure(ctx, WS_FA_BASES, n_bases + 64, &p))) return rc;
     if ((rc = ensure(ctx, WS_FA_OFFS, (n_recs + 2) * 8, &p))) return rc;
     if ((rc = ensure(ctx, WS_FA_SCAN, (2 * (n_recs + 1) + scan_tmp_words(n_recs + 1)) * 8, &p))) return rc;
-    return ensure(ctx, WS_STAGE_BASES, need + 64, &p);
+    if ((rc = ensure(ctx, WS_STAGE_BASES, need + 64, &p))) return rc;
+    const uint64_t nc = std::min<uint64_t>({host_bytes, need + 64, 4u << 20});
+    if (host && nc) {
+        HIP_TRY(ctx, hipMemcpyAsync(host, p, nc, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(p, host, nc, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    return NTC_OK;
 }
 }  // namespace ntc
 

@@ -53,8 +53,10 @@ int unpack_block_host(const ::ntc_block_meta &m, const uint8_t *payload, std::ve
 // The decode pipeline's device workspaces sized ahead for a batch of about n_recs records in
 // pay_bytes of inflated streams (capi.cpp): hipMalloc'd while the first batch inflates
 // rather than on its path.  Estimates: at most 3 values and one read per record, 48 bytes of
-// FASTA per record; a batch that needs more grows them as before.
-int reserve_decode(::ntc_ctx *ctx, uint64_t pay_bytes, uint64_t n_recs);
+// FASTA per record; a batch that needs more grows them as before.  host (pinned, host_bytes)
+// takes one copy each way of up to 4 MiB: the process's first large copies start the DMA
+// engines (7.7 ms before the first batch's text came back otherwise).
+int reserve_decode(::ntc_ctx *ctx, uint64_t pay_bytes, uint64_t n_recs, uint8_t *host, uint64_t host_bytes);
 struct PgzReader;
 PgzReader *pgz_open(const char *path, int threads);
 int pgz_read(PgzReader *r, char *dst, size_t cap, size_t *got);

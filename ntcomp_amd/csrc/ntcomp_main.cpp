@@ -143,6 +143,22 @@ std::vector<ntc_ctx *> open_gpus(const ntc_index_host *ix, const std::vector<int
                 dev_of[i] = -1;
                 return;
             }
+            // start the device's DMA engines, and load the code objects of the first batch's
+            // kernels that need no index (HIP loads one at its first launch: ~10 ms for the
+            // unpacker), here beside the index preparation rather than on the first batch's path
+            (void)ntc_ctx_set_option(ctxs[i], "warm_dma", 4 << 20);
+            if (decode_only) {
+                ntc_block_meta m0{};
+                uint8_t pay0[8] = {0};
+                uint64_t ok = 0, nr = 0, nb = 0;
+                (void)ntc_unpack_streams(ctxs[i], pay0, 8, &m0, 1, &ok, &nr, &nb);  // an empty block
+            } else {
+                static const uint8_t fq[] = "@r\nA\n+\nI\n";
+                uint8_t b1[8];
+                uint64_t offs[2], nb = 0;
+                int64_t bad = -1;
+                (void)ntc_fastq_parse(ctxs[i], fq, sizeof(fq) - 1, 1, b1, sizeof(b1), offs, &nb, &bad);  // one read
+            }
         }
     });
     ntc_index_prep *prep = nullptr;

@@ -1010,6 +1010,133 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
             sh.cv.notify_all();
         }
     };
+    // ---- GPU drivers ---------------------------------------------------------------------------
+    // A batch is complete when all of its blocks are in (or every block before its first
+    // damaged one, once no task of it is still running).  The assigner (below, in the
+    // writer's loop) fixes first_id in batch order.
+    std::vector<std::thread> gpus;
+    for (int c = 0; c < n_ctx; c++)
+        gpus.emplace_back([&, c] {
+            // While the pool inflates the first batches: one tiny unpack (an empty block) and
+            // one tiny decode (a one-base read), so the first real calls find the unpacker's
+            // and the formatter's code objects loaded (HIP loads them at a kernel's first
+            // launch: ~10 ms on the first batch's path otherwise)
+            if (gpu_unpack) {
+                ntc_block_meta m0{};
+                uint64_t ok = 0, nr = 0, nbs = 0, len = 0, brecs = 0, bpay = 0;
+                uint8_t pay0[8] = {0}, txt[64];
+                const uint64_t rec1 = (uint64_t)(1u | 2u | (1u << 2)) << 56;  // first, short, 1 base "A"
+                for (uint64_t i = c * bpb; i < std::min<uint64_t>((c + 1) * bpb, blocks.size()); i++) {
+                    brecs += blocks[i].n_recs;
+                    bpay += blocks[i].pay;
+                }
+                // ... and the device workspaces sized for the first batch (hipMalloc'd here)
+                trace("warm-up start", c);
+                const int w1 = ntc_unpack_streams(ctxs[c], pay0, 8, &m0, 1, &ok, &nr, &nbs);
+                trace("warm-up unpack", c);
+                const int w2 = w1 ? w1 : ntc_decode_fasta(ctxs[c], &rec1, 1, 1, 1, 1, txt, sizeof(txt), &len);
+                trace("warm-up decode", c);
+                const int w3 = w2 ? w2 : ntc::reserve_decode(ctxs[c], bpay, brecs, nullptr, 0);
+                trace("warm-up reserve", c);
+                if (w3) {
+                    sh.fail(NTC_ERR_HIP, std::string("decode: ") + ntc_last_error(ctxs[c]));
+                    return;
+                }
+            }
+            for (uint64_t b = (uint64_t)c;; b += (uint64_t)n_ctx) {
+                DSlot *slp;
+                if (gpu_unpack) {
+                    // the batch's streams decoded on the device as soon as every block of it is
+                    // inflated (or found damaged): its read count numbers the batches after it
+                    {
+                        std::unique_lock<std::mutex> g(sh.mu);
+                        sh.cv.wait(g, [&] {
+                            return sh.error != NTC_OK || b >= n_batches || (stop_batch >= 0 && (int64_t)b > stop_batch) ||
+                                   (slot_of(b).batch == b && slot_of(b).finished == slot_of(b).n_blocks);
+                        });
+                        if (sh.error != NTC_OK || b >= n_batches || (stop_batch >= 0 && (int64_t)b > stop_batch)) return;
+                        slp = &slot_of(b);
+                    }
+                    DSlot &sl = *slp;
+                    const uint64_t nb = sl.bad_block >= 0 ? (uint64_t)sl.bad_block : sl.n_blocks;
+                    const auto tg = Clock::now();
+                    uint64_t ok = 0, nr = 0, nbs = 0;
+                    const int rc = ntc_unpack_streams(ctxs[c], sl.pay, sl.n_pay, sl.metas.data(), nb, &ok, &nr, &nbs);
+                    add_time(t_gpu, secs(tg, Clock::now()));
+                    if (rc) {
+                        sh.fail(rc, std::string("decode: ") + ntc_last_error(ctxs[c]));
+                        return;
+                    }
+                    {
+                        std::unique_lock<std::mutex> g(sh.mu);
+                        if (ok < nb) {  // a block the device could not decode: the output ends before it
+                            sl.bad_block = (int)ok;
+                            if (stop_batch < 0 || (int64_t)b < stop_batch) stop_batch = (int64_t)b;
+                        }
+                        sl.n_reads = nr;
+                        sl.n_bases = nbs;
+                        sl.unpacked = true;
+                        trace("unpacked", b);
+                        assign_ahead();
+                        sh.cv.notify_all();
+                        sh.cv.wait(g, [&] { return sh.error != NTC_OK || sl.ready; });
+                        if (sh.error != NTC_OK) return;
+                    }
+                    const uint64_t need = sl.n_bases + 7 * sl.n_reads + digits_total(sl.first_id, sl.n_reads) + 64;
+                    const auto tf = Clock::now();
+                    if (!ensure_pinned((void **)&sl.text, &sl.cap_text, need)) {
+                        sh.fail(NTC_ERR_HIP, "pinned host allocation failed");
+                        return;
+                    }
+                    uint64_t len = 0;
+                    const int rf = ntc_decode_fasta_unpacked(ctxs[c], sl.first_id, sl.text, sl.cap_text, &len);
+                    add_time(t_gpu, secs(tf, Clock::now()));
+                    if (rf) {
+                        sh.fail(rf, std::string("decode: ") + ntc_last_error(ctxs[c]));
+                        return;
+                    }
+                    std::lock_guard<std::mutex> g(sh.mu);
+                    sl.text_len = len;
+                    sl.decoded = true;
+                    trace("decoded", b);
+                    S.gpu_done_s = secs(t0, Clock::now());
+                    sh.cv.notify_all();
+                    continue;
+                }
+                {
+                    std::unique_lock<std::mutex> g(sh.mu);
+                    sh.cv.wait(g, [&] {
+                        return sh.error != NTC_OK || b >= n_batches || (stop_batch >= 0 && (int64_t)b > stop_batch) ||
+                               (slot_of(b).batch == b && slot_of(b).ready);
+                    });
+                    if (sh.error != NTC_OK || b >= n_batches || (stop_batch >= 0 && (int64_t)b > stop_batch)) return;
+                    slp = &slot_of(b);
+                }
+                DSlot &sl = *slp;
+                const uint64_t nrec = sl.n_recs;
+                const uint64_t need = sl.n_bases + 7 * sl.n_reads + digits_total(sl.first_id, sl.n_reads) + 64;
+                const auto tg = Clock::now();
+                if (!ensure_pinned((void **)&sl.text, &sl.cap_text, need)) {
+                    sh.fail(NTC_ERR_HIP, "pinned host allocation failed");
+                    return;
+                }
+                uint64_t len = 0;
+                const int rc = ntc_decode_fasta(ctxs[c], sl.recs, nrec, sl.n_reads, sl.n_bases, sl.first_id, sl.text,
+                                                sl.cap_text, &len);
+                add_time(t_gpu, secs(tg, Clock::now()));
+                if (rc) {
+                    sh.fail(rc, std::string("decode: ") + ntc_last_error(ctxs[c]));
+                    return;
+                }
+                std::lock_guard<std::mutex> g(sh.mu);
+                sl.text_len = len;
+                sl.decoded = true;
+                trace("decoded", b);
+                S.gpu_done_s = secs(t0, Clock::now());
+                sh.cv.notify_all();
+            }
+        });
+
     // ---- pinned buffers of the first batches, allocated in parallel -----------------------------
     // (each is mapped, touched and registered: ~10 ms for a batch's 21 MB of text, which the
     // first batch would otherwise wait for in turn; later batches reuse them).  The text size
@@ -1132,128 +1259,6 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
                     S.reader_done_s = secs(t0, Clock::now());
                 if (sl.finished == sl.n_blocks) trace("inflated", b);
                 if (!gpu_unpack && sl.finished == sl.n_blocks) assign_ahead();
-                sh.cv.notify_all();
-            }
-        });
-
-    // ---- GPU drivers ---------------------------------------------------------------------------
-    // A batch is complete when all of its blocks are in (or every block before its first
-    // damaged one, once no task of it is still running).  The assigner (below, in the
-    // writer's loop) fixes first_id in batch order.
-    std::vector<std::thread> gpus;
-    for (int c = 0; c < n_ctx; c++)
-        gpus.emplace_back([&, c] {
-            // While the pool inflates the first batches: one tiny unpack (an empty block) and
-            // one tiny decode (a one-base read), so the first real calls find the unpacker's
-            // and the formatter's code objects loaded (HIP loads them at a kernel's first
-            // launch: ~10 ms on the first batch's path otherwise)
-            if (gpu_unpack) {
-                ntc_block_meta m0{};
-                uint64_t ok = 0, nr = 0, nbs = 0, len = 0, brecs = 0, bpay = 0;
-                uint8_t pay0[8] = {0}, txt[64];
-                const uint64_t rec1 = (uint64_t)(1u | 2u | (1u << 2)) << 56;  // first, short, 1 base "A"
-                for (uint64_t i = c * bpb; i < std::min<uint64_t>((c + 1) * bpb, blocks.size()); i++) {
-                    brecs += blocks[i].n_recs;
-                    bpay += blocks[i].pay;
-                }
-                // ... and the device workspaces sized for the first batch (hipMalloc'd here)
-                if (ntc_unpack_streams(ctxs[c], pay0, 8, &m0, 1, &ok, &nr, &nbs) ||
-                    ntc_decode_fasta(ctxs[c], &rec1, 1, 1, 1, 1, txt, sizeof(txt), &len) ||
-                    ntc::reserve_decode(ctxs[c], bpay, brecs)) {
-                    sh.fail(NTC_ERR_HIP, std::string("decode: ") + ntc_last_error(ctxs[c]));
-                    return;
-                }
-            }
-            for (uint64_t b = (uint64_t)c;; b += (uint64_t)n_ctx) {
-                DSlot *slp;
-                if (gpu_unpack) {
-                    // the batch's streams decoded on the device as soon as every block of it is
-                    // inflated (or found damaged): its read count numbers the batches after it
-                    {
-                        std::unique_lock<std::mutex> g(sh.mu);
-                        sh.cv.wait(g, [&] {
-                            return sh.error != NTC_OK || b >= n_batches || (stop_batch >= 0 && (int64_t)b > stop_batch) ||
-                                   (slot_of(b).batch == b && slot_of(b).finished == slot_of(b).n_blocks);
-                        });
-                        if (sh.error != NTC_OK || b >= n_batches || (stop_batch >= 0 && (int64_t)b > stop_batch)) return;
-                        slp = &slot_of(b);
-                    }
-                    DSlot &sl = *slp;
-                    const uint64_t nb = sl.bad_block >= 0 ? (uint64_t)sl.bad_block : sl.n_blocks;
-                    const auto tg = Clock::now();
-                    uint64_t ok = 0, nr = 0, nbs = 0;
-                    const int rc = ntc_unpack_streams(ctxs[c], sl.pay, sl.n_pay, sl.metas.data(), nb, &ok, &nr, &nbs);
-                    add_time(t_gpu, secs(tg, Clock::now()));
-                    if (rc) {
-                        sh.fail(rc, std::string("decode: ") + ntc_last_error(ctxs[c]));
-                        return;
-                    }
-                    {
-                        std::unique_lock<std::mutex> g(sh.mu);
-                        if (ok < nb) {  // a block the device could not decode: the output ends before it
-                            sl.bad_block = (int)ok;
-                            if (stop_batch < 0 || (int64_t)b < stop_batch) stop_batch = (int64_t)b;
-                        }
-                        sl.n_reads = nr;
-                        sl.n_bases = nbs;
-                        sl.unpacked = true;
-                        trace("unpacked", b);
-                        assign_ahead();
-                        sh.cv.notify_all();
-                        sh.cv.wait(g, [&] { return sh.error != NTC_OK || sl.ready; });
-                        if (sh.error != NTC_OK) return;
-                    }
-                    const uint64_t need = sl.n_bases + 7 * sl.n_reads + digits_total(sl.first_id, sl.n_reads) + 64;
-                    const auto tf = Clock::now();
-                    if (!ensure_pinned((void **)&sl.text, &sl.cap_text, need)) {
-                        sh.fail(NTC_ERR_HIP, "pinned host allocation failed");
-                        return;
-                    }
-                    uint64_t len = 0;
-                    const int rf = ntc_decode_fasta_unpacked(ctxs[c], sl.first_id, sl.text, sl.cap_text, &len);
-                    add_time(t_gpu, secs(tf, Clock::now()));
-                    if (rf) {
-                        sh.fail(rf, std::string("decode: ") + ntc_last_error(ctxs[c]));
-                        return;
-                    }
-                    std::lock_guard<std::mutex> g(sh.mu);
-                    sl.text_len = len;
-                    sl.decoded = true;
-                    trace("decoded", b);
-                    S.gpu_done_s = secs(t0, Clock::now());
-                    sh.cv.notify_all();
-                    continue;
-                }
-                {
-                    std::unique_lock<std::mutex> g(sh.mu);
-                    sh.cv.wait(g, [&] {
-                        return sh.error != NTC_OK || b >= n_batches || (stop_batch >= 0 && (int64_t)b > stop_batch) ||
-                               (slot_of(b).batch == b && slot_of(b).ready);
-                    });
-                    if (sh.error != NTC_OK || b >= n_batches || (stop_batch >= 0 && (int64_t)b > stop_batch)) return;
-                    slp = &slot_of(b);
-                }
-                DSlot &sl = *slp;
-                const uint64_t nrec = sl.n_recs;
-                const uint64_t need = sl.n_bases + 7 * sl.n_reads + digits_total(sl.first_id, sl.n_reads) + 64;
-                const auto tg = Clock::now();
-                if (!ensure_pinned((void **)&sl.text, &sl.cap_text, need)) {
-                    sh.fail(NTC_ERR_HIP, "pinned host allocation failed");
-                    return;
-                }
-                uint64_t len = 0;
-                const int rc = ntc_decode_fasta(ctxs[c], sl.recs, nrec, sl.n_reads, sl.n_bases, sl.first_id, sl.text,
-                                                sl.cap_text, &len);
-                add_time(t_gpu, secs(tg, Clock::now()));
-                if (rc) {
-                    sh.fail(rc, std::string("decode: ") + ntc_last_error(ctxs[c]));
-                    return;
-                }
-                std::lock_guard<std::mutex> g(sh.mu);
-                sl.text_len = len;
-                sl.decoded = true;
-                trace("decoded", b);
-                S.gpu_done_s = secs(t0, Clock::now());
                 sh.cv.notify_all();
             }
         });

@@ -186,5 +186,5 @@ int ntc_encode_pack_fastq(ntc_ctx *ctx, const uint8_t *fastq, uint64_t bytes, ui
 
 namespace ntc {
 // the pipeline's device workspace reservation (capi.cpp): nothing to size on the host
-int reserve_decode(ntc_ctx *ctx, uint64_t, uint64_t) { return ctx ? NTC_OK : NTC_ERR_INVALID_ARG; }
+int reserve_decode(ntc_ctx *ctx, uint64_t, uint64_t, uint8_t *, uint64_t) { return ctx ? NTC_OK : NTC_ERR_INVALID_ARG; }
 }  // namespace ntc

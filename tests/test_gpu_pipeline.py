@@ -327,3 +327,14 @@ def test_decode_only_upload(setup):
     assert np.array_equal(r2, recs)
     for x in (full, dec, shared):
         x.close()
+
+
+def test_warm_dma_option():
+    """"warm_dma" copies that many bytes each way now (the CLI starts the DMA engines beside
+    the index preparation); out-of-range sizes are NTC_ERR_INVALID_ARG."""
+    ctx = nt.GpuContext(0)
+    ctx.set_option("warm_dma", 4 << 20)
+    for bad in (0, -1, (1 << 30) + 1):
+        with pytest.raises(nt.NtcError):
+            ctx.set_option("warm_dma", bad)
+    ctx.close()
