@@ -143,22 +143,17 @@ std::vector<ntc_ctx *> open_gpus(const ntc_index_host *ix, const std::vector<int
                 dev_of[i] = -1;
                 return;
             }
-            // start the device's DMA engines, and load the code objects of the first batch's
-            // kernels that need no index (HIP loads one at its first launch: ~10 ms for the
-            // unpacker), here beside the index preparation rather than on the first batch's path
+            // decode: start the device's DMA engines and load the unpacker's code object (HIP
+            // loads one at its first launch) here beside the index preparation rather than on
+            // the first batch's path: first batch decoded at 8 ms instead of 16-30, pipeline
+            // 0.160 against 0.164 s (median of 4 on one box, profiles/round5/warm_ab/).  Encode
+            // measured no better with the same (0.107 against 0.097 s), so it does not.
+            if (!decode_only || std::getenv("NTC_NO_WARM")) continue;
             (void)ntc_ctx_set_option(ctxs[i], "warm_dma", 4 << 20);
-            if (decode_only) {
-                ntc_block_meta m0{};
-                uint8_t pay0[8] = {0};
-                uint64_t ok = 0, nr = 0, nb = 0;
-                (void)ntc_unpack_streams(ctxs[i], pay0, 8, &m0, 1, &ok, &nr, &nb);  // an empty block
-            } else {
-                static const uint8_t fq[] = "@r\nA\n+\nI\n";
-                uint8_t b1[8];
-                uint64_t offs[2], nb = 0;
-                int64_t bad = -1;
-                (void)ntc_fastq_parse(ctxs[i], fq, sizeof(fq) - 1, 1, b1, sizeof(b1), offs, &nb, &bad);  // one read
-            }
+            ntc_block_meta m0{};
+            uint8_t pay0[8] = {0};
+            uint64_t ok = 0, nr = 0, nb = 0;
+            (void)ntc_unpack_streams(ctxs[i], pay0, 8, &m0, 1, &ok, &nr, &nb);  // an empty block
         }
     });
     ntc_index_prep *prep = nullptr;

@@ -1021,7 +1021,7 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
             // one tiny decode (a one-base read), so the first real calls find the unpacker's
             // and the formatter's code objects loaded (HIP loads them at a kernel's first
             // launch: ~10 ms on the first batch's path otherwise)
-            if (gpu_unpack) {
+            if (gpu_unpack && !std::getenv("NTC_NO_WARM")) {
                 ntc_block_meta m0{};
                 uint64_t ok = 0, nr = 0, nbs = 0, len = 0, brecs = 0, bpay = 0;
                 uint8_t pay0[8] = {0}, txt[64];
