@@ -79,27 +79,38 @@ __device__ __forceinline__ uint32_t pack4(uint32_t w, uint32_t absent_tab, bool 
 #define NTC_PACK16 1  // k_pack: 16 characters per thread (one coalesced uint4 load, one u32 store)
 #endif
 #if NTC_PACK16
-#ifndef NTC_PACK_UNROLL
-#define NTC_PACK_UNROLL 4  // 16-character chunks per thread, their loads issued together
-#endif
-// Thread t of block g packs chunks c = g * 256 U + k * 256 + t (k < U = NTC_PACK_UNROLL) of 16
-// characters each: chunk c into the 32-bit half c of the 2-bit stream (Q word c / 2, low half
-// for even c).  A 16-byte aligned batch start (uniform over the grid) takes the fast path:
-// the thread's U aligned uint4 loads first (each k a wave reading 1 KB contiguous), then the
-// packing; otherwise two aligned loads are realigned per byte.  Halves past the batch's last
-// character, up to the end of its last Q word, are written as zero.  `bound` (>= the batch's
-// bases) only sizes the grid; the true count is offs[n] - offs[0].
-__device__ __forceinline__ void pack_chunk_slow(const Enc4Args &a, const uint8_t *B, uint64_t total, uint64_t c,
-                                                uint32_t *Q32) {
-    const uint64_t x0 = c * 16;
+// Thread t packs characters [16t, 16t + 16) into the 32-bit half t of the 2-bit stream (Q
+// word t / 2, low half for even t).  A 16-byte aligned batch start (uniform over the grid)
+// takes the fast path: one aligned uint4 load per lane, a wave reading 1 KB contiguous;
+// otherwise two aligned loads are realigned per byte.  Halves past the batch's last
+// character, up to the end of its last Q word, are written as zero.  `bound` (>= the
+// batch's bases) only sizes the grid; the true count is offs[n] - offs[0].
+__global__ __launch_bounds__(256) void k_pack(Enc4Args a, uint64_t bound) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t x0 = t * 16;
+    const uint64_t total = a.offs[a.n_reads] - a.offs[0];
+    (void)bound;
+    if (t >= 2 * ((total + 31) / 32)) return;
+    uint32_t *Q32 = reinterpret_cast<uint32_t *>(a.Q);
     if (x0 >= total) {
-        Q32[c] = 0u;
+        Q32[t] = 0u;
         return;
     }
+    const uint8_t *B = a.bases + a.offs[0];
     const uint32_t absent = a.ix.absent;
     const uint32_t n = total - x0 < 16 ? (uint32_t)(total - x0) : 16u;
-    // 16-byte blocks never cross a page, so reading a whole block that holds the batch's
-    // last byte stays inside its allocation
+    if ((((uintptr_t)B) & 15) == 0 && n == 16) {
+        const uint32_t absent_tab = (absent & 1u) | ((absent >> 1) & 1u) << 8 | ((absent >> 2) & 1u) << 16 |
+                                    ((absent >> 3) & 1u) << 24;
+        const uint4 v = *reinterpret_cast<const uint4 *>(B + x0);
+        bool ok = true;
+        Q32[t] = pack4(v.x, absent_tab, ok) | pack4(v.y, absent_tab, ok) << 8 | pack4(v.z, absent_tab, ok) << 16 |
+                 pack4(v.w, absent_tab, ok) << 24;
+        if (!ok) pack_report_bad(a, B, x0, 16, absent);
+        return;
+    }
+    // unaligned start or the last partial chunk: 16-byte blocks never cross a page, so
+    // reading a whole block that holds the batch's last byte stays inside its allocation
     const uint8_t *end = B + total;
     const uint8_t *p = B + x0;
     const uintptr_t al = (uintptr_t)p & ~(uintptr_t)15;
@@ -118,53 +129,20 @@ __device__ __forceinline__ void pack_chunk_slow(const Enc4Args &a, const uint8_t
     uint32_t acc = 0;
     bool bad = false;
 #pragma unroll
-    for (uint32_t i = 0; i < 16; i++) {
-        const uint32_t o = sh + i;
+    for (uint32_t c = 0; c < 16; c++) {
+        const uint32_t o = sh + c;
         const uint32_t word = o >> 2;
         uint32_t wv = w[0];
 #pragma unroll
         for (uint32_t q = 1; q < 8; q++) wv = (word == q) ? w[q] : wv;
         const uint32_t ch = (wv >> (8 * (o & 3))) & 0xFFu;
-        if (i < n) {
+        if (c < n) {
             bad |= !is_acgt(ch) || ((absent >> fast_code(ch)) & 1u);
-            acc |= fast_code(ch) << (2 * i);
+            acc |= fast_code(ch) << (2 * c);
         }
     }
-    Q32[c] = acc;
+    Q32[t] = acc;
     if (bad) pack_report_bad(a, B, x0, n, absent);
-}
-__global__ __launch_bounds__(256) void k_pack(Enc4Args a, uint64_t bound) {
-    constexpr uint32_t U = NTC_PACK_UNROLL;
-    const uint64_t c0 = (uint64_t)blockIdx.x * 256 * U + threadIdx.x;
-    const uint64_t total = a.offs[a.n_reads] - a.offs[0];
-    const uint64_t nh = 2 * ((total + 31) / 32);  // halves to write
-    (void)bound;
-    if (c0 >= nh) return;
-    uint32_t *Q32 = reinterpret_cast<uint32_t *>(a.Q);
-    const uint8_t *B = a.bases + a.offs[0];
-    const uint64_t full = total / 16;  // chunks of 16 characters
-    if ((((uintptr_t)B) & 15) == 0 && c0 + (uint64_t)(U - 1) * 256 < full) {
-        const uint32_t absent = a.ix.absent;
-        const uint32_t absent_tab = (absent & 1u) | ((absent >> 1) & 1u) << 8 | ((absent >> 2) & 1u) << 16 |
-                                    ((absent >> 3) & 1u) << 24;
-        uint4 v[U];
-#pragma unroll
-        for (uint32_t k = 0; k < U; k++) v[k] = *reinterpret_cast<const uint4 *>(B + (c0 + (uint64_t)k * 256) * 16);
-#pragma unroll
-        for (uint32_t k = 0; k < U; k++) {
-            bool ok = true;
-            const uint64_t c = c0 + (uint64_t)k * 256;
-            Q32[c] = pack4(v[k].x, absent_tab, ok) | pack4(v[k].y, absent_tab, ok) << 8 |
-                     pack4(v[k].z, absent_tab, ok) << 16 | pack4(v[k].w, absent_tab, ok) << 24;
-            if (!ok) pack_report_bad(a, B, c * 16, 16, absent);
-        }
-        return;
-    }
-    for (uint32_t k = 0; k < U; k++) {
-        const uint64_t c = c0 + (uint64_t)k * 256;
-        if (c >= nh) break;
-        pack_chunk_slow(a, B, total, c, Q32);
-    }
 }
 #else
 // Thread b packs characters [32b, 32b + 32).  `bound` (>= the batch's bases) only sizes
@@ -1035,12 +1013,7 @@ int ms4_blocks_per_cu() {
 
 void launch_encode4(const Enc4Args &a, uint64_t total, uint32_t ms_blocks, hipStream_t s, hipEvent_t ev_ms_begin,
                     hipEvent_t ev_ms_end) {
-#if NTC_PACK16
-    hipLaunchKernelGGL(k_pack, grid_for(((total + 31) / 32 * 2 + NTC_PACK_UNROLL - 1) / NTC_PACK_UNROLL), dim3(256), 0, s, a,
-                       total);
-#else
-    hipLaunchKernelGGL(k_pack, grid_for((total + 31) / 32), dim3(256), 0, s, a, total);
-#endif
+    hipLaunchKernelGGL(k_pack, grid_for((total + 31) / 32 * (NTC_PACK16 ? 2 : 1)), dim3(256), 0, s, a, total);
     (void)hipEventRecord(ev_ms_begin, s);
     const uint64_t need = (a.n_reads + 255) / 256;
     if (a.ix.joint)
