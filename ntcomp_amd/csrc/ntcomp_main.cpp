@@ -138,6 +138,7 @@ std::vector<ntc_ctx *> open_gpus(const ntc_index_host *ix, const std::vector<int
     std::thread creator([&] {
         for (size_t i = 0; i < ctxs.size(); i++) {
             dev_of[i] = devs[i / (size_t)(per_gpu > 0 ? per_gpu : 1)];
+            const auto tc = Clock::now();
             if (ntc_ctx_create(dev_of[i], &ctxs[i])) {
                 create_rc = NTC_ERR_HIP;
                 dev_of[i] = -1;
@@ -148,6 +149,8 @@ std::vector<ntc_ctx *> open_gpus(const ntc_index_host *ix, const std::vector<int
             // the first batch's path: first batch decoded at 8 ms instead of 16-30, pipeline
             // 0.160 against 0.164 s (median of 4 on one box, profiles/round5/warm_ab/).  Encode
             // measured no better with the same (0.107 against 0.097 s), so it does not.
+            if (std::getenv("NTC_INIT_TRACE"))
+                std::fprintf(stderr, "[init] context %zu created in %.3f ms\n", i, 1e3 * since(tc));
             if (!decode_only || std::getenv("NTC_NO_WARM")) continue;
             (void)ntc_ctx_set_option(ctxs[i], "warm_dma", 4 << 20);
             ntc_block_meta m0{};
@@ -156,9 +159,13 @@ std::vector<ntc_ctx *> open_gpus(const ntc_index_host *ix, const std::vector<int
             (void)ntc_unpack_streams(ctxs[i], pay0, 8, &m0, 1, &ok, &nr, &nb);  // an empty block
         }
     });
+    const auto ti = Clock::now();
+    const bool itr = std::getenv("NTC_INIT_TRACE") != nullptr;  // start-up timeline on stderr
     ntc_index_prep *prep = nullptr;
     const int prep_rc = ntc_index_prepare(&v, &prep);
+    if (itr) std::fprintf(stderr, "[init] %.3f ms index prepared\n", 1e3 * since(ti));
     creator.join();
+    if (itr) std::fprintf(stderr, "[init] %.3f ms contexts created\n", 1e3 * since(ti));
     if (create_rc) {
         for (size_t i = 0; i < ctxs.size(); i++)
             if (dev_of[i] < 0) die("no usable GPU " + std::to_string(devs[i / (size_t)(per_gpu > 0 ? per_gpu : 1)]));
@@ -178,6 +185,7 @@ std::vector<ntc_ctx *> open_gpus(const ntc_index_host *ix, const std::vector<int
         }
     }
     ntc_index_prep_free(prep);
+    if (itr) std::fprintf(stderr, "[init] %.3f ms index uploaded\n", 1e3 * since(ti));
     return ctxs;
 }
 int per_gpu_of(const Args &a, int def) {
