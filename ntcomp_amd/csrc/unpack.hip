@@ -196,7 +196,10 @@ __device__ __forceinline__ uint64_t block_exscan(uint64_t v, uint64_t *tot, uint
 //   k_rice_count  true codes per segment (marks from its entry to its end + PRE), per tile;
 //   k_rice_scan   a wave per stream: the tiles' first value indices, the stream's status;
 //   k_rice_decode each segment's true codes into place.
-constexpr int kRiceSegBits = 512;
+#ifndef NTC_RICE_SEG_BITS
+#define NTC_RICE_SEG_BITS 512
+#endif
+constexpr int kRiceSegBits = NTC_RICE_SEG_BITS;  // a multiple of 64
 constexpr int kRiceTileSegs = 64;
 constexpr uint64_t kDeadPos = ~0ull, kNoEntry = ~0ull;
 constexpr uint32_t kNoNext = 0xFFFFFFFFu;
@@ -468,7 +471,10 @@ __global__ __launch_bounds__(kRiceTileSegs) void k_rice_decode(const uint64_t *p
 //   k_mb_decode  a tile follows its entry through its segments in LDS, scans the segments'
 //                code counts and decodes each segment's true codes into place.
 // The work is L transfers of every bit, spread over all CUs (a tile per workgroup).
-constexpr int kMbSegBits = 256;   // bits per segment (>= 64 > l + 1)
+#ifndef NTC_MB_SEG_BITS
+#define NTC_MB_SEG_BITS 256
+#endif
+constexpr int kMbSegBits = NTC_MB_SEG_BITS;  // bits per segment (>= 64 > l + 1; a multiple of 64)
 constexpr int kMbTileSegs = 256;  // segments (threads) per tile
 constexpr uint8_t kMbDead = 255;  // a chain that ran past the stream's end
 constexpr int kMbWalkTiles = 128; // tiles per LDS chunk of k_mb_walk
