@@ -78,6 +78,29 @@ struct Bits64 {
     }
 };
 
+// The workgroup's words staged in LDS (sw: words w0 .. w0 + nl - 1, byte-swapped), positions
+// outside the window read global memory; no cursor: a peek is two LDS loads issued together
+// and no branch on the lane's position history (the lanes of a wave decode different codes).
+struct WinBits {
+    const uint64_t *w;
+    uint64_t nwords;
+    const uint64_t *sw;
+    uint64_t w0, nl;
+    __device__ __forceinline__ uint64_t peek(uint64_t pos) const {
+        const uint64_t i = pos >> 6, rel = i - w0;
+        uint64_t hi, lo;
+        if (rel + 1 < nl) {
+            hi = sw[rel];
+            lo = sw[rel + 1];
+        } else {
+            hi = i < nwords ? bswap64(w[i]) : 0;
+            lo = i + 1 < nwords ? bswap64(w[i + 1]) : 0;
+        }
+        const uint32_t sh = (uint32_t)(pos & 63);
+        return sh ? (hi << sh) | (lo >> (64 - sh)) : hi;
+    }
+};
+
 struct Code {
     uint64_t len;  // bits (0: no code here -- it runs past the end of the stream)
     uint64_t val;  // the value the reference's decoder returns (minimal binary: v - 1)
@@ -85,9 +108,18 @@ struct Code {
 };
 
 // Rice (param p): zeros up to a one, then p bits
-__device__ __forceinline__ Code rice_at(Bits64 &bt, uint64_t pos, uint32_t p) {
+template <class Bits>
+__device__ __forceinline__ Code rice_at(Bits &bt, uint64_t pos, uint32_t p) {
     const uint64_t nbits = bt.nwords * 64;
     uint64_t q = 0, at = pos;
+    if (pos < nbits) {  // the usual code: unary part, stop bit and p bits within one peek
+        const uint64_t x = bt.peek(pos);
+        const uint32_t z = x ? (uint32_t)__builtin_clzll(x) : 64u;
+        if (z + 1 + p <= 64 && pos + z + 1 + p <= nbits) {
+            const uint64_t rest = z + 1 < 64 ? x << (z + 1) : 0;
+            return {z + 1 + p, ((uint64_t)z << p) | (p ? rest >> (64 - p) : 0), false};
+        }
+    }
     for (;;) {
         if (at >= nbits) return {0, 0, false};
         const uint64_t x = bt.peek(at);
@@ -111,7 +143,8 @@ __device__ __forceinline__ Code rice_at(Bits64 &bt, uint64_t pos, uint32_t p) {
 }
 
 // minimal binary (max = param): l = floor(log2 param), limit = 2^(l+1) - param
-__device__ __forceinline__ Code mb_at(Bits64 &bt, uint64_t pos, uint32_t l, uint64_t limit) {
+template <class Bits>
+__device__ __forceinline__ Code mb_at(Bits &bt, uint64_t pos, uint32_t l, uint64_t limit) {
     const uint64_t nbits = bt.nwords * 64;
     if (pos + l > nbits) return {0, 0, false};
     const uint64_t x = bt.peek(pos);
@@ -261,10 +294,7 @@ __global__ __launch_bounds__(kRiceTileSegs) void k_rice_a(const uint64_t *payloa
     stage_words(sw, payload + x.s.word_off, x.s.nwords, w0, kRiceWin);
     if (!x.active) return;
     uint64_t *m = marks + x.s.word_off;
-    Bits64 bt{payload + x.s.word_off, x.s.nwords};
-    bt.sw = sw;
-    bt.w0 = w0;
-    bt.nl = kRiceWin;
+    WinBits bt{payload + x.s.word_off, x.s.nwords, sw, w0, kRiceWin};
     const uint32_t p = (uint32_t)x.s.param;
     uint64_t pos = x.a, word = 0, wi = x.a >> 6;
     bool dead = false;
@@ -304,10 +334,7 @@ __global__ __launch_bounds__(kRiceTileSegs) void k_rice_b(const uint64_t *payloa
         q = x.nbits;
         if (x.b < x.nbits) fl |= kNotSimple;  // the stream's codes end inside it
     } else {
-        Bits64 bt{payload + x.s.word_off, x.s.nwords};
-        bt.sw = sw;
-        bt.w0 = w0;
-        bt.nl = kRiceWin;
+        WinBits bt{payload + x.s.word_off, x.s.nwords, sw, w0, kRiceWin};
         const uint32_t p = (uint32_t)x.s.param;
         const uint64_t lim = x.b + 8ull * kRiceSegBits;
         while (q < x.nbits) {
@@ -370,16 +397,44 @@ __global__ __launch_bounds__(64) void k_rice_walk(const uint64_t *payload, const
     if (!(fl & kNotSimple)) return;
     const uint64_t g0 = (uint64_t)ref.first_tile * kRiceTileSegs, ns = (uint64_t)ref.n_tiles * kRiceTileSegs;
     for (uint64_t i = t; i < ns; i += 64) w.E[g0 + i] = kNoEntry;
-    __syncthreads();
+    // the chain's segments in increasing order (NEXT > the segment): their NEXT / Y staged in
+    // LDS a chunk at a time, lane 0 following the chain through each chunk
+    constexpr uint32_t kChunk = 512;
+    __shared__ uint32_t s_nx[kChunk];
+    __shared__ uint64_t s_y[kChunk];
+    __shared__ uint64_t s_v, s_yy;
+    __shared__ int s_end;
     if (t == 0) {
-        uint64_t v = 0, y = 0;
-        for (;;) {
-            w.E[g0 + v] = y;
-            const uint32_t nx = w.NEXT[g0 + v];
-            if (nx == kNoNext) break;
-            y = w.Y[g0 + v];
-            v = nx;
+        s_v = 0;
+        s_yy = 0;
+        s_end = 0;
+    }
+    __syncthreads();
+    for (uint64_t c0 = 0; c0 < ns; c0 += kChunk) {
+        if (s_end) break;  // (uniform: read after a barrier)
+        const uint64_t nc = ns - c0 < kChunk ? ns - c0 : kChunk;
+        if (s_v >= c0 + nc) continue;  // the chain skips this chunk
+        for (uint32_t i = t; i < nc; i += 64) {
+            s_nx[i] = w.NEXT[g0 + c0 + i];
+            s_y[i] = w.Y[g0 + c0 + i];
         }
+        __syncthreads();
+        if (t == 0) {
+            uint64_t v = s_v, y = s_yy;
+            while (v < c0 + nc) {
+                w.E[g0 + v] = y;
+                const uint32_t nx = s_nx[v - c0];
+                if (nx == kNoNext) {
+                    s_end = 1;
+                    break;
+                }
+                y = s_y[v - c0];
+                v = nx;
+            }
+            s_v = v;
+            s_yy = y;
+        }
+        __syncthreads();
     }
 }
 
@@ -439,10 +494,7 @@ __global__ __launch_bounds__(kRiceTileSegs) void k_rice_decode(const uint64_t *p
     const uint64_t off = w.TOFF[blockIdx.x] + inc - cnt;
     int err = 0;
     if (cnt && off < x.s.n) {
-        Bits64 bt{payload + x.s.word_off, x.s.nwords};
-        bt.sw = sw;
-        bt.w0 = w0;
-        bt.nl = kRiceWin;
+        WinBits bt{payload + x.s.word_off, x.s.nwords, sw, w0, kRiceWin};
         uint64_t p = w.E[x.g];
         for (uint64_t j = 0; j < cnt && off + j < x.s.n; j++) {
             const Code c = rice_at(bt, p, (uint32_t)x.s.param);
@@ -463,9 +515,9 @@ __global__ __launch_bounds__(kRiceTileSegs) void k_rice_decode(const uint64_t *p
 // can start at past the segment's first bit, where that chain leaves the segment (the first
 // code start past it, at most l bits on) and how many codes it holds.  Transfers compose, so
 // the true entries come from a two-level walk:
-//   k_mb_tab     a thread per segment (kMbSegBits bits) computes its L transfers; lane e of a
-//                tile (kMbTileSegs segments) follows entry e through the tile's segments in
-//                LDS -> the tile's own transfer;
+//   k_mb_tab     a thread per (entry, segment) pair computes that transfer (segments of
+//                kMbSegBits bits); lane e of a tile (kMbTileSegs segments) follows entry e
+//                through the tile's segments in LDS -> the tile's own transfer;
 //   k_mb_walk    a wave per stream follows the true entry from tile to tile (bit 0 enters
 //                tile 0 at offset 0) -> each tile's entry and its codes' first value index;
 //   k_mb_decode  a tile follows its entry through its segments in LDS, scans the segments'
@@ -475,7 +527,8 @@ __global__ __launch_bounds__(kRiceTileSegs) void k_rice_decode(const uint64_t *p
 #define NTC_MB_SEG_BITS 256
 #endif
 constexpr int kMbSegBits = NTC_MB_SEG_BITS;  // bits per segment (>= 64 > l + 1; a multiple of 64)
-constexpr int kMbTileSegs = 256;  // segments (threads) per tile
+constexpr int kMbTileSegs = 256;  // segments per tile (threads of k_mb_decode)
+constexpr int kMbTabThreads = 1024;  // k_mb_tab: a thread per (entry, segment) pair
 constexpr uint8_t kMbDead = 255;  // a chain that ran past the stream's end
 constexpr int kMbWalkTiles = 128; // tiles per LDS chunk of k_mb_walk
 constexpr uint32_t kMbWin = kMbTileSegs * kMbSegBits / 64 + 2;  // LDS words: the tile + the last code
@@ -495,9 +548,9 @@ __device__ __forceinline__ MbParams mb_params(const UnpackStream &s) {
 
 // transfer tables: X[(tile * 64 + e) * kMbTileSegs + seg] exit offsets, C[...] code counts
 // (entry-major, so a tile's lanes store and load consecutive bytes); TX / TC the tiles' own
-__global__ __launch_bounds__(kMbTileSegs) void k_mb_tab(const uint64_t *payload, const UnpackStream *st,
-                                                       const UnpTile *tiles, uint8_t *X, uint16_t *C, uint8_t *TX,
-                                                       uint32_t *TC) {
+__global__ __launch_bounds__(kMbTabThreads) void k_mb_tab(const uint64_t *payload, const UnpackStream *st,
+                                                         const UnpTile *tiles, uint8_t *X, uint16_t *C, uint8_t *TX,
+                                                         uint32_t *TC) {
     const UnpTile tl = tiles[blockIdx.x];
     const UnpackStream s = st[tl.si];
     const MbParams q = mb_params(s);
@@ -508,32 +561,32 @@ __global__ __launch_bounds__(kMbTileSegs) void k_mb_tab(const uint64_t *payload,
     const uint64_t seg0 = (uint64_t)tl.tile * kMbTileSegs;
     const uint64_t w0 = seg0 * kMbSegBits / 64;
     stage_words(sw, payload + s.word_off, s.nwords, w0, kMbWin);
-    const uint64_t a = (seg0 + t) * kMbSegBits, b = a + kMbSegBits < q.nbits ? a + kMbSegBits : q.nbits;
     const uint64_t tbase = (uint64_t)blockIdx.x * 64 * kMbTileSegs;
-    if (a < q.nbits) {
-        Bits64 bt{payload + s.word_off, s.nwords};
-        bt.sw = sw;
-        bt.w0 = w0;
-        bt.nl = kMbWin;
-        for (uint32_t e = 0; e < q.L; e++) {
-            uint64_t pos = a + e;
-            uint32_t cnt = 0;
-            bool dead = false;
-            while (pos < b) {
-                const Code c = mb_at(bt, pos, q.l, q.limit);
-                if (!c.len) {
-                    dead = true;
-                    break;
-                }
-                pos += c.len;
-                cnt++;
+    // a thread per (entry, segment) pair, consecutive threads on consecutive segments of one
+    // entry (so the stores below are consecutive bytes): each chain covers one segment
+    for (uint32_t idx = (uint32_t)t; idx < q.L * kMbTileSegs; idx += kMbTabThreads) {
+        const uint32_t e = idx / kMbTileSegs, u = idx % kMbTileSegs;
+        const uint64_t a = (seg0 + u) * kMbSegBits;
+        if (a >= q.nbits) continue;
+        const uint64_t b = a + kMbSegBits < q.nbits ? a + kMbSegBits : q.nbits;
+        WinBits bt{payload + s.word_off, s.nwords, sw, w0, kMbWin};
+        uint64_t pos = a + e;
+        uint32_t cnt = 0;
+        bool dead = false;
+        while (pos < b) {
+            const Code c = mb_at(bt, pos, q.l, q.limit);
+            if (!c.len) {
+                dead = true;
+                break;
             }
-            const uint8_t x = dead ? kMbDead : (uint8_t)(pos - b);
-            sX[e * kMbTileSegs + t] = x;
-            sC[e * kMbTileSegs + t] = (uint16_t)cnt;
-            X[tbase + (uint64_t)e * kMbTileSegs + t] = x;
-            C[tbase + (uint64_t)e * kMbTileSegs + t] = (uint16_t)cnt;
+            pos += c.len;
+            cnt++;
         }
+        const uint8_t x = dead ? kMbDead : (uint8_t)(pos - b);
+        sX[idx] = x;
+        sC[idx] = (uint16_t)cnt;
+        X[tbase + idx] = x;
+        C[tbase + idx] = (uint16_t)cnt;
     }
     __syncthreads();
     if ((uint32_t)t < q.L) {
@@ -625,10 +678,7 @@ __global__ __launch_bounds__(kMbTileSegs) void k_mb_decode(const uint64_t *paylo
     uint64_t tot;
     const uint64_t off = TP[blockIdx.x] + block_exscan<kMbTileSegs>(cnt, &tot, sh);
     if (cnt && off < s.n) {
-        Bits64 bt{payload + s.word_off, s.nwords};
-        bt.sw = sw;
-        bt.w0 = w0;
-        bt.nl = kMbWin;
+        WinBits bt{payload + s.word_off, s.nwords, sw, w0, kMbWin};
         uint64_t p = (seg0 + t) * kMbSegBits + en;
         for (uint64_t j = 0; j < cnt && off + j < s.n; j++) {
             const Code c = mb_at(bt, p, q.l, q.limit);
@@ -848,7 +898,7 @@ void launch_unpack(const UnpackDev &d, hipStream_t s) {
     uint8_t *TX = (uint8_t *)(TP + nt);
     uint8_t *TE = TX + nt * 64;
     if (nt)
-        hipLaunchKernelGGL(k_mb_tab, dim3(d.n_mb_tiles), dim3(kMbTileSegs), 0, s, d.payload, d.st, d.mb_tiles, X, C, TX,
+        hipLaunchKernelGGL(k_mb_tab, dim3(d.n_mb_tiles), dim3(kMbTabThreads), 0, s, d.payload, d.st, d.mb_tiles, X, C, TX,
                            TC);
     hipLaunchKernelGGL(k_mb_walk, dim3(d.n_mb_streams), dim3(64), 0, s, d.st, d.mb_streams, TX, TC, TE, TP, d.status);
     if (nt)
