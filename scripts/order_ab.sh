@@ -1,5 +1,6 @@
 #!/bin/bash
 # A/B: k_ms4's reads in minimizer order (NTC_READ_ORDER=1) against read order, alternating.
+# (The NTC_READ_ORDER build measured slower and was reverted: DESIGN.md §9, profiles/round5/ab_read_order/.)
 set -e
 O=gpurun_out/order_ab
 mkdir -p $O
