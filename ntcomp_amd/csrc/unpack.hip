@@ -24,7 +24,7 @@
 //   for each of the l + 1 offsets a code can start at, and the true entries follow from
 //   composed tile transfers.
 //
-// k_zip_count + k_zip_write (a workgroup per 16,384 records of a block) zip the four value
+// k_zip_count + k_zip_write (a workgroup per 4,096 records of a block) zip the four value
 // streams back into u64 records with two block scans (long records -> s1/s2 index, short
 // records -> base offset; each segment starts from the counts of the ones before it), check
 // what read_block_impl checks (stream sizes, flags past the streams), and sums the reads
