@@ -4,6 +4,7 @@
 //   pwriteW   W threads, one pwrite each per batch (the round-5 writer)
 //   mmapW     ftruncate per batch, the batch's range mapped shared, W threads populate
 //             (MADV_POPULATE_WRITE) and copy their part, munmap
+//   odirect1  one O_DIRECT pwrite per batch from a 4 KiB-aligned buffer (no page cache)
 // usage: write_bw DIR [total_MB] [batch_MB] [W]    -> one JSON line per mode
 #include <fcntl.h>
 #include <sys/mman.h>
@@ -11,6 +12,7 @@
 #include <sys/vfs.h>
 #include <unistd.h>
 
+#include <cerrno>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -39,11 +41,31 @@ int main(int argc, char **argv) {
     struct statfs sf;
     statfs(dir.c_str(), &sf);
     const long page = sysconf(_SC_PAGESIZE);
-    for (const char *mode : {"pwrite1", "pwriteW", "mmapW", "mmapW_nopop"}) {
+    // O_DIRECT needs an aligned source: a 4 KiB-aligned copy of the batch
+    uint8_t *asrc = nullptr;
+    if (posix_memalign((void **)&asrc, 4096, batch) != 0) return 1;
+    memcpy(asrc, src.data(), batch);
+    const char *modes_env = getenv("WRITE_BW_MODES");
+    std::vector<std::string> modes = {"pwrite1", "pwriteW", "mmapW", "mmapW_nopop", "odirect1"};
+    if (modes_env) {
+        modes.clear();
+        for (const char *q = modes_env; *q;) {
+            const char *c = strchr(q, ',');
+            modes.push_back(c ? std::string(q, c - q) : std::string(q));
+            if (!c) break;
+            q = c + 1;
+        }
+    }
+    for (const std::string &ms : modes) {
+        const char *mode = ms.c_str();
         const std::string path = dir + "/write_bw.out";
         unlink(path.c_str());
-        const int fd = open(path.c_str(), O_RDWR | O_CREAT | O_TRUNC, 0644);
-        if (fd < 0) return 1;
+        const bool direct = !strcmp(mode, "odirect1");
+        const int fd = open(path.c_str(), O_RDWR | O_CREAT | O_TRUNC | (direct ? O_DIRECT : 0), 0644);
+        if (fd < 0) {
+            printf("{\"mode\": \"%s\", \"ok\": false, \"open_errno\": %d}\n", mode, errno);
+            continue;
+        }
         const double t0 = now();
         size_t pos = 0;
         bool ok = true;
@@ -51,6 +73,9 @@ int main(int argc, char **argv) {
             const size_t n = std::min(batch, total - pos);
             if (!strcmp(mode, "pwrite1")) {
                 ok = pwrite(fd, src.data(), n, (off_t)pos) == (ssize_t)n;
+            } else if (direct) {
+                const size_t na = n / 4096 * 4096;  // (the batch size is a multiple of 4 KiB here)
+                ok = pwrite(fd, asrc, na, (off_t)pos) == (ssize_t)na;
             } else if (!strcmp(mode, "pwriteW")) {
                 std::vector<std::thread> ts;
                 std::atomic<bool> good{true};
