@@ -210,6 +210,32 @@ def test_decode_file_truncated_and_damaged_blocks(setup, tmp_path, unpack):
     ctx.close()
 
 
+def test_decode_file_stream_damage_found_after_inflate(setup, tmp_path, unpack):
+    """A block whose gzip members are intact but whose streams are not (its flag stream's
+    header claims 1000 more values than its codes hold) ends the output after the blocks
+    before it, found by the GPU unpacker (default) or by the host pool alike, as
+    decode_block's Err ends the reference's loop (main.rs:202)."""
+    d, genome, ix = setup
+    ctx = nt.GpuContext(0)
+    ctx.upload(ix)
+    reads, offs = ragged(genome, 4 * 65536 + 99, 33)
+    path, ends = encoded_file(ctx, tmp_path, reads, offs)
+    data = path.read_bytes()
+    a, b = ends[1][0], ends[2][0]  # block 2
+    meta, pay, used = nt.read_block_streams(data[a:b])
+    assert used == b - a
+    meta.stream[2].num_u64 += 1000
+    p = tmp_path / "sd.dat"
+    p.write_bytes(data[:a] + nt.deflate_block(meta, pay) + data[b:])
+    nr = ends[1][1]
+    for bpb in (1, 3):
+        with open(tmp_path / "o.fa", "wb") as f:
+            st = nt.decode_file([ctx], str(p), f.fileno(), threads=4, blocks_per_batch=bpb)
+        assert (tmp_path / "o.fa").read_bytes() == fasta_of(reads, offs[:nr + 1]), (unpack, bpb)
+        assert (st["blocks"], st["reads"], st["dropped_blocks"]) == (2, nr, 3), (unpack, bpb)
+    ctx.close()
+
+
 def test_cli_decode_to_a_pipe(setup, tmp_path):
     """stdout a pipe (not seekable): the writer falls back to write(2) in order."""
     d, genome, ix = setup
