@@ -228,6 +228,7 @@ def cmd_decode(args):
 def main(argv=None):
     ap = argparse.ArgumentParser(prog="ntcomp", description="Sequencing data compression with SBWT + k-bounded "
                                  "matching statistics; encode/decode hot path on MI355X.")
+    ap.add_argument("-V", "--version", action="version", version="ntcomp 0.1.0")  # Cargo.toml:3, clap's `version`
     sub = ap.add_subparsers(dest="command")
     b = sub.add_parser("build", help="Build the compression dictionary")
     b.add_argument("seq_files", nargs="*", help="Sequence data file(s).")

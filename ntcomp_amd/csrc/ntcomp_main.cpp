@@ -29,6 +29,7 @@
 namespace {
 
 using Clock = std::chrono::steady_clock;
+constexpr const char *kVersion = "0.1.0";  // the reference's Cargo.toml version
 double since(Clock::time_point t) { return std::chrono::duration<double>(Clock::now() - t).count(); }
 
 [[noreturn]] void die(const std::string &msg) {
@@ -72,13 +73,25 @@ bool is_switch(const std::string &o) {
     return false;
 }
 
+void usage(FILE *f = stderr);
+
 Args parse(int argc, char **argv, int from) {
     Args a;
     for (int i = from; i < argc; i++) {
         std::string s = argv[i];
         if (s.size() > 1 && s[0] == '-') {
             const size_t eq = s.find('=');
-            if (eq != std::string::npos && s.rfind("--", 0) == 0) {
+            if (s == "-h" || s == "--help") {  // clap: help on stdout, exit 0
+                usage(stdout);
+                std::exit(0);
+            }
+            if (s == "-V" || s == "--version") {
+                std::printf("ntcomp %s\n", kVersion);
+                std::exit(0);
+            }
+            if (s.size() > 2 && s[1] != '-' && takes_value(s.substr(0, 2))) {  // clap's attached short value: -t8, -k31
+                a.kv.push_back({s.substr(0, 2), s.substr(2)});
+            } else if (eq != std::string::npos && s.rfind("--", 0) == 0) {
                 const std::string name = s.substr(0, eq);
                 if (!takes_value(name)) die("unexpected argument '" + s + "'");
                 a.kv.push_back({name, s.substr(eq + 1)});
@@ -381,8 +394,8 @@ int cmd_build(const Args &a) {
     return 0;
 }
 
-void usage() {
-    std::fprintf(stderr,
+void usage(FILE *f) {
+    std::fprintf(f,
                  "Sequencing data compression with SBWT + k-bounded matching statistics; encode/decode hot path on "
                  "MI355X.\n\nusage: ntcomp build -o PREFIX [-k K] [-m MEM_GB] [--temp-dir DIR] FILES...\n"
                  "       ntcomp encode -i PREFIX FILE > encoded.dat\n"
@@ -397,6 +410,14 @@ int main(int argc, char **argv) {
         return 2;
     }
     const std::string cmd = argv[1];
+    if (cmd == "-h" || cmd == "--help" || cmd == "help") {
+        usage(stdout);
+        return 0;
+    }
+    if (cmd == "-V" || cmd == "--version") {
+        std::printf("ntcomp %s\n", kVersion);
+        return 0;
+    }
     const Args a = parse(argc, argv, 2);
     if (cmd == "build") return cmd_build(a);
     if (cmd == "encode" || cmd == "decode") {

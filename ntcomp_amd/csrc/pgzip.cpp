@@ -261,20 +261,26 @@ bool read_dynamic(Bits &b, Table &lit, Table &dist) {
 }
 
 // ---- inflate ----------------------------------------------------------------------------
-enum InfRc { kInfBoundary = 0, kInfFinal = 1, kInfError = -1 };
+// kInfLimit: the output passed max_out (a true start in data that compresses better than
+// the chunk budget assumes): not evidence of a false candidate, so speculation stops there
+enum InfRc { kInfBoundary = 0, kInfFinal = 1, kInfError = -1, kInfLimit = -2 };
 
 // 16-bit symbol output: p[0 .. kWin) is the window (markers or bytes), symbols follow; grown
-// with realloc (no zero fill: a chunk's buffer is written once)
+// with realloc (no zero fill: a chunk's buffer is written once).  Every allocation holds
+// kSlack symbols past cap: a match copies 8 symbols a step, so a 258-symbol match admitted at
+// x + 262 <= cap may store up to x + 264.
+constexpr size_t kSlack = 8;
 struct Out {
     uint16_t *p = nullptr;
     size_t n = 0, cap = 0;
+    size_t min_ref = SIZE_MAX;  // lowest symbol index a match copied from (window reach check)
     Out() = default;
     Out(const Out &) = delete;
     Out &operator=(const Out &) = delete;
     ~Out() { std::free(p); }
     bool reserve(size_t c) {
         if (c <= cap) return true;
-        void *q = std::realloc(p, c * 2);
+        void *q = std::realloc(p, (c + kSlack) * 2);
         if (!q) return false;
         p = (uint16_t *)q;
         cap = c;
@@ -283,10 +289,14 @@ struct Out {
 };
 
 // Inflate blocks from bit `start` into o (symbols appended after o.n), stopping at the first
-// block boundary at or after stop_bit (kInfBoundary), after the final block (kInfFinal), or
-// on invalid data or an output past max_out symbols (kInfError).  *end = the bit reached.
+// block boundary at or after stop_bit (kInfBoundary), after the final block (kInfFinal), on
+// invalid data (kInfError) or on an output past max_out symbols (kInfLimit).  Symbols below
+// index lo are not part of the member (the window in front of a member's start): a distance
+// reaching them is invalid, "invalid distance too far back" in zlib.  o.min_ref records the
+// lowest index any match copied from, so that a speculative chunk (lo = 0, its window is
+// markers) can be checked once the member's valid window is known.  *end = the bit reached.
 int inflate_blocks(const uint8_t *in, uint64_t n, uint64_t start, uint64_t stop_bit, Out &o, uint64_t max_out,
-                   uint64_t *end) {
+                   uint64_t lo, uint64_t *end) {
     Bits b(in, n, start);
     Table dl, dd;
     if (!o.reserve(o.n + (1u << 20))) return kInfError;
@@ -305,7 +315,11 @@ int inflate_blocks(const uint8_t *in, uint64_t n, uint64_t start, uint64_t stop_
             b.refill();
             const uint32_t len = b.get(16), nlen = b.get(16);
             if ((len ^ 0xFFFF) != nlen) break;
-            if (o.n + len > max_out || !o.reserve(o.n + len + 4096)) break;
+            if (o.n + len > max_out) {
+                rc = kInfLimit;
+                break;
+            }
+            if (!o.reserve(o.n + len + 4096)) break;
             uint32_t left = len;
             while (left && b.cnt >= 8) {  // whole bytes still in the bit buffer
                 o.p[o.n++] = (uint16_t)b.get(8);
@@ -338,8 +352,8 @@ int inflate_blocks(const uint8_t *in, uint64_t n, uint64_t start, uint64_t stop_
         uint64_t bb = b.buf, ip = b.ip;
         uint32_t bc = b.cnt;
         uint16_t *op = o.p;
-        size_t x = o.n, cap = o.cap;
-        bool ok = true;
+        size_t x = o.n, cap = o.cap, mref = o.min_ref;
+        bool ok = true, limit = false;
         for (;;) {
             if (bc < 48) {
                 if (ip + 8 <= n) {
@@ -360,12 +374,17 @@ int inflate_blocks(const uint8_t *in, uint64_t n, uint64_t start, uint64_t stop_
             }
             if (x + 262 > cap) {  // room for one match (258) or literals
                 o.n = x;
-                if (x + 262 > max_out || !o.reserve(std::min<size_t>(max_out, std::max<size_t>(2 * cap, x + 4096)) + 8)) {
+                if (x + 262 > max_out) {
+                    ok = false;
+                    limit = true;
+                    break;
+                }
+                if (!o.reserve(std::min<size_t>(max_out, std::max<size_t>(2 * cap, x + 4096)))) {
                     ok = false;
                     break;
                 }
                 op = o.p;
-                cap = o.cap - 8;
+                cap = o.cap;
             }
             uint32_t e = L[bb & ((1u << kLitBits) - 1)];
             if (((e >> 4) & 0xF) == kSub) {
@@ -412,10 +431,11 @@ int inflate_blocks(const uint8_t *in, uint64_t n, uint64_t start, uint64_t stop_
             const uint32_t dist = (f >> 16) + (uint32_t)(bb & ((1u << de) - 1));
             bb >>= de;
             bc -= de;
-            if (dist > x) {  // o holds the kWin window in front
+            if (dist > x - lo) {  // o holds the kWin window in front, valid from lo
                 ok = false;
                 break;
             }
+            if (x - dist < mref) mref = x - dist;
             const uint16_t *src = op + x - dist;
             uint16_t *d = op + x;
             if (dist >= 8) {  // 8 symbols (16 bytes) a step; the buffer has 8 symbols of slack
@@ -432,6 +452,11 @@ int inflate_blocks(const uint8_t *in, uint64_t n, uint64_t start, uint64_t stop_
         b.cnt = bc;
         b.ip = ip;
         o.n = x;
+        o.min_ref = mref;
+        if (limit) {
+            rc = kInfLimit;
+            break;
+        }
         if (!ok || b.overrun()) break;
         if (final) {
             rc = kInfFinal;
@@ -651,15 +676,20 @@ struct PgzReader {
             if (!c.out.reserve(kWin + chunk_bytes() * 6)) return;  // ~ a FASTQ chunk's output
             for (uint32_t j = 0; j < kWin; j++) c.out.p[j] = (uint16_t)(kMarker + j);
             c.out.n = kWin;
+            c.out.min_ref = SIZE_MAX;
             uint64_t end = 0;
-            const int rc = inflate_blocks(in, n, p, c.b1, c.out, max_out_per_chunk, &end);
-            if (rc != kInfError) {
+            const int rc = inflate_blocks(in, n, p, c.b1, c.out, max_out_per_chunk, 0, &end);
+            if (rc >= 0) {
                 c.start = p;
                 c.end = end;
                 c.rc = rc;
                 return;
             }
             c.out.n = 0;
+            // past the output budget: a start this well compressed is likely true, and every
+            // later candidate in the chunk would inflate as far again -- leave the chunk to the
+            // resolver's sequential gap
+            if (rc == kInfLimit) return;
             st_false++;
             if (c.b0 == 0) return;
             from = p + 1;
@@ -708,9 +738,9 @@ struct PgzReader {
         for (uint32_t j = 0; j < kWin; j++) o.p[j] = win[j];
         o.n = kWin;
         uint64_t end = 0;
-        const int rc = inflate_blocks(in, n, pos, stop, o, UINT64_MAX, &end);
+        const int rc = inflate_blocks(in, n, pos, stop, o, UINT64_MAX, kWin - win_valid, &end);
         st_gap_bits += end - pos;
-        if (rc == kInfError) {
+        if (rc < 0) {
             failed = true;
             return false;
         }
@@ -757,6 +787,11 @@ struct PgzReader {
                 if (!gap(c->start)) return;
             if (ended || failed) return;
             if (c->rc != kInfError && pos == c->start) {
+                // the chunk's matches may only reach the member's own bytes in the window
+                if (c->out.min_ref != SIZE_MAX && c->out.min_ref < kWin - win_valid) {
+                    failed = true;
+                    return;
+                }
                 Piece pc;
                 pc.len = c->out.n - kWin;
                 pc.win = win;  // markers resolve against the member's window before the chunk
@@ -806,7 +841,10 @@ PgzReader *pgz_open(const char *path, int threads) {
     r->T = (unsigned)std::max(1, threads);
     r->ahead = r->T + 4;
     r->nchunks = (r->n + chunk_bytes() - 1) / chunk_bytes();
-    r->max_out_per_chunk = kWin + kMaxChunkSymbols;
+    // NTC_PGZ_MAXOUT (symbols, for tests) lowers the per-chunk output budget
+    const char *mo = std::getenv("NTC_PGZ_MAXOUT");
+    const long long mov = mo ? std::atoll(mo) : 0;
+    r->max_out_per_chunk = kWin + (mov >= 1024 ? (uint64_t)mov : kMaxChunkSymbols);
     for (unsigned t = 0; t < r->T; t++) r->th.emplace_back([r] { r->worker(); });
     return r;
 }

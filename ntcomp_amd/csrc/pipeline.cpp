@@ -832,6 +832,7 @@ struct DBlock {
     uint64_t a, len;   // byte range of the block
     uint64_t n_recs;   // records (the flag stream's num_u64)
     uint64_t pay;      // bytes of its four inflated streams (8 x encoded_size each)
+    bool bad;          // a header that cannot describe its gzip stream: damaged, never sized
 };
 
 struct DSlot {  // one batch in flight
@@ -916,22 +917,33 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
     ::close(fd);
     auto le32 = [&](uint64_t p) { return (uint64_t)data[p] | (uint64_t)data[p + 1] << 8 | (uint64_t)data[p + 2] << 16 |
                                          (uint64_t)data[p + 3] << 24; };
+    // A block's buffers are sized from its headers before anything is inflated, so each
+    // header is checked against its own gzip stream first: the ISIZE trailer must equal
+    // 8 x encoded_size, which deflate cannot exceed 1032 x block_size, and stream 2 (Rice: one
+    // bit per value at least) bounds num_u64.  A block that fails is damaged -- the output ends
+    // before it, as the reference's loop ends at decode_block's Err (main.rs:202) -- instead of
+    // a pinned allocation sized from garbage.
     std::vector<DBlock> blocks;
     for (uint64_t pos = 32; pos < fsize;) {  // after the 32-byte file header (main.rs:196-198)
         uint64_t p = pos, nrec = 0, pay = 0;
-        bool whole = true;
+        bool whole = true, bad = false;
         for (int s = 0; s < 4 && whole; s++) {
             if (p + 32 > fsize) {
                 whole = false;
                 break;
             }
+            const uint64_t bs = le32(p), enc = le32(p + 12);
             if (s == 2) nrec = le32(p + 8);
-            pay += 8 * le32(p + 12);
-            p += 32 + le32(p);
+            if (bs < 18 || p + 32 + bs > fsize || le32(p + 32 + bs - 4) != ((8 * enc) & 0xFFFFFFFFULL) ||
+                8 * enc > 1032 * bs || (s == 2 && nrec > 64 * enc))
+                bad = true;
+            pay += 8 * enc;
+            p += 32 + bs;
             if (p > fsize) whole = false;
         }
         if (!whole) break;
-        blocks.push_back(DBlock{pos, p - pos, nrec, pay});
+        // a bad block is sized as nothing; the unzip pool reports it damaged
+        blocks.push_back(bad ? DBlock{pos, p - pos, 0, 0, true} : DBlock{pos, p - pos, nrec, pay, false});
         pos = p;
     }
     const uint64_t n_batches = (blocks.size() + bpb - 1) / bpb;
@@ -1233,7 +1245,10 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
                 uint64_t used = 0, nr = 0, numr = 0, reads = 0, bases = 0;
                 const DBlock &db = blocks[blk];
                 int rc;
-                if (gpu_unpack) {  // inflate only: the streams are decoded on the GPU
+                if (db.bad) {
+                    rc = NTC_ERR_FORMAT;
+                    if (gpu_unpack) sl.metas[blk - sl.first_block].status = rc;
+                } else if (gpu_unpack) {  // inflate only: the streams are decoded on the GPU
                     ntc_block_meta &m = sl.metas[blk - sl.first_block];
                     rc = ntc_read_block_streams(data + db.a, db.len, &used, sl.pay + poff, db.pay, &m);
                     if (rc == NTC_OK && (m.n_recs != db.n_recs || used != db.len)) rc = NTC_ERR_FORMAT;

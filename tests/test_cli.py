@@ -355,6 +355,28 @@ def test_native_cli_rejects_unknown_options(tmp_path):
         assert r.returncode != 0 and b"unexpected argument" in r.stderr, (args, r.stderr)
 
 
+def test_native_cli_accepts_clap_forms(tmp_path):
+    """Forms clap accepts (src/cli.rs): an attached short value (`-k31`, `-t2`, `-p5`),
+    `-h`/`--help` (usage on stdout, exit 0) and `-V`/`--version` (Cargo.toml's version)."""
+    g = nt.synth_genome(11, 12_000).tobytes().decode()
+    (tmp_path / "a.fa").write_text(">a\n" + g + "\n")
+    subprocess.run([NATIVE, "build", "-o", str(tmp_path / "x"), "-k31", "-t2", "-p5", "--builder", "host",
+                    str(tmp_path / "a.fa")], check=True, stderr=subprocess.PIPE)
+    subprocess.run([NATIVE, "build", "-o", str(tmp_path / "y"), "-k", "31", "-t", "2", "-p", "5", "--builder", "host",
+                    str(tmp_path / "a.fa")], check=True, stderr=subprocess.PIPE)
+    for ext in (".sbwt", ".lcs"):
+        assert (tmp_path / ("x" + ext)).read_bytes() == (tmp_path / ("y" + ext)).read_bytes(), ext
+    assert nt.Index.load(str(tmp_path / "x")).k == 31
+    for args in (["-h"], ["--help"], ["build", "-h"], ["encode", "--help"]):
+        r = subprocess.run([NATIVE, *args], capture_output=True)
+        assert r.returncode == 0 and b"usage" in r.stdout, args
+    for args in (["-V"], ["--version"], ["decode", "-V"]):
+        r = subprocess.run([NATIVE, *args], capture_output=True)
+        assert r.returncode == 0 and r.stdout.strip() == b"ntcomp 0.1.0", args
+    r = subprocess.run([sys.executable, "-m", "ntcomp_amd", "--version"], cwd=REPO, capture_output=True)
+    assert r.returncode == 0 and b"ntcomp 0.1.0" in r.stdout
+
+
 @pytest.mark.gpu
 def test_native_cli_encode_decode_equal_python_cli(tmp_path):
     """`ntcomp encode|decode` (native) and `python -m ntcomp_amd encode|decode` write the same

@@ -12,6 +12,7 @@ import bz2
 import gzip
 import lzma
 import os
+import struct
 import subprocess
 
 import numpy as np
@@ -238,6 +239,18 @@ def test_pipelines_under_sanitizers(san, encoded, tmp_path, kind):
     got = run(san[kind], "decode", d / "idx", tmp_path / "bad.dat", tmp_path / "b.fa", 4, 1, 2)
     assert int(got["rc"]) == 0 and int(got["blocks"]) == 2 and int(got["dropped"]) == 2, got
     assert (tmp_path / "b.fa").read_bytes() == fasta[:fasta.index(b">seq.%d\n" % (2 * 65536 + 1))]
+    # third block: a stream header's encoded_size (or num_u64) damaged, its gzip data intact --
+    # a damaged block that ends the output, not a 32 GiB pinned allocation
+    for field, stream in ((12, 1), (12, 3), (8, 2)):
+        bad = bytearray(data)
+        p = pos
+        for _ in range(stream):
+            p += 32 + int.from_bytes(data[p:p + 4], "little")
+        bad[p + field:p + field + 4] = b"\xff\xff\xff\xff"
+        (tmp_path / "bad2.dat").write_bytes(bytes(bad))
+        got = run(san[kind], "decode", d / "idx", tmp_path / "bad2.dat", tmp_path / "b2.fa", 4, 1, 2)
+        assert int(got["rc"]) == 0 and int(got["blocks"]) == 2 and int(got["dropped"]) == 2, (field, stream, got)
+        assert (tmp_path / "b2.fa").read_bytes() == fasta[:fasta.index(b">seq.%d\n" % (2 * 65536 + 1))]
     # a read with a base absent from the index: the pipeline reports it, nothing hangs
     fq = (d / "r.fq").read_bytes().replace(b"\n+\n", b"\n+\n", 1)
     lines = fq.split(b"\n")
@@ -356,14 +369,33 @@ def _gzip_cases():
     flip[len(flip) // 2] ^= 0x5A
     bad = {"trunc.fq.gz": bytes(g6[:-100]), "crc.fq.gz": bytes(crc), "isize.fq.gz": bytes(isz),
            "flip.fq.gz": bytes(flip), "trunc_multi.fq.gz": ok["multi.fq.gz"][:-9]}
+    # period-10 bases: 258-byte matches at distance 10 (8-symbol match copies) end on every
+    # offset of the chunk buffers (the copy's slack past the reserved size)
+    per = b"ACGTTGCAAC" * 600
+    ok["period.fq.gz"] = gzip.compress(b"".join(b"@p%d\n%s\n+\n%s\n" % (i, per[i % 10:][:4000 + i], b"I" * (4000 + i))
+                                                for i in range(60)), 9)
+
+    def preset(data, dictionary):  # a member whose matches reach into a preset dictionary
+        c = zlib.compressobj(6, zlib.DEFLATED, -15, 8, zlib.Z_DEFAULT_STRATEGY, zdict=dictionary)
+        raw = c.compress(data) + c.flush()
+        return (b"\x1f\x8b\x08\x00\x00\x00\x00\x00\x00\xff" + raw
+                + struct.pack("<II", zlib.crc32(data), len(data) & 0xFFFFFFFF))
+
+    # distances that reach before the member's first byte: zlib / libdeflate refuse them
+    # ("invalid distance too far back") even with a matching CRC; so must the parallel reader,
+    # in its first chunk, in a later member (the stale window of the one before) and in a gap
+    bad["farback.fq.gz"] = preset(fq, fq[:20000])
+    bad["farback_multi.fq.gz"] = gzip.compress(fq[:h], 6) + preset(fq[h:], fq[h - 30000:h])
     return ok, bad
 
 
-def test_parallel_gzip_under_sanitizers(san, tmp_path):
+@pytest.mark.parametrize("maxout", [None, 4096])
+def test_parallel_gzip_under_sanitizers(san, tmp_path, maxout):
     """Non-BGZF gzip through the parallel inflater (NTC_PGZ_MIN=0, 1-3 KiB chunks: hundreds
     of speculative chunk starts, false candidates and gaps) under ASan/UBSan and TSan: the
     same records as the production reader (libdeflate / zlib on one thread) for every block
-    type, and the same error for damaged members."""
+    type, and the same error for damaged members.  maxout: a per-chunk output budget of 4 K
+    symbols (NTC_PGZ_MAXOUT), so that true starts hit it and their chunks fall to the gaps."""
     ok, bad = _gzip_cases()
     for name, data in {**ok, **bad}.items():
         (tmp_path / name).write_bytes(data)
@@ -371,6 +403,8 @@ def test_parallel_gzip_under_sanitizers(san, tmp_path):
         assert (exp[0] == 0) == (name in ok), (name, exp)
         for kind, chunk in (("asan", 1024), ("tsan", 3000)):
             env = dict(ENV, NTC_PGZ_MIN="0", NTC_PGZ_CHUNK=str(chunk))
+            if maxout:
+                env["NTC_PGZ_MAXOUT"] = str(maxout)
             r = subprocess.run([san[kind], "fastx", str(tmp_path / name), "4", "500", str(1 << 16), "1"], env=env,
                                stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=600)
             err = r.stderr.decode(errors="replace")
