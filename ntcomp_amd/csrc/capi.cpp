@@ -106,6 +106,7 @@ struct ntc_ctx {
     int filter_opt = -1;     // SCAN pre-filter at the next upload: -1 auto (off when saturated), 0 off, 1 on
     int64_t filter_density_ppm = -1;  // presence density of the filter level at the last upload
     int joint_opt = -1;      // joint path runs at the next upload: -1 auto (fragmented path cover), 0 off, 1 on
+    int path_link_opt = path_link_on() ? 1 : 0;  // path cover: unitigs linked across branches (default) or not
     int win_opt = -1;        // SCAN window words at the next upload: -1 auto (U >= 4), 0 off, 1 on
     int decode_only_opt = 0;  // the next upload builds only what decode needs (walk table): no path
                               // cover, suffix table or SCAN words; encode calls then fail
@@ -823,6 +824,20 @@ int upload_prepared(ntc_ctx *ctx, const ntc_index_prep &prep) {
         HIP_TRY(ctx, hipMemsetAsync(prv, 0xFF, n * 4, ctx->stream));
         HIP_TRY(ctx, hipMemsetAsync(cnt, 0, 16, ctx->stream));
         launch_path_edges(pa, prv, ctx->stream);
+        if (ctx->path_link_opt) {  // unitigs linked across branches (derived.cpp link_unitigs)
+            void *d_want, *d_bpred;
+            if ((rc = talloc(n * 4, &d_want)) || (rc = talloc(n * 8, &d_bpred))) {
+                free_tmp();
+                return rc;
+            }
+            const uint4 *su = launch_path_rank(prv, (uint32_t)n, (uint4 *)d_sta, (uint4 *)d_stb, ctx->stream);
+            HIP_TRY(ctx, hipMemsetAsync(d_len, 0, n * 4, ctx->stream));
+            launch_path_lengths(pa, su, prv, (uint32_t *)d_len, (uint32_t *)d_vals, cnt + 2, ctx->stream);
+            HIP_TRY(ctx, hipMemsetAsync(d_want, 0xFF, n * 4, ctx->stream));
+            HIP_TRY(ctx, hipMemsetAsync(d_bpred, 0xFF, n * 8, ctx->stream));
+            launch_path_link(pa, su, (const uint32_t *)d_len, (uint32_t *)d_want, (unsigned long long *)d_bpred, prv,
+                             ctx->stream);
+        }
         const uint4 *st = launch_path_rank(prv, (uint32_t)n, (uint4 *)d_sta, (uint4 *)d_stb, ctx->stream);
         launch_path_cut(pa, st, prv, cnt, ctx->stream);
         uint32_t cut = 0;
@@ -1026,6 +1041,11 @@ int ntc_ctx_set_option(ntc_ctx *ctx, const char *key, int64_t value) {
         ctx->joint_opt = (int)value;
         return NTC_OK;
     }
+    if (std::strcmp(key, "path_link") == 0) {  // applies to the next ntc_index_upload
+        if (value != 0 && value != 1) return set_err(ctx, NTC_ERR_INVALID_ARG, "path_link must be 0 or 1");
+        ctx->path_link_opt = (int)value;
+        return NTC_OK;
+    }
     if (std::strcmp(key, "win") == 0) {  // applies to the next ntc_index_upload
         if (value < -1 || value > 1) return set_err(ctx, NTC_ERR_INVALID_ARG, "win must be -1 (auto), 0 or 1");
         ctx->win_opt = (int)value;
@@ -1097,6 +1117,7 @@ int ntc_ctx_get_option(const ntc_ctx *ctx, const char *key, int64_t *value) {
     else if (std::strcmp(key, "filter") == 0) *value = ctx->has_index ? (ctx->dix.filt_f != 0) : ctx->filter_opt;
     else if (std::strcmp(key, "joint") == 0) *value = ctx->has_index ? (int64_t)ctx->dix.joint : ctx->joint_opt;
     else if (std::strcmp(key, "win") == 0) *value = ctx->has_index ? (ctx->dix.win_w != nullptr) : ctx->win_opt;
+    else if (std::strcmp(key, "path_link") == 0) *value = ctx->path_link_opt;
     else if (std::strcmp(key, "filter_density_ppm") == 0) *value = ctx->filter_density_ppm;
     else if (std::strcmp(key, "n_paths") == 0) *value = (int64_t)ctx->n_paths;
     else if (std::strcmp(key, "path_text_len") == 0) *value = (int64_t)ctx->path_text_len;

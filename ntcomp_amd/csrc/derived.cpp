@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <string>
 #include <thread>
 
@@ -219,6 +220,62 @@ void fork_words(const HostIndex &ix, const Derived &dv, const std::vector<uint8_
     }
 }
 
+bool path_link_on() {
+    const char *e = std::getenv("NTC_PATH_LINK");
+    return !(e && std::atoi(e) == 0);
+}
+
+// Unitig linking: a unitig's last node t whose successors y (each the first node of its own
+// unitig) branch is joined to one of them, and so is a unitig's first node with several
+// predecessors: t -> y is added when y is t's preferred successor AND t is y's preferred
+// predecessor, preference going to the SHORTER unitig (then the smaller node).  In a
+// collection of strains the unitigs through the sites every strain shares are short -- some
+// strain branches off at almost every position -- while a strain's own variant spans one
+// long, unbranched unitig (k nodes per SNP), so linking short unitigs strings the shared
+// sequence into long paths and leaves the rare variants as their own paths.  A read then
+// follows one path through the sites its strain shares with the others instead of hopping
+// at every branch (L31: 18.7 fork hops per read with unitigs only).  Any edge of the graph is
+// a valid path edge: the kernels stop a run wherever the read leaves the path and take the
+// SBWT's own extension there (encode_core.h), so only speed depends on the choice.  The
+// device builds the same cover (kernels.hip k_link_*).
+void link_unitigs(const HostIndex &ix, const Derived &dv, const std::vector<uint8_t> &dummy,
+                  std::vector<uint32_t> &nxt, std::vector<uint32_t> &prv) {
+    const uint64_t n = ix.n;
+    const uint32_t k = ix.k;
+    std::vector<uint32_t> ulen(n, 0);  // nodes of the unitig each real node lies on (0: a cycle)
+    for (uint64_t z = 1; z < n; z++) {
+        if (dummy[z] || prv[z] != kNoNode) continue;
+        uint32_t c = 0;
+        for (uint32_t y = (uint32_t)z; y != kNoNode; y = nxt[y]) c++;
+        for (uint32_t y = (uint32_t)z; y != kNoNode; y = nxt[y]) ulen[y] = c;
+    }
+    std::vector<uint64_t> best_pred(n, UINT64_MAX);
+    std::vector<uint32_t> want(n, kNoNode);
+    for (uint64_t t = 1; t < n; t++) {
+        if (dummy[t] || !ulen[t] || nxt[t] != kNoNode) continue;
+        uint64_t h = t;  // the (k-1)-suffix group's first node holds the labels
+        while (h > 0 && ix.lcs[h] >= k - 1) h--;
+        const uint32_t m = labels_of(dv, h);
+        uint64_t best = UINT64_MAX;
+        const uint64_t mine = (uint64_t)ulen[t] << 32 | t;
+        for (int c = 0; c < 4; c++) {
+            if (!((m >> c) & 1u)) continue;
+            const uint32_t y = dv.C[c] + host_rank(dv, c, h);
+            if (dummy[y] || prv[y] != kNoNode || !ulen[y]) continue;
+            best = std::min(best, (uint64_t)ulen[y] << 32 | y);
+            best_pred[y] = std::min(best_pred[y], mine);
+        }
+        if (best != UINT64_MAX) want[t] = (uint32_t)best;
+    }
+    for (uint64_t t = 1; t < n; t++) {
+        const uint32_t y = want[t];
+        if (y != kNoNode && best_pred[y] == ((uint64_t)ulen[t] << 32 | t)) {
+            nxt[t] = y;
+            prv[y] = (uint32_t)t;
+        }
+    }
+}
+
 // Path cover = the unitigs of the de Bruijn graph on real k-mers: edge z -> y when z is
 // alone in its (k-1)-suffix group, has exactly one successor y, and neither is a dummy
 // (y then has z as its only predecessor).  Paths start at real nodes without an in-edge;
@@ -237,6 +294,7 @@ void build_paths(const HostIndex &ix, Derived &dv) {
         nxt[z] = path_succ(ix, dv, dummy, z);
         if (nxt[z] != kNoNode) prv[nxt[z]] = (uint32_t)z;
     }
+    if (path_link_on()) link_unitigs(ix, dv, dummy, nxt, prv);
     std::vector<uint8_t> start(n, 0), seen(n, 0);
     for (uint64_t z = 1; z < n; z++)
         if (!dummy[z] && prv[z] == kNoNode) {

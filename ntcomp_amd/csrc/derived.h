@@ -33,6 +33,9 @@ constexpr uint32_t kNoNode = 0xFFFFFFFFu;
 // Builds the path cover on the host (fills has_paths, tlen, pstream, colex_at,
 // pos_of_node, puniq); test emulation -- the upload builds the same cover on the device.
 void build_paths(const HostIndex &ix, Derived &dv);
+// the path cover links unitigs across branches (derived.cpp link_unitigs) unless
+// NTC_PATH_LINK=0; the upload's default for ctx option "path_link"
+bool path_link_on();
 // FNV-1a over the path-cover arrays (pstream, colex_at, pos_of_node, puniq) at the sizes
 // build_paths gives them: lets a test compare the device-built cover with the host one.
 inline uint64_t path_cover_hash(const uint4 *pstream, const uint32_t *colex_at, const uint32_t *pos_of_node,

@@ -2,11 +2,12 @@
 // (src/main.rs:138) and kbo::index::load_sbwt (src/main.rs:149, :190).  Like the reference,
 // encode and decode both want the two files side by side (README.md:44).  Two layouts:
 //
-// kIndexOwn (default): this library's own, all integers little-endian:
+// kIndexOwn (`--index-format own`): this library's own, all integers little-endian:
 //   .sbwt: "NTCSBWT1" u64 version=1, u64 n, u64 k, u64 C[4], u64 nwords, 4 x nwords u64
 //   .lcs : "NTCLCS01" u64 n, n bytes
 //
-// kIndexSbwtRs: a RESTATEMENT of sbwt 0.3.11 / kbo 0.5.1 serialisation [ext, recalled --
+// kIndexSbwtRs (the default since round 5, as the reference always writes this layout,
+// main.rs:138): a RESTATEMENT of sbwt 0.3.11 / kbo 0.5.1 serialisation [ext, recalled --
 // PARITY UNPINNED: neither crate nor any reference-written index exists offline, so this
 // layout is written from memory of the published crates and may differ from theirs].
 // Built on simple-sds conventions (every integer a little-endian u64 word):
@@ -21,11 +22,26 @@
 //           (first character most significant) its colex interval as u64 start, u64 end
 //           ([0, 0) when absent; p = 0: the single range [0, n))
 //   .lcs  = IntVector of n entries, width = bits of k
-// Written with every Option None; read tolerantly (Options are skipped by their size).
-// load_index detects the layout from the first 8 bytes.
+// The reference builds its index with build_select = true (main.rs:118-119): sbwt's
+// SubsetMatrix rows carry rank support (always: the search needs it) and select support
+// (access_kmer, which the reference's decode calls, lib.rs:258, 286, 291), no select_zero.
+// So each row is written with Some(rank), Some(select), None, as restated from simple-sds
+// 0.3 [ext, recalled, unpinned]:
+//   RankSupport   = Vec<(u64, u64)>: per 512-bit superblock (ones before it, the cumulative
+//                   ones before each of its words 1..7 as 9-bit fields, word j at bit 9 (j-1))
+//   SelectSupport = Vec<(u64, u64)> samples, IntVector long, IntVector short: the ones in
+//                   superblocks of 4096; per superblock (position of its first one, offset):
+//                   a superblock spanning more than 2^16 bits is "long" and lists every one's
+//                   position in long (width = bits of the vector length, offset into long);
+//                   else short holds, per block of 64 ones, the block's first one relative to
+//                   the superblock's first (16 bits, offset into short).
+// Read tolerantly: Options are skipped by their size, Some or None, so files with or without
+// the supports load.  load_index detects the layout from the first 8 bytes.
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "ntc_internal.h"
 
@@ -86,6 +102,72 @@ bool skip_option(FILE *f) {
     return rd64(f, sz) && (sz == 0 || std::fseek(f, (long)(sz * 8), SEEK_CUR) == 0);
 }
 
+// simple-sds IntVector body: len, width, RawVector of the packed fields
+void int_vector(const std::vector<uint64_t> &v, uint64_t width, std::vector<uint64_t> &out) {
+    std::vector<uint64_t> packed((v.size() * width + 63) / 64, 0);
+    for (uint64_t i = 0; i < v.size(); i++) {
+        const uint64_t bit = i * width, x = width == 64 ? v[i] : v[i] & ((1ULL << width) - 1);
+        packed[bit >> 6] |= x << (bit & 63);
+        if ((bit & 63) + width > 64) packed[(bit >> 6) + 1] |= x >> (64 - (bit & 63));
+    }
+    out.push_back(v.size());
+    out.push_back(width);
+    out.push_back(v.size() * width);
+    out.push_back(packed.size());
+    out.insert(out.end(), packed.begin(), packed.end());
+}
+
+// RankSupport words (see the header) of an n-bit row
+std::vector<uint64_t> rank_support(const uint64_t *w, uint64_t n) {
+    const uint64_t nw = (n + 63) / 64, sb = (nw + 7) / 8;
+    std::vector<uint64_t> out{sb};
+    uint64_t before = 0;
+    for (uint64_t s = 0; s < sb; s++) {
+        uint64_t rel = 0, in = 0;
+        for (uint64_t j = 0; j < 8 && 8 * s + j < nw; j++) {
+            if (j) rel |= in << (9 * (j - 1));
+            in += (uint64_t)__builtin_popcountll(w[8 * s + j]);
+        }
+        out.push_back(before);
+        out.push_back(rel);
+        before += in;
+    }
+    return out;
+}
+
+// SelectSupport words (see the header) of an n-bit row
+std::vector<uint64_t> select_support(const uint64_t *w, uint64_t n) {
+    constexpr uint64_t kSuper = 4096, kLongBits = 1ULL << 16, kBlock = 64;
+    std::vector<uint64_t> ones;
+    const uint64_t nw = (n + 63) / 64;
+    for (uint64_t i = 0; i < nw; i++)
+        for (uint64_t x = w[i]; x; x &= x - 1) ones.push_back(64 * i + (uint64_t)__builtin_ctzll(x));
+    uint64_t width = 1;
+    while (width < 64 && (1ULL << width) < n) width++;
+    std::vector<uint64_t> samples, lng, shrt;
+    for (uint64_t a = 0; a < ones.size(); a += kSuper) {
+        const uint64_t b = std::min<uint64_t>(ones.size(), a + kSuper);
+        if (ones[b - 1] - ones[a] + 1 > kLongBits) {
+            samples.push_back(ones[a]);
+            samples.push_back(lng.size());
+            lng.insert(lng.end(), ones.begin() + (long)a, ones.begin() + (long)b);
+        } else {
+            samples.push_back(ones[a]);
+            samples.push_back(shrt.size());
+            for (uint64_t i = a; i < b; i += kBlock) shrt.push_back(ones[i] - ones[a]);
+        }
+    }
+    std::vector<uint64_t> out{samples.size() / 2};
+    out.insert(out.end(), samples.begin(), samples.end());
+    int_vector(lng, width, out);
+    int_vector(shrt, 16, out);
+    return out;
+}
+
+bool wr_option(FILE *f, const std::vector<uint64_t> &body) {  // Some(T): size in words, then T
+    return wr64(f, body.size()) && wr(f, body.data(), body.size() * 8);
+}
+
 bool save_sbwt_rs(const HostIndex &ix, const std::string &prefix, std::string &err) {
     {
         File f(prefix + ".sbwt", "wb");
@@ -95,8 +177,10 @@ bool save_sbwt_rs(const HostIndex &ix, const std::string &prefix, std::string &e
         for (int c = 0; c < 4 && ok; c++) {
             uint64_t ones = 0;
             for (uint64_t x : ix.rows[c]) ones += (uint64_t)__builtin_popcountll(x);
-            ok = wr64(f.f, ones) && wr_raw(f.f, ix.rows[c].data(), ix.n) && wr64(f.f, 0) && wr64(f.f, 0) &&
-                 wr64(f.f, 0);
+            // Some(rank), Some(select), None(select_zero): build_select = true (main.rs:119)
+            ok = wr64(f.f, ones) && wr_raw(f.f, ix.rows[c].data(), ix.n) &&
+                 wr_option(f.f, rank_support(ix.rows[c].data(), ix.n)) &&
+                 wr_option(f.f, select_support(ix.rows[c].data(), ix.n)) && wr64(f.f, 0);
         }
         ok = ok && wr64(f.f, 4);
         for (int c = 0; c < 4 && ok; c++) ok = wr64(f.f, ix.C[c]);

@@ -266,6 +266,11 @@ void launch_path_edges(const PathArgs &a, uint32_t *prv, hipStream_t s);
 // list ranking by pointer jumping: st[z] = {start node, distance, min node on the way, 0};
 // returns the buffer (a or b) holding the result
 uint4 *launch_path_rank(const uint32_t *prv, uint32_t n, uint4 *a, uint4 *b, hipStream_t s);
+// unitig linking (derived.cpp link_unitigs): st = the ranking of the unitig edges in prv,
+// len[start] = unitig lengths (launch_path_lengths), want preset to all ones, best_pred to
+// all ones (64-bit); adds the chosen t -> y edges to prv
+void launch_path_link(const PathArgs &a, const uint4 *st, const uint32_t *len, uint32_t *want,
+                      unsigned long long *best_pred, uint32_t *prv, hipStream_t s);
 // fork blocks after each path end (k >= kForkBlockMinK), after launch_path_place
 void launch_path_forks(const PathArgs &a, const uint4 *st, const uint32_t *len, const uint64_t *base,
                        const uint32_t *pos_of_node, const uint4 *pstream, uint32_t *colex_at, hipStream_t s);

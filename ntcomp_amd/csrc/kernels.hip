@@ -1086,6 +1086,54 @@ __global__ __launch_bounds__(256) void k_path_edges(PathArgs a, uint32_t *prv) {
     if (!path_dummy(a.dummy, y)) prv[y] = z;
 }
 
+// ---- unitig linking (derived.cpp link_unitigs, in parallel) ------------------------------
+// After k_path_edges + one ranking (st) and the unitig lengths (len[start]): each unitig's
+// last node t names its preferred successor y (a unitig's first node; the shortest unitig,
+// then the smallest node) and offers itself to every successor y with the key (its unitig's
+// length, t), kept by a 64-bit atomicMin; t -> y becomes a path edge when both choose each
+// other.  Nodes on pure cycles (their rank reached no start) take no part, as on the host.
+__global__ __launch_bounds__(256) void k_link_want(PathArgs a, const uint4 *st, const uint32_t *prv,
+                                                   const uint32_t *len, uint32_t *want,
+                                                   unsigned long long *best_pred) {
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    if (t == 0 || t >= a.n || path_dummy(a.dummy, t)) return;
+    const uint4 e = st[t];
+    if (prv[e.x] != 0xFFFFFFFFu) return;  // on a cycle
+    const uint32_t L = len[e.x];
+    if (e.y + 1 != L) return;  // not its unitig's last node
+    uint32_t h = t;
+    while (h > 0 && a.lcs[h] >= a.k - 1) h--;  // the (k-1)-suffix group's first node holds the labels
+    const unsigned long long mine = (unsigned long long)L << 32 | t;
+    unsigned long long best = ~0ull;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const uint2 w = a.rank[(uint64_t)c * a.rwords + (h >> 5)];
+        if (!((w.y >> (h & 31)) & 1u)) continue;
+        const uint32_t y = rank_word(w, h);
+        if (path_dummy(a.dummy, y) || prv[y] != 0xFFFFFFFFu) continue;
+        const unsigned long long ky = (unsigned long long)len[y] << 32 | y;  // y starts its unitig
+        best = ky < best ? ky : best;
+        atomicMin(best_pred + y, mine);
+    }
+    if (best != ~0ull) want[t] = (uint32_t)best;
+}
+
+__global__ __launch_bounds__(256) void k_link_apply(const uint4 *st, const uint32_t *len, const uint32_t *want,
+                                                    const unsigned long long *best_pred, uint32_t n, uint32_t *prv) {
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= n) return;
+    const uint32_t y = want[t];
+    if (y == 0xFFFFFFFFu) return;
+    if (best_pred[y] == ((unsigned long long)len[st[t].x] << 32 | t)) prv[y] = t;  // one winner per y
+}
+
+void launch_path_link(const PathArgs &a, const uint4 *st, const uint32_t *len, uint32_t *want,
+                      unsigned long long *best_pred, uint32_t *prv, hipStream_t s) {
+    hipLaunchKernelGGL(k_link_want, grid_for(a.n), dim3(256), 0, s, a, st, (const uint32_t *)prv, len, want, best_pred);
+    hipLaunchKernelGGL(k_link_apply, grid_for(a.n), dim3(256), 0, s, st, len, (const uint32_t *)want,
+                       (const unsigned long long *)best_pred, a.n, prv);
+}
+
 __global__ __launch_bounds__(256) void k_path_rank_init(const uint32_t *prv, uint32_t n, uint4 *st) {
     const uint32_t z = blockIdx.x * 256u + threadIdx.x;
     if (z >= n) return;

@@ -73,6 +73,126 @@ def test_index_sbwt_rs_layout_round_trip(tmp_path, k):
         assert np.array_equal(x.lcs, ix.lcs)
 
 
+def _words_from(blob, off):
+    return np.frombuffer(blob[off:off + (len(blob) - off) // 8 * 8], dtype="<u8")
+
+
+def _read_rows(blob):
+    L = int.from_bytes(blob[:8], "little")
+    w = _words_from(blob, 8 + L)
+    pos, rows = 0, []
+    for _ in range(4):
+        ones, bits, nw = int(w[pos]), int(w[pos + 1]), int(w[pos + 2])
+        words = w[pos + 3:pos + 3 + nw]
+        pos += 3 + nw
+        opts = []
+        for _ in range(3):
+            sz = int(w[pos])
+            opts.append(None if sz == 0 else w[pos + 1:pos + 1 + sz].copy())
+            pos += 1 + sz
+        rows.append((ones, bits, words.copy(), opts))
+    return rows, w, pos
+
+
+def _unpack(words, n, width):
+    v = np.zeros(n, dtype=np.uint64)
+    for i in range(n):
+        b = i * width
+        x = int(words[b >> 6]) >> (b & 63)
+        if (b & 63) + width > 64:
+            x |= int(words[(b >> 6) + 1]) << (64 - (b & 63))
+        v[i] = x & ((1 << width) - 1)
+    return v
+
+
+@pytest.mark.parametrize("k,sparse", [(15, False), (31, False), (31, True)])
+def test_sbwt_rs_rows_carry_rank_and_select(tmp_path, k, sparse):
+    """The reference builds with build_select = true (main.rs:118-119) and its decode calls
+    access_kmer, which needs select (lib.rs:258, 286, 291): each subset-matrix row is written
+    with Some(rank support), Some(select support), None(select_zero) [simple-sds, ext,
+    recalled, unpinned].  Checked by an independent reader: the rank samples equal the ones
+    before each 512-bit superblock and the 9-bit in-superblock counts, select answers every
+    one's position from its superblock sample + block sample, and the file loads back."""
+    g = nt.synth_genome(77 + k, 300_000)
+    if sparse:  # T in ~0.3 % of positions: row T's superblocks of 4096 ones span > 2^16 bits ("long")
+        rng = np.random.default_rng(k)
+        g = np.frombuffer(b"ACG", np.uint8)[rng.integers(0, 3, 600_000)]
+        g[rng.integers(0, len(g), 2000)] = ord("T")
+    ix = nt.Index.build([g.tobytes()], k, add_revcomp=not sparse)
+    ix.save(tmp_path / "a", layout="sbwt-rs")
+    rows, _, _ = _read_rows((tmp_path / "a.sbwt").read_bytes())
+    n_long = 0
+    for c, (ones, bits, words, (rank, sel, selz)) in enumerate(rows):
+        assert bits == ix.n and np.array_equal(words, ix.rows[c][:len(words)])
+        assert rank is not None and sel is not None and selz is None, c
+        row = np.unpackbits(words.view(np.uint8), bitorder="little")[:bits].astype(np.int64)
+        assert ones == int(row.sum())
+        # rank: Vec<(u64, u64)> of ceil(words / 8) superblocks
+        nsb = int(rank[0])
+        assert nsb == (len(words) + 7) // 8 and len(rank) == 1 + 2 * nsb
+        wc = np.array([bin(int(x)).count("1") for x in words], dtype=np.int64)
+        for s in range(nsb):
+            assert int(rank[1 + 2 * s]) == int(wc[:8 * s].sum())
+            for j in range(1, 8):
+                if 8 * s + j < len(words):
+                    assert (int(rank[2 + 2 * s]) >> (9 * (j - 1))) & 511 == int(wc[8 * s:8 * s + j].sum())
+        # select: samples, long IntVector, short IntVector
+        ns = int(sel[0])
+        samples = sel[1:1 + 2 * ns].reshape(-1, 2)
+        p = 1 + 2 * ns
+        ln, lw, _, lnw = (int(x) for x in sel[p:p + 4])
+        lvals = _unpack(sel[p + 4:p + 4 + lnw], ln, lw)
+        p += 4 + lnw
+        sn, sw, _, snw = (int(x) for x in sel[p:p + 4])
+        assert sw == 16 and p + 4 + snw == len(sel)
+        svals = _unpack(sel[p + 4:p + 4 + snw], sn, sw)
+        pos1 = np.flatnonzero(row)
+        assert ns == (len(pos1) + 4095) // 4096
+        for i in range(0, len(pos1), 997):  # select(i) for a sample of ones
+            first, off = (int(x) for x in samples[i // 4096])
+            a = i // 4096 * 4096
+            assert first == pos1[a]
+            b = min(len(pos1), a + 4096)
+            if pos1[b - 1] - pos1[a] + 1 > 1 << 16:
+                assert lvals[off + i - a] == pos1[i]
+                n_long += 1
+            else:  # the block's first one, then a scan of the row
+                bs = first + int(svals[off + (i - a) // 64])
+                assert bs == pos1[a + (i - a) // 64 * 64]
+    assert (n_long > 0) == sparse
+    b = nt.Index.load(tmp_path / "a")
+    assert all(np.array_equal(x, y) for x, y in zip(b.rows, ix.rows)) and np.array_equal(b.lcs, ix.lcs)
+
+
+def test_sbwt_rs_reader_skips_options_of_any_size(tmp_path):
+    """The reader skips each row's Options by their size: a hand-built file with all three
+    Some (select_zero too, arbitrary payloads) and one with all three None load the same."""
+    import struct
+    g = nt.synth_genome(3, 20_000)
+    ix = nt.Index.build([g.tobytes()], 21)
+    ix.save(tmp_path / "a", layout="sbwt-rs")
+    blob = (tmp_path / "a.sbwt").read_bytes()
+    L = int.from_bytes(blob[:8], "little")
+    head, body = blob[:8 + L], blob[8 + L:]
+    rows, w, end = _read_rows(blob)
+    for variant in ("all_some", "all_none"):
+        out = bytearray(head)
+        for ones, bits, words, opts in rows:
+            out += struct.pack("<QQQ", ones, bits, len(words)) + words.tobytes()
+            for j, o in enumerate(opts):
+                if variant == "all_none":
+                    out += struct.pack("<Q", 0)
+                else:
+                    pay = o if o is not None else np.arange(5 + j, dtype="<u8")
+                    out += struct.pack("<Q", len(pay)) + pay.astype("<u8").tobytes()
+        out += body[end * 8:]
+        (tmp_path / f"{variant}.sbwt").write_bytes(bytes(out))
+        (tmp_path / f"{variant}.lcs").write_bytes((tmp_path / "a.lcs").read_bytes())
+        b = nt.Index.load(tmp_path / variant)
+        assert (b.n, b.k) == (ix.n, ix.k)
+        assert all(np.array_equal(x, y) for x, y in zip(b.rows, ix.rows)) and np.array_equal(b.lcs, ix.lcs)
+
+
 @pytest.mark.parametrize("k,p", [(7, 1), (7, 3), (15, 4), (31, 5)])
 def test_prefix_table_equals_search_by_definition(k, p):
     """-p/--prefix-precalc (src/cli.rs:46): every p-mer's colex interval (sbwt's

@@ -341,6 +341,10 @@ def test_cli_build_writes_sbwt_rs_layout_by_default(tmp_path):
         assert (tmp_path / ("n" + ext)).read_bytes() == (tmp_path / ("p" + ext)).read_bytes(), ext
     assert (tmp_path / "n.sbwt").read_bytes()[:8] != b"NTCSBWT1"
     assert (tmp_path / "own.sbwt").read_bytes()[:8] == b"NTCSBWT1"
+    # build_select = true (main.rs:118-119): every row carries rank and select, not select_zero
+    from test_builder import _read_rows
+    for _, _, _, (rank, sel, selz) in _read_rows((tmp_path / "n.sbwt").read_bytes())[0]:
+        assert rank is not None and len(rank) > 0 and sel is not None and len(sel) > 0 and selz is None
     a, b = nt.Index.load(str(tmp_path / "n")), nt.Index.load(str(tmp_path / "own"))
     assert a.prefix_table()[0] == 8 and a.k == b.k == 31 and a.n == b.n
     assert all(np.array_equal(x, y) for x, y in zip(a.rows, b.rows)) and np.array_equal(a.lcs, b.lcs)

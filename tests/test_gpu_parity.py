@@ -384,20 +384,32 @@ def test_gpu_long_reads(ctx):
     assert np.array_equal(out, bases) and np.array_equal(o2, offs)
 
 
-def test_gpu_path_cover_equals_host_cover(ctx):
-    """ntc_index_upload builds the path cover on the device (list ranking, cycle cuts);
-    it must be the host build_paths cover byte for byte (the one the emulation tests run)."""
+@pytest.mark.parametrize("link", [1, 0])
+def test_gpu_path_cover_equals_host_cover(ctx, monkeypatch, link):
+    """ntc_index_upload builds the path cover on the device (list ranking, cycle cuts, and
+    with path_link the unitigs linked across branches: k_link_want / k_link_apply); it must
+    be the host build_paths cover byte for byte (the one the emulation tests run), on single
+    genomes, repeats, cycles and strain collections (where the linking changes the cover)."""
     from emu_lib import emu_path_cover
+    monkeypatch.setenv("NTC_PATH_LINK", str(link))
     g = nt.synth_genome(44, 60_000).tobytes()
+    gg = nt.synth_genome(45, 40_000)
+    st = nt.synth_strains(gg, 5, 40, 2000)
+    coll = [gg.tobytes()] + [st[i].tobytes() for i in range(40)]
     cases = [([g], 31), ([g], 91), ([g[:20_000]], 7), ([b"ACGGTCATTC" * 20, b"TTGACCAGGATC" * 15, g[:3000]], 31),
-             ([(g[:500] * 30), g[:7000]], 15), ([b"ACGTTGCA" * 100], 2), ([g[:30_000]], 255)]
-    for seqs, k in cases:
-        ix = nt.Index.build(seqs, k)
-        ctx.upload(ix)
-        h, tlen, npaths = emu_path_cover(ix.n, k, ix.rows, ix.C, ix.lcs)
-        assert ctx.get_option("path_text_len") == tlen, k
-        assert ctx.get_option("n_paths") == npaths, k
-        assert ctx.get_option("path_hash") & ((1 << 64) - 1) == h, k
+             ([(g[:500] * 30), g[:7000]], 15), ([b"ACGTTGCA" * 100], 2), ([g[:30_000]], 255), (coll, 31),
+             (coll, 91), (coll[:6], 23)]
+    ctx.set_option("path_link", link)
+    try:
+        for seqs, k in cases:
+            ix = nt.Index.build(seqs, k)
+            ctx.upload(ix)
+            h, tlen, npaths = emu_path_cover(ix.n, k, ix.rows, ix.C, ix.lcs)
+            assert ctx.get_option("path_text_len") == tlen, k
+            assert ctx.get_option("n_paths") == npaths, k
+            assert ctx.get_option("path_hash") & ((1 << 64) - 1) == h, k
+    finally:
+        ctx.set_option("path_link", 1)
 
 
 def test_gpu_host_api_splits_large_batches_into_passes(ctx):

@@ -144,6 +144,33 @@ def test_emulated_periodic_genome_cycles(k):
         assert np.array_equal(goff, eoff) and np.array_equal(got, exp)
 
 
+@pytest.mark.parametrize("k", [23, 31, 91])
+def test_emulated_linked_path_cover_strain_collection(k, monkeypatch):
+    """Unitigs linked across branches (derived.cpp link_unitigs, the default): in a strain
+    collection the shared sequence becomes a few long paths (fewer paths than unitigs), a
+    read's runs leave them at its own variants and sequencing errors, and the records are
+    the oracle's with linking on and off, with and without joint runs."""
+    from emu_lib import emu_path_cover
+    g = nt.synth_genome(21, 30_000)
+    st = nt.synth_strains(g, 6, 60, 1500)
+    texts = [g] + [st[i] for i in range(60)]
+    ix = nt.Index.build([t.tobytes() for t in texts], k)
+    monkeypatch.setenv("NTC_PATH_LINK", "0")
+    _, tlen0, np0 = emu_path_cover(ix.n, k, ix.rows, ix.C, ix.lcs)
+    monkeypatch.setenv("NTC_PATH_LINK", "1")
+    _, tlen1, np1 = emu_path_cover(ix.n, k, ix.rows, ix.C, ix.lcs)
+    assert np1 < np0 and tlen1 == tlen0 - k * (np0 - np1)  # a path takes its node count + k text positions
+    reads = nt.synth_reads(np.concatenate(texts), 8, 0, 1500, 150, 10_000)
+    offs = np.arange(0, 1500 * 150 + 1, 150, dtype=np.uint64)
+    exp, eoff = OracleIndex(ix.n, k, ix.rows, ix.C, ix.lcs).encode(reads, offs)
+    for link in ("1", "0"):
+        monkeypatch.setenv("NTC_PATH_LINK", link)
+        for joint in ("1", "0"):
+            monkeypatch.setenv("NTC_EMU_JOINT", joint)
+            got, goff = emu_encode(ix.n, k, ix.rows, ix.C, ix.lcs, reads, offs)
+            assert np.array_equal(goff, eoff) and np.array_equal(got, exp), (link, joint)
+
+
 @pytest.mark.parametrize("block", [1, 3, 7, 256])
 def test_emulated_staged_decode_block_sizes(block, monkeypatch):
     # k_dec_rec stages a block's output words in LDS and writes words shared with other
