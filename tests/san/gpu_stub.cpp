@@ -4,9 +4,17 @@
 // ntc_encode_pack_batch; ntc_encode_pack_batch = the C oracle's encode (oracle/ntcomp_oracle.c, the
 // test checker) + the host packer (ntc_pack_block); ntc_decode_fasta = the oracle's decode
 // + ">seq.N" lines.  Nothing here ships: the product path is capi.cpp + the HIP kernels.
+//
+// -DNTC_STUB_MEMO (the host-ceiling build, scripts/host_ceiling.py): each entry point keeps
+// its first result per batch shape (reads, or blocks) and answers every later call of that
+// shape with a copy of it, so the GPU stage costs one copy of its output -- what the
+// pipeline's host threads (ingest, inflate, deflate, writes) can sustain is then measured
+// with the device out of the way.  Only for inputs whose batches repeat (fixed-length reads).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -39,6 +47,41 @@ ntc_ctx *stub_ctx_new(const orc_index *ix) {
 }
 void stub_ctx_free(ntc_ctx *c) { delete c; }
 
+#ifdef NTC_STUB_MEMO
+namespace {
+struct EncMemo {
+    std::vector<ntc_block_meta> meta;
+    std::vector<uint8_t> payload;
+    uint64_t n_bases = 0;
+};
+std::mutex g_memo_mu;
+std::map<uint64_t, EncMemo> g_enc;                 // by n_reads
+std::map<uint64_t, std::vector<uint64_t>> g_unp;   // by n_blocks: the records
+std::map<uint64_t, std::string> g_text;            // by n_reads: the FASTA text
+bool enc_hit(uint64_t n_reads, uint32_t block_reads, ntc_block_meta *meta, uint8_t **payload, uint64_t *payload_bytes,
+             uint64_t *n_bases) {
+    std::lock_guard<std::mutex> g(g_memo_mu);
+    auto it = g_enc.find(n_reads);
+    if (it == g_enc.end()) return false;
+    const uint64_t nb = (n_reads + block_reads - 1) / block_reads;
+    std::memcpy(meta, it->second.meta.data(), nb * sizeof(ntc_block_meta));
+    *payload = (uint8_t *)std::malloc(it->second.payload.size() + 1);
+    std::memcpy(*payload, it->second.payload.data(), it->second.payload.size());
+    *payload_bytes = it->second.payload.size();
+    if (n_bases) *n_bases = it->second.n_bases;
+    return true;
+}
+void enc_keep(uint64_t n_reads, uint32_t block_reads, const ntc_block_meta *meta, const uint8_t *payload,
+              uint64_t payload_bytes, uint64_t n_bases) {
+    std::lock_guard<std::mutex> g(g_memo_mu);
+    EncMemo &m = g_enc[n_reads];
+    m.meta.assign(meta, meta + (n_reads + block_reads - 1) / block_reads);
+    m.payload.assign(payload, payload + payload_bytes);
+    m.n_bases = n_bases;
+}
+}  // namespace
+#endif
+
 extern "C" {
 
 const char *ntc_last_error(const ntc_ctx *ctx) { return ctx ? ctx->err.c_str() : "no context"; }
@@ -49,6 +92,9 @@ int ntc_encode_pack_batch(ntc_ctx *ctx, const uint8_t *bases, const uint64_t *of
     *payload = nullptr;
     *payload_bytes = 0;
     if (bad_read) *bad_read = -1;
+#ifdef NTC_STUB_MEMO
+    if (enc_hit(n_reads, block_reads, meta, payload, payload_bytes, nullptr)) return NTC_OK;
+#endif
     const uint64_t total = n_reads ? offs[n_reads] - offs[0] : 0;
     std::vector<uint64_t> recs(total + 1), roff(n_reads + 1);
     std::vector<uint64_t> rel(n_reads + 1);
@@ -76,11 +122,25 @@ int ntc_encode_pack_batch(ntc_ctx *ctx, const uint8_t *bases, const uint64_t *of
     *payload = (uint8_t *)std::malloc(all.size() ? all.size() : 1);
     if (!all.empty()) std::memcpy(*payload, all.data(), all.size());
     *payload_bytes = all.size();
+#ifdef NTC_STUB_MEMO
+    enc_keep(n_reads, block_reads, meta, all.data(), all.size(), total);
+#endif
     return NTC_OK;
 }
 
 int ntc_decode_fasta(ntc_ctx *ctx, const uint64_t *recs, uint64_t n_recs, uint64_t n_reads, uint64_t n_bases,
                      uint64_t first_id, uint8_t *out, uint64_t out_capacity, uint64_t *out_len) {
+#ifdef NTC_STUB_MEMO
+    {
+        std::lock_guard<std::mutex> g(g_memo_mu);
+        auto it = g_text.find(n_reads);
+        if (it != g_text.end() && it->second.size() <= out_capacity) {
+            std::memcpy(out, it->second.data(), it->second.size());
+            *out_len = it->second.size();
+            return NTC_OK;
+        }
+    }
+#endif
     std::vector<uint8_t> b(n_bases + 1);
     std::vector<uint64_t> ro(n_reads + 2);
     uint64_t got_reads = 0;
@@ -103,6 +163,10 @@ int ntc_decode_fasta(ntc_ctx *ctx, const uint64_t *recs, uint64_t n_recs, uint64
         return NTC_ERR_CAPACITY;
     }
     std::memcpy(out, text.data(), text.size());
+#ifdef NTC_STUB_MEMO
+    std::lock_guard<std::mutex> g(g_memo_mu);
+    g_text[n_reads] = text;
+#endif
     return NTC_OK;
 }
 
@@ -110,8 +174,28 @@ int ntc_decode_fasta(ntc_ctx *ctx, const uint64_t *recs, uint64_t n_recs, uint64
 int ntc_unpack_streams(ntc_ctx *ctx, const uint8_t *payload, uint64_t payload_bytes, const ntc_block_meta *metas,
                        uint64_t n_blocks, uint64_t *n_blocks_ok, uint64_t *n_reads, uint64_t *n_bases) {
     (void)payload_bytes;
-    ctx->unp.clear();
     ctx->unp_reads = ctx->unp_bases = 0;
+#ifdef NTC_STUB_MEMO
+    {
+        std::lock_guard<std::mutex> g(g_memo_mu);
+        auto it = g_unp.find(n_blocks);
+        bool clean = true;
+        for (uint64_t i = 0; i < n_blocks; i++) clean = clean && !metas[i].status;
+        if (clean && it != g_unp.end()) {
+            if (ctx->unp.data() != it->second.data()) ctx->unp = it->second;
+            for (uint64_t w : ctx->unp) {
+                const uint32_t flag = (uint32_t)(w >> 56);
+                ctx->unp_reads += flag & 1;
+                ctx->unp_bases += (flag & 2) ? (flag >> 2) : ((w >> 32) & 0xFFFFFFu);
+            }
+            *n_blocks_ok = n_blocks;
+            if (n_reads) *n_reads = ctx->unp_reads;
+            if (n_bases) *n_bases = ctx->unp_bases;
+            return NTC_OK;
+        }
+    }
+#endif
+    ctx->unp.clear();
     uint64_t ok = 0;
     std::vector<uint64_t> r;
     for (; ok < n_blocks; ok++) {
@@ -126,6 +210,12 @@ int ntc_unpack_streams(ntc_ctx *ctx, const uint8_t *payload, uint64_t payload_by
     *n_blocks_ok = ok;
     if (n_reads) *n_reads = ctx->unp_reads;
     if (n_bases) *n_bases = ctx->unp_bases;
+#ifdef NTC_STUB_MEMO
+    if (ok == n_blocks) {
+        std::lock_guard<std::mutex> g(g_memo_mu);
+        g_unp[n_blocks] = ctx->unp;
+    }
+#endif
     return NTC_OK;
 }
 
@@ -142,6 +232,9 @@ int ntc_encode_pack_fastq(ntc_ctx *ctx, const uint8_t *fastq, uint64_t bytes, ui
     *payload = nullptr;
     *payload_bytes = 0;
     if (bad_read) *bad_read = -1;
+#ifdef NTC_STUB_MEMO
+    if (enc_hit(n_reads, block_reads, meta, payload, payload_bytes, n_bases)) return NTC_OK;
+#endif
     std::vector<uint64_t> nl;
     for (uint64_t i = 0; i < bytes; i++)
         if (fastq[i] == '\n') nl.push_back(i);
