@@ -79,6 +79,9 @@ def main():
     ov = np.zeros(K, dtype=np.uint64)
     L.emu_trace_report(out.ctypes.data)
     L.emu_trace_overlap(ov.ctypes.data)
+    stp = np.zeros(K, dtype=np.uint64)
+    L.emu_trace_steps.argtypes = [ctypes.c_void_p]
+    L.emu_trace_steps(stp.ctypes.data)
     st = np.zeros(16, dtype=np.uint64)
     L.emu_stats.argtypes = [ctypes.c_void_p]
     L.emu_stats(st.ctypes.data)
@@ -88,10 +91,11 @@ def main():
     print(f"reads {n}, records/read {len(recs) / n:.2f}, k={args.k}, err_ppm={args.err_ppm}, "
           f"order {args.order}, lines counted per {args.group} reads")
     for ph, name in enumerate(["ms", "parse"]):
-        print(f"-- {name}: loads/read {req[ph].sum():.2f}, lines/read {lines[ph].sum():.2f}")
+        print(f"-- {name}: loads/read {req[ph].sum():.2f}, lines/read {lines[ph].sum():.2f}"
+              + (f", lines distinct per step (no L2 reuse across steps) {stp.sum() / n:.2f}" if ph == 0 else ""))
         for i in np.argsort(-lines[ph]):
             if req[ph][i] > 0:
-                extra = f"  (also touched by ms: {ov[i] / n:5.2f})" if ph == 1 else ""
+                extra = f"  (also touched by ms: {ov[i] / n:5.2f})" if ph == 1 else f"  per step {stp[i] / n:6.2f}"
                 print(f"   {KINDS[i]:12s} loads {req[ph][i]:7.2f}  lines {lines[ph][i]:6.2f}{extra}")
     if args.json:
         import hashlib
@@ -110,6 +114,7 @@ def main():
             "reads": n, "k": args.k, "genome_bp": args.genome_bp, "strains": args.strains,
             "err_ppm": args.err_ppm, "records_per_read": round(len(recs) / n, 4),
             "k_ms4_lines_per_read": round(float(lines[0].sum()), 4),
+            "k_ms4_step_lines_per_read": round(float(stp.sum()) / n, 4),
             "k_parse4_lines_per_read": round(float(lines[1].sum()), 4),
             "k_ms4_by_structure": {KINDS[i]: round(float(lines[0][i]), 4) for i in range(K) if lines[0][i] > 0},
             "k_parse4_by_structure": {KINDS[i]: round(float(lines[1][i]), 4) for i in range(K) if lines[1][i] > 0}}

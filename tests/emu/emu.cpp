@@ -23,7 +23,13 @@ int g_phase = -1;
 std::unordered_set<uint64_t> g_lines[2][kTrKinds];
 uint64_t g_req[2][kTrKinds], g_ltot[2][kTrKinds], g_reads;
 uint64_t g_over[kTrKinds];  // parse lines the MS phase of the same reads touched too
+// per lane step (one k_ms4 wave iteration): lines distinct within the step.  Between two
+// iterations of one lane an XCD's L2 (4 MB) sees ~14 K other lanes' lines, so a line a read
+// touches again in a later iteration is fetched again: the step count is the fetch estimate.
+std::unordered_set<uint64_t> g_step_lines;
+uint64_t g_step_ltot[kTrKinds];
 void trace_phase(int ph) { g_phase = ph; }
+void trace_step() { g_step_lines.clear(); }
 uint64_t g_group = 0, g_in_group = 0;  // NTC_TRACE_GROUP=G: distinct lines per G consecutive reads
 void trace_read_done() {
     if (g_group == 0) {
@@ -47,6 +53,11 @@ void ntc_touch(int kind, const void *p) {
     if (g_phase < 0) return;
     g_req[g_phase][kind]++;
     g_lines[g_phase][kind].insert((uint64_t)(uintptr_t)p >> 7);
+    if (g_phase == 0 && g_step_lines.insert(((uint64_t)(uintptr_t)p >> 7) * kTrKinds + kind).second) g_step_ltot[kind]++;
+}
+extern "C" void emu_trace_steps(uint64_t *out) {  // [K]: MS lines distinct per step, summed; cleared
+    for (int b = 0; b < kTrKinds; b++) out[b] = g_step_ltot[b];
+    memset(g_step_ltot, 0, sizeof g_step_ltot);
 }
 extern "C" void emu_trace_report(uint64_t *out) {  // [reads, req[2][K], lines[2][K]]
     out[0] = g_reads;
@@ -74,6 +85,7 @@ extern "C" void emu_trace_overlap(uint64_t *out) {  // [K]: parse lines also tou
 namespace {
 inline void trace_phase(int) {}
 inline void trace_read_done() {}
+inline void trace_step() {}
 }  // namespace
 #endif
 
@@ -208,20 +220,27 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
                 // staged through the ECOMB slots with entry 0 carrying the count, S secondary
                 // slots, an overflow pool reserved at the first entry past them; 8 record slots
                 // then the record pool (capi.cpp encode4_impl)
-                std::vector<uint64_t> Q(len / 32 + 3, 0);
+                // the read at its position-space offset within a 128-byte line (qo = offs[r] mod
+                // 512 characters, k_pack's layout), so that traced Q lines match the kernels'
+                std::vector<uint64_t> Qt(len / 32 + 3, 0), Qbuf((len + 512) / 32 + 3 + 16, 0);
+                uint64_t *Qa = Qbuf.data() + ((16 - (((uintptr_t)Qbuf.data() >> 3) & 15)) & 15);  // 128 B aligned
+                const uint32_t q0 = (uint32_t)(offs[r] & 511);
                 std::vector<Entry> Ed(kEntSlot), Es(emu_S), Ep(len + 8);
                 std::vector<uint4> stage((kStageSlots + 1) * 256);
                 std::vector<uint64_t> R2(kRecSlot), Rp(len + 8);
                 unsigned long long pcnt = 0, rcnt = 0, status = ~0ull;
                 uint32_t obase = 0, rbase = 0;
-                rc = pack_read(bases + offs[r], len, Q.data(), d.absent);
+                rc = pack_read(bases + offs[r], len, Qt.data(), d.absent);
+                for (uint32_t i = 0; rc == 0 && i < len; i++)
+                    Qa[(q0 + i) >> 5] |= ((Qt[i >> 5] >> (2 * (i & 31))) & 3ull) << (2 * ((q0 + i) & 31));
                 uint32_t ne = 0;
-                const MsBufs bufs{Q.data(), Es.data(), Ed.data(), 1, stage.data(), kEntSlot, emu_S, Ep.data(),
+                const MsBufs bufs{Qa, Es.data(), Ed.data(), 1, stage.data(), kEntSlot, emu_S, Ep.data(),
                                   Ep.size(), &pcnt, &obase, &status};
                 auto run = [&](auto &ms) {
                     trace_phase(0);
-                    ms.start(d, 0, len, 0, Q.data());
+                    ms.start(d, q0, len, 0, Qa);
                     for (;;) {
+                        trace_step();
                         int st = ms.step(d, bufs);
                         if (st < 0) { rc = st; break; }
                         if (st == 1) break;
@@ -250,7 +269,7 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
                 const Entry *E2 = ne2 > kEntSlot + emu_S ? Ep.data() + obase - kEntSlot - emu_S : nullptr;
                 const RecPool rp{Rp.data(), Rp.size(), &rcnt, &rbase, &status, 0};
                 if (rc == 0)
-                    rc = parse_read(d, Q.data(), 0, E1, ne2, len, R2.data(), nullptr, 1, Ed.data(), 1, pre, E2, emu_S,
+                    rc = parse_read(d, Qa, q0, E1, ne2, len, R2.data(), nullptr, 1, Ed.data(), 1, pre, E2, emu_S,
                                     &rp);
                 trace_read_done();
                 if (spill_stats && rc >= 0) {
@@ -268,7 +287,7 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
                     }
                 }
                 if (d_out && rc >= 0)
-                    read_ms(d, Q.data(), 0, E1, ne2, len, d_out + (offs[r] - offs[0]), s_out + (offs[r] - offs[0]),
+                    read_ms(d, Qa, q0, E1, ne2, len, d_out + (offs[r] - offs[0]), s_out + (offs[r] - offs[0]),
                             Ed.data(), 1, E2, emu_S);
                 if (rc >= 0) {
                     if (status != ~0ull) return NTC_ERR_CAPACITY;
