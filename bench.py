@@ -91,6 +91,7 @@ def parse_args(argv=None):
     ap.add_argument("--strains", type=int, default=10)
     ap.add_argument("--strain-snp-ppm", type=int, default=10_000)
     ap.add_argument("--strain-reads", type=int, default=10_000_000)
+    ap.add_argument("--strain-inflight", type=int, default=1, help="S91 device calls in flight (contexts)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--dry-run", action="store_true",
@@ -760,9 +761,11 @@ def main():
     if "strains" in configs:
         strains = nt.synth_strains(genome, 3, args.strains, args.strain_snp_ppm)
         texts = [genome] + [strains[i] for i in range(args.strains)]
-        index = setup_index(texts, "S", 1)
-        sctx = ctxs[:1]  # S91 runs one call at a time: two in flight measured 3 % slower (k_ms4 is
-        # already at 0.89 of the line rate there, and two persistent grids only compete)
+        # S91 calls in flight (--strain-inflight): round 5 measured two 3 % slower than one (k_ms4
+        # at 0.89 of the line rate then, two persistent grids only competing)
+        n_s = max(1, min(args.strain_inflight, len(ctxs) or 1))
+        index = setup_index(texts, "S", n_s)
+        sctx = ctxs[:n_s]
         coll = np.concatenate(texts)
         ns = args.strain_reads if world == 1 else min(args.strain_reads, n)
         fs, ns = shard_mod.read_range(rank, world, ns)

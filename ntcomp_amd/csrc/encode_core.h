@@ -20,8 +20,9 @@
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 #ifndef NTC_NT
 #define NTC_NT 17  // streaming (nontemporal) hints, bit mask: 1 table entries, 16 entry stores,
-                   // 2 exact presence bits, 4 path stream, 8 query words, 32 pair words (k_ms4),
-                   // 64 fork block entries
+                   // 2 exact presence bits, 4 path stream, 8 query words, 32 pair / window words
+                   // (k_ms4), 64 fork block entries, 128 rank words (k_ms4), 256 colex_at and
+                   // pos_of_node (k_ms4)
 #endif
 
 // Line tracing for the test-only emulator (tests/emu, -DNTC_TRACE): every index load
@@ -214,6 +215,16 @@ NTC_HD uint2 load2_stream(const uint2 *p) {
     return load2(p);
 #endif
 }
+template <int kBit>
+NTC_HD uint2 load2h(const uint2 *p) {  // load2 with the NTC_NT hint kBit
+#ifdef __HIP_DEVICE_COMPILE__
+    if constexpr ((NTC_NT & kBit) != 0) {
+        const uint64_t v = __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(p));
+        return mk2((uint32_t)v, (uint32_t)(v >> 32));
+    }
+#endif
+    return load2(p);
+}
 NTC_HD uint32_t rank_word(uint2 w, uint32_t x) {  // C[c] + rank_c(x) from x's word
     return w.x + (uint32_t)__builtin_popcount(w.y & ((1u << (x & 31)) - 1u));
 }
@@ -223,7 +234,7 @@ NTC_HD void extend(const DevIndex &ix, int c, uint32_t l, uint32_t r, uint32_t &
     const uint2 *row = ix.rank + (uint64_t)c * ix.rwords;
     NTC_TOUCH(kTrRank, row + (l >> 5));
     NTC_TOUCH(kTrRank, row + (r >> 5));
-    const uint2 a = load2(row + (l >> 5)), b = load2(row + (r >> 5));
+    const uint2 a = load2h<128>(row + (l >> 5)), b = load2h<128>(row + (r >> 5));
     nl = rank_word(a, l);
     nr = rank_word(b, r);
 }
@@ -1239,7 +1250,7 @@ struct MsLaneT {
         jy() = 0xFFFFFFFFu;
         if (ix.has_paths && r == l + 1 && d >= ix.t_jump) {
             NTC_TOUCH(kTrPon, ix.pos_of_node + l);
-            j = ix.pos_of_node[l];
+            j = ld_hint<256>(ix.pos_of_node + l);
             try_run = j != 0xFFFFFFFFu;
         }
         else if (kJoint && ix.has_paths && r > l + 1 && d >= ix.t_jump && d + 1 < ix.k) {
@@ -1288,8 +1299,8 @@ struct MsLaneT {
         if (kJoint && try_run && jy() == kJointPending) {
             NTC_TOUCH(kTrPon, ix.pos_of_node + l);
             NTC_TOUCH(kTrPon, ix.pos_of_node + r - 1);
-            j = ix.pos_of_node[l];
-            jy() = ix.pos_of_node[r - 1];
+            j = ld_hint<256>(ix.pos_of_node + l);
+            jy() = ld_hint<256>(ix.pos_of_node + r - 1);
             if (j == 0xFFFFFFFFu || jy() == 0xFFFFFFFFu) {
                 jy() = 0xFFFFFFFFu;
                 try_run = false;  // on with the extension at p
@@ -1479,8 +1490,8 @@ struct MsLaneT {
                 if (m > 0 || nohop) {
                     NTC_TOUCH(kTrColex, ix.colex_at + j + m);
                     NTC_TOUCH(kTrColex, ix.colex_at + jy() + m);
-                    l = ix.colex_at[j + m] & 0x7FFFFFFFu;
-                    r = (ix.colex_at[jy() + m] & 0x7FFFFFFFu) + 1;
+                    l = ld_hint<256>(ix.colex_at + j + m) & 0x7FFFFFFFu;
+                    r = (ld_hint<256>(ix.colex_at + jy() + m) & 0x7FFFFFFFu) + 1;
                 }
                 jy() = 0xFFFFFFFFu;
                 m = 0;  // on into the EXT block below, in this same call
@@ -1880,7 +1891,7 @@ struct MsLaneT {
         if (!covers(p + 1 - U, p)) window(b, p + 1 - U);
         if (mode == kModeBrkLong) {  // the run broke at a long p: extend from the node before p
             NTC_TOUCH(kTrColex, ix.colex_at + j);
-            l = ix.colex_at[j] & 0x7FFFFFFFu;
+            l = ld_hint<256>(ix.colex_at + j) & 0x7FFFFFFFu;
             r = l + 1;
             mode = kModeExt;
 #if !NTC_CHAIN
@@ -1903,7 +1914,7 @@ struct MsLaneT {
                 NTC_TOUCH(kTrBits, ix.pair_w + M);
                 NTC_TOUCH(kTrColex, ix.colex_at + j);
                 const uint32_t pw = ld_hint<32>(ix.pair_w + M);
-                const uint32_t v = ix.colex_at[j] & 0x7FFFFFFFu;  // node before p, for a long p
+                const uint32_t v = ld_hint<256>(ix.colex_at + j) & 0x7FFFFFFFu;  // node before p, for a long p
                 if (!((pw >> (4 + c)) & 1u)) {
                     p += 1;
                     mode = kModeScan;
@@ -1919,7 +1930,7 @@ struct MsLaneT {
             NTC_TOUCH(kTrTabU, ix.tab + tab_base(U) + key_at(p, U));
             const uint2 te = load2_stream(ix.tab + tab_base(U) + key_at(p, U));
             NTC_TOUCH(kTrColex, ix.colex_at + j);
-            const uint32_t v = ix.colex_at[j] & 0x7FFFFFFFu;  // node before p, for a long p
+            const uint32_t v = ld_hint<256>(ix.colex_at + j) & 0x7FFFFFFFu;  // node before p, for a long p
             if (!tab_long(te)) {
                 skip_short(b, te, U);
                 return p >= len ? 1 : 0;

@@ -1,8 +1,12 @@
 // Host-side internal types shared by the builder, index I/O and the C ABI.
 #pragma once
+#include <condition_variable>
 #include <cstddef>
 #include <cstdint>
+#include <functional>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace ntc {
@@ -27,6 +31,60 @@ bool save_index(const HostIndex &ix, const std::string &prefix, std::string &err
 bool load_index(const std::string &prefix, HostIndex &ix, std::string &err);  // either layout
 enum { kIndexOwn = 0, kIndexSbwtRs = 1 };  // ntc_index_save_as layouts (index_io.cpp)
 bool save_index_as(const HostIndex &ix, const std::string &prefix, int layout, std::string &err);
+
+// T - 1 helper threads that run one job at a time together with the caller (pipeline.cpp:
+// the reader's copy + scan of each batch; pgzip.cpp: the symbol conversion of each read;
+// spawning threads per batch costs ~1 ms a batch): run(f) calls f(t) on every thread,
+// t = 0 the caller, and returns when all are done.
+struct Gang {
+    std::mutex mu;
+    std::condition_variable go, done;
+    std::function<void(int)> job;
+    uint64_t gen = 0;
+    int running = 0;
+    bool stop = false;
+    std::vector<std::thread> th;
+    explicit Gang(int T) {
+        for (int t = 1; t < T; t++)
+            th.emplace_back([this, t] {
+                uint64_t seen = 0;
+                for (;;) {
+                    std::function<void(int)> j;
+                    {
+                        std::unique_lock<std::mutex> g(mu);
+                        go.wait(g, [&] { return stop || gen != seen; });
+                        if (stop) return;
+                        seen = gen;
+                        j = job;
+                    }
+                    j(t);
+                    std::lock_guard<std::mutex> g(mu);
+                    if (--running == 0) done.notify_all();
+                }
+            });
+    }
+    int size() const { return (int)th.size() + 1; }
+    void run(const std::function<void(int)> &f) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            job = f;
+            running = (int)th.size();
+            gen++;
+        }
+        go.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> g(mu);
+        done.wait(g, [&] { return running == 0; });
+    }
+    ~Gang() {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            stop = true;
+        }
+        go.notify_all();
+        for (auto &x : th) x.join();
+    }
+};
 
 }  // namespace ntc
 

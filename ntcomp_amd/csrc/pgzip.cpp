@@ -269,7 +269,25 @@ enum InfRc { kInfBoundary = 0, kInfFinal = 1, kInfError = -1, kInfLimit = -2 };
 // with realloc (no zero fill: a chunk's buffer is written once).  Every allocation holds
 // kSlack symbols past cap: a match copies 8 symbols a step, so a 258-symbol match admitted at
 // x + 262 <= cap may store up to x + 264.
+//
+// The buffers are anonymous mappings in 2 MiB units with transparent huge pages requested
+// (NTC_PGZ_THP=0: malloc/realloc): a reader keeps ~T + 4 chunk buffers of ~26 MB, and with
+// 4 KiB pages faulting them in and unmapping them at the end cost the pipeline tens of
+// milliseconds.
 constexpr size_t kSlack = 8;
+bool thp_on() {
+    static const bool on = [] {
+        const char *e = std::getenv("NTC_PGZ_THP");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
+size_t map_bytes(size_t symbols) { return (((symbols + kSlack) * 2) + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1); }
+void sym_free(uint16_t *p, size_t cap) {
+    if (!p) return;
+    if (thp_on()) munmap(p, map_bytes(cap));
+    else std::free(p);
+}
 struct Out {
     uint16_t *p = nullptr;
     size_t n = 0, cap = 0;
@@ -277,13 +295,23 @@ struct Out {
     Out() = default;
     Out(const Out &) = delete;
     Out &operator=(const Out &) = delete;
-    ~Out() { std::free(p); }
+    ~Out() { sym_free(p, cap); }
     bool reserve(size_t c) {
         if (c <= cap) return true;
-        void *q = std::realloc(p, (c + kSlack) * 2);
-        if (!q) return false;
+        if (!thp_on()) {
+            void *q = std::realloc(p, (c + kSlack) * 2);
+            if (!q) return false;
+            p = (uint16_t *)q;
+            cap = c;
+            return true;
+        }
+        const size_t nb = map_bytes(c);
+        void *q = p ? mremap(p, map_bytes(cap), nb, MREMAP_MAYMOVE)
+                    : mmap(nullptr, nb, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (q == MAP_FAILED) return false;
+        madvise(q, nb, MADV_HUGEPAGE);
         p = (uint16_t *)q;
-        cap = c;
+        cap = nb / 2 - kSlack;
         return true;
     }
 };
@@ -608,6 +636,7 @@ struct PgzReader {
     // chunk output buffers kept for reuse (fresh ones fault their pages in under the process's
     // memory-map lock, which serialised the workers)
     std::vector<std::pair<uint16_t *, size_t>> pool;
+    std::unique_ptr<Gang> conv;  // pgz_read's conversion + CRC threads
     void recycle(Chunk &c) {
         if (!c.out.p) return;
         std::lock_guard<std::mutex> g(mu);
@@ -625,15 +654,26 @@ struct PgzReader {
                          (unsigned long long)nchunks, (unsigned long long)st_chunks_ok.load(),
                          (unsigned long long)st_false.load(), st_gap_bits.load() / 8e6, st_spec_ns.load() / 1e9,
                          st_find_ns.load() / 1e9, st_wait_ns / 1e9, st_conv_ns / 1e9);
+        const auto c0 = std::chrono::steady_clock::now();
         {
             std::lock_guard<std::mutex> g(mu);
             stop = true;
         }
         cv.notify_all();
         for (auto &t : th) t.join();
-        for (auto &b : pool) std::free(b.first);
+        const auto c1 = std::chrono::steady_clock::now();
+        for (auto &b : pool) sym_free(b.first, b.second);
+        const auto c2 = std::chrono::steady_clock::now();
         if (in) munmap((void *)in, n);
         if (fd >= 0) close(fd);
+        if (std::getenv("NTC_PGZ_STATS")) {
+            const auto c3 = std::chrono::steady_clock::now();
+            auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+                return std::chrono::duration<double, std::milli>(b - a).count();
+            };
+            std::fprintf(stderr, "pgz close: join %.2f ms, free %zu buffers %.2f ms, unmap %.2f ms\n", ms(c0, c1),
+                         pool.size(), ms(c1, c2), ms(c2, c3));
+        }
     }
 
     void worker() {
@@ -924,11 +964,12 @@ int pgz_read(PgzReader *r, char *dst, size_t cap, size_t *got) {
             s.crc = crcf(0, d, s.len);
         }
     };
-    std::vector<std::thread> th;
-    const unsigned T = (unsigned)std::min<size_t>(r->T, sl.size());
-    for (unsigned t = 1; t < T; t++) th.emplace_back(work);
-    work();
-    for (auto &x : th) x.join();
+    if (sl.size() > 1) {  // the reader's conversion gang (created at the first read that needs it)
+        if (!r->conv) r->conv.reset(new Gang((int)r->T));
+        r->conv->run([&](int) { work(); });
+    } else {
+        work();
+    }
     r->st_conv_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();
     // CRC per member, in order; the pieces consumed
     size_t si = 0;

@@ -137,58 +137,6 @@ struct Batch {  // one pinned buffer of the ring
     bool busy = false;
 };
 
-// T - 1 helper threads that run one job at a time together with the caller (the reader's
-// copy + scan of each batch; spawning threads per batch costs ~1 ms a batch)
-struct Gang {
-    std::mutex mu;
-    std::condition_variable go, done;
-    std::function<void(int)> job;
-    uint64_t gen = 0;
-    int running = 0;
-    bool stop = false;
-    std::vector<std::thread> th;
-    explicit Gang(int T) {
-        for (int t = 1; t < T; t++)
-            th.emplace_back([this, t] {
-                uint64_t seen = 0;
-                for (;;) {
-                    std::function<void(int)> j;
-                    {
-                        std::unique_lock<std::mutex> g(mu);
-                        go.wait(g, [&] { return stop || gen != seen; });
-                        if (stop) return;
-                        seen = gen;
-                        j = job;
-                    }
-                    j(t);
-                    std::lock_guard<std::mutex> g(mu);
-                    if (--running == 0) done.notify_all();
-                }
-            });
-    }
-    int size() const { return (int)th.size() + 1; }
-    void run(const std::function<void(int)> &f) {
-        {
-            std::lock_guard<std::mutex> g(mu);
-            job = f;
-            running = (int)th.size();
-            gen++;
-        }
-        go.notify_all();
-        f(0);
-        std::unique_lock<std::mutex> g(mu);
-        done.wait(g, [&] { return running == 0; });
-    }
-    ~Gang() {
-        {
-            std::lock_guard<std::mutex> g(mu);
-            stop = true;
-        }
-        go.notify_all();
-        for (auto &x : th) x.join();
-    }
-};
-
 // Copy n bytes of FASTQ text into dst (16-byte aligned) and scan them on the way: the
 // newlines, and the first line inside the piece that starts with '\n' or '\r' (a blank
 // line, which the host parser skips between records; the piece's first byte is the caller's).
@@ -293,6 +241,13 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
     const int engine = o.deflate_engine;
     ntc_pipeline_stats S{};
     const auto t0 = Clock::now();
+    // NTC_PIPE_TRACE=n: the first n batches' (and blocks') events on stderr, ms from the start
+    const char *etr = std::getenv("NTC_PIPE_TRACE");
+    const uint64_t etrace_n = etr ? (uint64_t)std::atoll(etr) : 0;
+    auto etrace = [&](const char *what, uint64_t b) {
+        if (b < etrace_n) std::fprintf(stderr, "[pipe] %8.3f ms %s %llu\n", 1e3 * secs(t0, Clock::now()), what,
+                                       (unsigned long long)b);
+    };
 
     ntc_fastx *fx = nullptr;
     int rc = ntc_fastx_open(in_path, &fx);
@@ -382,7 +337,7 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
     // input left, -1 = hand over to the host parser (a blank line before the cut, a line
     // count that is not a multiple of 4 at the end, a block too large for one call), -2 = the
     // decoder failed
-    auto fill_text = [&](Gang &gang, Batch &b, bool &eof) -> int {
+    auto fill_text = [&](ntc::Gang &gang, Batch &b, bool &eof) -> int {
         const uint64_t kMaxText = (1ull << 32) - (64u << 20);  // ntc_encode_pack_fastq takes < 4 GiB
         uint64_t want_cap = (uint64_t)((double)per_batch * rec_bytes * 1.03) + (256u << 10);
         std::vector<FqScan> sc;
@@ -488,7 +443,7 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
         int prev = -1;
         uint64_t carry = 0;  // reads at the tail of ring[prev] past its processed blocks
         bool as_text = text != nullptr || streamed;
-        std::unique_ptr<Gang> gang(as_text ? new Gang(RT) : nullptr);
+        std::unique_ptr<ntc::Gang> gang(as_text ? new ntc::Gang(RT) : nullptr);
         for (;;) {
             int bi;
             {
@@ -512,6 +467,7 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
                     next_read += b.n_process;
                     next_block += (b.n_process + BR - 1) / BR;
                     text_batches++;
+                    etrace("read batch", batch_no);
                     {
                         std::lock_guard<std::mutex> g(sh.mu);
                         b.busy = true;
@@ -662,6 +618,7 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
                     return;
                 }
                 std::shared_ptr<uint8_t> pl(payload, ntc_buffer_free);
+                etrace("gpu done, first block", b.first_block);
                 std::lock_guard<std::mutex> g(sh.mu);
                 S.gpu_done_s = secs(t0, Clock::now());
                 S.bases += b.is_text ? nb : b.offs[b.n_process] - b.offs[0];
@@ -762,6 +719,7 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
         }
         for (int q = 0; q < 4; q++) ntc_buffer_free(out.part[q]);
         add_time(t_write, secs(tw, Clock::now()));
+        etrace("written block", blk);
     }
     {
         std::lock_guard<std::mutex> g(sh.mu);
@@ -770,9 +728,11 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
         }
         sh.cv.notify_all();
     }
+    etrace("all written", 0);
     reader.join();
     for (auto &t : gpus) t.join();
     for (auto &t : pool) t.join();
+    etrace("threads joined", 0);
     for (auto &kv : done)
         for (int q = 0; q < 4; q++) ntc_buffer_free(kv.second.part[q]);
     for (auto &b : ring) {
@@ -780,7 +740,9 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
         pinned_free(b.offs);
         pinned_free(b.text);
     }
+    etrace("buffers freed", 0);
     ntc_fastx_close(fx);
+    etrace("input closed", 0);
     const int result = sh.error == -1 ? NTC_OK : sh.error;
     S.alloc_s += t_pin.load();
     S.parse_s = t_parse.load();
