@@ -1492,6 +1492,14 @@ struct MsLaneT {
                     NTC_TOUCH(kTrColex, ix.colex_at + jy() + m);
                     l = ld_hint<256>(ix.colex_at + j + m) & 0x7FFFFFFFu;
                     r = (ld_hint<256>(ix.colex_at + jy() + m) & 0x7FFFFFFFu) + 1;
+#if defined(NTC_STATS) && !defined(__HIP_DEVICE_COMPILE__)
+                    if (p < len) {  // (emulator census) the stop's first/last node: edge of the read's character?
+                        const int c = (int)((Q[(qo + p) >> 5] >> (2 * ((qo + p) & 31))) & 3u);
+                        const bool el = (ix.rank[(uint64_t)c * ix.rwords + (l >> 5)].y >> (l & 31)) & 1u;
+                        const bool er = (ix.rank[(uint64_t)c * ix.rwords + ((r - 1) >> 5)].y >> ((r - 1) & 31)) & 1u;
+                        NTC_STAT(el && er ? 8 : (el || er ? 9 : 10));
+                    }
+#endif
                 }
                 jy() = 0xFFFFFFFFu;
                 m = 0;  // on into the EXT block below, in this same call
@@ -1507,6 +1515,13 @@ struct MsLaneT {
                 }
                 gj = j;
                 ge = p;
+#if defined(NTC_STATS) && !defined(__HIP_DEVICE_COMPILE__)
+                {  // (emulator census) the node before the break: edge of the read's character?
+                    const uint32_t v = ix.colex_at[j] & 0x7FFFFFFFu;
+                    const int c = (int)((Q[(qo + p) >> 5] >> (2 * ((qo + p) & 31))) & 3u);
+                    NTC_STAT(((ix.rank[(uint64_t)c * ix.rwords + (v >> 5)].y >> (v & 31)) & 1u) ? 11 : 12);
+                }
+#endif
                 // the run broke at p (mostly a sequencing error): table first
                 window(b, p + 1 - U);
                 mode = kModeBrk;
