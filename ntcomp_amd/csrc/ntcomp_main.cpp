@@ -13,6 +13,7 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <ctime>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -409,6 +410,11 @@ int main(int argc, char **argv) {
         usage();
         return 2;
     }
+    if (std::getenv("NTC_INIT_TRACE")) {  // the wall-clock instant main starts (after the loader)
+        struct timespec ts;
+        clock_gettime(CLOCK_REALTIME, &ts);
+        std::fprintf(stderr, "[init] main at %.6f\n", ts.tv_sec + 1e-9 * ts.tv_nsec);
+    }
     const std::string cmd = argv[1];
     if (cmd == "-h" || cmd == "--help" || cmd == "help") {
         usage(stdout);
@@ -427,8 +433,16 @@ int main(int argc, char **argv) {
         // teardown.  Exiting with the contexts alive cost more (wall clock after main 0.10-0.13 s
         // against 0.05-0.08 s with them freed first, 10 M-read encode, scripts/exit_cost.py).
         std::fflush(stdout);
+        const bool itr = std::getenv("NTC_INIT_TRACE") != nullptr;
+        const auto te = Clock::now();
         for (auto *c : g_ctxs) ntc_ctx_destroy(c);
         ntc_index_free(g_ix);
+        if (itr) {  // the exit timeline: contexts freed, then the wall-clock instant of _exit
+            struct timespec ts;
+            clock_gettime(CLOCK_REALTIME, &ts);
+            std::fprintf(stderr, "[exit] contexts freed in %.3f ms; _exit at %.6f\n", 1e3 * since(te),
+                         ts.tv_sec + 1e-9 * ts.tv_nsec);
+        }
         std::fflush(stderr);
         if (std::getenv("NTC_CLEAN_EXIT")) return rc;  // exit handlers run (a profiler writes its trace there)
         _exit(rc);
