@@ -783,10 +783,34 @@ NTC_HD void tab_ds(const DevIndex &ix, const uint64_t *Q, uint64_t qo, uint32_t 
     s = e.x;
 }
 
-// consecutive set bits at positions a, a-1, ... (at most maxn) of bitvector w
+// consecutive set bits at positions a, a-1, ... (at most maxn) of bitvector w.  The word
+// holding a and the one below it are loaded together (NTC_ONES_PAIR): a run that crosses
+// into the lower word (C31: up to ~100 positions of d = k per record) then costs one
+// round trip instead of two dependent ones.
+#ifndef NTC_ONES_PAIR
+#define NTC_ONES_PAIR 1
+#endif
 NTC_HD uint32_t ones_down(const uint64_t *w, uint32_t a, uint32_t maxn) {
     uint32_t cnt = 0;
     int64_t pos = a;
+#if NTC_ONES_PAIR
+    {
+        const uint32_t wi = (uint32_t)(pos >> 6), b = (uint32_t)(pos & 63);
+        NTC_TOUCH(kTrPuniq, w + wi);
+        const uint64_t hiw = w[wi], low = w[wi > 0 ? wi - 1 : 0];  // both issued before either is used
+        const uint64_t x = ~hiw << (63 - b);
+        const uint32_t z = x ? (uint32_t)__builtin_clzll(x) : 64u;
+        if (z <= b || wi == 0 || maxn <= b + 1) return (z <= b ? z : b + 1) < maxn ? (z <= b ? z : b + 1) : maxn;
+        NTC_TOUCH(kTrPuniq, w + wi - 1);
+        cnt = b + 1;
+        const uint64_t y = ~low;
+        const uint32_t z2 = y ? (uint32_t)__builtin_clzll(y) : 64u;
+        if (z2 < 64) { cnt += z2; return cnt < maxn ? cnt : maxn; }
+        cnt += 64;
+        pos -= b + 1 + 64;
+        if (pos < 0) return cnt < maxn ? cnt : maxn;
+    }
+#endif
     while (cnt < maxn) {
         const uint32_t wi = (uint32_t)(pos >> 6), b = (uint32_t)(pos & 63);
         NTC_TOUCH(kTrPuniq, w + wi);
@@ -878,6 +902,7 @@ struct EntryView {
         int32_t hi = e;
         Entry eg{0, 0, 0, 0};
         bool have = false;
+
         while (hi - g > 1) {
             const int32_t mid = (g + hi) >> 1;
             const Entry em = at(mid);

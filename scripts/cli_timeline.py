@@ -29,6 +29,10 @@ def main():
     cmd, idx, inp = args[:3]
     env = dict(os.environ, NTC_INIT_TRACE="1")
     for _ in range(reps):
+        # a fresh output file, as scripts/e2e_bench.py does: truncating the previous run's
+        # output makes ext4 (auto_da_alloc) start its writeback at the last close
+        if os.path.exists("/tmp/ntc_cli_timeline.out"):
+            os.unlink("/tmp/ntc_cli_timeline.out")
         t0 = time.time()
         with open("/tmp/ntc_cli_timeline.out", "wb") as f:
             r = subprocess.run([BIN, cmd, "-i", idx, inp, "--stats", *extra], stdout=f, stderr=subprocess.PIPE, env=env)
