@@ -94,7 +94,7 @@ struct ntc_ctx {
         uint64_t n_reads, total_bases, cap;
         uint64_t *rec_out, *rec_offs;
     } call4{};
-    uint32_t ent_slots_opt = 0;     // secondary entry slots per read (0: auto, 24 with joint runs, else 4)
+    uint32_t ent_slots_opt = 0;     // secondary entry slots per read (0: auto, 16 with joint runs, else 4)
     double epool_per_read = 4.0;    // overflow pools: a floor per read (the test hook pool_per_read sets it)
     double rpool_per_read = 1.0;
     double epool_per_base = 0.0;    // and what the last call's reads reserved per base (learn_pool_rates)
@@ -216,8 +216,10 @@ uint32_t ent_slots(const ntc_ctx *ctx) {
     if (ctx->ent_slots_opt) return ctx->ent_slots_opt;
     // entries per read past the dense 4 (tests/emu NTC_EMU_SPILL, 1 % errors): random genome
     // k = 91 reads rarely spill (6 %, 0.07 % past 8); a strain collection with joint runs and
-    // fork hops spills on 98 % of reads, 2.6 % past 20, 0.17 % past 24
-    return ctx->has_index && ctx->dix.joint ? 20u : 4u;
+    // fork hops spills on 98 % of reads.  With the linked path cover (round 6) S91's reads
+    // have fewer run entries: 16 secondary slots measured 131.2-131.7 Gbases/s against
+    // 129.9-130.9 with 20 (3 runs each, one box); the overflow pool takes the rest
+    return ctx->has_index && ctx->dix.joint ? 16u : 4u;
 }
 
 // v4: pack -> persistent MS -> parse -> scan -> emit, all in position space.

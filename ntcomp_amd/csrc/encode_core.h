@@ -783,12 +783,14 @@ NTC_HD void tab_ds(const DevIndex &ix, const uint64_t *Q, uint64_t qo, uint32_t 
     s = e.x;
 }
 
-// consecutive set bits at positions a, a-1, ... (at most maxn) of bitvector w.  The word
-// holding a and the one below it are loaded together (NTC_ONES_PAIR): a run that crosses
-// into the lower word (C31: up to ~100 positions of d = k per record) then costs one
-// round trip instead of two dependent ones.
+// consecutive set bits at positions a, a-1, ... (at most maxn) of bitvector w.
+// NTC_ONES_PAIR=1 loads the word holding a and the one below it together, so that a run
+// crossing into the lower word (C31: up to ~100 positions of d = k per record) costs one
+// round trip instead of two dependent ones; A/B on one box (round 6, 3 runs each): C31
+// 309.7-311.7 Gbases/s with it, 309.9-310.4 without -- the parse's time is not there, so
+// it stays off.
 #ifndef NTC_ONES_PAIR
-#define NTC_ONES_PAIR 1
+#define NTC_ONES_PAIR 0
 #endif
 NTC_HD uint32_t ones_down(const uint64_t *w, uint32_t a, uint32_t maxn) {
     uint32_t cnt = 0;

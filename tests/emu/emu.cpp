@@ -199,9 +199,9 @@ extern "C" int emu_encode(const ntc_index_view *v, const uint8_t *bases, const u
     // NTC_EMU_SPILL=1: spill footprint of the v4 layout (entries past kEntSlot, records past
     // kRecSlot) -> stderr, for sizing the spill pools
     const bool spill_stats = getenv("NTC_EMU_SPILL") && atoi(getenv("NTC_EMU_SPILL"));
-    // secondary entry slots (capi.cpp ent_slots: 20 with joint runs, else 4; NTC_EMU_SLOTS overrides)
+    // secondary entry slots (capi.cpp ent_slots: 16 with joint runs, else 4; NTC_EMU_SLOTS overrides)
     const char *es_env = getenv("NTC_EMU_SLOTS");
-    const uint32_t emu_S = es_env ? (uint32_t)atoi(es_env) : (d.joint ? 20u : 4u);
+    const uint32_t emu_S = es_env ? (uint32_t)atoi(es_env) : (d.joint ? 16u : 4u);
     uint64_t sp_reads_e = 0, sp_ent = 0, sp_reads_r = 0, sp_rec = 0, sp_len_e = 0, sp_len_r = 0, sp_rem_e = 0;
     uint64_t ne_hist[9] = {0};  // reads with ne > 4 + 4 * i
     for (uint64_t t = 0; t < tiles; t++) {

@@ -31,7 +31,7 @@ def test_pools_rerun_on_a_strain_collection():
     offs = np.arange(0, n * L + 1, L, dtype=np.uint64)
     ref = nt.GpuContext(0)
     ref.upload(ix)
-    assert ref.get_option("joint") == 1 and ref.get_option("ent_slots") == 20
+    assert ref.get_option("joint") == 1 and ref.get_option("ent_slots") == 16
     exp, eoff = ref.encode(reads, offs)
     orc = OracleIndex(ix.n, 91, ix.rows, ix.C, ix.lcs)
     m = 3000
