@@ -908,7 +908,15 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
         blocks.push_back(bad ? DBlock{pos, p - pos, 0, 0, true} : DBlock{pos, p - pos, nrec, pay, false});
         pos = p;
     }
-    const uint64_t n_batches = (blocks.size() + bpb - 1) / bpb;
+    // Batch 0 holds one block when batches hold more (NTC_FIRST_BATCH_BLOCKS overrides): the
+    // writer -- the pipeline's bound, one file's page-cache writes -- starts on the first
+    // block's text instead of waiting for a whole batch's inflate, unpack and walk
+    const char *fbe = std::getenv("NTC_FIRST_BATCH_BLOCKS");
+    const uint64_t b0n = std::max<uint64_t>(1, std::min<uint64_t>(bpb, fbe ? (uint64_t)std::atoll(fbe) : 1));
+    auto batch_first = [&](uint64_t b) -> uint64_t { return b == 0 ? 0 : b0n + (b - 1) * bpb; };
+    auto batch_of = [&](uint64_t blk) -> uint64_t { return blk < b0n ? 0 : 1 + (blk - b0n) / bpb; };
+    auto batch_end = [&](uint64_t b) -> uint64_t { return std::min<uint64_t>(blocks.size(), batch_first(b + 1)); };
+    const uint64_t n_batches = blocks.empty() ? 0 : batch_of(blocks.size() - 1) + 1;
     S.alloc_s = secs(t0, Clock::now());
 
     const int NB = n_ctx + 2;
@@ -1000,11 +1008,17 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
                 uint64_t ok = 0, nr = 0, nbs = 0, len = 0, brecs = 0, bpay = 0;
                 uint8_t pay0[8] = {0}, txt[64];
                 const uint64_t rec1 = (uint64_t)(1u | 2u | (1u << 2)) << 56;  // first, short, 1 base "A"
-                for (uint64_t i = c * bpb; i < std::min<uint64_t>((c + 1) * bpb, blocks.size()); i++) {
-                    brecs += blocks[i].n_recs;
-                    bpay += blocks[i].pay;
+                // (the larger of this context's first two batches: batch 0 is one block)
+                for (uint64_t b2 = (uint64_t)c; b2 < n_batches && b2 <= (uint64_t)c + (uint64_t)n_ctx; b2 += (uint64_t)n_ctx) {
+                    uint64_t r2 = 0, p2 = 0;
+                    for (uint64_t i = batch_first(b2); i < batch_end(b2); i++) {
+                        r2 += blocks[i].n_recs;
+                        p2 += blocks[i].pay;
+                    }
+                    brecs = std::max(brecs, r2);
+                    bpay = std::max(bpay, p2);
                 }
-                // ... and the device workspaces sized for the first batch (hipMalloc'd here)
+                // ... and the device workspaces sized for the first batches (hipMalloc'd here)
                 trace("warm-up start", c);
                 const int w1 = ntc_unpack_streams(ctxs[c], pay0, 8, &m0, 1, &ok, &nr, &nbs);
                 trace("warm-up unpack", c);
@@ -1121,7 +1135,7 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
         for (uint64_t j = 0; j < (uint64_t)NB && j < n_batches; j++)
             pre.emplace_back([&, j] {
                 uint64_t nr = 0, np = 0;
-                for (uint64_t i = j * bpb; i < std::min<uint64_t>((j + 1) * bpb, blocks.size()); i++) {
+                for (uint64_t i = batch_first(j); i < batch_end(j); i++) {
                     nr += blocks[i].n_recs;
                     np += blocks[i].pay;
                 }
@@ -1149,17 +1163,17 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
                     std::unique_lock<std::mutex> g(sh.mu);
                     auto exhausted = [&] {
                         return sh.error != NTC_OK || next_task >= blocks.size() ||
-                               (stop_batch >= 0 && (int64_t)(next_task / bpb) > stop_batch);
+                               (stop_batch >= 0 && (int64_t)batch_of(next_task) > stop_batch);
                     };
                     sh.cv.wait(g, [&] {
                         if (exhausted()) return true;
-                        const uint64_t nb = next_task / bpb;
+                        const uint64_t nb = batch_of(next_task);
                         const DSlot &sl = slot_of(nb);
                         return sl.batch == nb || sl.batch == ~0ULL;
                     });
                     if (exhausted()) return;
                     blk = next_task++;
-                    b = blk / bpb;
+                    b = batch_of(blk);
                     DSlot &sl = slot_of(b);
                     first = sl.batch != b;
                     if (first) {
@@ -1173,8 +1187,8 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
                         fresh.metas.swap(sl.metas);
                         sl = std::move(fresh);
                         sl.batch = b;
-                        sl.first_block = b * bpb;
-                        sl.n_blocks = std::min<uint64_t>(bpb, blocks.size() - sl.first_block);
+                        sl.first_block = batch_first(b);
+                        sl.n_blocks = batch_end(b) - sl.first_block;
                         for (uint64_t i = 0; i < sl.n_blocks; i++) {
                             sl.n_recs += blocks[sl.first_block + i].n_recs;
                             sl.n_pay += blocks[sl.first_block + i].pay;

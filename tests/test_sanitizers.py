@@ -226,6 +226,15 @@ def test_pipelines_under_sanitizers(san, encoded, tmp_path, kind):
     got = run(san[kind], "decode", d / "idx", tmp_path / "e.dat", tmp_path / "o.fa", 4, 1, 2)
     assert int(got["rc"]) == 0, got
     assert (tmp_path / "o.fa").read_bytes() == fasta
+    # batches of 3 blocks after a first batch of one (the writer starts on the first block)
+    for fb in ("1", "2", "3"):
+        ENV["NTC_FIRST_BATCH_BLOCKS"] = fb
+        try:
+            got = run(san[kind], "decode", d / "idx", tmp_path / "e.dat", tmp_path / "o3.fa", 4, 3, 2)
+        finally:
+            del ENV["NTC_FIRST_BATCH_BLOCKS"]
+        assert int(got["rc"]) == 0 and int(got["blocks"]) == 4, (fb, got)
+        assert (tmp_path / "o3.fa").read_bytes() == fasta, fb
     if nt.libdeflate_available():
         got = run(san[kind], "encode", d / "idx", d / "r.fq", tmp_path / "l.dat", 3, 2, 1, 1)
         assert int(got["rc"]) == 0
