@@ -908,11 +908,12 @@ int ntc_decode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
         blocks.push_back(bad ? DBlock{pos, p - pos, 0, 0, true} : DBlock{pos, p - pos, nrec, pay, false});
         pos = p;
     }
-    // Batch 0 holds one block when batches hold more (NTC_FIRST_BATCH_BLOCKS overrides): the
-    // writer -- the pipeline's bound, one file's page-cache writes -- starts on the first
-    // block's text instead of waiting for a whole batch's inflate, unpack and walk
+    // NTC_FIRST_BATCH_BLOCKS=n: batch 0 holds n blocks, the others blocks_per_batch.  A
+    // one-block first batch (the writer -- the pipeline's bound -- starting sooner) measured
+    // no better on the box: the first write still came at ~20 ms, pipeline 0.160-0.198 s
+    // against 0.166-0.178 s (profiles/round6/e2e_first_batch/), so the default stays bpb.
     const char *fbe = std::getenv("NTC_FIRST_BATCH_BLOCKS");
-    const uint64_t b0n = std::max<uint64_t>(1, std::min<uint64_t>(bpb, fbe ? (uint64_t)std::atoll(fbe) : 1));
+    const uint64_t b0n = std::max<uint64_t>(1, std::min<uint64_t>(bpb, fbe ? (uint64_t)std::atoll(fbe) : bpb));
     auto batch_first = [&](uint64_t b) -> uint64_t { return b == 0 ? 0 : b0n + (b - 1) * bpb; };
     auto batch_of = [&](uint64_t blk) -> uint64_t { return blk < b0n ? 0 : 1 + (blk - b0n) / bpb; };
     auto batch_end = [&](uint64_t b) -> uint64_t { return std::min<uint64_t>(blocks.size(), batch_first(b + 1)); };
