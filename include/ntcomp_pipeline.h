@@ -54,15 +54,6 @@ typedef struct ntc_pipeline_stats {
 int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int out_fd, const ntc_pipeline_opts *opts,
                     ntc_pipeline_stats *stats);
 
-/* Optional: start opening in_path on a host thread (a single gzip member's parallel inflate
- * starts with it) while the caller creates the contexts and uploads the index; the next
- * ntc_encode_file on the same path takes the opened input over.  An open error is returned
- * by that ntc_encode_file.  ntc_encode_prefetch_drop closes a prefetched input not taken
- * over (also done by the next ntc_encode_prefetch).  No counterpart in the reference, whose
- * input is opened after the index is loaded (main.rs:141-158).                          */
-int ntc_encode_prefetch(const char *in_path);
-void ntc_encode_prefetch_drop(void);
-
 /* Reads encoded.dat at in_path (mapped), writes FASTA to out_fd (not closed): ">seq.i\n"
  * + bases + "\n" per read, i from 1 across the file (main.rs:204).  opts->threads sizes the
  * inflate pool, opts->blocks_per_batch the GPU call (<= 0: 2; batch_bases and

@@ -44,7 +44,7 @@ EXPORTED = [
     "ntc_encode_pack_fastq", "ntc_read_block_into", "ntc_read_block_streams", "ntc_unpack_streams",
     "ntc_unpacked_records", "ntc_decode_fasta_unpacked",
     "ntc_fastx_open", "ntc_fastx_next_batch", "ntc_fastx_close", "ntc_fasta_format", "ntc_fastx_next_batch_into",
-    "ntc_fastx_set_threads", "ntc_host_threads", "ntc_encode_file", "ntc_encode_prefetch", "ntc_encode_prefetch_drop", "ntc_decode_fasta",
+    "ntc_fastx_set_threads", "ntc_host_threads", "ntc_encode_file", "ntc_decode_fasta",
     "ntc_decode_file", "ntc_build_index_device", "ntc_build_index_device_ex", "ntc_index_set_prefix_precalc",
     "ntc_index_prefix_table", "ntc_index_share", "ntc_index_prepare", "ntc_index_upload_prepared", "ntc_index_prep_free",
 ]
@@ -219,8 +219,6 @@ def lib():
         "ntc_fastx_set_threads": (I, [P, I]),
         "ntc_host_threads": (I, []),
         "ntc_encode_file": (I, [P, I, ctypes.c_char_p, I, ctypes.POINTER(PipelineOpts), ctypes.POINTER(PipelineStats)]),
-        "ntc_encode_prefetch": (I, [ctypes.c_char_p]),
-        "ntc_encode_prefetch_drop": (None, []),
         "ntc_fasta_format": (I, [P, P, u64, u64, ctypes.POINTER(P), ctypes.POINTER(u64)]),
         "ntc_decode_fasta": (I, [P, P, u64, u64, u64, u64, P, u64, ctypes.POINTER(u64)]),
         "ntc_decode_file": (I, [P, I, ctypes.c_char_p, I, ctypes.POINTER(PipelineOpts), ctypes.POINTER(PipelineStats)]),
@@ -824,19 +822,6 @@ def encode_file(ctxs, in_path, out_fd, threads=0, blocks_per_batch=4, batch_base
     return _run_pipeline("ntc_encode_file", ctxs, in_path, out_fd,
                          PipelineOpts(threads, blocks_per_batch, batch_bases, DEFLATE_ENGINES[deflate],
                                       1 if host_parse else 0))
-
-
-def encode_prefetch(in_path):
-    """Open in_path on a host thread now (a single gzip member starts inflating), so that the
-    next encode_file of the same path takes it over (ntc_encode_prefetch): the CLI calls it
-    before the index load and the GPU start.  encode_prefetch_drop() closes one not taken."""
-    rc = lib().ntc_encode_prefetch(os.fsencode(in_path))
-    if rc:
-        raise NtcError(rc, "ntc_encode_prefetch")
-
-
-def encode_prefetch_drop():
-    lib().ntc_encode_prefetch_drop()
 
 
 def decode_file(ctxs, in_path, out_fd, threads=0, blocks_per_batch=2):

@@ -16,7 +16,6 @@ main.rs:138), with the -p prefix lookup table (unpinned offline -- DESIGN.md sec
 --index-format own writes this library's own layout.  encode/decode read either.
 """
 import argparse
-import os
 import sys
 
 
@@ -168,8 +167,6 @@ def cmd_encode(args):
     block packer per context, deflate on the host pool, blocks written in file order."""
     import ntcomp_amd as nt
     st = _Stats(args.stats)
-    if os.environ.get("NTC_PREFETCH", "1") != "0":  # the input opens while the index loads and the GPUs start
-        nt.encode_prefetch(args.query_file)
     log("Loading SBWT index...")
     index = st.wrap("index_load", nt.Index.load)(args.index_prefix)
     ctxs = _open_gpus(index, _devices(args), st, args.contexts_per_gpu)

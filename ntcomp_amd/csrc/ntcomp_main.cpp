@@ -217,9 +217,6 @@ int cmd_encode(const Args &a) {
     if (a.pos.size() != 1) die("encode: one query file");
     const std::string prefix = a.get("-i", "--index", "");
     if (prefix.empty()) die("encode: -i/--index is required");
-    // the input opens (a gzip member starts inflating) while the index loads and the GPUs start
-    const char *pf = std::getenv("NTC_PREFETCH");
-    if (!pf || std::atoi(pf) != 0) (void)ntc_encode_prefetch(a.pos[0].c_str());
     info("Loading SBWT index...");
     ntc_index_host *ix = nullptr;
     if (ntc_index_load(prefix.c_str(), &ix)) die("cannot load index " + prefix);

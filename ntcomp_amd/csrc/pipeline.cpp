@@ -220,73 +220,9 @@ struct Shared {
     }
 };
 
-// ntc_encode_prefetch: the input opened on a host thread while the caller starts the GPU
-// contexts (HIP runtime start + index upload, 0.15-0.27 s of a CLI encode).  A single gzip
-// member's parallel inflater starts its workers at open, so they inflate the first chunks in
-// that time; a mapped plain FASTQ can have its pages mapped (NTC_PREFETCH_POPULATE=1).
-struct Prefetch {
-    std::mutex m;
-    std::string path;
-    std::thread th;
-    ntc_fastx *fx = nullptr;
-    int rc = NTC_OK;
-    bool active = false;
-};
-Prefetch &prefetch_slot() {
-    static Prefetch *p = new Prefetch;  // never destroyed: an exit() with the open thread still running
-    return *p;                          // must not run ~thread on a joinable thread
-}
-// the prefetched input of path, its opening finished; false when there is none for path
-bool adopt_prefetch(const char *path, ntc_fastx **fx, int *rc) {
-    Prefetch &p = prefetch_slot();
-    std::lock_guard<std::mutex> g(p.m);
-    if (!p.active || p.path != path) return false;
-    if (p.th.joinable()) p.th.join();
-    *fx = p.fx;
-    *rc = p.rc;
-    p.fx = nullptr;
-    p.active = false;
-    return true;
-}
-
 }  // namespace
 
 extern "C" {
-
-int ntc_encode_prefetch(const char *in_path) {
-    if (!in_path) return NTC_ERR_INVALID_ARG;
-    ntc_encode_prefetch_drop();
-    Prefetch &p = prefetch_slot();
-    std::lock_guard<std::mutex> g(p.m);
-    p.path = in_path;
-    p.fx = nullptr;
-    p.rc = NTC_OK;
-    try {
-        p.th = std::thread([&p] {
-            p.rc = ntc_fastx_open(p.path.c_str(), &p.fx);
-            const char *pop = std::getenv("NTC_PREFETCH_POPULATE");
-            uint64_t n = 0;
-            const uint8_t *text = p.rc == NTC_OK && pop && std::atoi(pop) > 0 ? ntc::fastx_mapped(p.fx, &n) : nullptr;
-            if (text && n) {
-                const uintptr_t a0 = (uintptr_t)text & ~(uintptr_t)4095;
-                (void)madvise((void *)a0, n + ((uintptr_t)text - a0), 22 /* MADV_POPULATE_READ */);
-            }
-        });
-    } catch (...) {
-        return NTC_ERR_IO;  // no thread: the encode opens the input itself
-    }
-    p.active = true;
-    return NTC_OK;
-}
-
-void ntc_encode_prefetch_drop(void) {
-    Prefetch &p = prefetch_slot();
-    std::lock_guard<std::mutex> g(p.m);
-    if (p.th.joinable()) p.th.join();
-    if (p.fx) ntc_fastx_close(p.fx);
-    p.fx = nullptr;
-    p.active = false;
-}
 
 int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int out_fd, const ntc_pipeline_opts *opts,
                     ntc_pipeline_stats *stats) {
@@ -314,8 +250,7 @@ int ntc_encode_file(ntc_ctx *const *ctxs, int n_ctx, const char *in_path, int ou
     };
 
     ntc_fastx *fx = nullptr;
-    int rc = NTC_OK;
-    if (!adopt_prefetch(in_path, &fx, &rc)) rc = ntc_fastx_open(in_path, &fx);
+    int rc = ntc_fastx_open(in_path, &fx);
     if (rc) return rc;
     ntc_fastx_set_threads(fx, T);
     // a mapped plain FASTQ goes to the GPU as text

@@ -182,13 +182,6 @@ static int cmd_pipe(bool enc, char **a, int n) {
     ntc_pipeline_stats st{};
     int rc = 0;
     double best = 1e30;
-    // NTC_SAN_PREFETCH=1: the input prefetched (ntc_encode_prefetch) and taken over by the
-    // first encode; =2: prefetched under another spelling of its path, so never taken over
-    // and dropped at the end
-    const char *pf = std::getenv("NTC_SAN_PREFETCH");
-    const int pfm = pf ? std::atoi(pf) : 0;
-    if (enc && pfm == 1) ntc_encode_prefetch(a[1]);
-    if (enc && pfm == 2) ntc_encode_prefetch((std::string("/.") + a[1]).c_str());
     for (int rep = 0; rep <= reps; rep++) {
         const int fd = ::open(a[2], O_WRONLY | O_CREAT | O_TRUNC, 0644);
         const auto t0 = std::chrono::steady_clock::now();
@@ -205,7 +198,6 @@ static int cmd_pipe(bool enc, char **a, int n) {
                     "first_batch_s=%.4f reader_done_s=%.4f ",
                     best, st.bases / best / 1e9, st.parse_s, st.gpu_s, st.deflate_s, st.write_s, st.alloc_s,
                     st.first_batch_s, st.reader_done_s);
-    ntc_encode_prefetch_drop();
     for (auto *c : ctxs) stub_ctx_free(c);
     orc_index_free(o);
     std::printf("rc=%d reads=%llu bases=%llu blocks=%llu dropped=%llu bad=%lld text=%d\n", rc,
