@@ -45,10 +45,14 @@
 namespace {
 
 uint8_t norm_table[256];
-bool norm_init = false;
 
+void fill_norm();
+// once per process, thread-safe: ntc_fastx_open may run on several threads at once
 void init_norm() {
-    if (norm_init) return;
+    static std::once_flag once;
+    std::call_once(once, fill_norm);
+}
+void fill_norm() {
     for (int c = 0; c < 256; c++) norm_table[c] = 'N';
     for (const char *p = "ACGTN-"; *p; p++) norm_table[(uint8_t)*p] = (uint8_t)*p;
     norm_table[(uint8_t)'a'] = 'A';
@@ -65,7 +69,6 @@ void init_norm() {
         norm_table[(uint8_t)(*p - 'A' + 'a')] = (uint8_t)*p;
     }
     for (const char *p = " \t\r\n"; *p; p++) norm_table[(uint8_t)*p] = 0;  // dropped
-    norm_init = true;
 }
 
 // growable byte buffer without zero-fill (std::vector::resize would touch every new byte)
@@ -1157,25 +1160,25 @@ struct ntc_fastx {
 extern "C" {
 
 int ntc_host_threads(void) {
-    static int cached = 0;
-    if (cached) return cached;
-    int n = 0;
-    if (const char *v = std::getenv("NTC_THREADS")) n = std::atoi(v);
-    if (n <= 0) {
-        cpu_set_t set;
-        n = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : (int)std::thread::hardware_concurrency();
-        if (FILE *f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {  // cgroup v2 CPU quota
-            char q[32] = {0};
-            unsigned long long period = 0;
-            if (std::fscanf(f, "%31s %llu", q, &period) == 2 && std::strcmp(q, "max") != 0 && period) {
-                const unsigned long long quota = std::strtoull(q, nullptr, 10);
-                const int lim = (int)((quota + period - 1) / period);
-                if (lim > 0 && lim < n) n = lim;
+    static const int cached = [] {  // once, thread-safe (inputs may open on several threads at once)
+        int n = 0;
+        if (const char *v = std::getenv("NTC_THREADS")) n = std::atoi(v);
+        if (n <= 0) {
+            cpu_set_t set;
+            n = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : (int)std::thread::hardware_concurrency();
+            if (FILE *f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {  // cgroup v2 CPU quota
+                char q[32] = {0};
+                unsigned long long period = 0;
+                if (std::fscanf(f, "%31s %llu", q, &period) == 2 && std::strcmp(q, "max") != 0 && period) {
+                    const unsigned long long quota = std::strtoull(q, nullptr, 10);
+                    const int lim = (int)((quota + period - 1) / period);
+                    if (lim > 0 && lim < n) n = lim;
+                }
+                std::fclose(f);
             }
-            std::fclose(f);
         }
-    }
-    cached = std::max(1, n);
+        return std::max(1, n);
+    }();
     return cached;
 }
 
