@@ -384,6 +384,29 @@ def test_gpu_long_reads(ctx):
     assert np.array_equal(out, bases) and np.array_equal(o2, offs)
 
 
+def test_gpu_record_length_limit(ctx):
+    """The 24-bit match length (lib.rs:226: dictionary_max < 16777216, NTC_ERR_LENGTH for the
+    reference's assert): one exact read of a unique 16.8 Mbp sequence at k = 31 parses into a
+    record of 31m + 1 bases (the jump loop steps back k at a time, lib.rs:193-203) and a
+    short head.  At 2^24 + 16 bases the long record is 2^24 - 15 (bit-exact vs the oracle,
+    decoded back); at 2^24 + 17 it would be 2^24 + 16: the call fails with NTC_ERR_LENGTH."""
+    genome = nt.synth_genome(21, (1 << 24) + 1000)
+    ix = nt.Index.build([genome.tobytes()], 31, threads=8)
+    ctx.upload(ix)
+    g = genome.tobytes()
+    bases, offs = pack_reads([g[5:5 + (1 << 24) + 16]])
+    got, goff = ctx.encode(bases, offs)
+    exp, eoff = OracleIndex(ix.n, 31, ix.rows, ix.C, ix.lcs).encode(bases, offs)
+    assert np.array_equal(goff, eoff) and np.array_equal(got, exp)
+    assert len(got) == 2 and (int(got[0]) >> 32) & 0xFFFFFF == (1 << 24) - 15 and (int(got[1]) >> 32) & 0xFFFFFF == 31
+    out, o2 = ctx.decode(got)
+    assert np.array_equal(out, bases) and np.array_equal(o2, offs)
+    bases, offs = pack_reads([g[100:300], g[5:5 + (1 << 24) + 17]])
+    with pytest.raises(nt.NtcError) as e:
+        ctx.encode(bases, offs)
+    assert e.value.code == 4 and e.value.bad_read == 1
+
+
 @pytest.mark.parametrize("link", [1, 0])
 def test_gpu_path_cover_equals_host_cover(ctx, monkeypatch, link):
     """ntc_index_upload builds the path cover on the device (list ranking, cycle cuts, and
