@@ -384,6 +384,48 @@ def test_gpu_long_reads(ctx):
     assert np.array_equal(out, bases) and np.array_equal(o2, offs)
 
 
+def test_gpu_reference_fasta_data_shape(ctx):
+    """The reference's own test (tests/fasta_data.rs:28-101) in its shape, on the GPU: 7
+    random contigs shorter than 2,000 bases, an index of them at k = 255 with reverse
+    complements, each contig encoded against it, blocks of 3 records written after a file
+    header (write_block_to, the last block num_records % 3) and decoded back block by block
+    (`while let Ok(records) = decode_block`).  Seeded numpy contigs, not the `random` crate's
+    (absent here).  A self-encoded contig parses into long records plus a head that is short
+    only when it has <= 11 bases, and a block with no short record makes write_block_to err
+    (minimal_binary_encode of the empty stream 4, encode.rs:80), which the test's `let _ =`
+    drops: with this seed blocks 1 and 2 are written and block 3 (contig 7) is dropped, so
+    the decode returns the first 6 contigs in order, bit-exact against the oracle's records."""
+    rng = np.random.default_rng(5)
+    alpha = np.frombuffer(b"ACGT", dtype=np.uint8)
+    contigs = [alpha[rng.integers(0, 4, int(rng.integers(1, 2000)))].tobytes() for _ in range(7)]
+    ix = nt.Index.build(contigs, 255)
+    ctx.upload(ix)
+    orc = OracleIndex(ix.n, 255, ix.rows, ix.C, ix.lcs)
+    buf, written = nt.file_header(), []
+    for i in range(0, 7, 3):
+        grp = contigs[i:i + 3]
+        bases, offs = pack_reads(grp)
+        recs, roff = ctx.encode(bases, offs)
+        exp, eoff = orc.encode(bases, offs)
+        assert np.array_equal(roff, eoff) and np.array_equal(recs, exp)
+        try:
+            buf += nt.write_block(recs, len(grp))
+            written += grp
+        except nt.NtcError as e:
+            assert e.code == 3  # write_block_to's Err (no short record in the block)
+    assert written == contigs[:6]
+    pos, got = 32, []
+    while True:
+        try:
+            recs, used, nrec = nt.read_block(buf[pos:])
+        except nt.NtcError:
+            break
+        pos += used
+        out, o2 = ctx.decode(recs)
+        got += [out[o2[j]:o2[j + 1]].tobytes() for j in range(len(o2) - 1)]
+    assert pos == len(buf) and got == written
+
+
 def test_gpu_record_length_limit(ctx):
     """The 24-bit match length (lib.rs:226: dictionary_max < 16777216, NTC_ERR_LENGTH for the
     reference's assert): one exact read of a unique 16.8 Mbp sequence at k = 31 parses into a
