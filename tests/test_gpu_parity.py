@@ -390,8 +390,9 @@ def test_gpu_reference_fasta_data_shape(ctx):
     complements, each contig encoded against it, blocks of 3 records written after a file
     header (write_block_to, the last block num_records % 3) and decoded back block by block
     (`while let Ok(records) = decode_block`).  Seeded numpy contigs, not the `random` crate's
-    (absent here).  A self-encoded contig parses into long records plus a head that is short
-    only when it has <= 11 bases, and a block with no short record makes write_block_to err
+    (absent here).  A contig of more than k bases parses into long records plus a head that
+    is short only when it has <= 11 bases (one shorter than k has no k-mer in the index and
+    parses into short records), and a block with no short record makes write_block_to err
     (minimal_binary_encode of the empty stream 4, encode.rs:80), which the test's `let _ =`
     drops: with this seed blocks 1 and 2 are written and block 3 (contig 7) is dropped, so
     the decode returns the first 6 contigs in order, bit-exact against the oracle's records."""
