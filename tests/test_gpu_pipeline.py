@@ -66,6 +66,45 @@ def test_encode_file_equals_blockwise_host_codec(setup, tmp_path, n, L, bpb, bat
     ctx.close()
 
 
+def test_encode_file_fasta_contigs_k255(tmp_path):
+    """The reference's other input shape: a multi-contig FASTA (src/main.rs:158 reads any
+    fastX), line-wrapped at 60 with lowercase stretches, normalised as needletail's
+    normalize(true) does (main.rs:162), at k = 255: ntc_encode_file's bytes equal the
+    container of the normalised contigs' records, and ntc_decode_file gives them back."""
+    genome = nt.synth_genome(31, 300_000)
+    ix = nt.Index.build([genome.tobytes()], 255)
+    ix.save(str(tmp_path / "idx"))
+    ctx = nt.GpuContext(0)
+    ctx.upload(ix)
+    rng = np.random.default_rng(4)
+    g = genome.tobytes()
+    contigs, text = [], bytearray()
+    for i in range(300):
+        L = int(rng.integers(1, 5000))
+        st = int(rng.integers(0, len(g) - L))
+        c = bytearray(g[st:st + L])
+        if i % 3 == 0:  # a lowercase stretch
+            a0 = int(rng.integers(0, L))
+            c[a0:a0 + 200] = bytes(c[a0:a0 + 200]).lower()
+        contigs.append(bytes(c).upper())
+        text += b">contig_%d some description\n" % i
+        text += b"".join(bytes(c[j:j + 60]) + b"\n" for j in range(0, L, 60))
+    fa = tmp_path / "c.fa"
+    fa.write_bytes(bytes(text))
+    bases = np.frombuffer(b"".join(contigs), dtype=np.uint8)
+    offs = np.cumsum([0] + [len(c) for c in contigs]).astype(np.uint64)
+    recs, roff = ctx.encode(bases, offs)
+    exp = nt.file_header() + nt.write_block(recs, len(contigs))
+    with open(tmp_path / "e.dat", "wb") as f:
+        st = nt.encode_file([ctx], str(fa), f.fileno(), threads=4)
+    assert st["reads"] == len(contigs) and st["bases"] == len(bases)
+    assert (tmp_path / "e.dat").read_bytes() == exp
+    with open(tmp_path / "d.fa", "wb") as f:
+        nt.decode_file([ctx], str(tmp_path / "e.dat"), f.fileno(), threads=4)
+    assert (tmp_path / "d.fa").read_bytes() == b"".join(b">seq.%d\n%s\n" % (i + 1, c) for i, c in enumerate(contigs))
+    ctx.close()
+
+
 def test_encode_file_reports_bad_read(setup, tmp_path):
     d, genome, ix = setup
     ctx = nt.GpuContext(0)
