@@ -37,7 +37,10 @@ roofline.algorithmic: the bytes THIS design must move per launch -- encode: the 
 profiles/algorithmic_lines.json, scripts/trace_lines.py --json) x reads; decode: one 128 B
 walk-table line per 112 bases of each long record, plus 8 B per record in and 1 B per base
 out -- over the kernel time (algorithmic frac), and traffic / algorithmic bytes (waste:
-1.0 = every line fetched once per read).
+1.0 = every line fetched once per read).  Encode also gives the lines counted distinct per
+lane step (step_lines_per_read: a line a read touches again in a later step counted again,
+as an L2 that keeps nothing across a lane's steps would fetch it) and the traffic against
+those (waste_vs_step_lines < 1: L2 kept some lines across steps).
 cpu_baseline: the faithful C oracle (oracle/ntcomp_oracle.c, test infrastructure) on one
 pinned host core, rank 0 at N = 1, on a bounded sample; it is also the parity checker.  The
 reference encoder is single-threaded (main.rs:162-173), so one core is the faithful figure;
@@ -222,9 +225,14 @@ def alg_encode(alg, wl, units, kernel_ms, traffic):
     if not w:
         return None
     per = w["k_ms4_lines_per_read"] * 128
-    return algorithmic(per * units, units, "read", kernel_ms, traffic,
-                       f"{w['k_ms4_lines_per_read']} distinct 128 B lines per read (emulator trace of "
-                       f"{w['reads']} reads, encode_core.h {w['encode_core_sha256']}) x reads")
+    r = algorithmic(per * units, units, "read", kernel_ms, traffic,
+                    f"{w['k_ms4_lines_per_read']} distinct 128 B lines per read (emulator trace of "
+                    f"{w['reads']} reads, encode_core.h {w['encode_core_sha256']}) x reads")
+    step = w.get("k_ms4_step_lines_per_read")
+    if step:  # the same lines counted distinct per lane step: no L2 reuse across a lane's steps
+        r["step_lines_per_read"] = step
+        r["waste_vs_step_lines"] = round(traffic / (step * 128 * units), 3) if traffic else None
+    return r
 
 
 def alg_decode(recs, bases, kernel_ms, traffic):
