@@ -148,8 +148,10 @@ bool build_table(const uint8_t *len, uint32_t n, uint32_t tbits, int kind, Table
     return t.e.size() < (1u << 16);
 }
 
+// The fixed tables are never destroyed: a reader closed on a detached thread (pgz_close) may
+// still have a worker inflating when the process runs its static destructors at exit.
 const Table &fixed_lit() {
-    static Table t = [] {
+    static const Table *t = new Table([] {
         uint8_t l[288];
         for (int i = 0; i < 144; i++) l[i] = 8;
         for (int i = 144; i < 256; i++) l[i] = 9;
@@ -158,18 +160,18 @@ const Table &fixed_lit() {
         Table x;
         build_table(l, 288, kLitBits, 0, x);
         return x;
-    }();
-    return t;
+    }());
+    return *t;
 }
 const Table &fixed_dist() {
-    static Table t = [] {
+    static const Table *t = new Table([] {
         uint8_t l[32];  // 30 and 31 complete the code and decode as invalid
         for (int i = 0; i < 32; i++) l[i] = 5;
         Table x;
         build_table(l, 32, kDistBits, 1, x);
         return x;
-    }();
-    return t;
+    }());
+    return *t;
 }
 
 // ---- bit input ---------------------------------------------------------------------------
