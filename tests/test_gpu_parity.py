@@ -593,6 +593,37 @@ def test_gpu_random_cases_equal_oracle(ctx):
         assert np.array_equal(out, bases) and np.array_equal(o2, offs), (i, k)
 
 
+def test_gpu_random_collections_equal_oracle():
+    """Random strain collections through the GPU (round 6's linked path cover, joint runs and
+    fork hops on many small structures): a genome of 2-40 kbp plus 1-11 strains at 0.1-5 %
+    substitutions, k from 11 to 255, the cover linked or not (ctx option path_link), reads
+    of 20-400 bases drawn across the collection with 0-2 % errors; records bit-exact vs the
+    oracle and decode(encode(x)) == x."""
+    rng = np.random.default_rng(606)
+    ctx = nt.GpuContext(0)
+    for i in range(24):
+        k = int(rng.choice([11, 15, 23, 31, 47, 63, 91, 127, 191, 255]))
+        genome = nt.synth_genome(int(rng.integers(1, 1 << 30)), int(rng.integers(2_000, 40_000)))
+        ns = int(rng.integers(1, 12))
+        strains = nt.synth_strains(genome, int(rng.integers(1, 1 << 30)), ns,
+                                   int(rng.choice([1_000, 5_000, 20_000, 50_000])))
+        texts = [genome] + [strains[j] for j in range(ns)]
+        ix = nt.Index.build([t.tobytes() for t in texts], k)
+        ctx.set_option("path_link", i % 2)
+        ctx.upload(ix)
+        n, L = int(rng.integers(50, 800)), int(rng.integers(20, 400))
+        reads = nt.synth_reads(np.concatenate(texts), int(rng.integers(1, 1 << 30)), 0, n, L,
+                               int(rng.choice([0, 5_000, 20_000])))
+        offs = np.arange(0, n * L + 1, L, dtype=np.uint64)
+        orc = OracleIndex(ix.n, k, ix.rows, ix.C, ix.lcs)
+        exp, eoff = orc.encode(reads, offs)
+        got, goff = ctx.encode(reads, offs)
+        assert np.array_equal(goff, eoff) and np.array_equal(got, exp), (i, k, ns)
+        out, o2 = ctx.decode(got)
+        assert np.array_equal(out, reads) and np.array_equal(o2, offs), (i, k, ns)
+    ctx.close()
+
+
 def test_gpu_suffix_table_depth_15():
     """The deepest suffix table (U = 15, 8.6 GB top level; the default for indexes of more than
     ~17 M nodes) gives the same records as the oracle on the C91 index."""
