@@ -770,7 +770,9 @@ def main():
         strains = nt.synth_strains(genome, 3, args.strains, args.strain_snp_ppm)
         texts = [genome] + [strains[i] for i in range(args.strains)]
         # S91 calls in flight (--strain-inflight): round 5 measured two 3 % slower than one (k_ms4
-        # at 0.89 of the line rate then, two persistent grids only competing)
+        # at 0.89 of the line rate then, two persistent grids only competing); round 6, with the
+        # linked cover, 131.3-133.9 against 130.7-132.4 Gbases/s (3 runs each, one box,
+        # profiles/round6/ab_strain_inflight/): within the noise, one stays the default
         n_s = max(1, min(args.strain_inflight, len(ctxs) or 1))
         index = setup_index(texts, "S", n_s)
         sctx = ctxs[:n_s]
