@@ -1081,6 +1081,14 @@ constexpr uint32_t kStageSlots = 4;  // 64 B: one write request instead of four 
 constexpr uint32_t kNeInE0 = 0x7FFFFFu;
 NTC_HD uint32_t entry0_count(const Entry &e0) { return (e0.dk >> 8) & kNeInE0; }
 
+// NTC_QCACHE: the non-joint run loop keeps its query words as two aligned pairs across chunks
+// (MsLaneT::qA0..qB1).  It takes k_ms4 to 72 VGPRs, so the non-joint build runs at 7 waves
+// (NTC_MS_WAVES): A/B on one box, 3 runs each, C91 k_ms4 2.70-2.72 -> 2.60-2.64 ms, step
+// 4.31-4.33 -> 4.26-4.27 ms (351.6-351.9 against 346.5-347.9 Gbases/s); 7 waves without the
+// cache 2.67-2.68 ms, 4.34-4.37 ms (profiles/round6/ab_qcache/).  The joint build has no room.
+#ifndef NTC_QCACHE
+#define NTC_QCACHE 1
+#endif
 // kJoint: joint path runs over multi-node intervals (note_single); k_ms4 is built both ways
 // and the upload picks one (ctx option "joint"), since the code costs C91 ~1 % of k_ms4
 template <bool kJoint>
@@ -1099,6 +1107,15 @@ struct MsLaneT {
     // kModeBs); a separate field costs k_ms4 a wave of occupancy (72 VGPRs is the 7-wave limit).
     NTC_HD uint32_t &jy() { return l1; }
     bool try_run;
+#if NTC_QCACHE
+    // (non-joint build) the run loop's query words as two aligned pairs, pair qpa (words
+    // 2 qpa, 2 qpa + 1) and pair qpa + 1: the next 64-character chunk of a run needs at most
+    // one new pair, so the loop loads 16 aligned bytes instead of 24 at each chunk and none
+    // when the run stopped inside the chunk before.  Q does not change during a launch, so a
+    // pair held from an earlier read stays valid.
+    uint64_t qA0 = 0, qA1 = 0, qB0 = 0, qB1 = 0;
+    uint32_t qpa = 0xFFFFFFFFu;
+#endif
 
     // Q (NTC_START_WINDOW): the read-start window is loaded here, so that its round trip
     // overlaps the other lanes' run loads instead of adding one to the read-start block
@@ -1390,9 +1407,29 @@ struct MsLaneT {
                 const uint64_t q = qo + p + m - pre;
                 const uint64_t qi = q >> 5;
                 const uint32_t qs = (uint32_t)(q & 31) * 2;
-                uint64_t w0, w1;
-                load_w2(Q + qi, w0, w1);
-                const uint64_t w2 = Q[qi + 2];
+                uint64_t w0, w1, w2;
+#if NTC_QCACHE
+                if constexpr (!kJoint) {
+                    const uint32_t a2 = (uint32_t)(qi >> 1);  // words qi .. qi + 2 lie in pairs a2, a2 + 1
+                    const bool hit = a2 == qpa, slide = qpa != 0xFFFFFFFFu && a2 == qpa + 1;
+                    uint64_t L0 = slide ? qB0 : qA0, L1 = slide ? qB1 : qA1, H0 = qB0, H1 = qB1;
+                    if (!hit && !slide) load_w2(Q + 2 * (uint64_t)a2, L0, L1);
+                    if (!hit) load_w2(Q + 2 * (uint64_t)a2 + 2, H0, H1);
+                    qpa = a2;
+                    qA0 = L0;
+                    qA1 = L1;
+                    qB0 = H0;
+                    qB1 = H1;
+                    const bool odd = qi & 1;
+                    w0 = odd ? L1 : L0;
+                    w1 = odd ? H0 : L1;
+                    w2 = odd ? H1 : H0;
+                } else
+#endif
+                {
+                    load_w2(Q + qi, w0, w1);
+                    w2 = Q[qi + 2];
+                }
                 const uint64_t qa = qs ? ((w0 >> qs) | (w1 << (64 - qs))) : w0;
                 const uint64_t qb2 = qs ? ((w1 >> qs) | (w2 << (64 - qs))) : w1;
                 const uint64_t xa = qa ^ pa, xb = qb2 ^ pb;

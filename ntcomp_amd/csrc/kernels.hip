@@ -287,13 +287,14 @@ __device__ __forceinline__ uint32_t parse_one(const Enc4Args &a, uint64_t r) {
     return (uint32_t)rc;
 }
 
-// waves per SIMD k_ms4 is compiled for: without joint runs 8 (64 VGPRs, no scratch: 20 KB of LDS
-// per block, 8 blocks = the CU's 160 KB), with them 7 (72 VGPRs, no scratch, 22 KB of LDS).  The
+// waves per SIMD k_ms4 is compiled for: without joint runs 7 with the query-word cache (72 VGPRs,
+// no scratch, 20 KB of LDS per block; 8 at 64 VGPRs without it, 8 blocks = the CU's 160 KB), with
+// them 7 (72 VGPRs, no scratch, 22 KB of LDS).  The
 // joint build's lane state fits 72 since round 5 (32-bit read id, the overflow reservation read
 // back from obase, the binary search's best interval in LDS, the queue bounds in SGPRs): A/B on
 // one box, S91 k_ms4 10.71 -> 10.42 ms at 7 waves; C91 unchanged at 8 (2.69 -> 2.68 ms)
 #ifndef NTC_MS_WAVES
-#define NTC_MS_WAVES 8
+#define NTC_MS_WAVES (NTC_QCACHE ? 7 : 8)  // the query-word cache takes 72 VGPRs (encode_core.h)
 #endif
 #ifndef NTC_MS_WAVES_J
 #define NTC_MS_WAVES_J 7
