@@ -228,6 +228,9 @@ int encode4_impl(ntc_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_offs, u
                  uint64_t total_bases, uint64_t *d_rec_out, uint64_t cap, uint64_t *d_rec_offs) {
     if (ctx->index_decode_only)
         return set_err(ctx, NTC_ERR_NO_INDEX, "the index was uploaded for decode only (ctx option decode_only)");
+    // k_ms4's query-word cache names 16-byte pairs of the 2-bit stream by a 32-bit index
+    // (encode_core.h NTC_QCACHE): a call stays below 2^38 bases (256 Gi, more than HBM holds)
+    if (total_bases >= (1ull << 38)) return set_err(ctx, NTC_ERR_CAPACITY, "2^38 bases or more in one call: split the batch");
     Enc4Args a{};
     a.ix = ctx->dix;
     a.bases = d_bases;
